@@ -1,0 +1,108 @@
+/*
+ * libvcg_hip — MI355X (gfx950) native kernels for the video-segment-point clip scorer of
+ * SeoYeonnLee/Video-Chapter-Generation (TwoStream = TSM-ResNet-50 + BERT-base + ChapterHead).
+ *
+ * C ABI conventions
+ *   - device pointers + explicit int sizes; no torch types; `dtype` is VCG_F32 (0) or VCG_BF16 (1)
+ *     and selects the storage type of activation tensors (parameters/grads are always fp32);
+ *   - activations are NHWC (vision) / row-major [tokens][hidden] (text);
+ *   - every call is asynchronous on `stream` and returns 0 or a negative vcg_status; the
+ *     message of the last failure on the calling thread is vcg_last_error();
+ *   - workspaces are caller-allocated; size them with the matching *_ws_bytes query;
+ *   - gradients are ACCUMULATED (+=) into fp32 buffers so micro-batch accumulation is free.
+ *
+ * Each entry point cites the reference code it replaces (paths relative to
+ * video_chapter_generation/ in the reference repository).
+ */
+#ifndef VCG_HIP_H
+#define VCG_HIP_H
+#include <hip/hip_runtime.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VCG_API
+enum { VCG_F32 = 0, VCG_BF16 = 1 };
+enum { VCG_OK = 0, VCG_ERR_INVALID = -1, VCG_ERR_UNSUPPORTED = -2, VCG_ERR_HIP = -3 };
+enum { VCG_ACT_NONE = 0, VCG_ACT_RELU = 1, VCG_ACT_GELU = 2, VCG_ACT_TANH = 3, VCG_ACT_GELU_BWD = 4 };
+
+/* ---- library ---------------------------------------------------------------------------- */
+VCG_API const char* vcg_last_error(void);
+VCG_API int vcg_version(void);
+VCG_API int vcg_init(int device);      /* per-device handle; fails unless the device is gfx950 */
+VCG_API int vcg_finalize(void);
+VCG_API int vcg_sync(hipStream_t stream);
+
+/* ---- MFMA implicit-GEMM engine (igemm.hip) ---------------------------------------------- */
+/* torchvision conv2d inside Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15,68-77), with
+ * TemporalShift.shift (ops/temporal_shift.py:33-51, inserted by make_temporal_shift :133-144)
+ * fused into the input gather; optional BatchNorm partial statistics from the epilogue. */
+VCG_API int vcg_conv_stats_tiles(int M);
+VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
+/* autograd of conv2d: input gradient (transposed-conv gather) */
+VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, hipStream_t stream);
+/* autograd of conv2d: weight gradient, split-K over pixels, written in OIHW (state-dict layout) */
+VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad);
+VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
+/* nn.Linear / BertSelfAttention matmuls (HF BertModel via model/lang/bert_hugface.py:20; ChapterHead
+ * projections model/fusion/two_stream.py:60-61,79-85) */
+VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B, long long ldb, void* C, long long ldc, const float* bias, int act, const void* residual, long long ldr, void* aux, float alpha, hipStream_t stream);
+VCG_API int vcg_gemm_batched(int dtype, int transA, int transB, int M, int N, int K, const void* A, long long lda, long long a_so, long long a_si, const void* B, long long ldb, long long b_so, long long b_si, void* C, long long ldc, long long c_so, long long c_si, int batch_outer, int batch_inner, const float* bias, int act, float alpha, hipStream_t stream);
+VCG_API long long vcg_gemm_splitk_ws_bytes(int dtype, int M, int N, int K);
+VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B, long long ldb, float* out, int accumulate, float* ws, long long ws_bytes, hipStream_t stream);
+
+/* ---- vision support (vision.hip) --------------------------------------------------------- */
+/* nn.BatchNorm2d (train: batch stats + running update; eval: running stats; the test driver's
+ * batch-stat eval test_video_segment_point.py:116-122) */
+VCG_API int vcg_bn_finalize(const float* stats, int mtiles, int M, int C, const float* gamma, const float* beta, float* mean_out, float* invstd_out, float* scale_out, float* shift_out, float* running_mean, float* running_var, float momentum, float eps, hipStream_t s);
+VCG_API int vcg_bn_eval_params(const float* gamma, const float* beta, const float* rm, const float* rv, float eps, int C, float* mean_out, float* invstd_out, float* scale, float* shift, hipStream_t s);
+VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const void* res, const float* rscale, const float* rshift, int relu, void* out, long long P, int C, hipStream_t s);
+VCG_API long long vcg_bn_bwd_ws_bytes(long long P, int C);
+VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean, const float* invstd, long long P, int C, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, int accumulate, hipStream_t s);
+VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, long long count, int train_stats, void* dy, void* gout, long long P, int C, hipStream_t s);
+/* torchvision stem maxpool 3x3/2 and avgpool + fc=Identity (resnet50_tsm.py:19) */
+VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* idx, int N, int H, int W, int C, hipStream_t s);
+VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C, hipStream_t s);
+VCG_API int vcg_avgpool_fwd(int dtype, const void* x, float* y, int N, int HW, int C, hipStream_t s);
+VCG_API int vcg_avgpool_bwd(int dtype, const float* dy, void* dx, int N, int HW, int C, hipStream_t s);
+/* rearrange 'b t c h w -> (b t) c h w' (two_stream.py:183) + NCHW->NHWC staging */
+VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cpad, hipStream_t s);
+VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int KH, int KW, int Cpad, int transposed, hipStream_t s);
+VCG_API int vcg_cast_from_f32(int dtype, const float* in, void* out, long long n, hipStream_t s);
+VCG_API int vcg_cast_to_f32(int dtype, const void* in, float* out, long long n, hipStream_t s);
+/* TemporalShift.shift (ops/temporal_shift.py:33-51) on NCHW; direction 1 = its adjoint */
+VCG_API int vcg_tsm_shift(int dtype, const void* x, void* y, long long n_batch, int T, int C, long long HW, int fold_div, int direction, hipStream_t s);
+VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other, void* dx, long long NT, int T, long long HW, int C, int fold, hipStream_t s);
+
+/* ---- BERT support (bert.hip) ------------------------------------------------------------- */
+VCG_API int vcg_embed_ln_fwd(int dtype, const long long* ids, const float* word, const float* pos, const float* type, const float* gamma, const float* beta, void* out, float* mean, float* rstd, int B, int L, int H, float eps, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API long long vcg_ln_bwd_ws_bytes(int rows, int H);
+VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, const float* word, const float* pos, const float* type, const float* gamma, const float* mean, const float* rstd, float* word_grad, float* pos_grad, float* type_grad, float* gamma_grad, float* beta_grad, float* ws, long long ws_bytes, int B, int L, int H, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_ln_fwd(int dtype, const void* x, const void* res, const float* gamma, const float* beta, void* out, float* mean, float* rstd, int rows, int H, float eps, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* res, const float* gamma, const float* mean, const float* rstd, void* dx, void* dres, float* gamma_grad, float* beta_grad, float* ws, long long ws_bytes, int rows, int H, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API long long vcg_colsum_ws_bytes(int rows, int N);
+VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, float* out, int accumulate, float* ws, long long ws_bytes, hipStream_t s);
+VCG_API int vcg_attn_softmax_fwd(int dtype, const void* S, const long long* mask, void* P, void* Pd, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_attn_softmax_bwd(int dtype, const void* dPd, const void* P, void* dS, int Z, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_tanh_bwd(int dtype, const void* dy, const void* t, void* dx, long long n, hipStream_t s);
+
+/* ---- fusion head + loss (head.hip): ChapterHead mlp (two_stream.py:51-95), softmax (:189),
+ *      F.cross_entropy (train_video_segment_point.py:165) ----------------------------------- */
+VCG_API int vcg_head_mlp_fwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* bias, float* logits, float* prob, int B, int T, int hid, int O, hipStream_t s);
+VCG_API int vcg_head_mlp_bwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* dlogits, void* dV, void* dL, float* dW, float* dbias, int B, int T, int hid, int O, hipStream_t s);
+VCG_API int vcg_cross_entropy_fwd(const float* logits, const long long* labels, float* loss, int B, int C, hipStream_t s);
+VCG_API int vcg_cross_entropy_bwd(const float* logits, const long long* labels, const float* dloss, float* dlogits, int B, int C, hipStream_t s);
+
+/* ---- optimiser (optim.hip): clip_grad_norm_ (train_video_segment_point.py:204) + AdamW with the
+ *      two groups of TwoStream.configure_optimizers (two_stream.py:127-169) ------------------- */
+VCG_API long long vcg_sumsq_ws_bytes(void);
+VCG_API int vcg_sumsq(const float* x, long long n, float* ws, float* out, hipStream_t s);
+VCG_API int vcg_adamw(float* p, const float* g, float* m, float* v, const unsigned char* wd_flags, int flag_shift, long long n, float lr, float beta1, float beta2, float eps, float wd, float step_size, float bc2_sqrt, const float* sumsq, float max_norm, float grad_scale, void* bf16_shadow, hipStream_t s);
+
+/* ---- synthetic inputs (synth.hip): seeded clip windows / weights, bit-identical to numpy ---- */
+VCG_API int vcg_synth(int kind, void* out, long long n, unsigned long long key, double a, double b, hipStream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

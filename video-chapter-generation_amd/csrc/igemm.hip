@@ -1,0 +1,794 @@
+// MFMA implicit-GEMM engine for gfx950.
+//
+// One kernel template computes  C[M][N] = sum_k A[m][k] * B[n][k]  where A and B are
+// *gathered* operands:
+//   OP_DENSE_K   row-major [rows][K] (k contiguous)            -> linear fwd X, W
+//   OP_IM2COL    implicit im2col of an NHWC activation          -> conv fwd A (TSM shift fused)
+//   OP_DGRAD     transposed-conv gather of an NHWC gradient     -> conv dgrad A
+//   OP_DENSE_MN  [K][cols] (cols contiguous)                    -> wgrad dy^T, linear dW / dX
+//   OP_IM2COL_T  im2col^T of an NHWC activation (k = pixel)     -> conv wgrad B (TSM fused)
+// K-contiguous operands are staged in LDS as [rows][BK] and read with ds_read_b64/b128;
+// MN-contiguous operands are staged as [BK][cols] and read with ds_read_b64_tr_b16 (bf16).
+// Both sides use the same permutation of k inside a BK tile, so the dot product is exact.
+//
+// Replaces the ATen conv / addmm kernels reached from torchvision ResNet-50
+// (reference video_chapter_generation/model/vision/resnet50_tsm.py:15) and HF BertModel
+// (model/lang/bert_hugface.py:20) on the TwoStream hot path (model/fusion/two_stream.py:172-194).
+#include "common.h"
+
+namespace vcg {
+
+enum { OP_DENSE_K = 0, OP_IM2COL = 1, OP_DGRAD = 2, OP_DENSE_MN = 3, OP_IM2COL_T = 4 };
+enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2 };
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
+
+template <typename T> struct Cfg;
+template <> struct Cfg<float> { static constexpr int VEC = 4, BK = 16, LDK = 20; };   // 80-B rows
+template <> struct Cfg<bf16_t> { static constexpr int VEC = 8, BK = 32, LDK = 40; };  // 80-B rows
+
+template <typename T, int COLS> struct LdMN {
+  // padded element stride of a [BK][COLS] tile (bank-conflict-free for the fragment reads)
+  static constexpr int v = sizeof(T) == 2 ? (COLS == 128 ? 144 : 80) : (COLS == 128 ? 132 : 68);
+};
+
+constexpr bool is_kcontig(int mode) { return mode == OP_DENSE_K || mode == OP_IM2COL || mode == OP_DGRAD; }
+
+struct FastDiv {  // q = n / d for 0 <= n < 2^31
+  uint32_t d, m, s;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  uint32_t hi = __umulhi(n, f.m);
+  return (uint32_t)(((uint64_t)hi + n) >> f.s);
+}
+
+struct OpArgs {
+  const void* ptr;
+  long long ld;   // dense modes: leading dimension in elements
+  int rows;       // number of valid rows (K-contig) / cols (MN-contig)
+  // conv geometry (gather modes)
+  int N, H, W, C, logC;  // gathered tensor is NHWC [N][H][W][C] (C power of two)
+  int GH, GW;            // grid that indexes the rows (IM2COL: output; DGRAD: dx; IM2COL_T: dy)
+  int KH, KW, stride, pad;
+  int tsm_T, tsm_fold;   // TSM temporal shift fused into the gather (fold = 0: off)
+  FastDiv fd_ghw, fd_gw, fd_T;
+};
+
+struct GemmParams {
+  int M, N, K;
+  int k_per_split;  // multiple of BK
+  OpArgs a, b;
+  void* C;
+  long long ldc;
+  const float* bias;
+  int act;
+  const void* residual;
+  long long ldr;
+  void* aux;  // optional copy of the pre-activation value
+  float alpha;
+  float* stats;  // EPI_STATS: float2 [N][mtiles] (mean, M2) per column per m-tile
+  float* ws;     // EPI_SPLITK: fp32 slabs [split][M][N]
+  // batched mode (batch_inner > 0): blockIdx.z = zo * batch_inner + zi selects element offsets
+  int batch_inner;
+  long long a_so, a_si, b_so, b_si, c_so, c_si;
+};
+
+// ------------------------------------------------------------------------------------
+// Tile loaders: global -> registers -> LDS
+// ------------------------------------------------------------------------------------
+template <typename T, int ROWS, int MODE> struct Loader {
+  static constexpr int VEC = Cfg<T>::VEC, BK = Cfg<T>::BK;
+  static constexpr int NC = ROWS * 4 / 256;  // 16-B chunks per thread (BK/VEC == 4)
+  static constexpr bool KC = is_kcontig(MODE);
+  static constexpr int CPR = ROWS / VEC;  // MN-contig: chunks per k-row
+
+  uint4 reg[NC];
+  // per-chunk state
+  const T* ptr[NC];   // DENSE_K / DENSE_MN base pointer (null = invalid row/col)
+  int ra[NC], rb[NC], rc[NC];  // gather coordinates
+  int sub[NC];        // k offset (K-contig) or k-row (MN-contig) of the chunk inside a tile
+  int lds_off[NC];
+
+  __device__ __forceinline__ void init(const OpArgs& a, int row0, int tid) {
+    const T* base = reinterpret_cast<const T*>(a.ptr);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int q = tid + j * 256;
+      if constexpr (KC) {
+        const int row = q >> 2;
+        const int kc = (q & 3) * VEC;
+        sub[j] = kc;
+        lds_off[j] = row * Cfg<T>::LDK + kc;
+        const int r = row0 + row;
+        const bool valid = r < a.rows;
+        if constexpr (MODE == OP_DENSE_K) {
+          ptr[j] = valid ? base + (long long)r * a.ld : nullptr;
+        } else {
+          // decompose the row into (n, y, x) over the row grid
+          const int n = r / (a.GH * a.GW);
+          const int rem = r - n * a.GH * a.GW;
+          const int y = rem / a.GW;
+          const int x = rem - y * a.GW;
+          ptr[j] = valid ? base + (long long)n * a.H * a.W * a.C : nullptr;
+          if constexpr (MODE == OP_IM2COL) {
+            ra[j] = y * a.stride - a.pad;
+            rb[j] = x * a.stride - a.pad;
+            rc[j] = a.tsm_fold > 0 ? (n % a.tsm_T) : 0;
+          } else {  // DGRAD: rows are dx pixels, gathered tensor is dy [N][H][W][C]
+            ra[j] = y + a.pad;
+            rb[j] = x + a.pad;
+            rc[j] = 0;
+          }
+        }
+      } else {
+        const int krow = q / CPR;
+        const int cc = (q - krow * CPR) * VEC;
+        sub[j] = krow;
+        lds_off[j] = krow * LdMN<T, ROWS>::v + cc;
+        const int col = row0 + cc;
+        const bool valid = col < a.rows;
+        if constexpr (MODE == OP_DENSE_MN) {
+          ptr[j] = valid ? base + col : nullptr;
+        } else {  // IM2COL_T: col = (tap, ci) over the NHWC activation
+          const int tap = col >> a.logC;
+          const int ci = col & (a.C - 1);
+          const int kh = tap / a.KW;
+          const int kw = tap - kh * a.KW;
+          ptr[j] = (valid && tap < a.KH * a.KW) ? base + ci : nullptr;
+          ra[j] = kh - a.pad;
+          rb[j] = kw - a.pad;
+          int dt = 0;
+          if (a.tsm_fold > 0) dt = ci < a.tsm_fold ? 1 : (ci < 2 * a.tsm_fold ? -1 : 0);
+          rc[j] = dt;
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(const OpArgs& a, int k0, int kend) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const T* p = nullptr;
+      if constexpr (MODE == OP_DENSE_K) {
+        const int k = k0 + sub[j];
+        if (ptr[j] && k < kend) p = ptr[j] + k;
+      } else if constexpr (MODE == OP_IM2COL) {
+        const int k = k0 + sub[j];
+        const int tap = k >> a.logC;
+        const int c = k & (a.C - 1);
+        const int kh = tap / a.KW;
+        const int kw = tap - kh * a.KW;
+        const int ih = ra[j] + kh, iw = rb[j] + kw;
+        if (ptr[j] && k < kend && kh < a.KH && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
+          long long off = ((long long)(ih * a.W + iw) << a.logC) + c;
+          bool ok = true;
+          if (a.tsm_fold > 0) {
+            const int dt = c < a.tsm_fold ? 1 : (c < 2 * a.tsm_fold ? -1 : 0);
+            const int t2 = rc[j] + dt;
+            ok = t2 >= 0 && t2 < a.tsm_T;
+            off += (long long)dt * a.H * a.W * a.C;
+          }
+          if (ok) p = ptr[j] + off;
+        }
+      } else if constexpr (MODE == OP_DGRAD) {
+        const int k = k0 + sub[j];
+        const int tap = k >> a.logC;
+        const int c = k & (a.C - 1);
+        const int kh = tap / a.KW;
+        const int kw = tap - kh * a.KW;
+        int yy = ra[j] - kh, xx = rb[j] - kw;
+        bool ok = ptr[j] && k < kend && kh < a.KH && yy >= 0 && xx >= 0;
+        if (a.stride == 2) {
+          ok = ok && ((yy | xx) & 1) == 0;
+          yy >>= 1;
+          xx >>= 1;
+        }
+        ok = ok && yy < a.H && xx < a.W;
+        if (ok) p = ptr[j] + (((long long)(yy * a.W + xx)) << a.logC) + c;
+      } else if constexpr (MODE == OP_DENSE_MN) {
+        const int k = k0 + sub[j];
+        if (ptr[j] && k < kend) p = ptr[j] + (long long)k * a.ld;
+      } else {  // IM2COL_T
+        const int k = k0 + sub[j];
+        if (ptr[j] && k < kend) {
+          const uint32_t n = fdiv((uint32_t)k, a.fd_ghw);
+          const int rem = k - (int)n * a.GH * a.GW;
+          const int y = (int)fdiv((uint32_t)rem, a.fd_gw);
+          const int x = rem - y * a.GW;
+          const int ih = y * a.stride + ra[j], iw = x * a.stride + rb[j];
+          bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+          int n2 = (int)n;
+          if (rc[j] != 0) {
+            const int t = (int)n - (int)fdiv(n, a.fd_T) * a.tsm_T;
+            const int t2 = t + rc[j];
+            ok = ok && t2 >= 0 && t2 < a.tsm_T;
+            n2 += rc[j];
+          }
+          if (ok) p = ptr[j] + ((((long long)n2 * a.H + ih) * a.W + iw) << a.logC);
+        }
+      }
+      reg[j] = p ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+    }
+  }
+
+  __device__ __forceinline__ void store(T* lds) const {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) *reinterpret_cast<uint4*>(lds + lds_off[j]) = reg[j];
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// Fragment reads (LDS -> registers), shared by the A and B sides.
+// lane = 16*g + i. bf16: element j of the 16x16x32 fragment is k = 4g + 16*(j>>2) + (j&3).
+// f32: k-step s of the 16x16x4 fragment is k = 4g + s.
+// ------------------------------------------------------------------------------------
+template <typename T, int ROWS, bool KC> struct Frag;
+
+template <int ROWS> struct Frag<bf16_t, ROWS, true> {
+  typedef s16x8 type;
+  static __device__ __forceinline__ s16x8 read(const bf16_t* lds, int r0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const bf16_t* p = lds + (r0 + i) * Cfg<bf16_t>::LDK + 4 * g;
+    s16x4 lo = *reinterpret_cast<const s16x4*>(p);
+    s16x4 hi = *reinterpret_cast<const s16x4*>(p + 16);
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+};
+template <int ROWS> struct Frag<bf16_t, ROWS, false> {
+  typedef s16x8 type;
+  static __device__ __forceinline__ s16x8 read(const bf16_t* lds, int r0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const int q = i >> 2, pp = i & 3;
+    constexpr int LD = LdMN<bf16_t, ROWS>::v;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const bf16_t* p0 = lds + (4 * g + q) * LD + r0 + 4 * pp;
+    const bf16_t* p1 = p0 + 16 * LD;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+};
+template <int ROWS> struct Frag<float, ROWS, true> {
+  typedef f32x4 type;
+  static __device__ __forceinline__ f32x4 read(const float* lds, int r0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    return *reinterpret_cast<const f32x4*>(lds + (r0 + i) * Cfg<float>::LDK + 4 * g);
+  }
+};
+template <int ROWS> struct Frag<float, ROWS, false> {
+  typedef f32x4 type;
+  static __device__ __forceinline__ f32x4 read(const float* lds, int r0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    constexpr int LD = LdMN<float, ROWS>::v;
+    const float* p = lds + (4 * g) * LD + r0 + i;
+    return f32x4{p[0], p[LD], p[2 * LD], p[3 * LD]};
+  }
+};
+
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16_t> {
+  static __device__ __forceinline__ void run(f32x4& acc, const s16x8& a, const s16x8& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+};
+template <> struct Mfma<float> {
+  static __device__ __forceinline__ void run(f32x4& acc, const f32x4& a, const f32x4& b) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  if (act == ACT_GELU) return gelu_erf(v);
+  if (act == ACT_TANH) return tanhf(v);
+  return v;
+}
+
+template <typename T, int ROWS, int MODE> constexpr int tile_elems() {
+  return is_kcontig(MODE) ? ROWS * Cfg<T>::LDK : Cfg<T>::BK * LdMN<T, ROWS>::v;
+}
+template <typename T, int BM, int BN, int AM, int BMD, int EPI> constexpr int smem_bytes() {
+  constexpr int mainloop = 2 * (tile_elems<T, BM, AM>() + tile_elems<T, BN, BMD>()) * (int)sizeof(T);
+  constexpr int epi = EPI == EPI_SPLITK ? 0 : BM * (BN + 16 / (int)sizeof(T)) * (int)sizeof(T) + 2 * 1024 * 4;
+  return mainloop > epi ? mainloop : epi;
+}
+
+// ------------------------------------------------------------------------------------
+// The kernel: 256 threads = 4 waves (2x2), wave tile (BM/2)x(BN/2) of 16x16 MFMA tiles.
+// ------------------------------------------------------------------------------------
+template <typename T, int BM, int BN, int AM, int BMD, int EPI>
+__global__ __launch_bounds__(256) void igemm_kernel(GemmParams p) {
+  constexpr int BK = Cfg<T>::BK, VEC = Cfg<T>::VEC;
+  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int AE = tile_elems<T, BM, AM>(), BE = tile_elems<T, BN, BMD>();
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<T, BM, BN, AM, BMD, EPI>()];
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = As + 2 * AE;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  int kb = blockIdx.z * p.k_per_split;
+  OpArgs oa = p.a, ob = p.b;
+  T* Cout = reinterpret_cast<T*>(p.C);
+  const T* Res = reinterpret_cast<const T*>(p.residual);
+  if (p.batch_inner > 0) {
+    const int zo = blockIdx.z / p.batch_inner, zi = blockIdx.z - zo * p.batch_inner;
+    kb = 0;
+    oa.ptr = reinterpret_cast<const T*>(oa.ptr) + zo * p.a_so + zi * p.a_si;
+    ob.ptr = reinterpret_cast<const T*>(ob.ptr) + zo * p.b_so + zi * p.b_si;
+    Cout += zo * p.c_so + zi * p.c_si;
+    if (Res) Res += zo * p.c_so + zi * p.c_si;
+  }
+  const int ke = min(p.K, kb + p.k_per_split);
+
+  Loader<T, BM, AM> la;
+  Loader<T, BN, BMD> lb;
+  la.init(oa, m0, tid);
+  lb.init(ob, n0, tid);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = (ke - kb + BK - 1) / BK;
+  if (ntiles > 0) {
+    la.load(oa, kb, ke);
+    lb.load(ob, kb, ke);
+    la.store(As);
+    lb.store(Bs);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) {
+      la.load(oa, kb + (t + 1) * BK, ke);
+      lb.load(ob, kb + (t + 1) * BK, ke);
+    }
+    const T* Ac = As + cur * AE;
+    const T* Bc = Bs + cur * BE;
+    typename Frag<T, BM, is_kcontig(AM)>::type af[MT];
+    typename Frag<T, BN, is_kcontig(BMD)>::type bfr[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) af[i] = Frag<T, BM, is_kcontig(AM)>::read(Ac, wm * (BM / 2) + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bfr[j] = Frag<T, BN, is_kcontig(BMD)>::read(Bc, wn * (BN / 2) + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
+    if (t + 1 < ntiles) {
+      la.store(As + (cur ^ 1) * AE);
+      lb.store(Bs + (cur ^ 1) * BE);
+    }
+    __syncthreads();
+  }
+
+  const int g = lane >> 4, ci = lane & 15;
+  if constexpr (EPI == EPI_SPLITK) {
+    float* ws = p.ws + (long long)blockIdx.z * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = n0 + wn * (BN / 2) + j * 16 + ci;
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * (BM / 2) + i * 16 + g * 4 + r;
+          if (row < p.M) ws[(long long)row * p.N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  } else {
+    // Stage alpha*acc + bias as T in LDS, then write 16-B vectors (residual / act / aux / stats).
+    constexpr int LDC = BN + VEC;
+    T* Cs = reinterpret_cast<T*>(smem);
+    float* red = reinterpret_cast<float*>(smem + BM * LDC * sizeof(T));
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int lc = wn * (BN / 2) + j * 16 + ci;
+      const float bv = (p.bias && n0 + lc < p.N) ? p.bias[n0 + lc] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = wm * (BM / 2) + i * 16 + g * 4 + r;
+          Cs[lr * LDC + lc] = from_f<T>(acc[i][j][r] * p.alpha + bv);
+        }
+    }
+    __syncthreads();
+    constexpr int CPR = BN / VEC;          // 16-B chunks per tile row
+    constexpr int RPP = 256 / CPR;         // rows per pass
+    const int cc = (tid % CPR) * VEC;
+    const int rr = tid / CPR;
+    const int col = n0 + cc;
+    float csum[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) csum[e] = 0.f;
+    for (int lr = rr; lr < BM; lr += RPP) {
+      const int row = m0 + lr;
+      if (row >= p.M || col >= p.N) continue;
+      float v[VEC];
+      load16<T>(Cs + lr * LDC + cc, v);
+      if (Res) {
+        float rv[VEC];
+        load16<T>(Res + (long long)row * p.ldr + col, rv);
+        if (p.act == ACT_GELU_BWD) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) v[e] *= gelu_erf_grad(rv[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) v[e] += rv[e];
+        }
+      }
+      if (p.aux) store16<T>(reinterpret_cast<T*>(p.aux) + (long long)row * p.ldc + col, v);
+      if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) v[e] = apply_act(v[e], p.act);
+      }
+      store16<T>(Cout + (long long)row * p.ldc + col, v);
+      if constexpr (EPI == EPI_STATS) {
+        // statistics of the values as stored (rounded to T)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) csum[e] += to_f<T>(from_f<T>(v[e]));
+      }
+    }
+    if constexpr (EPI == EPI_STATS) {
+      // Per-column (mean, M2) over this tile's valid rows, two passes over the staged tile.
+      // The stats epilogue is only used without residual/activation, so the staged value
+      // (rounded to T) is exactly the stored value that BN will normalise.
+      const int valid_rows = min(BM, p.M - m0);
+      if (tid < 2 * BN) red[tid] = 0.f;
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) atomicAdd(&red[cc + e], csum[e]);
+      __syncthreads();
+      float mean[VEC], m2[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        mean[e] = red[cc + e] / (float)valid_rows;
+        m2[e] = 0.f;
+      }
+      for (int lr = rr; lr < BM; lr += RPP) {
+        const int row = m0 + lr;
+        if (row >= p.M || col >= p.N) continue;
+        float v[VEC];
+        load16<T>(Cs + lr * LDC + cc, v);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float d = v[e] - mean[e];
+          m2[e] += d * d;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) atomicAdd(&red[BN + cc + e], m2[e]);
+      __syncthreads();
+      if (rr == 0 && col < p.N) {
+        const int mtiles = gridDim.y;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          float2 st = make_float2(mean[e], red[BN + cc + e]);
+          reinterpret_cast<float2*>(p.stats)[(long long)(col + e) * mtiles + blockIdx.y] = st;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Host-side launch helpers
+// ------------------------------------------------------------------------------------
+static int ilog2_exact(int c) {
+  int l = 0;
+  while ((1 << l) < c) ++l;
+  return (1 << l) == c ? l : -1;
+}
+
+static OpArgs dense_op(const void* ptr, long long ld, int rows) {
+  OpArgs a{};
+  a.ptr = ptr;
+  a.ld = ld;
+  a.rows = rows;
+  return a;
+}
+
+template <typename T, int BM, int BN, int AM, int BMD, int EPI>
+static int launch(const GemmParams& p, int splits, hipStream_t s) {
+  dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
+  hipLaunchKernelGGL((igemm_kernel<T, BM, BN, AM, BMD, EPI>), grid, dim3(256), 0, s, p);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+// dispatch on BN (64 / 128) with BM = 128
+template <typename T, int AM, int BMD, int EPI>
+static int launch_bn(const GemmParams& p, int splits, hipStream_t s) {
+  if (p.N % 128 == 0 || p.N > 64 * 3) return launch<T, 128, 128, AM, BMD, EPI>(p, splits, s);
+  return launch<T, 128, 64, AM, BMD, EPI>(p, splits, s);
+}
+
+static int mtiles_of(int M) { return (M + 127) / 128; }
+
+template <typename T, int AM, int BMD>
+static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
+  if (epi == EPI_STORE) return launch_bn<T, AM, BMD, EPI_STORE>(p, splits, s);
+  if (epi == EPI_STATS) return launch_bn<T, AM, BMD, EPI_STATS>(p, splits, s);
+  return launch_bn<T, AM, BMD, EPI_SPLITK>(p, splits, s);
+}
+
+// split-K reduction: out[m][n] (+)= sum_s ws[s][m][n], with optional conv-weight layout permutation
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long MN, int N,
+                                     float* __restrict__ out, int accumulate, int conv_perm, int KH, int KW,
+                                     int Cpad, int Cin, float scale) {
+  long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (idx >= MN) return;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += ws[s * MN + idx];
+  v *= scale;
+  long long dst = idx;
+  if (conv_perm) {
+    // idx = m * N + n, m = cout, n = (kh*KW + kw)*Cpad + ci  ->  OIHW [cout][ci][kh][kw]
+    const int m = (int)(idx / N);
+    const int n = (int)(idx - (long long)m * N);
+    const int tap = n / Cpad;
+    const int ci = n - tap * Cpad;
+    if (ci >= Cin) return;
+    const int kh = tap / KW, kw = tap - (tap / KW) * KW;
+    dst = (((long long)m * Cin + ci) * KH + kh) * KW + kw;
+  }
+  if (accumulate) out[dst] += v;
+  else out[dst] = v;
+}
+
+static int choose_splits(int M, int N, int K, int BK) {
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  int splits = (1024 + tiles - 1) / tiles;
+  const int max_splits = (K + 16 * BK - 1) / (16 * BK);  // at least 16 k-tiles per split
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  return splits;
+}
+
+}  // namespace vcg
+
+using namespace vcg;
+
+// ====================================================================================
+// C ABI
+// ====================================================================================
+
+VCG_API int vcg_conv_stats_tiles(int M) { return mtiles_of(M); }
+
+// y[N*OH*OW][Cout] = conv(x[N][H][W][C], w[Cout][KH][KW][C]); optional BN partial stats.
+// TSM shift (reference ops/temporal_shift.py:33-51) fused into the A gather when tsm_fold > 0.
+VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W,
+                         int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold,
+                         hipStream_t stream) {
+  const int logC = ilog2_exact(C);
+  VCG_REQUIRE(logC >= 0, "C must be a power of two");
+  VCG_REQUIRE(dtype == VCG_F32 ? C >= 4 : C >= 8, "C too small for 16-B gathers");
+  VCG_REQUIRE(Cout % 64 == 0, "Cout must be a multiple of 64");
+  VCG_REQUIRE(tsm_fold == 0 || (tsm_T > 0 && N % tsm_T == 0 && tsm_fold % 8 == 0 && 2 * tsm_fold <= C),
+              "bad TSM geometry");
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  GemmParams p{};
+  p.M = N * OH * OW;
+  p.N = Cout;
+  p.K = KH * KW * C;
+  p.k_per_split = p.K + 64;
+  const bool dense = (KH == 1 && KW == 1 && stride == 1 && pad == 0 && tsm_fold == 0);
+  if (dense) {
+    p.a = dense_op(x, C, p.M);
+  } else {
+    OpArgs a{};
+    a.ptr = x; a.rows = p.M; a.N = N; a.H = H; a.W = W; a.C = C; a.logC = logC;
+    a.GH = OH; a.GW = OW; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+    a.tsm_T = tsm_T; a.tsm_fold = tsm_fold;
+    p.a = a;
+  }
+  p.b = dense_op(w, p.K, Cout);
+  p.C = y;
+  p.ldc = Cout;
+  p.alpha = 1.f;
+  p.stats = stats;
+  const int epi = stats ? EPI_STATS : EPI_STORE;
+  if (dtype == VCG_BF16) {
+    return dense ? run_gemm<bf16_t, OP_DENSE_K, OP_DENSE_K>(p, epi, 1, stream)
+                 : run_gemm<bf16_t, OP_IM2COL, OP_DENSE_K>(p, epi, 1, stream);
+  }
+  return dense ? run_gemm<float, OP_DENSE_K, OP_DENSE_K>(p, epi, 1, stream)
+               : run_gemm<float, OP_IM2COL, OP_DENSE_K>(p, epi, 1, stream);
+}
+
+// dx[N][H][W][C] = conv_transpose(dy[N][OH][OW][Cout], wt[C][KH][KW][Cout])
+VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H, int W, int C,
+                           int Cout, int KH, int KW, int stride, int pad, hipStream_t stream) {
+  const int logCo = ilog2_exact(Cout);
+  VCG_REQUIRE(logCo >= 0 && Cout >= 8, "Cout must be a power of two >= 8");
+  VCG_REQUIRE(C % 64 == 0, "C must be a multiple of 64");
+  VCG_REQUIRE(stride == 1 || stride == 2, "stride must be 1 or 2");
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  GemmParams p{};
+  p.M = N * H * W;
+  p.N = C;
+  p.K = KH * KW * Cout;
+  p.k_per_split = p.K + 64;
+  const bool dense = (KH == 1 && KW == 1 && stride == 1 && pad == 0);
+  if (dense) {
+    p.a = dense_op(dy, Cout, p.M);
+  } else {
+    OpArgs a{};
+    a.ptr = dy; a.rows = p.M; a.N = N; a.H = OH; a.W = OW; a.C = Cout; a.logC = logCo;
+    a.GH = H; a.GW = W; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+    p.a = a;
+  }
+  p.b = dense_op(wt, p.K, C);
+  p.C = dx;
+  p.ldc = C;
+  p.alpha = 1.f;
+  if (dtype == VCG_BF16) {
+    return dense ? run_gemm<bf16_t, OP_DENSE_K, OP_DENSE_K>(p, EPI_STORE, 1, stream)
+                 : run_gemm<bf16_t, OP_DGRAD, OP_DENSE_K>(p, EPI_STORE, 1, stream);
+  }
+  return dense ? run_gemm<float, OP_DENSE_K, OP_DENSE_K>(p, EPI_STORE, 1, stream)
+               : run_gemm<float, OP_DGRAD, OP_DENSE_K>(p, EPI_STORE, 1, stream);
+}
+
+static void wgrad_geometry(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad,
+                           int* M, int* Nn, int* K, int* splits) {
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  *M = Cout;
+  *Nn = KH * KW * C;
+  *K = N * OH * OW;
+  const int BK = dtype == VCG_BF16 ? 32 : 16;
+  *splits = choose_splits(*M, *Nn, *K, BK);
+}
+
+VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW,
+                                          int stride, int pad) {
+  int M, Nn, K, splits;
+  wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits);
+  return (long long)splits * M * Nn * 4;
+}
+
+// dw (fp32, OIHW [Cout][Cin][KH][KW]) (+)= sum_pixels dy (x) im2col(x). C = padded channels of x.
+VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, int accumulate, float* ws,
+                           long long ws_bytes, int N, int H, int W, int C, int Cin, int Cout, int KH, int KW,
+                           int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream) {
+  const int logC = ilog2_exact(C);
+  VCG_REQUIRE(logC >= 0, "C must be a power of two");
+  VCG_REQUIRE(Cout % 64 == 0, "Cout must be a multiple of 64");
+  int M, Nn, K, splits;
+  wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits);
+  VCG_REQUIRE(ws_bytes >= (long long)splits * M * Nn * 4, "workspace too small");
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  const int BK = dtype == VCG_BF16 ? 32 : 16;
+  GemmParams p{};
+  p.M = M;
+  p.N = Nn;
+  p.K = K;
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (K + kps - 1) / kps;
+  p.k_per_split = kps;
+  p.a = dense_op(dy, Cout, Cout);  // A[m=cout][k=pixel] = dy[pixel][cout]
+  OpArgs b{};
+  b.ptr = x; b.rows = Nn; b.N = N; b.H = H; b.W = W; b.C = C; b.logC = logC;
+  b.GH = OH; b.GW = OW; b.KH = KH; b.KW = KW; b.stride = stride; b.pad = pad;
+  b.tsm_T = tsm_T > 0 ? tsm_T : 1; b.tsm_fold = tsm_fold;
+  b.fd_ghw = make_fastdiv(OH * OW); b.fd_gw = make_fastdiv(OW); b.fd_T = make_fastdiv(b.tsm_T);
+  p.b = b;
+  p.ws = ws;
+  p.alpha = 1.f;
+  int rc = dtype == VCG_BF16 ? run_gemm<bf16_t, OP_DENSE_MN, OP_IM2COL_T>(p, EPI_SPLITK, splits, stream)
+                             : run_gemm<float, OP_DENSE_MN, OP_IM2COL_T>(p, EPI_SPLITK, splits, stream);
+  if (rc) return rc;
+  const long long MN = (long long)M * Nn;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, splits,
+                     MN, Nn, dw, accumulate, 1, KH, KW, C, Cin, 1.f);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+// C[M][N] = act(alpha * op(A) op(B)^T + bias + residual)
+//   transA = 0: A stored [M][lda>=K];  transA = 1: A stored [K][lda>=M]
+//   transB = 0: B stored [N][ldb>=K];  transB = 1: B stored [K][ldb>=N]
+VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                     const void* B, long long ldb, void* C, long long ldc, const float* bias, int act,
+                     const void* residual, long long ldr, void* aux, float alpha, hipStream_t stream) {
+  const int VEC = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(N % VEC == 0 && ldc % VEC == 0 && K % VEC == 0, "N, ldc, K must be multiples of 16 bytes");
+  VCG_REQUIRE(M > 0 && N > 0 && K > 0, "empty GEMM");
+  GemmParams p{};
+  p.M = M; p.N = N; p.K = K; p.k_per_split = K + 64;
+  p.a = dense_op(A, lda, M);
+  p.b = dense_op(B, ldb, N);
+  p.C = C; p.ldc = ldc; p.bias = bias; p.act = act; p.residual = residual; p.ldr = ldr; p.aux = aux;
+  p.alpha = alpha;
+#define VCG_GEMM_CASE(TT)                                                                   \
+  if (!transA && !transB) return run_gemm<TT, OP_DENSE_K, OP_DENSE_K>(p, EPI_STORE, 1, stream);   \
+  if (!transA && transB) return run_gemm<TT, OP_DENSE_K, OP_DENSE_MN>(p, EPI_STORE, 1, stream);   \
+  if (transA && !transB) return run_gemm<TT, OP_DENSE_MN, OP_DENSE_K>(p, EPI_STORE, 1, stream);   \
+  return run_gemm<TT, OP_DENSE_MN, OP_DENSE_MN>(p, EPI_STORE, 1, stream);
+  if (dtype == VCG_BF16) { VCG_GEMM_CASE(bf16_t) }
+  VCG_GEMM_CASE(float)
+#undef VCG_GEMM_CASE
+}
+
+VCG_API long long vcg_gemm_splitk_ws_bytes(int dtype, int M, int N, int K) {
+  const int splits = choose_splits(M, N, K, dtype == VCG_BF16 ? 32 : 16);
+  return (long long)splits * M * N * 4;
+}
+
+// out (fp32 [M][N]) (+)= op(A) op(B)^T, split over K (used for weight gradients).
+VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                            const void* B, long long ldb, float* out, int accumulate, float* ws, long long ws_bytes,
+                            hipStream_t stream) {
+  const int BK = dtype == VCG_BF16 ? 32 : 16;
+  int splits = choose_splits(M, N, K, BK);
+  VCG_REQUIRE(ws_bytes >= (long long)splits * M * N * 4, "workspace too small");
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (K + kps - 1) / kps;
+  GemmParams p{};
+  p.M = M; p.N = N; p.K = K; p.k_per_split = kps;
+  p.a = dense_op(A, lda, M);
+  p.b = dense_op(B, ldb, N);
+  p.ws = ws;
+  p.alpha = 1.f;
+  int rc;
+#define VCG_SK_CASE(TT)                                                                             \
+  if (!transA && !transB) rc = run_gemm<TT, OP_DENSE_K, OP_DENSE_K>(p, EPI_SPLITK, splits, stream);       \
+  else if (!transA && transB) rc = run_gemm<TT, OP_DENSE_K, OP_DENSE_MN>(p, EPI_SPLITK, splits, stream);  \
+  else if (transA && !transB) rc = run_gemm<TT, OP_DENSE_MN, OP_DENSE_K>(p, EPI_SPLITK, splits, stream);  \
+  else rc = run_gemm<TT, OP_DENSE_MN, OP_DENSE_MN>(p, EPI_SPLITK, splits, stream);
+  if (dtype == VCG_BF16) { VCG_SK_CASE(bf16_t) } else { VCG_SK_CASE(float) }
+#undef VCG_SK_CASE
+  if (rc) return rc;
+  const long long MN = (long long)M * N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, splits,
+                     MN, N, out, accumulate, 0, 1, 1, 1, 1, 1.f);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+// Batched C = act(alpha * op(A) op(B)^T + bias): element z = zo*batch_inner + zi of the batch
+// reads A + zo*a_so + zi*a_si (same for B, C). Used for the attention score / context products.
+// Operand rows/cols beyond M/N/K are zero-filled by the loaders; K need not be a multiple of
+// the 16-B vector when the A/B rows are padded with zeros up to it (attention P / dS buffers).
+VCG_API int vcg_gemm_batched(int dtype, int transA, int transB, int M, int N, int K, const void* A, long long lda,
+                             long long a_so, long long a_si, const void* B, long long ldb, long long b_so,
+                             long long b_si, void* C, long long ldc, long long c_so, long long c_si, int batch_outer,
+                             int batch_inner, const float* bias, int act, float alpha, hipStream_t stream) {
+  const int VEC = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(N % VEC == 0 && ldc % VEC == 0, "N and ldc must be multiples of 16 bytes");
+  VCG_REQUIRE(batch_outer > 0 && batch_inner > 0 && M > 0 && N > 0 && K > 0, "empty batched GEMM");
+  GemmParams p{};
+  p.M = M; p.N = N; p.K = K; p.k_per_split = K + 64;
+  p.a = dense_op(A, lda, M);
+  p.b = dense_op(B, ldb, N);
+  p.C = C; p.ldc = ldc; p.bias = bias; p.act = act; p.alpha = alpha;
+  p.batch_inner = batch_inner;
+  p.a_so = a_so; p.a_si = a_si; p.b_so = b_so; p.b_si = b_si; p.c_so = c_so; p.c_si = c_si;
+  const int z = batch_outer * batch_inner;
+#define VCG_BT_CASE(TT)                                                                   \
+  if (!transA && !transB) return run_gemm<TT, OP_DENSE_K, OP_DENSE_K>(p, EPI_STORE, z, stream);   \
+  if (!transA && transB) return run_gemm<TT, OP_DENSE_K, OP_DENSE_MN>(p, EPI_STORE, z, stream);   \
+  if (transA && !transB) return run_gemm<TT, OP_DENSE_MN, OP_DENSE_K>(p, EPI_STORE, z, stream);   \
+  return run_gemm<TT, OP_DENSE_MN, OP_DENSE_MN>(p, EPI_STORE, z, stream);
+  if (dtype == VCG_BF16) { VCG_BT_CASE(bf16_t) }
+  VCG_BT_CASE(float)
+#undef VCG_BT_CASE
+}

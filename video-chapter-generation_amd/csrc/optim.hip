@@ -1,0 +1,94 @@
+// Fused gradient-norm clipping + AdamW over the flat fp32 parameter buffer.
+//
+// Reproduces torch.nn.utils.clip_grad_norm_(params, 1.0) followed by torch.optim.AdamW with the
+// two parameter groups of TwoStream.configure_optimizers (reference model/fusion/two_stream.py:127-169,
+// driver train_video_segment_point.py:204-205). The clip coefficient is computed on the device from
+// the sum of squares, so the step never synchronises with the host.
+#include "common.h"
+
+using namespace vcg;
+
+namespace {
+
+__global__ void sumsq_part_kernel(const float* __restrict__ x, long long n, float* __restrict__ part) {
+  __shared__ float red[16];
+  double s = 0;  // per-thread double accumulation keeps the norm order-insensitive enough
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    s += (double)v * v;
+  }
+  const float r = block_sum((float)s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+__global__ void sumsq_final_kernel(const float* __restrict__ part, int nb, float* __restrict__ out) {
+  __shared__ double sd[256];
+  double s = 0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+  sd[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) sd[threadIdx.x] += sd[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)sd[0];
+}
+
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, const unsigned char* __restrict__ wd_flags, int flag_shift,
+                             long long n, float lr, float beta1, float beta2, float eps, float wd, float step_size,
+                             float bc2_sqrt, const float* __restrict__ sumsq, float max_norm, float grad_scale,
+                             bf16_t* __restrict__ shadow) {
+  float coef = grad_scale;
+  if (sumsq) {
+    const float norm = sqrtf(sumsq[0]) * grad_scale;
+    float c = max_norm / (norm + 1e-6f);
+    c = c < 1.f ? c : 1.f;
+    coef = grad_scale * c;
+  }
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * coef;
+    float pi = p[i];
+    const bool decay = wd_flags ? wd_flags[i >> flag_shift] != 0 : true;
+    if (decay) pi = pi * (1.f - lr * wd);
+    float mi = m[i];
+    mi = mi + (1.f - beta1) * (gi - mi);  // exp_avg.lerp_(grad, 1 - beta1)
+    float vi = v[i] * beta2;
+    vi = vi + (1.f - beta2) * gi * gi;    // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+    if (shadow) shadow[i] = f2bf(pi);
+  }
+}
+
+}  // namespace
+
+VCG_API long long vcg_sumsq_ws_bytes(void) { return 1024 * 4; }
+
+VCG_API int vcg_sumsq(const float* x, long long n, float* ws, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(sumsq_part_kernel, dim3(1024), dim3(256), 0, s, x, n, ws);
+  VCG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, s, ws, 1024, out);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+// One AdamW step. wd_flags: one byte per (1 << flag_shift) elements selecting the decay group
+// (null = decay everything). step_size = lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t).
+// sumsq (device scalar, nullable) enables clipping to max_norm; grad_scale (e.g. 1/world) is
+// applied to the gradients before clipping.
+VCG_API int vcg_adamw(float* p, const float* g, float* m, float* v, const unsigned char* wd_flags, int flag_shift,
+                      long long n, float lr, float beta1, float beta2, float eps, float wd, float step_size,
+                      float bc2_sqrt, const float* sumsq, float max_norm, float grad_scale, void* bf16_shadow,
+                      hipStream_t s) {
+  long long nb = (n + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nb), dim3(256), 0, s, p, g, m, v, wd_flags, flag_shift, n,
+                     lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, sumsq, max_norm, grad_scale,
+                     (bf16_t*)bf16_shadow);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}

@@ -1,0 +1,357 @@
+"""Tensor-level wrappers over the libvcg_hip C ABI.
+
+Every wrapper checks device / dtype / contiguity, passes raw device pointers plus sizes, and
+launches on torch's current HIP stream. There is no CPU or ATen fallback: a non-GPU tensor or
+a missing library raises.
+"""
+import torch
+
+from . import _lib
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_GELU_BWD = 0, 1, 2, 3, 4
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dt_code(dtype):
+    try:
+        return _DT[dtype]
+    except KeyError:
+        raise TypeError(f"unsupported storage dtype {dtype}; expected float32 or bfloat16")
+
+
+def torch_dtype(precision):
+    return {"fp32": torch.float32, "bf16": torch.bfloat16}[precision]
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def P(t):
+    """Device pointer of a contiguous GPU tensor (None passes NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("libvcg_hip ops need GPU tensors (no CPU fallback)")
+    return t.data_ptr()
+
+
+def _chk(t, dtype=None, name="tensor"):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be on the GPU (libvcg_hip has no CPU path)")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype != dtype:
+        raise RuntimeError(f"{name} has dtype {t.dtype}, expected {dtype}")
+
+
+def ws(nbytes, device):
+    return torch.empty((max(int(nbytes), 4) + 3) // 4, dtype=torch.float32, device=device)
+
+
+# ----------------------------------------------------------------------------- engine
+def conv_out_hw(H, W, KH, KW, stride, pad):
+    return (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+
+
+def stats_tiles(M):
+    return _lib.query("vcg_conv_stats_tiles", M)
+
+
+def conv_fwd(x, w, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, stats=None, out=None):
+    """x: NHWC [N,H,W,C]; w: [Cout,KH,KW,C] (same storage dtype). Returns y [N,OH,OW,Cout]."""
+    _chk(x, name="x")
+    _chk(w, x.dtype, "w")
+    OH, OW = conv_out_hw(H, W, KH, KW, stride, pad)
+    y = out if out is not None else torch.empty((N, OH, OW, Cout), dtype=x.dtype, device=x.device)
+    _lib.call("vcg_conv_fwd", dt_code(x.dtype), P(x), P(w), P(y), P(stats), N, H, W, C, Cout, KH, KW, stride, pad,
+              tsm_T, tsm_fold, stream())
+    return y
+
+
+def conv_dgrad(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, out=None):
+    """dy: NHWC [N,OH,OW,Cout]; wt: [C,KH,KW,Cout]. Returns dx [N,H,W,C]."""
+    _chk(dy, name="dy")
+    _chk(wt, dy.dtype, "wt")
+    dx = out if out is not None else torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    _lib.call("vcg_conv_dgrad", dt_code(dy.dtype), P(dy), P(wt), P(dx), N, H, W, C, Cout, KH, KW, stride, pad,
+              stream())
+    return dx
+
+
+def conv_wgrad(x, dy, dw, N, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, accumulate=True,
+               workspace=None):
+    """dw (fp32 OIHW [Cout,Cin,KH,KW]) += wgrad. x: NHWC with C (padded) channels."""
+    _chk(x, name="x")
+    _chk(dy, x.dtype, "dy")
+    _chk(dw, torch.float32, "dw")
+    nbytes = _lib.query("vcg_conv_wgrad_ws_bytes", dt_code(x.dtype), N, H, W, C, Cout, KH, KW, stride, pad)
+    if workspace is None or workspace.numel() * 4 < nbytes:
+        workspace = ws(nbytes, x.device)
+    _lib.call("vcg_conv_wgrad", dt_code(x.dtype), P(x), P(dy), P(dw), int(accumulate), P(workspace),
+              workspace.numel() * 4, N, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_T, tsm_fold, stream())
+    return workspace
+
+
+def conv_wgrad_ws_bytes(dtype, N, H, W, C, Cout, KH, KW, stride, pad):
+    return _lib.query("vcg_conv_wgrad_ws_bytes", dt_code(dtype), N, H, W, C, Cout, KH, KW, stride, pad)
+
+
+def gemm(A, B, M, N, K, lda, ldb, transA=False, transB=False, out=None, ldc=None, bias=None, act=ACT_NONE,
+         residual=None, ldr=None, aux=None, alpha=1.0):
+    """C[M,N] = act(alpha * op(A) @ op(B)^T + bias (+ residual)). A/B/C share the storage dtype.
+    transA=False: A is [M][lda]; True: A is [K][lda]. transB=False: B is [N][ldb]; True: [K][ldb]."""
+    if out is None:
+        out = torch.empty((M, N), dtype=A.dtype, device=A.device)
+        ldc = N
+    ldc = ldc if ldc is not None else N
+    _lib.call("vcg_gemm", dt_code(A.dtype), int(transA), int(transB), M, N, K, P(A), lda, P(B), ldb, P(out), ldc,
+              P(bias), act, P(residual), ldr if ldr is not None else ldc, P(aux), float(alpha), stream())
+    return out
+
+
+def gemm_batched(A, B, C, M, N, K, lda, ldb, ldc, a_so, a_si, b_so, b_si, c_so, c_si, batch_outer, batch_inner,
+                 transA=False, transB=False, bias=None, act=ACT_NONE, alpha=1.0):
+    _lib.call("vcg_gemm_batched", dt_code(A.dtype), int(transA), int(transB), M, N, K, P(A), lda, a_so, a_si, P(B),
+              ldb, b_so, b_si, P(C), ldc, c_so, c_si, batch_outer, batch_inner, P(bias), act, float(alpha), stream())
+    return C
+
+
+def gemm_splitk(A, B, out, M, N, K, lda, ldb, transA=False, transB=False, accumulate=True, workspace=None):
+    """out (fp32 [M,N]) (+)= op(A) @ op(B)^T, split over K."""
+    _chk(out, torch.float32, "out")
+    nbytes = _lib.query("vcg_gemm_splitk_ws_bytes", dt_code(A.dtype), M, N, K)
+    if workspace is None or workspace.numel() * 4 < nbytes:
+        workspace = ws(nbytes, A.device)
+    _lib.call("vcg_gemm_splitk", dt_code(A.dtype), int(transA), int(transB), M, N, K, P(A), lda, P(B), ldb, P(out),
+              int(accumulate), P(workspace), workspace.numel() * 4, stream())
+    return workspace
+
+
+# ----------------------------------------------------------------------------- vision
+def bn_finalize(stats, mtiles, M, C, gamma, beta, mean, invstd, scale, shift, running_mean=None, running_var=None,
+                momentum=0.1, eps=1e-5):
+    _lib.call("vcg_bn_finalize", P(stats), mtiles, M, C, P(gamma), P(beta), P(mean), P(invstd), P(scale), P(shift),
+              P(running_mean), P(running_var), float(momentum), float(eps), stream())
+
+
+def bn_eval_params(gamma, beta, rm, rv, eps, C, mean, invstd, scale, shift):
+    _lib.call("vcg_bn_eval_params", P(gamma), P(beta), P(rm), P(rv), float(eps), C, P(mean), P(invstd), P(scale),
+              P(shift), stream())
+
+
+def bn_apply(y, scale, shift, C, relu, res=None, rscale=None, rshift=None, out=None):
+    out = out if out is not None else torch.empty_like(y)
+    _lib.call("vcg_bn_apply", dt_code(y.dtype), P(y), P(scale), P(shift), P(res), P(rscale), P(rshift), int(relu),
+              P(out), y.numel() // C, C, stream())
+    return out
+
+
+def bn_bwd_reduce(dout, mask, y, mean, invstd, C, sum_g, sum_gx, dgamma=None, dbeta=None, workspace=None):
+    Pn = y.numel() // C
+    nbytes = _lib.query("vcg_bn_bwd_ws_bytes", Pn, C)
+    if workspace is None or workspace.numel() * 4 < nbytes:
+        workspace = ws(nbytes, y.device)
+    _lib.call("vcg_bn_bwd_reduce", dt_code(y.dtype), P(dout), P(mask), P(y), P(mean), P(invstd), Pn, C, P(workspace),
+              workspace.numel() * 4, P(sum_g), P(sum_gx), P(dgamma), P(dbeta), 1, stream())
+    return workspace
+
+
+def bn_bwd_apply(dout, mask, y, mean, invstd, gamma, sum_g, sum_gx, C, train_stats, gout=None, out=None):
+    Pn = y.numel() // C
+    dy = out if out is not None else torch.empty_like(y)
+    _lib.call("vcg_bn_bwd_apply", dt_code(y.dtype), P(dout), P(mask), P(y), P(mean), P(invstd), P(gamma), P(sum_g),
+              P(sum_gx), Pn, int(train_stats), P(dy), P(gout), Pn, C, stream())
+    return dy
+
+
+def maxpool_fwd(x, N, H, W, C):
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = torch.empty((N, OH, OW, C), dtype=x.dtype, device=x.device)
+    idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+    _lib.call("vcg_maxpool_fwd", dt_code(x.dtype), P(x), P(y), P(idx), N, H, W, C, stream())
+    return y, idx
+
+
+def maxpool_bwd(dy, idx, N, H, W, C):
+    dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    _lib.call("vcg_maxpool_bwd", dt_code(dy.dtype), P(dy), P(idx), P(dx), N, H, W, C, stream())
+    return dx
+
+
+def avgpool_fwd(x, N, HW, C):
+    y = torch.empty((N, C), dtype=torch.float32, device=x.device)
+    _lib.call("vcg_avgpool_fwd", dt_code(x.dtype), P(x), P(y), N, HW, C, stream())
+    return y
+
+
+def avgpool_bwd(dy, N, HW, C, dtype):
+    dx = torch.empty((N, HW, C), dtype=dtype, device=dy.device)
+    _lib.call("vcg_avgpool_bwd", dt_code(dtype), P(dy), P(dx), N, HW, C, stream())
+    return dx
+
+
+def frames_to_nhwc(src, N, C, H, W, Cpad, dtype):
+    _chk(src, torch.float32, "frames")
+    dst = torch.empty((N, H, W, Cpad), dtype=dtype, device=src.device)
+    _lib.call("vcg_frames_to_nhwc", dt_code(dtype), P(src), P(dst), N, C, H, W, Cpad, stream())
+    return dst
+
+
+def weight_prep(w, Cpad, dtype, transposed=False, out=None):
+    _chk(w, torch.float32, "weight")
+    Cout, Cin, KH, KW = w.shape
+    shape = (Cin, KH, KW, Cout) if transposed else (Cout, KH, KW, Cpad)
+    out = out if out is not None else torch.empty(shape, dtype=dtype, device=w.device)
+    _lib.call("vcg_weight_prep", dt_code(dtype), P(w), P(out), Cout, Cin, KH, KW, Cpad, int(transposed), stream())
+    return out
+
+
+def cast_from_f32(x, dtype, out=None):
+    _chk(x, torch.float32, "x")
+    out = out if out is not None else torch.empty(x.shape, dtype=dtype, device=x.device)
+    _lib.call("vcg_cast_from_f32", dt_code(dtype), P(x), P(out), x.numel(), stream())
+    return out
+
+
+def cast_to_f32(x, out=None):
+    out = out if out is not None else torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    _lib.call("vcg_cast_to_f32", dt_code(x.dtype), P(x), P(out), x.numel(), stream())
+    return out
+
+
+def tsm_shift(x, n_segment, fold_div, direction=0):
+    """Reference TemporalShift.shift on an NCHW tensor [n_batch*T, C, H, W] (direction 1 = adjoint)."""
+    _chk(x, name="x")
+    nt, c, h, w = x.shape
+    y = torch.empty_like(x)
+    _lib.call("vcg_tsm_shift", dt_code(x.dtype), P(x), P(y), nt // n_segment, n_segment, c, h * w, fold_div,
+              direction, stream())
+    return y
+
+
+def tsm_unshift_add(dshift, other, NT, T, HW, C, fold):
+    dx = torch.empty_like(dshift)
+    _lib.call("vcg_tsm_unshift_add", dt_code(dshift.dtype), P(dshift), P(other), P(dx), NT, T, HW, C, fold, stream())
+    return dx
+
+
+# ----------------------------------------------------------------------------- text
+def embed_ln_fwd(ids, word, pos, typ, gamma, beta, B, L, H, eps, dtype, p=0.0, seed=0):
+    out = torch.empty((B * L, H), dtype=dtype, device=ids.device)
+    mean = torch.empty(B * L, dtype=torch.float32, device=ids.device)
+    rstd = torch.empty(B * L, dtype=torch.float32, device=ids.device)
+    _lib.call("vcg_embed_ln_fwd", dt_code(dtype), P(ids), P(word), P(pos), P(typ), P(gamma), P(beta), P(out), P(mean),
+              P(rstd), B, L, H, float(eps), float(p), int(seed) & (2**64 - 1), stream())
+    return out, mean, rstd
+
+
+def embed_ln_bwd(dout, ids, word, pos, typ, gamma, mean, rstd, word_grad, pos_grad, type_grad, gamma_grad, beta_grad,
+                 B, L, H, p=0.0, seed=0):
+    nbytes = _lib.query("vcg_ln_bwd_ws_bytes", B * L, H)
+    w = ws(nbytes, dout.device)
+    _lib.call("vcg_embed_ln_bwd", dt_code(dout.dtype), P(dout), P(ids), P(word), P(pos), P(typ), P(gamma), P(mean),
+              P(rstd), P(word_grad), P(pos_grad), P(type_grad), P(gamma_grad), P(beta_grad), P(w), w.numel() * 4, B, L,
+              H, float(p), int(seed) & (2**64 - 1), stream())
+
+
+def ln_fwd(x, res, gamma, beta, rows, H, eps, p=0.0, seed=0):
+    out = torch.empty_like(x)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    _lib.call("vcg_ln_fwd", dt_code(x.dtype), P(x), P(res), P(gamma), P(beta), P(out), P(mean), P(rstd), rows, H,
+              float(eps), float(p), int(seed) & (2**64 - 1), stream())
+    return out, mean, rstd
+
+
+def ln_bwd(dout, x, res, gamma, mean, rstd, gamma_grad, beta_grad, rows, H, p=0.0, seed=0, want_dx=True,
+           want_dres=True):
+    dx = torch.empty_like(dout) if want_dx else None
+    dres = torch.empty_like(dout) if want_dres else None
+    nbytes = _lib.query("vcg_ln_bwd_ws_bytes", rows, H)
+    w = ws(nbytes, dout.device)
+    _lib.call("vcg_ln_bwd", dt_code(dout.dtype), P(dout), P(x), P(res), P(gamma), P(mean), P(rstd), P(dx), P(dres),
+              P(gamma_grad), P(beta_grad), P(w), w.numel() * 4, rows, H, float(p), int(seed) & (2**64 - 1), stream())
+    return dx, dres
+
+
+def colsum(x, ld, rows, N, out, accumulate=True):
+    nbytes = _lib.query("vcg_colsum_ws_bytes", rows, N)
+    w = ws(nbytes, x.device)
+    _lib.call("vcg_colsum", dt_code(x.dtype), P(x), ld, rows, N, P(out), int(accumulate), P(w), w.numel() * 4,
+              stream())
+
+
+def attn_softmax_fwd(S, mask, P_out, Pd_out, B, nh, L, Lp, scale, p=0.0, seed=0):
+    _lib.call("vcg_attn_softmax_fwd", dt_code(S.dtype), P(S), P(mask), P(P_out), P(Pd_out), B, nh, L, Lp,
+              float(scale), float(p), int(seed) & (2**64 - 1), stream())
+
+
+def attn_softmax_bwd(dPd, Pm, dS, Z, L, Lp, scale, p=0.0, seed=0):
+    _lib.call("vcg_attn_softmax_bwd", dt_code(dPd.dtype), P(dPd), P(Pm), P(dS), Z, L, Lp, float(scale), float(p),
+              int(seed) & (2**64 - 1), stream())
+
+
+def tanh_bwd(dy, t):
+    dx = torch.empty_like(dy)
+    _lib.call("vcg_tanh_bwd", dt_code(dy.dtype), P(dy), P(t), P(dx), dy.numel(), stream())
+    return dx
+
+
+# ----------------------------------------------------------------------------- head / loss
+def head_mlp_fwd(Vout, Lout, W, bias, B, T, hid, O):
+    logits = torch.empty((B, O), dtype=torch.float32, device=Vout.device)
+    prob = torch.empty((B, O), dtype=torch.float32, device=Vout.device)
+    _lib.call("vcg_head_mlp_fwd", dt_code(Vout.dtype), P(Vout), P(Lout), P(W), P(bias), P(logits), P(prob), B, T,
+              hid, O, stream())
+    return logits, prob
+
+
+def head_mlp_bwd(Vout, Lout, W, dlogits, dW, dbias, B, T, hid, O):
+    dV = torch.empty_like(Vout)
+    dL = torch.empty_like(Lout)
+    _lib.call("vcg_head_mlp_bwd", dt_code(Vout.dtype), P(Vout), P(Lout), P(W), P(dlogits), P(dV), P(dL), P(dW),
+              P(dbias), B, T, hid, O, stream())
+    return dV, dL
+
+
+def cross_entropy_fwd(logits, labels):
+    B, C = logits.shape
+    loss = torch.empty((), dtype=torch.float32, device=logits.device)
+    _lib.call("vcg_cross_entropy_fwd", P(logits), P(labels), P(loss), B, C, stream())
+    return loss
+
+
+def cross_entropy_bwd(logits, labels, dloss):
+    B, C = logits.shape
+    dlogits = torch.empty_like(logits)
+    _lib.call("vcg_cross_entropy_bwd", P(logits), P(labels), P(dloss), P(dlogits), B, C, stream())
+    return dlogits
+
+
+# ----------------------------------------------------------------------------- optimiser
+def sumsq(x, out, workspace=None):
+    if workspace is None:
+        workspace = ws(_lib.query("vcg_sumsq_ws_bytes"), x.device)
+    _lib.call("vcg_sumsq", P(x), x.numel(), P(workspace), P(out), stream())
+    return workspace
+
+
+def adamw(p, g, m, v, wd_flags, flag_shift, lr, beta1, beta2, eps, wd, step, sumsq_dev=None, max_norm=1.0,
+          grad_scale=1.0, shadow=None):
+    import math
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    step_size = lr / bc1
+    bc2_sqrt = math.sqrt(bc2)
+    _lib.call("vcg_adamw", P(p), P(g), P(m), P(v), P(wd_flags), flag_shift, p.numel(), float(lr), float(beta1),
+              float(beta2), float(eps), float(wd), float(step_size), float(bc2_sqrt), P(sumsq_dev), float(max_norm),
+              float(grad_scale), P(shadow), stream())
+
+
+# ----------------------------------------------------------------------------- synthetic data
+def synth(out, kind, key, a, b):
+    _lib.call("vcg_synth", int(kind), P(out), out.numel(), int(key) & (2**64 - 1), float(a), float(b), stream())
+    return out
