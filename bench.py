@@ -1,0 +1,232 @@
+#!/usr/bin/env python
+"""Benchmark: clip-windows/sec of a TwoStream train step (TSM-ResNet-50 + BERT-base + ChapterHead,
+16 frames x 224^2 + 128 tokens per window, B=64 windows per GPU, bf16, fused clip+AdamW) on 1..8
+MI355X, one process per GPU (torchrun), RCCL all-reduce overlapped with the backward.
+
+Prints ONE JSON line (rank 0). `roofline` prices the step against HBM with SURVEY Appendix A's
+algorithmic bytes per window; `cpu_baseline` times the CPU oracle (oracle/, test infrastructure)
+on a bounded sample on this host's cores.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "video-chapter-generation_amd"))
+sys.path.insert(0, REPO)
+
+METRIC = "clip-windows/sec (16f×224²+128tok) train-step at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
+N_PARAMS = 133355074
+
+
+# ----------------------------------------------------------------------------- roofline accounting
+def resnet_counts(HW):
+    """(fused-minimum activation elements, FLOPs) per frame at HWxHW."""
+    elems = 0.0
+    flops = 0.0
+    H = HW // 2
+    elems += 3 * HW * HW + 64 * H * H
+    flops += 2 * 64 * H * H * 3 * 49
+    Hm = (H - 1) // 2 + 1
+    elems += 64 * H * H + 64 * Hm * Hm  # maxpool in + out
+    H, Cin = Hm, 64
+    for mid, blocks, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+        for b in range(blocks):
+            s = stride if b == 0 else 1
+            Ho = (H - 1) // s + 1
+            elems += Cin * H * H + mid * H * H
+            flops += 2 * mid * H * H * Cin
+            elems += mid * H * H + mid * Ho * Ho
+            flops += 2 * mid * Ho * Ho * mid * 9
+            elems += mid * Ho * Ho + 4 * mid * Ho * Ho
+            flops += 2 * 4 * mid * Ho * Ho * mid
+            if b == 0:
+                elems += Cin * H * H + 4 * mid * Ho * Ho
+                flops += 2 * 4 * mid * Ho * Ho * Cin
+            elems += 4 * mid * Ho * Ho  # residual read
+            Cin, H = 4 * mid, Ho
+    elems += 2048 * H * H  # avgpool read
+    return elems, flops
+
+
+def bert_counts(L, H=768, I=3072, layers=12):
+    elems = layers * L * (13 * H + 2 * I) + 3 * L * H
+    flops = layers * (2 * L * H * 3 * H + 4 * 12 * L * L * 64 + 2 * L * H * H + 4 * L * H * I) + 2 * H * H
+    return elems, flops
+
+
+def window_costs(T, HW, L, B, s_bytes, train):
+    re, rf = resnet_counts(HW)
+    be, bf = bert_counts(L)
+    act = (re * T + be) * s_bytes
+    frames = T * 3 * HW * HW * 4
+    weights = N_PARAMS * s_bytes / B
+    if train:
+        nbytes = 3 * act + frames + (3 * N_PARAMS * s_bytes + 28 * N_PARAMS) / B
+        nflops = 3 * (rf * T + bf)
+    else:
+        nbytes = act + frames + weights
+        nflops = rf * T + bf
+    return nbytes, nflops
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(T, HW, L, threads, B=2, reps=2):
+    import torch
+    from oracle import model as om
+    from vcg_hip.build import build_two_stream
+    from vcg_hip import synth
+    torch.set_num_threads(threads)
+    m = build_two_stream(clip_frame_num=T, dropout=0.1)
+    sd = m.state_dict()
+    names = [n for n, _ in m.named_parameters()]
+    frames, ids, mask, labels = synth.clip_batch(B, T, HW, HW, L, seed=7)
+    times = []
+    for r in range(reps + 1):
+        params = {n: sd[n].detach().clone().requires_grad_() for n in names}
+        buffers = {n: sd[n].detach().clone() for n in sd if n not in params}
+        t0 = time.perf_counter()
+        om.train_step(params, buffers, frames, ids, mask, labels, lr=1e-5)
+        dt = time.perf_counter() - t0
+        if r > 0:
+            times.append(dt)
+    med = sorted(times)[len(times) // 2]
+    return {"value": B / med, "unit": "clip-windows/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle/ CPU fp32 train step (fwd+bwd+clip+AdamW, BN train, dropout 0.1) on B={B} windows of "
+                      f"{T}x{HW}^2 + {L} tokens; median of {reps} after 1 warm-up; {threads} threads"}
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="clip windows per GPU")
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--res", type=int, default=224)
+    ap.add_argument("--tokens", type=int, default=128)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--mode", default="train", choices=["train", "fwd"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from vcg_hip import _lib, synth
+    from vcg_hip.build import build_two_stream
+    from vcg_hip.ddp import GradAllReducer, broadcast_parameters
+    from vcg_hip.functions import cross_entropy
+
+    _lib.call("vcg_init", local)
+    B, T, HW, L = args.batch, args.frames, args.res, args.tokens
+    torch.manual_seed(123)
+    model = build_two_stream(clip_frame_num=T, seed=123, device=dev, precision=args.precision)
+    model.train(args.mode == "train")
+
+    class Cfg:
+        weight_decay = 0.01
+        learning_rate = 1e-5
+        betas = (0.9, 0.95)
+    opt = model.configure_optimizers(Cfg)
+    flat = model.native_flat()
+    reducer = GradAllReducer(flat)
+    if world > 1:
+        broadcast_parameters(model)
+        model.set_grad_hooks(reducer)
+        opt.grad_scale = 1.0 / world
+    frames, ids, mask, labels = synth.clip_batch(B, T, HW, HW, L, seed=123 + rank, device=dev)
+
+    def step():
+        if args.mode == "fwd":
+            with torch.no_grad():
+                model(frames, ids, mask)
+            return
+        opt.zero_grad()
+        logits, prob = model(frames, ids, mask)
+        loss = cross_entropy(logits, labels)
+        loss.backward()
+        reducer.finish()
+        opt.clip_and_step(1.0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / args.steps
+    ms = max(ms, wall * 1000.0 / args.steps)
+    if world > 1:
+        t = torch.tensor([ms], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+
+    if rank == 0:
+        windows = B * world
+        value = windows / (ms / 1000.0)
+        s_bytes = 2 if args.precision == "bf16" else 4
+        nbytes, nflops = window_costs(T, HW, L, B, s_bytes, args.mode == "train")
+        achieved = nbytes * B / (ms / 1000.0) / 1e9  # per GPU
+        tflops = nflops * B / (ms / 1000.0) / 1e12
+        traffic = None
+        tf = os.path.join(REPO, "profiles", f"traffic_{args.mode}_{args.precision}_b{B}.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                traffic = json.load(f).get("hbm_bytes_per_step")
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "clip-windows/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (seeded clip windows generated in HBM; random-init weights)",
+            "config": {"workload": f"TwoStream {args.mode} step: TSM-ResNet-50 + BERT-base + ChapterHead(mlp), "
+                                   f"B={B} windows/GPU of {T}x{HW}^2 frames + {L} tokens"
+                                   + (", fused clip+AdamW" if args.mode == "train" else ""),
+                       "global_batch": windows, "seq_len": L, "frames": T, "resolution": HW,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "scope": "whole step (all kernels) vs SURVEY App. A fused-minimum bytes "
+                                  f"({nbytes / 1e9:.3f} GB/window)",
+                         "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / MFMA_PEAK_TFLOPS[args.precision], 4)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 8)
+            try:
+                out["cpu_baseline"] = cpu_baseline(T, HW, L, threads)
+            except Exception as e:  # the GPU number stands on its own; report why the baseline is missing
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

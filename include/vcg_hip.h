@@ -77,7 +77,7 @@ VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other
 /* ---- BERT support (bert.hip) ------------------------------------------------------------- */
 VCG_API int vcg_embed_ln_fwd(int dtype, const long long* ids, const float* word, const float* pos, const float* type, const float* gamma, const float* beta, void* out, float* mean, float* rstd, int B, int L, int H, float eps, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API long long vcg_ln_bwd_ws_bytes(int rows, int H);
-VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, const float* word, const float* pos, const float* type, const float* gamma, const float* mean, const float* rstd, float* word_grad, float* pos_grad, float* type_grad, float* gamma_grad, float* beta_grad, float* ws, long long ws_bytes, int B, int L, int H, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, const float* word, const float* pos, const float* type, const float* gamma, const float* mean, const float* rstd, float* word_grad, float* pos_grad, float* type_grad, float* gamma_grad, float* beta_grad, float* ws, long long ws_bytes, int B, int L, int H, float dropout_p, unsigned long long seed, long long pad_idx, hipStream_t s);
 VCG_API int vcg_ln_fwd(int dtype, const void* x, const void* res, const float* gamma, const float* beta, void* out, float* mean, float* rstd, int rows, int H, float eps, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* res, const float* gamma, const float* mean, const float* rstd, void* dx, void* dres, float* gamma_grad, float* beta_grad, float* ws, long long ws_bytes, int rows, int H, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API long long vcg_colsum_ws_bytes(int rows, int N);
@@ -89,7 +89,7 @@ VCG_API int vcg_tanh_bwd(int dtype, const void* dy, const void* t, void* dx, lon
 /* ---- fusion head + loss (head.hip): ChapterHead mlp (two_stream.py:51-95), softmax (:189),
  *      F.cross_entropy (train_video_segment_point.py:165) ----------------------------------- */
 VCG_API int vcg_head_mlp_fwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* bias, float* logits, float* prob, int B, int T, int hid, int O, hipStream_t s);
-VCG_API int vcg_head_mlp_bwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* dlogits, void* dV, void* dL, float* dW, float* dbias, int B, int T, int hid, int O, hipStream_t s);
+VCG_API int vcg_head_mlp_bwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* dlogits, void* dV, void* dL, float* dW, float* dbias, int B, int T, int hid, int O, int relu_mask, hipStream_t s);
 VCG_API int vcg_cross_entropy_fwd(const float* logits, const long long* labels, float* loss, int B, int C, hipStream_t s);
 VCG_API int vcg_cross_entropy_bwd(const float* logits, const long long* labels, const float* dloss, float* dlogits, int B, int C, hipStream_t s);
 

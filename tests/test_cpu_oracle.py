@@ -1,0 +1,138 @@
+"""CPU suite: pins the oracle (oracle/) against the reference's golden vectors, and checks the
+host-side logic and the C-ABI library surface (no GPU compute)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _gold(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+@pytest.fixture(scope="module")
+def c1_params():
+    from vcg_hip.build import build_two_stream
+    from vcg_hip import synth
+    torch.set_num_threads(min(8, os.cpu_count() or 8))
+    m = build_two_stream(clip_frame_num=4, seed=123, bn_stats=dict(_gold("bn_running_stats.npz")), dropout=0.0)
+    return m
+
+
+def test_synthetic_inputs_match_golden():
+    from vcg_hip import synth
+    g = _gold("c1_fwd.npz")
+    frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=123)
+    assert np.array_equal(ids.numpy(), g["c1_ids"])
+    assert np.array_equal(mask.numpy(), g["c1_mask"])
+    assert np.array_equal(labels.numpy(), g["c1_labels"])
+    cs = g["c1_frames_checksum"]
+    assert abs(frames.double().sum().item() - cs[0]) < 1e-9 * cs[1]
+
+
+def test_state_dict_names_match_reference(c1_params):
+    g = _gold("c1_train.npz")
+    ref = [str(s) for s in g["train_grad_norm_names"]]
+    ours = [n for n, _ in c1_params.named_parameters()]
+    assert sorted(ours) == sorted(ref)
+    assert sum(p.numel() for p in c1_params.lang_model.parameters()) == 109482240
+    keys = set(c1_params.state_dict().keys())
+    assert "vision_model.layer1.0.conv1.net.weight" in keys
+    assert "vision_model.layer4.2.bn3.num_batches_tracked" in keys
+
+
+@pytest.mark.parametrize("mode", ["running", "batch"])
+def test_oracle_c1_forward_matches_reference(c1_params, mode):
+    from oracle import model as om
+    from vcg_hip import synth
+    g = _gold("c1_fwd.npz")
+    p = dict(c1_params.state_dict())
+    frames, ids, mask, _ = synth.clip_batch(2, 4, 112, 112, 32, seed=123)
+    with torch.no_grad():
+        lg, pr, ve, le = om.two_stream(p, frames, ids, mask, bn_mode=mode)
+    assert np.abs(lg.numpy() - g[f"c1_logits_{mode}"]).max() < 1e-5
+    assert np.abs(pr.numpy() - g[f"c1_prob_{mode}"]).max() < 1e-5
+    assert np.abs(le.numpy() - g["c1_lang_emb"]).max() < 1e-5
+    assert np.abs(ve.numpy() - g[f"c1_vision_emb_{mode}"]).max() < 1e-5
+
+
+def test_oracle_c1_train_step_matches_reference(c1_params):
+    from oracle import model as om
+    from vcg_hip import synth
+    g = _gold("c1_train.npz")
+    sd = c1_params.state_dict()
+    names = [n for n, _ in c1_params.named_parameters()]
+    params = {n: sd[n].detach().clone().requires_grad_() for n in names}
+    buffers = {n: sd[n].detach().clone() for n in sd if n not in params}
+    frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=123)
+    grads = {}
+    for n, t in params.items():
+        t.register_hook(lambda gr, n=n: grads.__setitem__(n, gr.detach().clone()))
+    loss, logits, total, opt = om.train_step(params, buffers, frames, ids, mask, labels, lr=float(g["train_lr"][0]))
+    assert abs(loss.item() - g["train_loss"][0]) < 1e-5
+    assert abs(total.item() - g["train_total_norm"][0]) < 1e-4 * g["train_total_norm"][0]
+    for key in [k for k in g.files if k.startswith("train_grad::")]:
+        n = key.split("::", 1)[1]
+        idx = g[f"train_idx::{n}"]
+        ref = g[key]
+        ours = grads[n].reshape(-1)[idx].numpy()
+        assert np.abs(ours - ref).max() <= 1e-4 * max(np.abs(ref).max(), 1e-12), n
+    for key in [k for k in g.files if k.startswith("train_rm::")]:
+        n = key.split("::", 1)[1]
+        assert np.abs(buffers[n + ".running_mean"].numpy() - g[key]).max() < 1e-5
+
+
+def test_tsm_oracle_bitexact():
+    from oracle import model as om
+    g = _gold("tsm_shift.npz")
+    x = torch.from_numpy(g["tsm_x"]).requires_grad_()
+    y = om.tsm_shift(x, 4, 8)
+    assert np.array_equal(y.detach().numpy(), g["tsm_y"])
+    (gx,) = torch.autograd.grad(y, x, torch.from_numpy(g["tsm_g"]))
+    assert np.array_equal(gx.numpy(), g["tsm_gx"])
+
+
+def test_eval_utils_known_answers():
+    from eval_utils.eval_utils import calculate_pr, convert_clip_label2cut_point
+    with open(os.path.join(GOLD, "eval_utils.json")) as f:
+        g = json.load(f)
+    assert convert_clip_label2cut_point([1, 0, 0, 0, 1, 1, 0, 0, 1, 1, 1, 1, 1, 0, 1, 0, 0, 0, 0, 1, 1], 16, 2) == \
+        [8, 26, 48, 64]
+    for c in g["convert_clip_label2cut_point"]:
+        assert convert_clip_label2cut_point(c["labels"], c["T"], c["off"]) == c["cut_points"]
+    for c in g["calculate_pr"]:
+        ours = calculate_pr(c["gt"], c["pred"])
+        assert len(ours) == 6
+        for a, b in zip(ours, c["pr"]):
+            assert (a is None and b is None) or abs(a - b) < 1e-12
+
+
+def test_optimizer_groups_match_reference_rule(c1_params):
+    from vcg_hip.optim import param_groups
+    from oracle.model import param_groups as oracle_groups
+    ours = param_groups(c1_params, 0.01)
+    ref = oracle_groups(list(c1_params.named_parameters()), 0.01)
+    for a, b in zip(ours, ref):
+        assert a["weight_decay"] == b["weight_decay"]
+        assert {id(t) for t in a["params"]} == {id(t) for t in b["params"]}
+
+
+def test_c_abi_library_exports_every_header_symbol():
+    from vcg_hip import _lib
+    protos = _lib.parse_header()
+    assert len(protos) > 40
+    lib = _lib.lib()  # binds every prototype; AttributeError if one is missing
+    for name in protos:
+        assert hasattr(lib, name)
+    assert lib.vcg_version() == 1
+
+
+def test_no_cpu_fallback():
+    """The product path refuses CPU tensors loudly."""
+    from vcg_hip import ops
+    with pytest.raises(RuntimeError):
+        ops.tsm_shift(torch.zeros(8, 64, 2, 2), 4, 8)

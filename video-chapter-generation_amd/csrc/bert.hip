@@ -127,9 +127,10 @@ __global__ void embed_ln_bwd_kernel(const T* __restrict__ dout, const long long*
 
 // word grad scatter-add (atomics), position grad (sum over batch), token-type grad (sum over all)
 __global__ void embed_scatter_kernel(const float* __restrict__ de, const long long* __restrict__ ids,
-                                     float* __restrict__ word_grad, int H, long long rows) {
+                                     float* __restrict__ word_grad, int H, long long rows, long long pad_idx) {
   const long long row = blockIdx.x;
   const long long id = ids[row];
+  if (id == pad_idx) return;  // nn.Embedding(padding_idx): the padding row never receives gradient
   for (int c = threadIdx.x; c < H; c += blockDim.x) atomicAdd(&word_grad[id * H + c], de[row * H + c]);
 }
 
@@ -395,7 +396,7 @@ VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, 
                              const float* type, const float* gamma, const float* mean, const float* rstd,
                              float* word_grad, float* pos_grad, float* type_grad, float* gamma_grad,
                              float* beta_grad, float* ws, long long ws_bytes, int B, int L, int H, float dropout_p,
-                             unsigned long long seed, hipStream_t s) {
+                             unsigned long long seed, long long pad_idx, hipStream_t s) {
   const int rows = B * L;
   VCG_REQUIRE(ws_bytes >= vcg_ln_bwd_ws_bytes(rows, H), "workspace too small");
   int rpb;
@@ -413,7 +414,8 @@ VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, 
                      beta_grad);
   VCG_LAUNCH_CHECK();
   if (word_grad) {
-    hipLaunchKernelGGL(embed_scatter_kernel, dim3(rows), dim3(256), 0, s, de, ids, word_grad, H, (long long)rows);
+    hipLaunchKernelGGL(embed_scatter_kernel, dim3(rows), dim3(256), 0, s, de, ids, word_grad, H, (long long)rows,
+                       pad_idx);
     VCG_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(embed_pos_type_kernel, dim3((H + 255) / 256), dim3(256), 0, s, de, pos_grad, type_grad, B, L, H);

@@ -51,7 +51,8 @@ __global__ void head_mlp_fwd_kernel(const T* __restrict__ Vout, const T* __restr
 template <typename T>
 __global__ void head_mlp_bwd_dF_kernel(const T* __restrict__ Vout, const T* __restrict__ Lout,
                                        const float* __restrict__ W, const float* __restrict__ dlogits,
-                                       T* __restrict__ dV, T* __restrict__ dL, int B, int Tn, int hid, int O) {
+                                       T* __restrict__ dV, T* __restrict__ dL, int B, int Tn, int hid, int O,
+                                       int relu_mask) {
   const int TH = Tn * hid, D = TH + hid;
   const long long total = (long long)B * D;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
@@ -59,7 +60,7 @@ __global__ void head_mlp_bwd_dF_kernel(const T* __restrict__ Vout, const T* __re
     float s = 0.f;
     for (int o = 0; o < O; ++o) s += dlogits[b * O + o] * W[(long long)o * D + d];
     const float f = fus(Vout, Lout, b, d, TH, hid);
-    const T v = from_f<T>(f > 0.f ? s : 0.f);
+    const T v = from_f<T>((!relu_mask || f > 0.f) ? s : 0.f);
     if (d < TH) dV[(long long)b * TH + d] = v;
     else dL[(long long)b * hid + d - TH] = v;
   }
@@ -132,19 +133,20 @@ VCG_API int vcg_head_mlp_fwd(int dtype, const void* Vout, const void* Lout, cons
 }
 
 VCG_API int vcg_head_mlp_bwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* dlogits,
-                             void* dV, void* dL, float* dW, float* dbias, int B, int T, int hid, int O, hipStream_t s) {
+                             void* dV, void* dL, float* dW, float* dbias, int B, int T, int hid, int O, int relu_mask,
+                             hipStream_t s) {
   const int D = (T + 1) * hid;
   const long long tot = (long long)B * D;
   const int g = (int)((tot + 255) / 256 > 4096 ? 4096 : (tot + 255) / 256);
   if (dtype == VCG_BF16) {
     hipLaunchKernelGGL(head_mlp_bwd_dF_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)Vout,
-                       (const bf16_t*)Lout, W, dlogits, (bf16_t*)dV, (bf16_t*)dL, B, T, hid, O);
+                       (const bf16_t*)Lout, W, dlogits, (bf16_t*)dV, (bf16_t*)dL, B, T, hid, O, relu_mask);
     if (dW)
       hipLaunchKernelGGL(head_mlp_bwd_dW_kernel<bf16_t>, dim3((D + 255) / 256), dim3(256), 0, s, (const bf16_t*)Vout,
                          (const bf16_t*)Lout, dlogits, dW, dbias, B, T, hid, O);
   } else {
     hipLaunchKernelGGL(head_mlp_bwd_dF_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)Vout, (const float*)Lout,
-                       W, dlogits, (float*)dV, (float*)dL, B, T, hid, O);
+                       W, dlogits, (float*)dV, (float*)dL, B, T, hid, O, relu_mask);
     if (dW)
       hipLaunchKernelGGL(head_mlp_bwd_dW_kernel<float>, dim3((D + 255) / 256), dim3(256), 0, s, (const float*)Vout,
                          (const float*)Lout, dlogits, dW, dbias, B, T, hid, O);

@@ -49,8 +49,9 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const float gi = g[i] * coef;
     float pi = p[i];
-    const bool decay = wd_flags ? wd_flags[i >> flag_shift] != 0 : true;
-    if (decay) pi = pi * (1.f - lr * wd);
+    const unsigned char fl = wd_flags ? wd_flags[i >> flag_shift] : 1;
+    if (fl == 2) continue;  // frozen parameter (requires_grad=False): torch skips params without grads
+    if (fl == 1) pi = pi * (1.f - lr * wd);
     float mi = m[i];
     mi = mi + (1.f - beta1) * (gi - mi);  // exp_avg.lerp_(grad, 1 - beta1)
     float vi = v[i] * beta2;
@@ -76,8 +77,8 @@ VCG_API int vcg_sumsq(const float* x, long long n, float* ws, float* out, hipStr
   return VCG_OK;
 }
 
-// One AdamW step. wd_flags: one byte per (1 << flag_shift) elements selecting the decay group
-// (null = decay everything). step_size = lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t).
+// One AdamW step. wd_flags: one byte per (1 << flag_shift) elements: 0 = no-decay group,
+// 1 = decay group, 2 = frozen (skipped); null = decay everything. step_size = lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t).
 // sumsq (device scalar, nullable) enables clipping to max_norm; grad_scale (e.g. 1/world) is
 // applied to the gradients before clipping.
 VCG_API int vcg_adamw(float* p, const float* g, float* m, float* v, const unsigned char* wd_flags, int flag_shift,

@@ -1,0 +1,109 @@
+"""Drop-in for reference model/fusion/two_stream.py (SelfAttention 8-48, ChapterHead 51-95,
+TwoStream 99-194) with the forward/backward executed by libvcg_hip on MI355X.
+
+TwoStream.forward(img_clip [B,T,3,H,W] f32, text_ids [B,L] i64, attention_mask [B,L] i64,
+return_emb=False) -> (logits [B,2], prob [B,2]) (+ vision_emb [B,T,2048], lang_emb [B,768]).
+`model.precision = "bf16"` switches activations / MFMA operands to bf16 (fp32 master weights,
+accumulation and statistics); the default "fp32" is the parity mode.
+"""
+import math
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from vcg_hip.nn import BertModel, NativeRoot, ResNet50, new_seed
+from vcg_hip.optim import configure_adamw
+
+
+class SelfAttention(nn.Module):
+    """Reference SelfAttention (two_stream.py:8-48): parameters and names only; the 'attn' head is
+    not on the native path yet (the benchmarked configuration is head_type='mlp')."""
+
+    def __init__(self, n_embd, n_head, output_size, attn_pdrop=0.1, resid_pdrop=0.1):
+        super().__init__()
+        assert n_embd % n_head == 0
+        self.n_head = n_head
+        self.n_embd = n_embd
+        self.key = nn.Linear(n_embd, n_embd)
+        self.query = nn.Linear(n_embd, n_embd)
+        self.value = nn.Linear(n_embd, n_embd)
+        self.attn_drop = nn.Dropout(attn_pdrop)
+        self.resid_drop = nn.Dropout(resid_pdrop)
+        self.proj = nn.Linear(n_embd, output_size)
+
+
+class ChapterHead(nn.Module):
+    def __init__(self, lang_emb_size, vision_emb_size, segment_size, hidden_size, output_size, head_type="mlp"):
+        super().__init__()
+        self.lang_emb_size = lang_emb_size
+        self.vision_emb_size = vision_emb_size
+        self.segment_size = segment_size
+        self.hidden_size = hidden_size
+        self.head_type = head_type
+        self.lang_proj_head = nn.Linear(lang_emb_size, hidden_size, bias=False)
+        self.vision_proj_head = nn.Linear(vision_emb_size, hidden_size, bias=False)
+        if head_type == "mlp":
+            self.head = nn.Linear((segment_size + 1) * hidden_size, output_size, bias=True)
+        elif head_type == "attn":
+            self.head = SelfAttention(hidden_size, 4, output_size)
+        else:
+            raise RuntimeError(f"Unknown head_type {head_type}")
+
+
+class TwoStream(NativeRoot, nn.Module):
+    def __init__(self, lang_model, vision_model, lang_embed_size, vision_embed_size, segment_size, hidden_size):
+        super().__init__()
+        if not isinstance(lang_model, BertModel) or not isinstance(vision_model, ResNet50):
+            raise TypeError("TwoStream expects the native BertModel (BertHugface.base_model) and ResNet50 "
+                            "(Resnet50TSM.base_model)")
+        self.lang_model = lang_model
+        self.vision_model = vision_model
+        self.segment_size = segment_size
+        self.lang_embed_size = lang_embed_size
+        self.vision_embed_size = vision_embed_size
+        self.hidden_size = hidden_size
+        self._vcg_hooks = None  # gradient-ready callback (DDP bucket all-reduce)
+
+    def build_chapter_head(self, output_size, head_type="mlp"):
+        self.fusion_head = ChapterHead(self.lang_embed_size, self.vision_embed_size, self.segment_size,
+                                       self.hidden_size, output_size, head_type)
+
+    def configure_optimizers(self, train_config):
+        return configure_adamw(self, train_config)
+
+    def set_grad_hooks(self, hooks):
+        """hooks(tag) is called from the backward when a branch's gradients are final."""
+        object.__setattr__(self, "_vcg_hooks", hooks)
+
+    def forward(self, img_clip, text_ids, attention_mask, return_emb=False):
+        from vcg_hip.bert import BertEncoderEngine
+        from vcg_hip.functions import BertFn, HeadFn, TrunkFn
+        from vcg_hip.head import HeadEngine
+        from vcg_hip.trunk import ResNetTrunk
+
+        f = self.native_flat()
+        dt = self.compute_dtype()
+        need_grad = torch.is_grad_enabled()
+        dev = img_clip.device
+        anchor = self._anchor(dev)
+        hooks = self._vcg_hooks
+        if self.training:
+            self._bump_bn_counters()
+        # language
+        if attention_mask is None:
+            attention_mask = torch.ones_like(text_ids)
+        bert = BertEncoderEngine(self.lang_model, f, dt)
+        lang_emb, _ = BertFn.apply(text_ids, attention_mask, anchor, bert, need_grad, new_seed(), hooks)
+        # vision: rearrange 'b t c h w -> (b t) c h w' (two_stream.py:183) is a view of a contiguous clip
+        batch_size = img_clip.shape[0]
+        img = img_clip.float().contiguous()
+        img = img.view(batch_size * img.shape[1], *img.shape[2:])
+        vision_emb = TrunkFn.apply(img, anchor, ResNetTrunk(self.vision_model, dt), need_grad, hooks)
+        # fusion
+        head = HeadEngine(self.fusion_head, f, dt)
+        binary_logits, binary_prob = HeadFn.apply(lang_emb, vision_emb, anchor, head, need_grad, hooks)
+        if return_emb:
+            lang_out = lang_emb if lang_emb.dtype == torch.float32 else lang_emb.float()
+            return binary_logits, binary_prob, vision_emb.view(batch_size, self.segment_size, -1), lang_out
+        return binary_logits, binary_prob

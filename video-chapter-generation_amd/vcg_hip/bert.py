@@ -1,0 +1,185 @@
+"""BERT-base encoder on libvcg_hip (HF BertModel semantics, eager attention), forward and a
+hand-written backward.
+
+Reference use: TwoStream.forward -> lang_model(input_ids, attention_mask).pooler_output
+(model/fusion/two_stream.py:172-179) with lang_model = BertModel('bert-base-uncased')
+(model/lang/bert_hugface.py:20). Per layer: fused QKV GEMM -> batched QK^T -> masked softmax
+(+dropout) -> batched PV -> out-proj GEMM -> LN(dropout(.)+res) -> FFN1 GEMM with erf-GELU
+epilogue -> FFN2 GEMM -> LN(dropout(.)+res); pooler = tanh(W h[:,0] + b).
+"""
+import math
+
+import torch
+
+from . import ops
+
+
+def _seed(base, layer, site):
+    return (base * 0x9E3779B1 + layer * 7919 + site * 104729) & ((1 << 63) - 1)
+
+
+class BertEncoderEngine:
+    def __init__(self, model, flat, dtype):
+        self.m = model
+        self.flat = flat
+        self.dtype = dtype
+
+    def _w(self, p):
+        return self.flat.compute_view(p, self.dtype)
+
+    def forward(self, ids, mask, need_grad, seed):
+        m, dt, flat = self.m, self.dtype, self.flat
+        cfg = m.config
+        B, L = ids.shape
+        H = cfg.hidden_size
+        nh = cfg.num_attention_heads
+        dh = H // nh
+        Lp = (L + 7) // 8 * 8
+        rows = B * L
+        train = m.training
+        p_h = cfg.hidden_dropout_prob if train else 0.0
+        p_a = cfg.attention_probs_dropout_prob if train else 0.0
+        eps = cfg.layer_norm_eps
+        scale = 1.0 / math.sqrt(dh)
+        dev = ids.device
+        ids = ids.contiguous()
+        mask = mask.to(torch.int64).contiguous()
+
+        emb = m.embeddings
+        h, e_mean, e_rstd = ops.embed_ln_fwd(ids, emb.word_embeddings.weight, emb.position_embeddings.weight,
+                                             emb.token_type_embeddings.weight, emb.LayerNorm.weight,
+                                             emb.LayerNorm.bias, B, L, H, eps, dt, p_h, _seed(seed, 0, 0))
+        saved_layers = []
+        for i, layer in enumerate(m.encoder.layer):
+            at = layer.attention
+            sq, sk, sv = at.self.query, at.self.key, at.self.value
+            Wqkv = flat.compute_contiguous([sq.weight, sk.weight, sv.weight], (3 * H, H), dt)
+            bqkv = flat.contiguous_view([sq.bias, sk.bias, sv.bias], (3 * H,), "data")
+            qkv_buf = torch.empty((rows + 8, 3 * H), dtype=dt, device=dev)  # +8 rows: padded key reads
+            qkv = qkv_buf[:rows]
+            ops.gemm(h, Wqkv, rows, 3 * H, H, H, H, out=qkv, ldc=3 * H, bias=bqkv)
+            Z = B * nh
+            S = torch.empty((Z, L, Lp), dtype=dt, device=dev)
+            ops.gemm_batched(qkv_buf, qkv_buf[:, H:], S, L, Lp, dh, 3 * H, 3 * H, Lp, L * 3 * H, dh, L * 3 * H, dh,
+                             nh * L * Lp, L * Lp, B, nh)
+            Pm = torch.empty_like(S)
+            Pd = torch.empty_like(S) if p_a > 0 else None
+            sa = _seed(seed, i + 1, 1)
+            ops.attn_softmax_fwd(S, mask, Pm, Pd, B, nh, L, Lp, scale, p_a, sa)
+            del S
+            Pv = Pd if Pd is not None else Pm
+            ctx = torch.empty((rows, H), dtype=dt, device=dev)
+            ops.gemm_batched(Pv, qkv_buf[:, 2 * H:], ctx, L, dh, L, Lp, 3 * H, H, nh * L * Lp, L * Lp, L * 3 * H, dh,
+                             L * H, dh, B, nh, transB=True)
+            ao = ops.gemm(ctx, self._w(at.output.dense.weight), rows, H, H, H, H, bias=at.output.dense.bias)
+            s1 = _seed(seed, i + 1, 2)
+            h1, m1, r1 = ops.ln_fwd(ao, h, at.output.LayerNorm.weight, at.output.LayerNorm.bias, rows, H, eps, p_h, s1)
+            inter, out = layer.intermediate.dense, layer.output.dense
+            I = inter.out_features
+            pre = torch.empty((rows, I), dtype=dt, device=dev) if need_grad else None
+            ff = ops.gemm(h1, self._w(inter.weight), rows, I, H, H, H, bias=inter.bias, act=ops.ACT_GELU, aux=pre)
+            fo = ops.gemm(ff, self._w(out.weight), rows, H, I, I, I, bias=out.bias)
+            s2 = _seed(seed, i + 1, 3)
+            h2, m2, r2 = ops.ln_fwd(fo, h1, layer.output.LayerNorm.weight, layer.output.LayerNorm.bias, rows, H, eps,
+                                    p_h, s2)
+            if need_grad:
+                saved_layers.append(dict(h=h, qkv_buf=qkv_buf, P=Pm, Pd=Pd, ctx=ctx, ao=ao, h1=h1, pre=pre, ff=ff,
+                                         fo=fo, m1=m1, r1=r1, m2=m2, r2=r2, sa=sa, s1=s1, s2=s2))
+            h = h2
+        pooled = None
+        if m.pooler is not None:
+            pd = m.pooler.dense
+            pooled = ops.gemm(h, self._w(pd.weight), B, H, H, L * H, H, bias=pd.bias, act=ops.ACT_TANH)
+        saved = None
+        if need_grad:
+            saved = dict(ids=ids, layers=saved_layers, e_mean=e_mean, e_rstd=e_rstd, h_last=h, pooled=pooled, B=B,
+                         L=L, Lp=Lp, H=H, nh=nh, dh=dh, p_h=p_h, p_a=p_a, scale=scale, seed=seed)
+        return pooled, h, saved
+
+    def backward(self, d_pooled, d_last, sv, hooks=None):
+        m, dt, flat = self.m, self.dtype, self.flat
+        B, L, Lp, H, nh, dh = sv["B"], sv["L"], sv["Lp"], sv["H"], sv["nh"], sv["dh"]
+        rows = B * L
+        p_h, p_a, scale, seed = sv["p_h"], sv["p_a"], sv["scale"], sv["seed"]
+        dev = sv["ids"].device
+        if d_last is not None:
+            dh_ = d_last.to(dt).contiguous().clone()
+        else:
+            dh_ = torch.zeros((rows, H), dtype=dt, device=dev)
+        if d_pooled is not None and m.pooler is not None:
+            pd = m.pooler.dense
+            dpp = ops.tanh_bwd(d_pooled.to(dt).contiguous(), sv["pooled"])
+            h_last = sv["h_last"]
+            if pd.weight.requires_grad:
+                ops.gemm_splitk(dpp, h_last, pd.weight.grad, H, H, B, H, L * H, transA=True, transB=True)
+                ops.colsum(dpp, H, B, H, pd.bias.grad)
+            # dh[b*L] += dpp @ Wp
+            ops.gemm(dpp, self._w(pd.weight), B, H, H, H, H, transB=True, out=dh_, ldc=L * H, residual=dh_, ldr=L * H)
+            if hooks is not None:
+                hooks(list(m.pooler.parameters()))
+        for i in reversed(range(len(sv["layers"]))):
+            s = sv["layers"].pop()
+            layer = m.encoder.layer[i]
+            at = layer.attention
+            inter, out = layer.intermediate.dense, layer.output.dense
+            I = inter.out_features
+            ln2 = layer.output.LayerNorm
+            dfo, dh1_res = ops.ln_bwd(dh_, s["fo"], s["h1"], ln2.weight, s["m2"], s["r2"], ln2.weight.grad,
+                                      ln2.bias.grad, rows, H, p_h, s["s2"])
+            ops.gemm_splitk(dfo, s["ff"], out.weight.grad, H, I, rows, H, I, transA=True, transB=True)
+            ops.colsum(dfo, H, rows, H, out.bias.grad)
+            dpre = ops.gemm(dfo, self._w(out.weight), rows, I, H, H, I, transB=True, act=ops.ACT_GELU_BWD,
+                            residual=s["pre"], ldr=I)
+            del dfo
+            ops.gemm_splitk(dpre, s["h1"], inter.weight.grad, I, H, rows, I, H, transA=True, transB=True)
+            ops.colsum(dpre, I, rows, I, inter.bias.grad)
+            dh1 = ops.gemm(dpre, self._w(inter.weight), rows, H, I, I, H, transB=True, residual=dh1_res, ldr=H)
+            del dpre, dh1_res
+            ln1 = at.output.LayerNorm
+            dao, dh_res = ops.ln_bwd(dh1, s["ao"], s["h"], ln1.weight, s["m1"], s["r1"], ln1.weight.grad,
+                                     ln1.bias.grad, rows, H, p_h, s["s1"])
+            od = at.output.dense
+            ops.gemm_splitk(dao, s["ctx"], od.weight.grad, H, H, rows, H, H, transA=True, transB=True)
+            ops.colsum(dao, H, rows, H, od.bias.grad)
+            dctx = ops.gemm(dao, self._w(od.weight), rows, H, H, H, H, transB=True)
+            del dao
+            # ---- attention backward
+            qkv_buf = s["qkv_buf"]
+            Z = B * nh
+            dPd = torch.empty((Z, L, Lp), dtype=dt, device=dev)
+            ops.gemm_batched(dctx, qkv_buf[:, 2 * H:], dPd, L, Lp, dh, H, 3 * H, Lp, L * H, dh, L * 3 * H, dh,
+                             nh * L * Lp, L * Lp, B, nh)
+            dqkv = torch.empty((rows, 3 * H), dtype=dt, device=dev)
+            Pv = s["Pd"] if s["Pd"] is not None else s["P"]
+            # dV = Pd^T dO
+            ops.gemm_batched(Pv, dctx, dqkv[:, 2 * H:], L, dh, L, Lp, H, 3 * H, nh * L * Lp, L * Lp, L * H, dh,
+                             L * 3 * H, dh, B, nh, transA=True, transB=True)
+            dS = torch.empty_like(dPd)
+            ops.attn_softmax_bwd(dPd, s["P"], dS, Z, L, Lp, scale, p_a, s["sa"])
+            del dPd
+            # dQ = dS K ; dK = dS^T Q
+            ops.gemm_batched(dS, qkv_buf[:, H:], dqkv, L, dh, L, Lp, 3 * H, 3 * H, nh * L * Lp, L * Lp, L * 3 * H, dh,
+                             L * 3 * H, dh, B, nh, transB=True)
+            ops.gemm_batched(dS, qkv_buf, dqkv[:, H:], L, dh, L, Lp, 3 * H, 3 * H, nh * L * Lp, L * Lp, L * 3 * H, dh,
+                             L * 3 * H, dh, B, nh, transA=True, transB=True)
+            del dS, dctx
+            sq, sk, svv = at.self.query, at.self.key, at.self.value
+            if sq.weight.requires_grad:
+                gW = flat.contiguous_view([sq.weight, sk.weight, svv.weight], (3 * H, H), "grad")
+                gb = flat.contiguous_view([sq.bias, sk.bias, svv.bias], (3 * H,), "grad")
+                ops.gemm_splitk(dqkv, s["h"], gW, 3 * H, H, rows, 3 * H, H, transA=True, transB=True)
+                ops.colsum(dqkv, 3 * H, rows, 3 * H, gb)
+            Wqkv = flat.compute_contiguous([sq.weight, sk.weight, svv.weight], (3 * H, H), dt)
+            dh_ = ops.gemm(dqkv, Wqkv, rows, H, 3 * H, 3 * H, H, transB=True, residual=dh_res, ldr=H)
+            del dqkv, dh_res, s
+            if hooks is not None:
+                hooks(list(layer.parameters()))
+        emb = m.embeddings
+        ops.embed_ln_bwd(dh_, sv["ids"], emb.word_embeddings.weight, emb.position_embeddings.weight,
+                         emb.token_type_embeddings.weight, emb.LayerNorm.weight, sv["e_mean"], sv["e_rstd"],
+                         emb.word_embeddings.weight.grad, emb.position_embeddings.weight.grad,
+                         emb.token_type_embeddings.weight.grad, emb.LayerNorm.weight.grad, emb.LayerNorm.bias.grad,
+                         B, L, H, p_h, _seed(seed, 0, 0),
+                         pad_idx=-1 if emb.word_embeddings.padding_idx is None else emb.word_embeddings.padding_idx)
+        if hooks is not None:
+            hooks(list(emb.parameters()))

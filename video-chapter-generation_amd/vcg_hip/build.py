@@ -1,0 +1,40 @@
+"""Model construction exactly as the reference drivers do it
+(train_video_segment_point.py:323-363, test_video_segment_point.py:69-100):
+
+    lang_model = BertHugface(pretrain_stage=False)
+    vision_model = Resnet50TSM(segments_size=clip_frame_num, shift_div=8, pretrain_stage=False)
+    model = TwoStream(lang_model.base_model, vision_model.base_model, lang_model.embed_size,
+                      vision_model.feature_dim, clip_frame_num, hidden_size=128)
+    model.build_chapter_head(output_size=2, head_type=head_type)
+"""
+import contextlib
+import io
+
+from . import synth
+
+
+def build_two_stream(clip_frame_num=16, hidden_size=128, head_type="mlp", dropout=None, seed=None, device=None,
+                     precision="fp32", bn_stats=None):
+    from model.fusion.two_stream import TwoStream
+    from model.lang.bert_hugface import BertHugface
+    from model.vision.resnet50_tsm import Resnet50TSM
+    from vcg_hip.nn import BertConfig
+
+    cfg = BertConfig(output_attentions=True)
+    if dropout is not None:
+        cfg.hidden_dropout_prob = dropout
+        cfg.attention_probs_dropout_prob = dropout
+    with contextlib.redirect_stdout(io.StringIO()):
+        lang_model = BertHugface(pretrain_stage=False, config=cfg)
+    vision_model = Resnet50TSM(segments_size=clip_frame_num, shift_div=8, pretrain_stage=False)
+    model = TwoStream(lang_model.base_model, vision_model.base_model, lang_model.embed_size, vision_model.feature_dim,
+                      clip_frame_num, hidden_size)
+    model.build_chapter_head(output_size=2, head_type=head_type)
+    if device is not None:
+        model = model.to(device)
+    if seed is not None:
+        synth.init_params(model, seed)  # on the GPU this runs the HIP generator (bit-identical to numpy)
+    if bn_stats is not None:
+        synth.load_bn_stats(model, bn_stats)
+    model.precision = precision
+    return model

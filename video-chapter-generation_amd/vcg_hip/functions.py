@@ -1,0 +1,95 @@
+"""autograd.Function glue: each Function runs a native engine forward and a hand-written native
+backward. Parameters are not Function inputs; their gradients are accumulated by the kernels
+directly into the flat .grad buffer. A zero-size `anchor` tensor (requires_grad) ties each
+Function into the autograd graph so `loss.backward()` reaches it even when its inputs are integer
+token ids or frames that need no gradient.
+"""
+import torch
+
+from . import ops
+
+
+class TrunkFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, engine, need_grad, hooks):
+        ctx.set_materialize_grads(False)
+        emb, saved = engine.forward(x, need_grad)
+        ctx.engine, ctx.saved, ctx.hooks = engine, saved, hooks
+        return emb
+
+    @staticmethod
+    def backward(ctx, d_emb):
+        if ctx.saved is None:
+            raise RuntimeError("TrunkFn: forward ran without saving activations (need_grad=False)")
+        if d_emb is not None:
+            ctx.engine.backward(d_emb, ctx.saved, hooks=ctx.hooks)
+        ctx.saved = None
+        return None, None, None, None, None
+
+
+class BertFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, mask, anchor, engine, need_grad, seed, hooks):
+        ctx.set_materialize_grads(False)
+        pooled, last, saved = engine.forward(ids, mask, need_grad, seed)
+        ctx.engine, ctx.saved, ctx.hooks = engine, saved, hooks
+        if pooled is None:
+            pooled = torch.zeros(0, device=ids.device)
+        return pooled, last
+
+    @staticmethod
+    def backward(ctx, d_pooled, d_last):
+        if ctx.saved is None:
+            raise RuntimeError("BertFn: forward ran without saving activations (need_grad=False)")
+        if d_pooled is not None or d_last is not None:
+            ctx.engine.backward(d_pooled if d_pooled is not None and d_pooled.numel() else None, d_last, ctx.saved,
+                                hooks=ctx.hooks)
+        ctx.saved = None
+        return None, None, None, None, None, None, None
+
+
+class HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lang, vis, anchor, engine, need_grad, hooks):
+        ctx.set_materialize_grads(False)
+        logits, prob, saved = engine.forward(lang, vis, need_grad)
+        ctx.engine, ctx.saved, ctx.hooks = engine, saved, hooks
+        ctx.save_for_backward(prob)
+        return logits, prob
+
+    @staticmethod
+    def backward(ctx, dlogits, dprob):
+        if ctx.saved is None:
+            raise RuntimeError("HeadFn: forward ran without saving activations (need_grad=False)")
+        (prob,) = ctx.saved_tensors
+        if dlogits is None:
+            dlogits = torch.zeros_like(prob)
+        if dprob is not None:
+            # softmax backward for a gradient through the returned probabilities (2-wide, host-light)
+            dlogits = dlogits + prob * (dprob - (dprob * prob).sum(1, keepdim=True))
+        dlang, dvis = ctx.engine.backward(dlogits, ctx.saved)
+        ctx.saved = None
+        if ctx.hooks is not None:
+            ctx.hooks(list(ctx.engine.h.parameters()))
+        return dlang, dvis, None, None, None, None
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    """Mean cross-entropy (F.cross_entropy, train_video_segment_point.py:165) on the native kernels."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        logits = logits.contiguous()
+        labels = labels.to(torch.int64).contiguous()
+        loss = ops.cross_entropy_fwd(logits, labels)
+        ctx.save_for_backward(logits, labels)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        logits, labels = ctx.saved_tensors
+        return ops.cross_entropy_bwd(logits, labels, dloss.contiguous()), None
+
+
+def cross_entropy(logits, labels):
+    return CrossEntropyFn.apply(logits, labels)

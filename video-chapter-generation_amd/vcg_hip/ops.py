@@ -249,12 +249,12 @@ def embed_ln_fwd(ids, word, pos, typ, gamma, beta, B, L, H, eps, dtype, p=0.0, s
 
 
 def embed_ln_bwd(dout, ids, word, pos, typ, gamma, mean, rstd, word_grad, pos_grad, type_grad, gamma_grad, beta_grad,
-                 B, L, H, p=0.0, seed=0):
+                 B, L, H, p=0.0, seed=0, pad_idx=-1):
     nbytes = _lib.query("vcg_ln_bwd_ws_bytes", B * L, H)
     w = ws(nbytes, dout.device)
     _lib.call("vcg_embed_ln_bwd", dt_code(dout.dtype), P(dout), P(ids), P(word), P(pos), P(typ), P(gamma), P(mean),
               P(rstd), P(word_grad), P(pos_grad), P(type_grad), P(gamma_grad), P(beta_grad), P(w), w.numel() * 4, B, L,
-              H, float(p), int(seed) & (2**64 - 1), stream())
+              H, float(p), int(seed) & (2**64 - 1), int(pad_idx), stream())
 
 
 def ln_fwd(x, res, gamma, beta, rows, H, eps, p=0.0, seed=0):
@@ -309,11 +309,11 @@ def head_mlp_fwd(Vout, Lout, W, bias, B, T, hid, O):
     return logits, prob
 
 
-def head_mlp_bwd(Vout, Lout, W, dlogits, dW, dbias, B, T, hid, O):
+def head_mlp_bwd(Vout, Lout, W, dlogits, dW, dbias, B, T, hid, O, relu_mask=True):
     dV = torch.empty_like(Vout)
     dL = torch.empty_like(Lout)
     _lib.call("vcg_head_mlp_bwd", dt_code(Vout.dtype), P(Vout), P(Lout), P(W), P(dlogits), P(dV), P(dL), P(dW),
-              P(dbias), B, T, hid, O, stream())
+              P(dbias), B, T, hid, O, int(relu_mask), stream())
     return dV, dL
 
 

@@ -79,6 +79,68 @@ def fill(t, kind, key, a, b):
     return t
 
 
+# ------------------------------------------------------------------------------ weights
+def init_rule(name, shape):
+    """(kind, a, b) for a TwoStream parameter name (reference state-dict naming).
+
+    vision convs: N(0, sqrt(2/fan_out)) (torchvision kaiming fan_out); vision BN gamma U(0.5,1.5)
+    (U(0.2,0.6) on bn3 / downsample.1 to keep the residual stream bounded), beta U(-0.2,0.2);
+    BERT Linear/Embedding N(0, 0.02), biases N(0, 0.02), LayerNorm gamma U(0.8,1.2), beta U(-0.1,0.1);
+    head Linear U(+-1/sqrt(fan_in)) (nn.Linear default bound)."""
+    leaf = name.rsplit(".", 1)[-1]
+    if len(shape) == 4:
+        fan_out = shape[0] * shape[2] * shape[3]
+        return KIND_NORMAL, 0.0, float(np.sqrt(2.0 / fan_out))
+    is_vision_bn = ("vision_model" in name or name.startswith(("bn", "layer"))) and len(shape) == 1 and (
+        ".bn" in "." + name or "downsample.1" in name)
+    if is_vision_bn:
+        if leaf == "weight":
+            small = ".bn3." in "." + name or "downsample.1" in name
+            return (KIND_UNIFORM, 0.2, 0.6) if small else (KIND_UNIFORM, 0.5, 1.5)
+        return KIND_UNIFORM, -0.2, 0.2
+    if "LayerNorm" in name:
+        return (KIND_UNIFORM, 0.8, 1.2) if leaf == "weight" else (KIND_UNIFORM, -0.1, 0.1)
+    if "fusion_head" in name or name.startswith(("head.", "lang_proj_head", "vision_proj_head")):
+        fan_in = shape[-1] if len(shape) == 2 else None
+        if fan_in is None:  # bias: bound from the matching weight's fan_in is not known here; use 1/sqrt(D)
+            fan_in = max(1, shape[0])
+        bound = 1.0 / np.sqrt(fan_in)
+        return KIND_UNIFORM, -bound, bound
+    return KIND_NORMAL, 0.0, 0.02
+
+
+def init_params(module, seed=123, prefix=""):
+    """Deterministically (re)initialise every parameter of `module` by name; works for CPU modules
+    (numpy twin) and GPU modules (HIP generator) with bit-identical results."""
+    import torch
+    with torch.no_grad():
+        for n, p in module.named_parameters():
+            full = prefix + n
+            kind, a, b = init_rule(full, tuple(p.shape))
+            if p.is_cuda and p.is_contiguous():
+                fill(p.data, kind, key_of(seed, full), a, b)
+            else:
+                v = fill_np(p.numel(), kind, key_of(seed, full), a, b)
+                p.data.copy_(torch.from_numpy(v).view(p.shape))
+            if full.endswith("word_embeddings.weight"):
+                p.data[0].zero_()  # HF init zeroes the padding row (padding_idx = 0)
+        for n, b in module.named_buffers():
+            if n.endswith("running_mean"):
+                b.zero_()
+            elif n.endswith("running_var"):
+                b.fill_(1.0)
+
+
+def load_bn_stats(module, stats, prefix=""):
+    """Copy running_mean / running_var from a {name: array} mapping (names relative to TwoStream)."""
+    import torch
+    with torch.no_grad():
+        for n, b in module.named_buffers():
+            full = prefix + n
+            if full in stats and (n.endswith("running_mean") or n.endswith("running_var")):
+                b.copy_(torch.as_tensor(np.asarray(stats[full])).to(b.device, b.dtype))
+
+
 # ------------------------------------------------------------------------------ clip windows
 def clip_batch(B, T, H, W, L, seed=123, device="cpu", vocab=30522):
     """Synthetic clip windows: frames ~ N(0,1) post-normalisation [B,T,3,H,W] f32,

@@ -1,0 +1,192 @@
+"""TSM-ResNet-50 trunk on libvcg_hip: NHWC activations, BN statistics from the conv epilogue,
+TSM shift fused into conv1's gather (fwd) and wgrad/dgrad (bwd).
+
+Mirrors torchvision resnet50 + make_temporal_shift(place='blockres') exactly as the reference
+builds it (model/vision/resnet50_tsm.py:15-19, ops/temporal_shift.py:104-146):
+  stem conv7x7/2 -> bn -> relu -> maxpool3x3/2 ; layer1..4 Bottleneck v1.5 (stride on conv2) with
+  conv1 = TemporalShift(conv1) ; avgpool ; fc = Identity.
+Backward is written by hand (autograd never sees the kernels) and accumulates weight / BN gradients
+straight into the parameters' flat fp32 .grad views.
+"""
+import torch
+
+from . import ops
+
+
+def bn_mode(bn):
+    """torch.nn.functional.batch_norm semantics for a BatchNorm2d module."""
+    has_running = bn.running_mean is not None and bn.running_var is not None
+    if bn.training:
+        return "train" if (bn.track_running_stats and has_running) else "batch"
+    return "running" if has_running else "batch"
+
+
+class BNState:
+    __slots__ = ("vec", "mean", "invstd", "scale", "shift", "mode", "count", "bn")
+
+    def __init__(self, C, device, mode, count, bn):
+        self.vec = torch.empty((4, C), dtype=torch.float32, device=device)
+        self.mean, self.invstd, self.scale, self.shift = self.vec[0], self.vec[1], self.vec[2], self.vec[3]
+        self.mode = mode
+        self.count = count
+        self.bn = bn
+
+
+def _conv_shape(conv):
+    KH, KW = conv.kernel_size
+    return conv.out_channels, conv.in_channels, KH, KW, conv.stride[0], conv.padding[0]
+
+
+def _tsm_info(conv1, Cin):
+    """(conv module, T, fold) for a possibly TemporalShift-wrapped conv."""
+    if hasattr(conv1, "net") and hasattr(conv1, "n_segment"):
+        return conv1.net, conv1.n_segment, Cin // conv1.fold_div
+    return conv1, 0, 0
+
+
+class ResNetTrunk:
+    def __init__(self, net, dtype):
+        self.net = net
+        self.dtype = dtype
+
+    # ---------------------------------------------------------------- helpers
+    def _wprep(self, conv, Cpad):
+        return ops.weight_prep(conv.weight.data, Cpad, self.dtype)
+
+    def _conv_bn(self, x, conv, bn, N, H, W, C, tsm_T=0, tsm_fold=0):
+        Cout, _, KH, KW, s, p = _conv_shape(conv)
+        OH, OW = ops.conv_out_hw(H, W, KH, KW, s, p)
+        M = N * OH * OW
+        mode = bn_mode(bn)
+        st = BNState(Cout, x.device, mode, M, bn)
+        w = self._wprep(conv, C)
+        if mode == "running":
+            y = ops.conv_fwd(x, w, N, H, W, C, Cout, KH, KW, s, p, tsm_T, tsm_fold)
+            ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, Cout, st.mean, st.invstd,
+                               st.scale, st.shift)
+        else:
+            mt = ops.stats_tiles(M)
+            stats = torch.empty((Cout, mt, 2), dtype=torch.float32, device=x.device)
+            y = ops.conv_fwd(x, w, N, H, W, C, Cout, KH, KW, s, p, tsm_T, tsm_fold, stats=stats)
+            upd = mode == "train"
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            ops.bn_finalize(stats, mt, M, Cout, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
+                            bn.running_mean if upd else None, bn.running_var if upd else None, mom, bn.eps)
+        return y, st, OH, OW
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, x, need_grad):
+        """x: [N, 3, H, W] fp32 frames ((b t) order). Returns (emb [N, 2048] fp32, saved)."""
+        net, dt = self.net, self.dtype
+        N, C0, H, W = x.shape
+        cpad = 8 if dt == torch.bfloat16 else 4
+        xs = ops.frames_to_nhwc(x.contiguous(), N, C0, H, W, cpad, dt)
+        y0, b0, H1, W1 = self._conv_bn(xs, net.conv1, net.bn1, N, H, W, cpad)
+        a0 = ops.bn_apply(y0, b0.scale, b0.shift, 64, relu=True)
+        mp, idx = ops.maxpool_fwd(a0, N, H1, W1, 64)
+        Hm, Wm = mp.shape[1], mp.shape[2]
+        saved = {"stem": (xs, y0, a0, idx, b0, N, H, W, cpad, H1, W1)} if need_grad else None
+        if not need_grad:
+            del y0, a0, idx
+        h, Hc, Wc = mp, Hm, Wm
+        blocks = []
+        for layer in (net.layer1, net.layer2, net.layer3, net.layer4):
+            for blk in layer:
+                h, rec, Hc, Wc = self._block_fwd(blk, h, N, Hc, Wc, need_grad)
+                if need_grad:
+                    blocks.append(rec)
+        emb = ops.avgpool_fwd(h, N, Hc * Wc, h.shape[-1])
+        if need_grad:
+            saved["blocks"] = blocks
+            saved["final"] = (N, Hc, Wc, h.shape[-1])
+        return emb, saved
+
+    def _block_fwd(self, blk, x, N, H, W, need_grad):
+        Cin = x.shape[-1]
+        conv1, T, fold = _tsm_info(blk.conv1, Cin)
+        planes = conv1.out_channels
+        y1, b1, _, _ = self._conv_bn(x, conv1, blk.bn1, N, H, W, Cin, T, fold)
+        a1 = ops.bn_apply(y1, b1.scale, b1.shift, planes, relu=True)
+        y2, b2, H2, W2 = self._conv_bn(a1, blk.conv2, blk.bn2, N, H, W, planes)
+        a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
+        y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes)
+        C3 = y3.shape[-1]
+        yd = bd = None
+        if blk.downsample is not None:
+            yd, bd, _, _ = self._conv_bn(x, blk.downsample[0], blk.downsample[1], N, H, W, Cin)
+            out = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale, rshift=bd.shift)
+        else:
+            out = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=x)
+        rec = None
+        if need_grad:
+            rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, y3=y3, yd=yd, out=out, b1=b1, b2=b2, b3=b3, bd=bd,
+                       N=N, H=H, W=W, H2=H2, W2=W2, Cin=Cin, planes=planes, C3=C3, T=T, fold=fold, conv1=conv1)
+        return out, rec, H2, W2
+
+    # ---------------------------------------------------------------- backward
+    def _bn_bwd(self, dout, mask, y, st, C, gout=None):
+        bn = st.bn
+        dev = y.device
+        sums = torch.empty((2, C), dtype=torch.float32, device=dev)
+        need_affine = bn.weight is not None and bn.weight.requires_grad
+        ops.bn_bwd_reduce(dout, mask, y, st.mean, st.invstd, C, sums[0], sums[1],
+                          bn.weight.grad if need_affine else None, bn.bias.grad if need_affine else None)
+        return ops.bn_bwd_apply(dout, mask, y, st.mean, st.invstd, bn.weight, sums[0], sums[1], C,
+                                train_stats=st.mode != "running", gout=gout)
+
+    def _wgrad(self, conv, x, dy, N, H, W, Cpad, T=0, fold=0):
+        if not conv.weight.requires_grad:
+            return
+        Cout, Cin, KH, KW, s, p = _conv_shape(conv)
+        ops.conv_wgrad(x, dy, conv.weight.grad, N, H, W, Cpad, Cin, Cout, KH, KW, s, p, T, fold, accumulate=True)
+
+    def _dgrad(self, conv, dy, N, H, W):
+        Cout, Cin, KH, KW, s, p = _conv_shape(conv)
+        wt = ops.weight_prep(conv.weight.data, Cin, self.dtype, transposed=True)
+        return ops.conv_dgrad(dy, wt, N, H, W, Cin, Cout, KH, KW, s, p)
+
+    def backward(self, d_emb, saved, hooks=None):
+        """d_emb: [N, 2048] fp32. Accumulates all trunk parameter grads; `hooks(params)` is told
+        when a block's gradients are final (DDP bucket all-reduce)."""
+        N, Hc, Wc, C = saved["final"]
+        dout = ops.avgpool_bwd(d_emb.contiguous(), N, Hc * Wc, C, self.dtype).view(N, Hc, Wc, C)
+        blocks = saved["blocks"]
+        while blocks:
+            rec = blocks.pop()  # frees the block's activations as soon as its backward is done
+            dout = self._block_bwd(rec, dout)
+            if hooks is not None:
+                hooks(list(rec["blk"].parameters()))
+            del rec
+        xs, y0, a0, idx, b0, N, H, W, cpad, H1, W1 = saved["stem"]
+        da0 = ops.maxpool_bwd(dout, idx, N, H1, W1, 64)
+        dy0 = self._bn_bwd(da0, a0, y0, b0, 64)
+        self._wgrad(self.net.conv1, xs, dy0, N, H, W, cpad)
+        if hooks is not None:
+            hooks(list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
+
+    def _block_bwd(self, r, dout):
+        blk = r["blk"]
+        N, H, W, H2, W2 = r["N"], r["H"], r["W"], r["H2"], r["W2"]
+        Cin, planes, C3, T, fold = r["Cin"], r["planes"], r["C3"], r["T"], r["fold"]
+        gout = torch.empty_like(dout)
+        dy3 = self._bn_bwd(dout, r["out"], r["y3"], r["b3"], C3, gout=gout)
+        self._wgrad(blk.conv3, r["a2"], dy3, N, H2, W2, planes)
+        da2 = self._dgrad(blk.conv3, dy3, N, H2, W2)
+        del dy3
+        dy2 = self._bn_bwd(da2, r["a2"], r["y2"], r["b2"], planes)
+        del da2
+        self._wgrad(blk.conv2, r["a1"], dy2, N, H, W, planes)
+        da1 = self._dgrad(blk.conv2, dy2, N, H, W)
+        del dy2
+        dy1 = self._bn_bwd(da1, r["a1"], r["y1"], r["b1"], planes)
+        del da1
+        self._wgrad(r["conv1"], r["x"], dy1, N, H, W, Cin, T, fold)
+        dxs = self._dgrad(r["conv1"], dy1, N, H, W)
+        del dy1
+        if blk.downsample is not None:
+            dyd = self._bn_bwd(gout, None, r["yd"], r["bd"], C3)
+            self._wgrad(blk.downsample[0], r["x"], dyd, N, H, W, Cin)
+            other = self._dgrad(blk.downsample[0], dyd, N, H, W)
+        else:
+            other = gout
+        return ops.tsm_unshift_add(dxs, other, N, T if T else 1, H * W, Cin, fold)
