@@ -134,18 +134,25 @@ __global__ void embed_scatter_kernel(const float* __restrict__ de, const long lo
   for (int c = threadIdx.x; c < H; c += blockDim.x) atomicAdd(&word_grad[id * H + c], de[row * H + c]);
 }
 
-__global__ void embed_pos_type_kernel(const float* __restrict__ de, float* __restrict__ pos_grad,
-                                      float* __restrict__ type_grad, int B, int L, int H) {
+// position grad: thread (l, c) sums the batch; the per-position sums also go to tmp [L][H]
+__global__ void embed_pos_kernel(const float* __restrict__ de, float* __restrict__ pos_grad, float* __restrict__ tmp,
+                                 int B, int L, int H) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = blockIdx.y;
+  if (c >= H) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += de[((long long)b * L + l) * H + c];
+  if (pos_grad) pos_grad[(long long)l * H + c] += s;
+  tmp[(long long)l * H + c] = s;
+}
+
+// token-type grad (type id 0 everywhere): sum of the per-position sums, fixed order
+__global__ void embed_type_kernel(const float* __restrict__ tmp, float* __restrict__ type_grad, int L, int H) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= H) return;
   double tot = 0;
-  for (int l = 0; l < L; ++l) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += de[((long long)b * L + l) * H + c];
-    if (pos_grad) pos_grad[(long long)l * H + c] += s;
-    tot += s;
-  }
-  if (type_grad) type_grad[c] += (float)tot;
+  for (int l = 0; l < L; ++l) tot += tmp[(long long)l * H + c];
+  type_grad[c] += (float)tot;
 }
 
 // ---------------------------------------------------------------- residual LayerNorm
@@ -244,16 +251,29 @@ __global__ void ln_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ 
   }
 }
 
-__global__ void colpair_finalize_kernel(const float* __restrict__ part, int nblocks, int H, float* g1, float* g2) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= H) return;
+// Column sums of partial rows (64 columns x 4 row-stripes per block, coalesced, fixed order):
+//   out1[c] (+)= sum_i part[i*stride + c] ; out2[c] (+)= sum_i part[i*stride + off2 + c]
+__global__ __launch_bounds__(256) void colred_kernel(const float* __restrict__ part, int nblocks, long long stride,
+                                                     int N, long long off2, float* out1, float* out2, int accumulate) {
+  __shared__ double sa[4][64], sb[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
   double a = 0, b = 0;
-  for (int i = 0; i < nblocks; ++i) {
-    a += part[(long long)i * 2 * H + c];
-    b += part[(long long)i * 2 * H + H + c];
+  if (c < N) {
+    for (int i = ty; i < nblocks; i += 4) {
+      a += part[(long long)i * stride + c];
+      if (out2) b += part[(long long)i * stride + off2 + c];
+    }
   }
-  if (g1) g1[c] += (float)a;
-  if (g2) g2[c] += (float)b;
+  sa[ty][tx] = a;
+  sb[ty][tx] = b;
+  __syncthreads();
+  if (ty == 0 && c < N) {
+    a = sa[0][tx] + sa[1][tx] + sa[2][tx] + sa[3][tx];
+    b = sb[0][tx] + sb[1][tx] + sb[2][tx] + sb[3][tx];
+    if (out1) out1[c] = (accumulate ? out1[c] : 0.f) + (float)a;
+    if (out2) out2[c] = (accumulate ? out2[c] : 0.f) + (float)b;
+  }
 }
 
 // ---------------------------------------------------------------- column sums (bias grads)
@@ -266,13 +286,6 @@ __global__ void colsum_part_kernel(const T* __restrict__ x, long long ld, int ro
     for (int r = r0; r < r1; ++r) s += to_f<T>(x[(long long)r * ld + c]);
     part[(long long)blockIdx.x * N + c] = s;
   }
-}
-__global__ void colsum_finalize_kernel(const float* __restrict__ part, int nblocks, int N, float* out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  double s = 0;
-  for (int i = 0; i < nblocks; ++i) s += part[(long long)i * N + c];
-  out[c] = (accumulate ? out[c] : 0.f) + (float)s;
 }
 
 // ---------------------------------------------------------------- attention softmax
@@ -410,16 +423,21 @@ VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, 
     hipLaunchKernelGGL(embed_ln_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dout, ids, word, pos,
                        type, gamma, mean, rstd, de, part, L, H, rpb, rows, dropout_p, (uint64_t)seed);
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colpair_finalize_kernel, dim3((H + 255) / 256), dim3(256), 0, s, part, nb, H, gamma_grad,
-                     beta_grad);
+  hipLaunchKernelGGL(colred_kernel, dim3((H + 63) / 64), dim3(256), 0, s, part, nb, (long long)2 * H, H, (long long)H,
+                     gamma_grad, beta_grad, 1);
   VCG_LAUNCH_CHECK();
   if (word_grad) {
     hipLaunchKernelGGL(embed_scatter_kernel, dim3(rows), dim3(256), 0, s, de, ids, word_grad, H, (long long)rows,
                        pad_idx);
     VCG_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(embed_pos_type_kernel, dim3((H + 255) / 256), dim3(256), 0, s, de, pos_grad, type_grad, B, L, H);
+  // the partial region is free again: reuse it for the per-position sums (2*nb >= L since rows >= L)
+  hipLaunchKernelGGL(embed_pos_kernel, dim3((H + 255) / 256, L), dim3(256), 0, s, de, pos_grad, part, B, L, H);
   VCG_LAUNCH_CHECK();
+  if (type_grad) {
+    hipLaunchKernelGGL(embed_type_kernel, dim3((H + 255) / 256), dim3(256), 0, s, part, type_grad, L, H);
+    VCG_LAUNCH_CHECK();
+  }
   return VCG_OK;
 }
 
@@ -453,8 +471,8 @@ VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* r
                        (const float*)res, gamma, mean, rstd, (float*)dx, (float*)dres, ws, H, rpb, rows, dropout_p,
                        (uint64_t)seed);
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colpair_finalize_kernel, dim3((H + 255) / 256), dim3(256), 0, s, ws, nb, H, gamma_grad,
-                     beta_grad);
+  hipLaunchKernelGGL(colred_kernel, dim3((H + 63) / 64), dim3(256), 0, s, ws, nb, (long long)2 * H, H, (long long)H,
+                     gamma_grad, beta_grad, 1);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -476,7 +494,8 @@ VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, 
   else
     hipLaunchKernelGGL(colsum_part_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)x, ld, rows, N, rpb, ws);
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colsum_finalize_kernel, dim3((N + 255) / 256), dim3(256), 0, s, ws, nb, N, out, accumulate);
+  hipLaunchKernelGGL(colred_kernel, dim3((N + 63) / 64), dim3(256), 0, s, ws, nb, (long long)N, N, 0LL, out,
+                     (float*)nullptr, accumulate);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

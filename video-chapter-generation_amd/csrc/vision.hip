@@ -75,235 +75,6 @@ __global__ void bn_eval_params_kernel(const float* gamma, const float* beta, con
   shift[c] = b - rm[c] * g * invstd;
 }
 
-// ------------------------------------------------------------------ BN apply
-// out = act(y*scale + shift + [res*rscale + rshift | res])
-template <typename T>
-__global__ void bn_apply_kernel(const T* __restrict__ y, const float* __restrict__ scale,
-                                const float* __restrict__ shift, const T* __restrict__ res,
-                                const float* __restrict__ rscale, const float* __restrict__ rshift, int relu,
-                                T* __restrict__ out, long long total_vec, int C) {
-  constexpr int VN = V<T>::N;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_vec;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long e0 = i * VN;
-    const int c0 = (int)(e0 % C);
-    float v[VN];
-    load16<T>(y + e0, v);
-#pragma unroll
-    for (int e = 0; e < VN; ++e) v[e] = v[e] * scale[c0 + e] + shift[c0 + e];
-    if (res) {
-      float r[VN];
-      load16<T>(res + e0, r);
-      if (rscale) {
-#pragma unroll
-        for (int e = 0; e < VN; ++e) v[e] += r[e] * rscale[c0 + e] + rshift[c0 + e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < VN; ++e) v[e] += r[e];
-      }
-    }
-    if (relu) {
-#pragma unroll
-      for (int e = 0; e < VN; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    store16<T>(out + e0, v);
-  }
-}
-
-// ------------------------------------------------------------------ BN backward
-// Partial per-channel sums of g and g*xhat, g = dout * [mask > 0] (mask optional).
-// Block = 256 threads handles rows [r0, r0 + rows_per_block) for all channels.
-template <typename T>
-__global__ void bn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ mask,
-                                     const T* __restrict__ y, const float* __restrict__ mean,
-                                     const float* __restrict__ invstd, int P, int C, int rows_per_block,
-                                     float* __restrict__ partial) {
-  constexpr int VN = V<T>::N;
-  extern __shared__ float sred[];  // [2][C]
-  const int cpr = C / VN;          // column chunks per row
-  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) sred[i] = 0.f;
-  __syncthreads();
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(P, r0 + rows_per_block);
-  if (cpr <= (int)blockDim.x) {
-    const int rpp = blockDim.x / cpr;
-    const int cc = (threadIdx.x % cpr) * VN;
-    const int rr = threadIdx.x / cpr;
-    float sg[VN], sgx[VN], mu[VN], is[VN];
-#pragma unroll
-    for (int e = 0; e < VN; ++e) { sg[e] = 0.f; sgx[e] = 0.f; mu[e] = mean[cc + e]; is[e] = invstd[cc + e]; }
-    if (rr < rpp) {
-      for (int r = r0 + rr; r < r1; r += rpp) {
-        const long long o = (long long)r * C + cc;
-        float d[VN], yv[VN];
-        load16<T>(dout + o, d);
-        load16<T>(y + o, yv);
-        if (mask) {
-          float m[VN];
-          load16<T>(mask + o, m);
-#pragma unroll
-          for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < VN; ++e) {
-          sg[e] += d[e];
-          sgx[e] += d[e] * (yv[e] - mu[e]) * is[e];
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < VN; ++e) {
-        atomicAdd(&sred[cc + e], sg[e]);
-        atomicAdd(&sred[C + cc + e], sgx[e]);
-      }
-    }
-  } else {
-    for (int ch = threadIdx.x; ch < cpr; ch += blockDim.x) {
-      const int cc = ch * VN;
-      float sg[VN], sgx[VN];
-#pragma unroll
-      for (int e = 0; e < VN; ++e) { sg[e] = 0.f; sgx[e] = 0.f; }
-      for (int r = r0; r < r1; ++r) {
-        const long long o = (long long)r * C + cc;
-        float d[VN], yv[VN];
-        load16<T>(dout + o, d);
-        load16<T>(y + o, yv);
-        if (mask) {
-          float m[VN];
-          load16<T>(mask + o, m);
-#pragma unroll
-          for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < VN; ++e) {
-          sg[e] += d[e];
-          sgx[e] += d[e] * (yv[e] - mean[cc + e]) * invstd[cc + e];
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < VN; ++e) { sred[cc + e] = sg[e]; sred[C + cc + e] = sgx[e]; }
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) partial[(long long)blockIdx.x * 2 * C + i] = sred[i];
-}
-
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nblocks, int C, float* sum_g,
-                                       float* sum_gx, float* dgamma, float* dbeta, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0, b = 0;
-  for (int i = 0; i < nblocks; ++i) {
-    a += partial[(long long)i * 2 * C + c];
-    b += partial[(long long)i * 2 * C + C + c];
-  }
-  sum_g[c] = (float)a;
-  sum_gx[c] = (float)b;
-  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)a;
-  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)b;
-}
-
-// dy = gamma*invstd*(g - sum_g/N - xhat*sum_gx/N)  (train / batch-stat mode)
-// dy = gamma*invstd*g                              (running-stat mode, train_stats = 0)
-// optionally gout = g (the masked upstream gradient, feeds the residual path)
-template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ mask,
-                                    const T* __restrict__ y, const float* __restrict__ mean,
-                                    const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                    const float* __restrict__ sum_g, const float* __restrict__ sum_gx,
-                                    float inv_count, int train_stats, T* __restrict__ dy, T* __restrict__ gout,
-                                    long long total_vec, int C) {
-  constexpr int VN = V<T>::N;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_vec;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long e0 = i * VN;
-    const int c0 = (int)(e0 % C);
-    float d[VN], yv[VN];
-    load16<T>(dout + e0, d);
-    if (mask) {
-      float m[VN];
-      load16<T>(mask + e0, m);
-#pragma unroll
-      for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
-    }
-    if (gout) store16<T>(gout + e0, d);
-    load16<T>(y + e0, yv);
-    float o[VN];
-#pragma unroll
-    for (int e = 0; e < VN; ++e) {
-      const int c = c0 + e;
-      const float k = (gamma ? gamma[c] : 1.f) * invstd[c];
-      if (train_stats) {
-        const float xh = (yv[e] - mean[c]) * invstd[c];
-        o[e] = k * (d[e] - sum_g[c] * inv_count - xh * sum_gx[c] * inv_count);
-      } else {
-        o[e] = k * d[e];
-      }
-    }
-    store16<T>(dy + e0, o);
-  }
-}
-
-// ------------------------------------------------------------------ pooling
-// max_pool2d(k=3, s=2, p=1) NHWC with argmax index (0..8, first max in (kh,kw) scan order)
-template <typename T>
-__global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int N,
-                                   int H, int W, int C, int OH, int OW) {
-  const long long total = (long long)N * OH * OW * C;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long long r = i / C;
-    const int ow = (int)(r % OW); r /= OW;
-    const int oh = (int)(r % OH);
-    const int n = (int)(r / OH);
-    float best = -INFINITY;
-    int bi = 0;
-    for (int kh = 0; kh < 3; ++kh) {
-      const int ih = oh * 2 - 1 + kh;
-      if (ih < 0 || ih >= H) continue;
-      for (int kw = 0; kw < 3; ++kw) {
-        const int iw = ow * 2 - 1 + kw;
-        if (iw < 0 || iw >= W) continue;
-        const float v = to_f<T>(x[(((long long)n * H + ih) * W + iw) * C + c]);
-        if (v > best || isnan(v)) { best = v; bi = kh * 3 + kw; }
-      }
-    }
-    y[i] = from_f<T>(best);
-    idx[i] = (uint8_t)bi;
-  }
-}
-
-template <typename T>
-__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx,
-                                   int N, int H, int W, int C, int OH, int OW) {
-  const long long total = (long long)N * H * W * C;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long long r = i / C;
-    const int iw = (int)(r % W); r /= W;
-    const int ih = (int)(r % H);
-    const int n = (int)(r / H);
-    float acc = 0.f;
-    // windows (oh, ow) with oh*2-1 <= ih <= oh*2+1
-    const int oh_lo = max(0, (ih - 1 + 1) / 2 - ((ih - 1 + 1) % 2 != 0 ? 0 : 0));
-    for (int oh = (ih) / 2 - 1; oh <= (ih + 1) / 2; ++oh) {
-      if (oh < 0 || oh >= OH) continue;
-      const int kh = ih - (oh * 2 - 1);
-      if (kh < 0 || kh > 2) continue;
-      for (int ow = iw / 2 - 1; ow <= (iw + 1) / 2; ++ow) {
-        if (ow < 0 || ow >= OW) continue;
-        const int kw = iw - (ow * 2 - 1);
-        if (kw < 0 || kw > 2) continue;
-        const long long o = (((long long)n * OH + oh) * OW + ow) * C + c;
-        if (idx[o] == kh * 3 + kw) acc += to_f<T>(dy[o]);
-      }
-    }
-    (void)oh_lo;
-    dx[i] = from_f<T>(acc);
-  }
-}
-
 // global average pool: x [N][HW][C] -> y [N][C] (fp32 out)
 template <typename T>
 __global__ void avgpool_fwd_kernel(const T* __restrict__ x, float* __restrict__ y, int HW, int C) {
@@ -404,39 +175,6 @@ __global__ void tsm_nchw_kernel(const T* __restrict__ x, T* __restrict__ y, long
   }
 }
 
-// NHWC gradient combine for a TSM block input: dx = unshift(dshift) + other
-template <typename T>
-__global__ void tsm_unshift_add_kernel(const T* __restrict__ dshift, const T* __restrict__ other, T* __restrict__ dx,
-                                       long long total_vec, int Tn, long long HWC, int C, int fold) {
-  constexpr int VN = V<T>::N;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_vec;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long e0 = i * VN;
-    const int c = (int)(e0 % C);
-    const long long nt = e0 / HWC;
-    const int t = (int)(nt % Tn);
-    int dt = 0;  // adjoint of the forward shift
-    if (fold > 0) {
-      if (c < fold) dt = -1;
-      else if (c < 2 * fold) dt = 1;
-    }
-    const int t2 = t + dt;
-    float a[VN];
-    if (t2 >= 0 && t2 < Tn) load16<T>(dshift + e0 + (long long)dt * HWC, a);
-    else {
-#pragma unroll
-      for (int e = 0; e < VN; ++e) a[e] = 0.f;
-    }
-    if (other) {
-      float b[VN];
-      load16<T>(other + e0, b);
-#pragma unroll
-      for (int e = 0; e < VN; ++e) a[e] += b[e];
-    }
-    store16<T>(dx + e0, a);
-  }
-}
-
 inline int grid_for(long long n, int bs = 256) {
   long long g = (n + bs - 1) / bs;
   if (g > 8192) g = 8192;
@@ -463,102 +201,6 @@ VCG_API int vcg_bn_eval_params(const float* gamma, const float* beta, const floa
                                int C, float* mean_out, float* invstd_out, float* scale, float* shift, hipStream_t s) {
   hipLaunchKernelGGL(bn_eval_params_kernel, dim3((C + 255) / 256), dim3(256), 0, s, gamma, beta, rm, rv, eps, C,
                      mean_out, invstd_out, scale, shift);
-  VCG_LAUNCH_CHECK();
-  return VCG_OK;
-}
-
-VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const void* res,
-                         const float* rscale, const float* rshift, int relu, void* out, long long P, int C,
-                         hipStream_t s) {
-  const int VN = dtype == VCG_BF16 ? 8 : 4;
-  VCG_REQUIRE(C % VN == 0, "C must be a multiple of the vector width");
-  const long long tv = P * C / VN;
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(grid_for(tv)), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
-                       (const bf16_t*)res, rscale, rshift, relu, (bf16_t*)out, tv, C);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_for(tv)), dim3(256), 0, s, (const float*)y, scale, shift,
-                       (const float*)res, rscale, rshift, relu, (float*)out, tv, C);
-  VCG_LAUNCH_CHECK();
-  return VCG_OK;
-}
-
-static int bn_bwd_blocks(long long P) {
-  long long rows = (P + 2047) / 2048;
-  if (rows < 16) rows = 16;
-  return (int)((P + rows - 1) / rows);
-}
-static int bn_bwd_rows(long long P) { return (int)((P + bn_bwd_blocks(P) - 1) / bn_bwd_blocks(P)); }
-
-VCG_API long long vcg_bn_bwd_ws_bytes(long long P, int C) { return (long long)bn_bwd_blocks(P) * 2 * C * 4 + 2 * C * 4; }
-
-// Per-channel sum_g / sum_gx (and optional dgamma/dbeta accumulation into fp32 grads).
-VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
-                              const float* invstd, long long P, int C, float* ws, long long ws_bytes, float* sum_g,
-                              float* sum_gx, float* dgamma, float* dbeta, int accumulate, hipStream_t s) {
-  const int VN = dtype == VCG_BF16 ? 8 : 4;
-  VCG_REQUIRE(C % VN == 0, "C must be a multiple of the vector width");
-  VCG_REQUIRE(ws_bytes >= vcg_bn_bwd_ws_bytes(P, C), "workspace too small");
-  const int rows = bn_bwd_rows(P);
-  const int nb = (int)((P + rows - 1) / rows);
-  const size_t shm = 2 * C * sizeof(float);
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, dim3(nb), dim3(256), shm, s, (const bf16_t*)dout,
-                       (const bf16_t*)mask, (const bf16_t*)y, mean, invstd, (int)P, C, rows, ws);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(nb), dim3(256), shm, s, (const float*)dout,
-                       (const float*)mask, (const float*)y, mean, invstd, (int)P, C, rows, ws);
-  VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, nb, C, sum_g, sum_gx, dgamma,
-                     dbeta, accumulate);
-  VCG_LAUNCH_CHECK();
-  return VCG_OK;
-}
-
-VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
-                             const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx,
-                             long long count, int train_stats, void* dy, void* gout, long long P, int C,
-                             hipStream_t s) {
-  const int VN = dtype == VCG_BF16 ? 8 : 4;
-  VCG_REQUIRE(C % VN == 0, "C must be a multiple of the vector width");
-  const long long tv = P * C / VN;
-  const float ic = 1.f / (float)count;
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(grid_for(tv)), dim3(256), 0, s, (const bf16_t*)dout,
-                       (const bf16_t*)mask, (const bf16_t*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats,
-                       (bf16_t*)dy, (bf16_t*)gout, tv, C);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_for(tv)), dim3(256), 0, s, (const float*)dout,
-                       (const float*)mask, (const float*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats,
-                       (float*)dy, (float*)gout, tv, C);
-  VCG_LAUNCH_CHECK();
-  return VCG_OK;
-}
-
-VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* idx, int N, int H, int W, int C,
-                            hipStream_t s) {
-  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  const long long tot = (long long)N * OH * OW * C;
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, dim3(grid_for(tot)), dim3(256), 0, s, (const bf16_t*)x,
-                       (bf16_t*)y, idx, N, H, W, C, OH, OW);
-  else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(grid_for(tot)), dim3(256), 0, s, (const float*)x, (float*)y,
-                       idx, N, H, W, C, OH, OW);
-  VCG_LAUNCH_CHECK();
-  return VCG_OK;
-}
-
-VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C,
-                            hipStream_t s) {
-  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  const long long tot = (long long)N * H * W * C;
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, dim3(grid_for(tot)), dim3(256), 0, s, (const bf16_t*)dy, idx,
-                       (bf16_t*)dx, N, H, W, C, OH, OW);
-  else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(grid_for(tot)), dim3(256), 0, s, (const float*)dy, idx,
-                       (float*)dx, N, H, W, C, OH, OW);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -644,17 +286,3 @@ VCG_API int vcg_tsm_shift(int dtype, const void* x, void* y, long long n_batch, 
   return VCG_OK;
 }
 
-VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other, void* dx, long long NT, int T,
-                                long long HW, int C, int fold, hipStream_t s) {
-  const int VN = dtype == VCG_BF16 ? 8 : 4;
-  VCG_REQUIRE(C % VN == 0 && (fold % VN == 0), "C and fold must be multiples of the vector width");
-  const long long tv = NT * HW * C / VN;
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(tsm_unshift_add_kernel<bf16_t>, dim3(grid_for(tv)), dim3(256), 0, s, (const bf16_t*)dshift,
-                       (const bf16_t*)other, (bf16_t*)dx, tv, T, HW * C, C, fold);
-  else
-    hipLaunchKernelGGL(tsm_unshift_add_kernel<float>, dim3(grid_for(tv)), dim3(256), 0, s, (const float*)dshift,
-                       (const float*)other, (float*)dx, tv, T, HW * C, C, fold);
-  VCG_LAUNCH_CHECK();
-  return VCG_OK;
-}

@@ -1,0 +1,492 @@
+// Streaming NHWC kernels of the vision trunk: BatchNorm apply (+residual, +ReLU), BatchNorm
+// backward (reduce + apply), max-pool fwd/bwd, and the TSM gradient combine.
+//
+// All are HBM-bound. Layout rule used throughout: a tensor [P][C] is a stream of 16-byte vectors
+// v = row * cpr + chunk (cpr = C / VN, a power of two). Blocks take contiguous runs of
+// 256 * ITER vectors, so when cpr divides 256 a thread's channel chunk never changes and its
+// per-channel parameters live in registers for the whole run; index math stays 32/64-bit
+// shifts and masks (no 64-bit division).
+#include "common.h"
+
+using namespace vcg;
+
+namespace {
+
+template <typename T> struct V { static constexpr int N = 16 / sizeof(T); };
+
+constexpr int EW_ITER = 8;
+constexpr int RED_ITER = 64;
+
+template <int VN>
+__device__ __forceinline__ void load_params(const float* __restrict__ p, int c0, float (&out)[VN]) {
+#pragma unroll
+  for (int e = 0; e < VN; e += 4) {
+    const float4 q = *reinterpret_cast<const float4*>(p + c0 + e);
+    out[e] = q.x; out[e + 1] = q.y; out[e + 2] = q.z; out[e + 3] = q.w;
+  }
+}
+
+__host__ __device__ inline int ilog2i(int x) {
+  int l = 0;
+  while ((1 << l) < x) ++l;
+  return l;
+}
+
+// ------------------------------------------------------------------ BN apply
+// out = act(y*scale + shift + [res*rscale + rshift | res])
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, const T* __restrict__ res,
+                                                       const float* __restrict__ rscale,
+                                                       const float* __restrict__ rshift, int relu,
+                                                       T* __restrict__ out, long long TV, int cpr) {
+  constexpr int VN = V<T>::N;
+  const long long base = (long long)blockIdx.x * (256 * EW_ITER) + threadIdx.x;
+  const bool fixed = cpr <= 256;
+  int c0 = (int)(base & (cpr - 1)) * VN;
+  float sc[VN], sh[VN], rs[VN], rb[VN];
+  load_params<VN>(scale, c0, sc);
+  load_params<VN>(shift, c0, sh);
+  if (rscale) {
+    load_params<VN>(rscale, c0, rs);
+    load_params<VN>(rshift, c0, rb);
+  }
+#pragma unroll 4
+  for (int it = 0; it < EW_ITER; ++it) {
+    const long long v = base + it * 256;
+    if (v >= TV) break;
+    if (!fixed && it > 0) {
+      c0 = (int)(v & (cpr - 1)) * VN;
+      load_params<VN>(scale, c0, sc);
+      load_params<VN>(shift, c0, sh);
+      if (rscale) {
+        load_params<VN>(rscale, c0, rs);
+        load_params<VN>(rshift, c0, rb);
+      }
+    }
+    float a[VN];
+    load16<T>(y + v * VN, a);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) a[e] = a[e] * sc[e] + sh[e];
+    if (res) {
+      float r[VN];
+      load16<T>(res + v * VN, r);
+      if (rscale) {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) a[e] += r[e] * rs[e] + rb[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) a[e] += r[e];
+      }
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) a[e] = fmaxf(a[e], 0.f);
+    }
+    store16<T>(out + v * VN, a);
+  }
+}
+
+// ------------------------------------------------------------------ BN backward
+// partial[block][2C]: per-channel sums of g and g*xhat over the block's vectors, g = dout*[mask>0]
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ mask,
+                                                            const T* __restrict__ y, const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, long long TV, int cpr,
+                                                            int C, float* __restrict__ partial) {
+  constexpr int VN = V<T>::N;
+  __shared__ float red[2 * 2048];
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.f;
+  __syncthreads();
+  const long long base = (long long)blockIdx.x * (256 * RED_ITER) + threadIdx.x;
+  if (cpr <= 256) {
+    const int c0 = (int)(base & (cpr - 1)) * VN;
+    float mu[VN], is[VN], sg[VN], sx[VN];
+    load_params<VN>(mean, c0, mu);
+    load_params<VN>(invstd, c0, is);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) { sg[e] = 0.f; sx[e] = 0.f; }
+#pragma unroll 4
+    for (int it = 0; it < RED_ITER; ++it) {
+      const long long v = base + it * 256;
+      if (v >= TV) break;
+      float d[VN], yv[VN];
+      load16<T>(dout + v * VN, d);
+      load16<T>(y + v * VN, yv);
+      if (mask) {
+        float m[VN];
+        load16<T>(mask + v * VN, m);
+#pragma unroll
+        for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        sg[e] += d[e];
+        sx[e] += d[e] * (yv[e] - mu[e]) * is[e];
+      }
+    }
+    // threads with the same chunk: t, t + cpr, ... -> LDS atomics (256/cpr adders per address)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      atomicAdd(&red[c0 + e], sg[e]);
+      atomicAdd(&red[C + c0 + e], sx[e]);
+    }
+  } else {
+    for (int it = 0; it < RED_ITER; ++it) {
+      const long long v = base + it * 256;
+      if (v >= TV) break;
+      const int c0 = (int)(v & (cpr - 1)) * VN;
+      float d[VN], yv[VN];
+      load16<T>(dout + v * VN, d);
+      load16<T>(y + v * VN, yv);
+      if (mask) {
+        float m[VN];
+        load16<T>(mask + v * VN, m);
+#pragma unroll
+        for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        atomicAdd(&red[c0 + e], d[e]);
+        atomicAdd(&red[C + c0 + e], d[e] * (yv[e] - mean[c0 + e]) * invstd[c0 + e]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += 256) partial[(long long)blockIdx.x * 2 * C + i] = red[i];
+}
+
+// Column sums of partial[nb][2C] -> sum_g, sum_gx (+ dgamma/dbeta): 64 channels x 4 row-stripes per block,
+// coalesced across channels, fixed summation order (deterministic).
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nb, int C,
+                                                              float* sum_g, float* sum_gx, float* dgamma,
+                                                              float* dbeta, int accumulate) {
+  __shared__ double sa[4][64], sb[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  double a = 0, b = 0;
+  if (c < C) {
+    for (int i = ty; i < nb; i += 4) {
+      a += partial[(long long)i * 2 * C + c];
+      b += partial[(long long)i * 2 * C + C + c];
+    }
+  }
+  sa[ty][tx] = a;
+  sb[ty][tx] = b;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    a = sa[0][tx] + sa[1][tx] + sa[2][tx] + sa[3][tx];
+    b = sb[0][tx] + sb[1][tx] + sb[2][tx] + sb[3][tx];
+    sum_g[c] = (float)a;
+    sum_gx[c] = (float)b;
+    if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)a;
+    if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)b;
+  }
+}
+
+// dy = A*g + B*y + Cc per channel (batch-stat BN backward folded to an affine map of (g, y)):
+//   A = gamma*invstd, B = -A*invstd*sum_gx/N, Cc = -A*sum_g/N - B*mean ; running mode: dy = A*g.
+// optionally gout = g (masked upstream gradient: the residual path)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ mask,
+                                                           const T* __restrict__ y, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ sum_g,
+                                                           const float* __restrict__ sum_gx, float inv_count,
+                                                           int train_stats, T* __restrict__ dy, T* __restrict__ gout,
+                                                           long long TV, int cpr) {
+  constexpr int VN = V<T>::N;
+  const long long base = (long long)blockIdx.x * (256 * EW_ITER) + threadIdx.x;
+  float A[VN], Bc[VN], Cc[VN];
+  int c_loaded = -1;
+#pragma unroll 4
+  for (int it = 0; it < EW_ITER; ++it) {
+    const long long v = base + it * 256;
+    if (v >= TV) break;
+    const int c0 = (int)(v & (cpr - 1)) * VN;
+    if (c0 != c_loaded) {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        const int c = c0 + e;
+        const float is = invstd[c];
+        const float a = (gamma ? gamma[c] : 1.f) * is;
+        A[e] = a;
+        if (train_stats) {
+          Bc[e] = -a * is * sum_gx[c] * inv_count;
+          Cc[e] = -a * sum_g[c] * inv_count - Bc[e] * mean[c];
+        } else {
+          Bc[e] = 0.f;
+          Cc[e] = 0.f;
+        }
+      }
+      c_loaded = c0;
+    }
+    float d[VN], yv[VN], o[VN];
+    load16<T>(dout + v * VN, d);
+    if (mask) {
+      float m[VN];
+      load16<T>(mask + v * VN, m);
+#pragma unroll
+      for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
+    }
+    if (gout) store16<T>(gout + v * VN, d);
+    if (train_stats) {
+      load16<T>(y + v * VN, yv);
+#pragma unroll
+      for (int e = 0; e < VN; ++e) o[e] = A[e] * d[e] + Bc[e] * yv[e] + Cc[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) o[e] = A[e] * d[e];
+    }
+    store16<T>(dy + v * VN, o);
+  }
+}
+
+// ------------------------------------------------------------------ max pool 3x3 / 2, pad 1
+// thread = (output pixel, 16-B channel chunk); first max in (kh, kw) scan order (torch CPU semantics)
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, int H, int W, int C, int OH,
+                                                          int OW, int lcpr, long long TV) {
+  constexpr int VN = V<T>::N;
+  const long long v = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (v >= TV) return;
+  const int chunk = (int)(v & ((1 << lcpr) - 1));
+  const int pix = (int)(v >> lcpr);
+  const int ow = pix % OW;
+  const int t = pix / OW;
+  const int oh = t % OH;
+  const int n = t / OH;
+  float best[VN];
+  uint8_t bi[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+  for (int kh = 0; kh < 3; ++kh) {
+    const int ih = oh * 2 - 1 + kh;
+    if (ih < 0 || ih >= H) continue;
+    for (int kw = 0; kw < 3; ++kw) {
+      const int iw = ow * 2 - 1 + kw;
+      if (iw < 0 || iw >= W) continue;
+      float a[VN];
+      load16<T>(x + (((long long)n * H + ih) * W + iw) * C + chunk * VN, a);
+#pragma unroll
+      for (int e = 0; e < VN; ++e)
+        if (a[e] > best[e] || isnan(a[e])) { best[e] = a[e]; bi[e] = (uint8_t)(kh * 3 + kw); }
+    }
+  }
+  store16<T>(y + v * VN, best);
+  uint8_t* ip = idx + v * VN;
+#pragma unroll
+  for (int e = 0; e < VN; ++e) ip[e] = bi[e];
+}
+
+// thread = (input pixel, chunk): sums dy over the <= 4 windows whose argmax is this pixel
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                          T* __restrict__ dx, int H, int W, int C, int OH, int OW,
+                                                          int lcpr, long long TV) {
+  constexpr int VN = V<T>::N;
+  const long long v = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (v >= TV) return;
+  const int chunk = (int)(v & ((1 << lcpr) - 1));
+  const int pix = (int)(v >> lcpr);
+  const int iw = pix % W;
+  const int t = pix / W;
+  const int ih = t % H;
+  const int n = t / H;
+  float acc[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) acc[e] = 0.f;
+  const int oh0 = ih / 2, oh1 = (ih + 1) / 2;  // windows with 2*oh-1 <= ih <= 2*oh+1
+  const int ow0 = iw / 2, ow1 = (iw + 1) / 2;
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    if (oh >= OH) continue;
+    const int kh = ih - (oh * 2 - 1);
+    if (kh < 0 || kh > 2) continue;
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      if (ow >= OW) continue;
+      const int kw = iw - (ow * 2 - 1);
+      if (kw < 0 || kw > 2) continue;
+      const long long o = (((long long)n * OH + oh) * OW + ow) * C + chunk * VN;
+      const uint8_t want = (uint8_t)(kh * 3 + kw);
+      float g[VN];
+      load16<T>(dy + o, g);
+      const uint8_t* ip = idx + o;
+#pragma unroll
+      for (int e = 0; e < VN; ++e)
+        if (ip[e] == want) acc[e] += g[e];
+    }
+  }
+  store16<T>(dx + v * VN, acc);
+}
+
+// ------------------------------------------------------------------ TSM gradient combine
+// dx = unshift(dshift) + other over NHWC [N*T][H][W][C] (adjoint of ops/temporal_shift.py:45-47)
+template <typename T>
+__global__ __launch_bounds__(256) void tsm_unshift_add_kernel(const T* __restrict__ dshift, const T* __restrict__ other,
+                                                              T* __restrict__ dx, long long TV, int lcpr, int HW,
+                                                              int Tn, int fold_chunks) {
+  constexpr int VN = V<T>::N;
+  const long long base = (long long)blockIdx.x * (256 * EW_ITER) + threadIdx.x;
+  const long long row_vecs = (long long)HW << lcpr;  // vectors per frame
+#pragma unroll 4
+  for (int it = 0; it < EW_ITER; ++it) {
+    const long long v = base + it * 256;
+    if (v >= TV) break;
+    const int chunk = (int)(v & ((1 << lcpr) - 1));
+    int dt = 0;
+    if (chunk < fold_chunks) dt = -1;
+    else if (chunk < 2 * fold_chunks) dt = 1;
+    float a[VN];
+    bool have = true;
+    if (dt != 0) {
+      const int frame = (int)(v / row_vecs);
+      const int t = frame % Tn;
+      have = (t + dt >= 0) && (t + dt < Tn);
+    }
+    if (have) load16<T>(dshift + (v + dt * row_vecs) * VN, a);
+    else {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) a[e] = 0.f;
+    }
+    if (other) {
+      float b[VN];
+      load16<T>(other + v * VN, b);
+#pragma unroll
+      for (int e = 0; e < VN; ++e) a[e] += b[e];
+    }
+    store16<T>(dx + v * VN, a);
+  }
+}
+
+inline unsigned blocks_for(long long TV, int per_block) { return (unsigned)((TV + per_block - 1) / per_block); }
+
+}  // namespace
+
+// ==================================================================== C ABI
+
+VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const void* res,
+                         const float* rscale, const float* rshift, int relu, void* out, long long P, int C,
+                         hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
+  const long long TV = P * C / VN;
+  const int cpr = C / VN;
+  if (TV == 0) return VCG_OK;
+  const unsigned g = blocks_for(TV, 256 * EW_ITER);
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
+                       (const bf16_t*)res, rscale, rshift, relu, (bf16_t*)out, TV, cpr);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)y, scale, shift,
+                       (const float*)res, rscale, rshift, relu, (float*)out, TV, cpr);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+static long long bn_bwd_blocks(long long P, int C, int VN) {
+  const long long TV = P * C / VN;
+  return (TV + 256 * RED_ITER - 1) / (256 * RED_ITER);
+}
+
+VCG_API long long vcg_bn_bwd_ws_bytes(long long P, int C) {
+  // sized for the smaller vector width (fp32) so one query serves both dtypes
+  return bn_bwd_blocks(P, C, 4) * 2 * C * 4 + 64;
+}
+
+VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
+                              const float* invstd, long long P, int C, float* ws, long long ws_bytes, float* sum_g,
+                              float* sum_gx, float* dgamma, float* dbeta, int accumulate, hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && C <= 2048, "C must be a power of two <= 2048");
+  VCG_REQUIRE(ws_bytes >= vcg_bn_bwd_ws_bytes(P, C), "workspace too small");
+  const long long TV = P * C / VN;
+  const int cpr = C / VN;
+  const long long nb = bn_bwd_blocks(P, C, VN);
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, dim3((unsigned)nb), dim3(256), 0, s, (const bf16_t*)dout,
+                       (const bf16_t*)mask, (const bf16_t*)y, mean, invstd, TV, cpr, C, ws);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, (const float*)dout,
+                       (const float*)mask, (const float*)y, mean, invstd, TV, cpr, C, ws);
+  VCG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, ws, (int)nb, C, sum_g, sum_gx,
+                     dgamma, dbeta, accumulate);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
+                             const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx,
+                             long long count, int train_stats, void* dy, void* gout, long long P, int C,
+                             hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
+  const long long TV = P * C / VN;
+  const float ic = 1.f / (float)count;
+  const unsigned g = blocks_for(TV, 256 * EW_ITER);
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)dout,
+                       (const bf16_t*)mask, (const bf16_t*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats,
+                       (bf16_t*)dy, (bf16_t*)gout, TV, C / VN);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)dout,
+                       (const float*)mask, (const float*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats,
+                       (float*)dy, (float*)gout, TV, C / VN);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* idx, int N, int H, int W, int C,
+                            hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int lcpr = ilog2i(C / VN);
+  const long long TV = (long long)N * OH * OW * (C / VN);
+  VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const bf16_t*)x,
+                       (bf16_t*)y, idx, H, W, C, OH, OW, lcpr, TV);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const float*)x,
+                       (float*)y, idx, H, W, C, OH, OW, lcpr, TV);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C,
+                            hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int lcpr = ilog2i(C / VN);
+  const long long TV = (long long)N * H * W * (C / VN);
+  VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const bf16_t*)dy, idx,
+                       (bf16_t*)dx, H, W, C, OH, OW, lcpr, TV);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const float*)dy, idx,
+                       (float*)dx, H, W, C, OH, OW, lcpr, TV);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other, void* dx, long long NT, int T,
+                                long long HW, int C, int fold, hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && fold % VN == 0, "C / fold must be multiples of the vector width");
+  const long long TV = NT * HW * C / VN;
+  const int lcpr = ilog2i(C / VN);
+  const unsigned g = blocks_for(TV, 256 * EW_ITER);
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(tsm_unshift_add_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)dshift,
+                       (const bf16_t*)other, (bf16_t*)dx, TV, lcpr, (int)HW, T, fold / VN);
+  else
+    hipLaunchKernelGGL(tsm_unshift_add_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)dshift,
+                       (const float*)other, (float*)dx, TV, lcpr, (int)HW, T, fold / VN);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
