@@ -1,0 +1,243 @@
+// Shared declarations of the MFMA implicit-GEMM engine (igemm.hip, igemm_fast.hip).
+#pragma once
+#include "common.h"
+
+namespace vcg {
+
+enum { OP_DENSE_K = 0, OP_IM2COL = 1, OP_DGRAD = 2, OP_DENSE_MN = 3, OP_IM2COL_T = 4 };
+enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2 };
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
+
+template <typename T> struct Cfg;
+template <> struct Cfg<float> { static constexpr int VEC = 4, BK = 16, LDK = 20; };   // 80-B rows
+template <> struct Cfg<bf16_t> { static constexpr int VEC = 8, BK = 32, LDK = 40; };  // 80-B rows
+
+template <typename T, int COLS> struct LdMN {
+  // padded element stride of a [BK][COLS] tile (bank-conflict-free for the fragment reads)
+  static constexpr int v = sizeof(T) == 2 ? (COLS == 128 ? 144 : 80) : (COLS == 128 ? 132 : 68);
+};
+
+constexpr bool is_kcontig(int mode) { return mode == OP_DENSE_K || mode == OP_IM2COL || mode == OP_DGRAD; }
+
+struct FastDiv {  // q = n / d for 0 <= n < 2^31
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  uint32_t hi = __umulhi(n, f.m);
+  return (uint32_t)(((uint64_t)hi + n) >> f.s);
+}
+
+struct OpArgs {
+  const void* ptr;
+  long long bytes;  // extent of the tensor behind ptr (buffer-descriptor range for LDS-DMA loads)
+  long long ld;   // dense modes: leading dimension in elements
+  int rows;       // number of valid rows (K-contig) / cols (MN-contig)
+  // conv geometry (gather modes)
+  int N, H, W, C, logC;  // gathered tensor is NHWC [N][H][W][C] (C power of two)
+  int GH, GW;            // grid that indexes the rows (IM2COL: output; DGRAD: dx; IM2COL_T: dy)
+  int KH, KW, stride, pad;
+  int tsm_T, tsm_fold;   // TSM temporal shift fused into the gather (fold = 0: off)
+  FastDiv fd_ghw, fd_gw, fd_T;
+};
+
+struct GemmParams {
+  int M, N, K;
+  int k_per_split;  // multiple of BK
+  OpArgs a, b;
+  void* C;
+  long long ldc;
+  const float* bias;
+  int act;
+  const void* residual;
+  long long ldr;
+  void* aux;  // optional copy of the pre-activation value
+  float alpha;
+  float* stats;  // EPI_STATS: float2 [N][mtiles] (mean, M2) per column per m-tile
+  float* ws;     // EPI_SPLITK: fp32 slabs [split][M][N]
+  // batched mode (batch_inner > 0): blockIdx.z = zo * batch_inner + zi selects element offsets
+  int batch_inner;
+  long long a_so, a_si, b_so, b_si, c_so, c_si;
+};
+
+
+template <typename T> __device__ __forceinline__ void load4(const T* p, float (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    const uint2 q = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+}
+template <typename T> __device__ __forceinline__ void store4(T* p, const float (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    uint2 q;
+    q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = q;
+  }
+}
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  if (act == ACT_GELU) return gelu_erf(v);
+  if (act == ACT_TANH) return tanhf(v);
+  return v;
+}
+
+
+// Sum over the 16 lanes of a DPP row (lanes 16g..16g+15); every lane of the row gets the total.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+// Bias of the 4*BN/32 columns a lane owns in the epilogue (zeros without bias / beyond N).
+template <int BN>
+__device__ __forceinline__ void load_bias(float (&bv)[BN / 32][4], const float* bias, int n0, int wn, int lane, int N) {
+#pragma unroll
+  for (int j = 0; j < BN / 32; ++j) {
+    const int n = n0 + wn * (BN / 2) + 4 * (lane >> 4) + j * 16;
+    float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (bias && n < N) b4 = *reinterpret_cast<const float4*>(bias + n);
+    bv[j][0] = b4.x; bv[j][1] = b4.y; bv[j][2] = b4.z; bv[j][3] = b4.w;
+  }
+}
+
+// Barrier for the epilogue's LDS exchange: waits only for this wave's LDS ops, so an LDS-DMA
+// prefetch of the next tile (fast kernel) stays in flight.
+__device__ __forceinline__ void ep_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
+
+// Epilogue shared by the generic and fast kernels: acc[i][j][r] = C[m][n] with
+// m = m0 + wm*(BM/2) + i*16 + (lane&15), n = n0 + wn*(BN/2) + j*16 + 4*(lane>>4) + r.
+// bv[j][r] is the bias of column nbase + j*16 + r (zeros when there is none; see load_bias).
+// EPI_STATS: `red` holds 4*BN floats that no other wave touches until the caller's next barrier;
+// the per-column (mean, M2) of this tile goes to stats[col][mtile] (float2, mtiles per column).
+// Each wave reduces its 64 rows in registers (two passes, DPP row sums), the two row-halves are
+// merged with Chan's formula after one barrier, and only then are the values stored, so the
+// barrier never waits on outstanding HBM writes.
+template <typename T, int BM, int BN, int EPI>
+__device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], const GemmParams& p, float* red,
+                                              const float (&bv)[BN / 32][4], T* Cout, const T* Res, int m0, int n0,
+                                              int wm, int wn, int lane, int mtile, int mtiles) {
+  constexpr int MT = BM / 32, NT = BN / 32;
+  const int g = lane >> 4, ci = lane & 15;
+  const int mbase = m0 + wm * (BM / 2) + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = nbase + j * 16;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int m = mbase + i * 16;
+      if (m >= p.M || n >= p.N) {
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha + bv[j][r];
+      if (Res) {
+        float rv[4];
+        load4<T>(Res + (long long)m * p.ldr + n, rv);
+        if (p.act == ACT_GELU_BWD) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] *= gelu_erf_grad(rv[r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+      }
+      if (p.aux) store4<T>(reinterpret_cast<T*>(p.aux) + (long long)m * p.ldc + n, v);
+      if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      }
+      if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = to_f<T>(from_f<T>(v[r]));  // the stored (rounded) value
+      } else {
+        store4<T>(Cout + (long long)m * p.ldc + n, v);
+      }
+    }
+  }
+  if constexpr (EPI == EPI_STATS) {
+    const int r0 = m0 + wm * (BM / 2);
+    const int cw = min(BM / 2, max(0, p.M - r0));  // valid rows of this wave's half
+    const float inv_cw = cw > 0 ? 1.f / (float)cw : 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) t += acc[i][j][r];  // rows beyond M are zero
+        t = row16_sum(t);
+        const float mean = t * inv_cw;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const float d = acc[i][j][r] - mean;
+          q += (mbase + i * 16 < p.M) ? d * d : 0.f;
+        }
+        q = row16_sum(q);
+        if (ci == 0) {
+          const int lc = wn * (BN / 2) + j * 16 + 4 * g + r;
+          red[wm * 2 * BN + lc] = mean;
+          red[wm * 2 * BN + BN + lc] = q;
+        }
+      }
+    ep_barrier();
+    if (wm == 0 && ci == 0) {
+      const float n1 = (float)min(BM / 2, max(0, p.M - m0));
+      const float n2 = (float)min(BM / 2, max(0, p.M - m0 - BM / 2));
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lc = wn * (BN / 2) + j * 16 + 4 * g + r;
+          const int col = n0 + lc;
+          if (col >= p.N) continue;
+          float mean = red[lc], m2 = red[BN + lc];
+          if (n2 > 0.f) {
+            const float mb = red[2 * BN + lc], d = mb - mean, nt = n1 + n2;
+            mean += d * (n2 / nt);
+            m2 += red[3 * BN + lc] + d * d * (n1 * n2 / nt);
+          }
+          reinterpret_cast<float2*>(p.stats)[(long long)col * mtiles + mtile] = make_float2(mean, m2);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = nbase + j * 16;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int m = mbase + i * 16;
+        if (m >= p.M || n >= p.N) continue;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        store4<T>(Cout + (long long)m * p.ldc + n, v);
+      }
+    }
+  }
+}
+
+int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
+
+}  // namespace vcg

@@ -14,72 +14,9 @@
 // Replaces the ATen conv / addmm kernels reached from torchvision ResNet-50
 // (reference video_chapter_generation/model/vision/resnet50_tsm.py:15) and HF BertModel
 // (model/lang/bert_hugface.py:20) on the TwoStream hot path (model/fusion/two_stream.py:172-194).
-#include "common.h"
+#include "igemm.h"
 
 namespace vcg {
-
-enum { OP_DENSE_K = 0, OP_IM2COL = 1, OP_DGRAD = 2, OP_DENSE_MN = 3, OP_IM2COL_T = 4 };
-enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2 };
-enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
-
-template <typename T> struct Cfg;
-template <> struct Cfg<float> { static constexpr int VEC = 4, BK = 16, LDK = 20; };   // 80-B rows
-template <> struct Cfg<bf16_t> { static constexpr int VEC = 8, BK = 32, LDK = 40; };  // 80-B rows
-
-template <typename T, int COLS> struct LdMN {
-  // padded element stride of a [BK][COLS] tile (bank-conflict-free for the fragment reads)
-  static constexpr int v = sizeof(T) == 2 ? (COLS == 128 ? 144 : 80) : (COLS == 128 ? 132 : 68);
-};
-
-constexpr bool is_kcontig(int mode) { return mode == OP_DENSE_K || mode == OP_IM2COL || mode == OP_DGRAD; }
-
-struct FastDiv {  // q = n / d for 0 <= n < 2^31
-  uint32_t d, m, s;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  f.d = d;
-  uint32_t s = 0;
-  while ((1ull << s) < d) ++s;
-  f.s = s;
-  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-  return f;
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  uint32_t hi = __umulhi(n, f.m);
-  return (uint32_t)(((uint64_t)hi + n) >> f.s);
-}
-
-struct OpArgs {
-  const void* ptr;
-  long long ld;   // dense modes: leading dimension in elements
-  int rows;       // number of valid rows (K-contig) / cols (MN-contig)
-  // conv geometry (gather modes)
-  int N, H, W, C, logC;  // gathered tensor is NHWC [N][H][W][C] (C power of two)
-  int GH, GW;            // grid that indexes the rows (IM2COL: output; DGRAD: dx; IM2COL_T: dy)
-  int KH, KW, stride, pad;
-  int tsm_T, tsm_fold;   // TSM temporal shift fused into the gather (fold = 0: off)
-  FastDiv fd_ghw, fd_gw, fd_T;
-};
-
-struct GemmParams {
-  int M, N, K;
-  int k_per_split;  // multiple of BK
-  OpArgs a, b;
-  void* C;
-  long long ldc;
-  const float* bias;
-  int act;
-  const void* residual;
-  long long ldr;
-  void* aux;  // optional copy of the pre-activation value
-  float alpha;
-  float* stats;  // EPI_STATS: float2 [N][mtiles] (mean, M2) per column per m-tile
-  float* ws;     // EPI_SPLITK: fp32 slabs [split][M][N]
-  // batched mode (batch_inner > 0): blockIdx.z = zo * batch_inner + zi selects element offsets
-  int batch_inner;
-  long long a_so, a_si, b_so, b_si, c_so, c_si;
-};
 
 // ------------------------------------------------------------------------------------
 // Tile loaders: global -> registers -> LDS
@@ -286,19 +223,12 @@ template <> struct Mfma<float> {
   }
 };
 
-__device__ __forceinline__ float apply_act(float v, int act) {
-  if (act == ACT_RELU) return fmaxf(v, 0.f);
-  if (act == ACT_GELU) return gelu_erf(v);
-  if (act == ACT_TANH) return tanhf(v);
-  return v;
-}
-
 template <typename T, int ROWS, int MODE> constexpr int tile_elems() {
   return is_kcontig(MODE) ? ROWS * Cfg<T>::LDK : Cfg<T>::BK * LdMN<T, ROWS>::v;
 }
 template <typename T, int BM, int BN, int AM, int BMD, int EPI> constexpr int smem_bytes() {
   constexpr int mainloop = 2 * (tile_elems<T, BM, AM>() + tile_elems<T, BN, BMD>()) * (int)sizeof(T);
-  constexpr int epi = EPI == EPI_SPLITK ? 0 : BM * (BN + 16 / (int)sizeof(T)) * (int)sizeof(T) + 2 * 1024 * 4;
+  constexpr int epi = EPI == EPI_STATS ? 4 * BN * 4 : 0;  // stats reduction reuses the main-loop LDS
   return mainloop > epi ? mainloop : epi;
 }
 
@@ -367,7 +297,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmParams p) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NT; ++j) Mfma<T>::run(acc[i][j], af[i], bfr[j]);
+      for (int j = 0; j < NT; ++j) Mfma<T>::run(acc[i][j], bfr[j], af[i]);  // D = C^T tile
     if (t + 1 < ntiles) {
       la.store(As + (cur ^ 1) * AE);
       lb.store(Bs + (cur ^ 1) * BE);
@@ -375,115 +305,29 @@ __global__ __launch_bounds__(256) void igemm_kernel(GemmParams p) {
     __syncthreads();
   }
 
+  // acc[i][j][r] = C[m = mbase + i*16 + ci][n = nbase + j*16 + 4g + r]  (operands swapped in the
+  // MFMA so each lane owns 4 consecutive output columns -> direct 8/16-byte stores, no LDS staging)
   const int g = lane >> 4, ci = lane & 15;
+  const int mbase = m0 + wm * (BM / 2) + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
   if constexpr (EPI == EPI_SPLITK) {
     float* ws = p.ws + (long long)blockIdx.z * p.M * p.N;
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MT; ++i) {
+      const int m = mbase + i * 16;
+      if (m >= p.M) continue;
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const int col = n0 + wn * (BN / 2) + j * 16 + ci;
-        if (col >= p.N) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * (BM / 2) + i * 16 + g * 4 + r;
-          if (row < p.M) ws[(long long)row * p.N + col] = acc[i][j][r];
-        }
+        const int n = nbase + j * 16;
+        if (n < p.N) *reinterpret_cast<f32x4*>(ws + (long long)m * p.N + n) = acc[i][j];
       }
+    }
     return;
   } else {
-    // Stage alpha*acc + bias as T in LDS, then write 16-B vectors (residual / act / aux / stats).
-    constexpr int LDC = BN + VEC;
-    T* Cs = reinterpret_cast<T*>(smem);
-    float* red = reinterpret_cast<float*>(smem + BM * LDC * sizeof(T));
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int lc = wn * (BN / 2) + j * 16 + ci;
-      const float bv = (p.bias && n0 + lc < p.N) ? p.bias[n0 + lc] : 0.f;
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int lr = wm * (BM / 2) + i * 16 + g * 4 + r;
-          Cs[lr * LDC + lc] = from_f<T>(acc[i][j][r] * p.alpha + bv);
-        }
-    }
-    __syncthreads();
-    constexpr int CPR = BN / VEC;          // 16-B chunks per tile row
-    constexpr int RPP = 256 / CPR;         // rows per pass
-    const int cc = (tid % CPR) * VEC;
-    const int rr = tid / CPR;
-    const int col = n0 + cc;
-    float csum[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) csum[e] = 0.f;
-    for (int lr = rr; lr < BM; lr += RPP) {
-      const int row = m0 + lr;
-      if (row >= p.M || col >= p.N) continue;
-      float v[VEC];
-      load16<T>(Cs + lr * LDC + cc, v);
-      if (Res) {
-        float rv[VEC];
-        load16<T>(Res + (long long)row * p.ldr + col, rv);
-        if (p.act == ACT_GELU_BWD) {
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) v[e] *= gelu_erf_grad(rv[e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) v[e] += rv[e];
-        }
-      }
-      if (p.aux) store16<T>(reinterpret_cast<T*>(p.aux) + (long long)row * p.ldc + col, v);
-      if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) {
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) v[e] = apply_act(v[e], p.act);
-      }
-      store16<T>(Cout + (long long)row * p.ldc + col, v);
-      if constexpr (EPI == EPI_STATS) {
-        // statistics of the values as stored (rounded to T)
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) csum[e] += to_f<T>(from_f<T>(v[e]));
-      }
-    }
-    if constexpr (EPI == EPI_STATS) {
-      // Per-column (mean, M2) over this tile's valid rows, two passes over the staged tile.
-      // The stats epilogue is only used without residual/activation, so the staged value
-      // (rounded to T) is exactly the stored value that BN will normalise.
-      const int valid_rows = min(BM, p.M - m0);
-      if (tid < 2 * BN) red[tid] = 0.f;
-      __syncthreads();
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) atomicAdd(&red[cc + e], csum[e]);
-      __syncthreads();
-      float mean[VEC], m2[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        mean[e] = red[cc + e] / (float)valid_rows;
-        m2[e] = 0.f;
-      }
-      for (int lr = rr; lr < BM; lr += RPP) {
-        const int row = m0 + lr;
-        if (row >= p.M || col >= p.N) continue;
-        float v[VEC];
-        load16<T>(Cs + lr * LDC + cc, v);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          const float d = v[e] - mean[e];
-          m2[e] += d * d;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) atomicAdd(&red[BN + cc + e], m2[e]);
-      __syncthreads();
-      if (rr == 0 && col < p.N) {
-        const int mtiles = gridDim.y;
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          float2 st = make_float2(mean[e], red[BN + cc + e]);
-          reinterpret_cast<float2*>(p.stats)[(long long)(col + e) * mtiles + blockIdx.y] = st;
-        }
-      }
-    }
+    __syncthreads();  // main-loop LDS reads done before `red` reuses it
+    float bv[BN / 32][4];
+    load_bias<BN>(bv, p.bias, n0, wn, lane, p.N);
+    gemm_epilogue<T, BM, BN, EPI>(acc, p, reinterpret_cast<float*>(smem), bv, Cout, Res, m0, n0, wm, wn, lane,
+                                  blockIdx.y, gridDim.y);
   }
 }
 
@@ -496,12 +340,23 @@ static int ilog2_exact(int c) {
   return (1 << l) == c ? l : -1;
 }
 
-static OpArgs dense_op(const void* ptr, long long ld, int rows) {
+// dense operand; `bytes` = extent of [rows][ld] with the last row K long (element size esz)
+static OpArgs dense_op(const void* ptr, long long ld, int rows, long long K = 0, int esz = 2) {
   OpArgs a{};
   a.ptr = ptr;
   a.ld = ld;
   a.rows = rows;
+  a.bytes = ((long long)(rows > 0 ? rows - 1 : 0) * ld + (K > 0 ? K : ld)) * esz;
   return a;
+}
+
+static bool fast_gemm_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VCG_FAST_GEMM");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
 }
 
 template <typename T, int BM, int BN, int AM, int BMD, int EPI>
@@ -523,6 +378,13 @@ static int mtiles_of(int M) { return (M + 127) / 128; }
 
 template <typename T, int AM, int BMD>
 static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
+  if constexpr (sizeof(T) == 2 && is_kcontig(AM) && BMD == OP_DENSE_K) {
+    const bool single = splits == 1 || p.batch_inner > 0;
+    if (fast_gemm_enabled() && epi != EPI_SPLITK && single && p.K % 8 == 0 && p.a.bytes < 0xFFFFFF00LL &&
+        p.b.bytes < 0xFFFFFF00LL && (!p.residual || AM == OP_DENSE_K) &&
+        !(epi == EPI_STATS && p.bias))
+      return run_fast_gemm(p, AM, epi, splits, s);
+  }
   if (epi == EPI_STORE) return launch_bn<T, AM, BMD, EPI_STORE>(p, splits, s);
   if (epi == EPI_STATS) return launch_bn<T, AM, BMD, EPI_STATS>(p, splits, s);
   return launch_bn<T, AM, BMD, EPI_SPLITK>(p, splits, s);
@@ -590,15 +452,16 @@ VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float
   p.k_per_split = p.K + 64;
   const bool dense = (KH == 1 && KW == 1 && stride == 1 && pad == 0 && tsm_fold == 0);
   if (dense) {
-    p.a = dense_op(x, C, p.M);
+    p.a = dense_op(x, C, p.M, C, dtype == VCG_BF16 ? 2 : 4);
   } else {
     OpArgs a{};
     a.ptr = x; a.rows = p.M; a.N = N; a.H = H; a.W = W; a.C = C; a.logC = logC;
     a.GH = OH; a.GW = OW; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
     a.tsm_T = tsm_T; a.tsm_fold = tsm_fold;
+    a.bytes = (long long)N * H * W * C * (dtype == VCG_BF16 ? 2 : 4);
     p.a = a;
   }
-  p.b = dense_op(w, p.K, Cout);
+  p.b = dense_op(w, p.K, Cout, p.K, dtype == VCG_BF16 ? 2 : 4);
   p.C = y;
   p.ldc = Cout;
   p.alpha = 1.f;
@@ -627,14 +490,15 @@ VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
   p.k_per_split = p.K + 64;
   const bool dense = (KH == 1 && KW == 1 && stride == 1 && pad == 0);
   if (dense) {
-    p.a = dense_op(dy, Cout, p.M);
+    p.a = dense_op(dy, Cout, p.M, Cout, dtype == VCG_BF16 ? 2 : 4);
   } else {
     OpArgs a{};
     a.ptr = dy; a.rows = p.M; a.N = N; a.H = OH; a.W = OW; a.C = Cout; a.logC = logCo;
     a.GH = H; a.GW = W; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+    a.bytes = (long long)N * OH * OW * Cout * (dtype == VCG_BF16 ? 2 : 4);
     p.a = a;
   }
-  p.b = dense_op(wt, p.K, C);
+  p.b = dense_op(wt, p.K, C, p.K, dtype == VCG_BF16 ? 2 : 4);
   p.C = dx;
   p.ldc = C;
   p.alpha = 1.f;
@@ -710,11 +574,15 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
                      const void* residual, long long ldr, void* aux, float alpha, hipStream_t stream) {
   const int VEC = dtype == VCG_BF16 ? 8 : 4;
   VCG_REQUIRE(N % VEC == 0 && ldc % VEC == 0 && K % VEC == 0, "N, ldc, K must be multiples of 16 bytes");
+  VCG_REQUIRE(residual == nullptr || ldr % 4 == 0, "ldr must be a multiple of 4");
   VCG_REQUIRE(M > 0 && N > 0 && K > 0, "empty GEMM");
   GemmParams p{};
   p.M = M; p.N = N; p.K = K; p.k_per_split = K + 64;
-  p.a = dense_op(A, lda, M);
-  p.b = dense_op(B, ldb, N);
+  const int esz = dtype == VCG_BF16 ? 2 : 4;
+  p.a = transA ? dense_op(A, lda, K, M, esz) : dense_op(A, lda, M, K, esz);
+  p.b = transB ? dense_op(B, ldb, K, N, esz) : dense_op(B, ldb, N, K, esz);
+  p.a.rows = M;
+  p.b.rows = N;
   p.C = C; p.ldc = ldc; p.bias = bias; p.act = act; p.residual = residual; p.ldr = ldr; p.aux = aux;
   p.alpha = alpha;
 #define VCG_GEMM_CASE(TT)                                                                   \
@@ -777,8 +645,13 @@ VCG_API int vcg_gemm_batched(int dtype, int transA, int transB, int M, int N, in
   VCG_REQUIRE(batch_outer > 0 && batch_inner > 0 && M > 0 && N > 0 && K > 0, "empty batched GEMM");
   GemmParams p{};
   p.M = M; p.N = N; p.K = K; p.k_per_split = K + 64;
-  p.a = dense_op(A, lda, M);
-  p.b = dense_op(B, ldb, N);
+  const int esz = dtype == VCG_BF16 ? 2 : 4;
+  p.a = transA ? dense_op(A, lda, K, M, esz) : dense_op(A, lda, M, K, esz);
+  p.b = transB ? dense_op(B, ldb, K, N, esz) : dense_op(B, ldb, N, K, esz);
+  p.a.rows = M;
+  p.b.rows = N;
+  p.a.bytes += ((long long)(batch_outer - 1) * a_so + (long long)(batch_inner - 1) * a_si) * esz;
+  p.b.bytes += ((long long)(batch_outer - 1) * b_so + (long long)(batch_inner - 1) * b_si) * esz;
   p.C = C; p.ldc = ldc; p.bias = bias; p.act = act; p.alpha = alpha;
   p.batch_inner = batch_inner;
   p.a_so = a_so; p.a_si = a_si; p.b_so = b_so; p.b_si = b_si; p.c_so = c_so; p.c_si = c_si;

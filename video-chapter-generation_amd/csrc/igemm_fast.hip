@@ -1,0 +1,279 @@
+// bf16 fast path of the implicit-GEMM engine for K-contiguous operands
+// (conv fwd with im2col/TSM gather, conv dgrad gather, dense linear layers / QK^T).
+//
+// Differences to the generic kernel (igemm.hip):
+//   * BK = 64 (two 16x16x32 MFMA k-steps per barrier pair);
+//   * operands go global -> LDS directly with buffer_load ... lds (LDS-DMA, 16 B per lane,
+//     1 KiB per wave instruction, no VGPR staging); conv zero padding / out-of-range rows come for
+//     free from the buffer descriptor's range check (out-of-range offset -> zeros);
+//   * LDS tile [rows][64] bf16 with 128-B rows, 16-B chunk c of row r at slot c ^ ((r >> 1) & 7):
+//     the global source address is pre-swizzled (LDS stays lane-linear, as LDS-DMA requires) and
+//     the fragment ds_read_b64s of a 32-lane half hit 64 distinct banks;
+//   * two LDS stages; tile t+1 is in flight while tile t is computed; counted vmcnt + raw
+//     s_barrier (never __syncthreads, which would drain the in-flight DMA).
+#include "igemm.h"
+
+namespace vcg {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int FBK = 64;
+
+__device__ __forceinline__ int fswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int ROWS, int MODE> struct FastLoader {
+  static constexpr int PER_WAVE = ROWS / 32;  // 1-KiB (8-row) slices per wave per tile
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t oob;
+  long long off[PER_WAVE];  // element offset of the row's base (-1 = invalid row)
+  int ra[PER_WAVE], rb[PER_WAVE], rc[PER_WAVE], kc[PER_WAVE];
+
+  __device__ __forceinline__ void init(const OpArgs& a, long long batch_off, int row0, int wave, int lane) {
+    const uint32_t nbytes = (uint32_t)min(a.bytes, (long long)0xFFFFFF00LL);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr), 0, nbytes, 0x00020000);
+    oob = nbytes;  // offset + 16 > num_records -> the load returns zeros
+#pragma unroll
+    for (int q = 0; q < PER_WAVE; ++q) {
+      const int r = (wave * PER_WAVE + q) * 8 + (lane >> 3);
+      kc[q] = 8 * fswz(r, lane & 7);
+      const int gr = row0 + r;
+      const bool valid = gr < a.rows;
+      if constexpr (MODE == OP_DENSE_K) {
+        off[q] = valid ? batch_off + (long long)gr * a.ld : -1;
+      } else {
+        const int n = gr / (a.GH * a.GW);
+        const int rem = gr - n * a.GH * a.GW;
+        const int y = rem / a.GW;
+        const int x = rem - y * a.GW;
+        off[q] = valid ? (long long)n * a.H * a.W * a.C : -1;
+        if constexpr (MODE == OP_IM2COL) {
+          ra[q] = y * a.stride - a.pad;
+          rb[q] = x * a.stride - a.pad;
+          rc[q] = a.tsm_fold > 0 ? (n % a.tsm_T) : 0;
+        } else {
+          ra[q] = y + a.pad;
+          rb[q] = x + a.pad;
+          rc[q] = 0;
+        }
+      }
+    }
+  }
+
+  // issue the LDS-DMA loads of one 64-wide k tile into `lds` (tile base, [ROWS][64] bf16)
+  __device__ __forceinline__ void issue(const OpArgs& a, int k0, int kend, bf16_t* lds, int wave) {
+#pragma unroll
+    for (int q = 0; q < PER_WAVE; ++q) {
+      const int k = k0 + kc[q];
+      long long e = -1;
+      if constexpr (MODE == OP_DENSE_K) {
+        if (off[q] >= 0 && k < kend) e = off[q] + k;
+      } else if constexpr (MODE == OP_IM2COL) {
+        const int tap = k >> a.logC;
+        const int c = k & (a.C - 1);
+        const int kh = tap / a.KW;
+        const int kw = tap - kh * a.KW;
+        const int ih = ra[q] + kh, iw = rb[q] + kw;
+        if (off[q] >= 0 && k < kend && kh < a.KH && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
+          long long o = off[q] + ((long long)(ih * a.W + iw) << a.logC) + c;
+          bool ok = true;
+          if (a.tsm_fold > 0) {
+            const int dt = c < a.tsm_fold ? 1 : (c < 2 * a.tsm_fold ? -1 : 0);
+            const int t2 = rc[q] + dt;
+            ok = t2 >= 0 && t2 < a.tsm_T;
+            o += (long long)dt * a.H * a.W * a.C;
+          }
+          if (ok) e = o;
+        }
+      } else {  // OP_DGRAD
+        const int tap = k >> a.logC;
+        const int c = k & (a.C - 1);
+        const int kh = tap / a.KW;
+        const int kw = tap - kh * a.KW;
+        int yy = ra[q] - kh, xx = rb[q] - kw;
+        bool ok = off[q] >= 0 && k < kend && kh < a.KH && yy >= 0 && xx >= 0;
+        if (a.stride == 2) {
+          ok = ok && ((yy | xx) & 1) == 0;
+          yy >>= 1;
+          xx >>= 1;
+        }
+        ok = ok && yy < a.H && xx < a.W;
+        if (ok) e = off[q] + (((long long)(yy * a.W + xx)) << a.logC) + c;
+      }
+      const uint32_t voff = e >= 0 ? (uint32_t)(e * 2) : oob;
+      bf16_t* slice = lds + (wave * PER_WAVE + q) * 512;  // 1 KiB per slice
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)slice, 16, voff, 0, 0, 0);
+    }
+  }
+};
+
+// 16x16x32 bf16 fragment of rows r0..r0+15, k-step s2 (0/1) of a swizzled [rows][64] tile.
+// Element j of lane 16g+i is k = 32*s2 + 4g + 16*(j>>2) + (j&3) (same map on both operands).
+__device__ __forceinline__ s16x8 fast_frag(const bf16_t* lds, int r0, int lane, int s2) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = r0 + i;
+  const int c1 = 4 * s2 + (g >> 1);
+  const bf16_t* rp = lds + row * 64 + 4 * (g & 1);
+  const s16x4 lo = *reinterpret_cast<const s16x4*>(rp + 8 * fswz(row, c1));
+  const s16x4 hi = *reinterpret_cast<const s16x4*>(rp + 8 * fswz(row, c1 + 2));
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__device__ __forceinline__ constexpr int waitcnt_vm(int n) {
+  // s_waitcnt simm16 for gfx9-family: vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 15 << 8 | vmcnt[5:4] << 14
+  return (n & 0xF) | (0x7 << 4) | (0xF << 8) | (((n >> 4) & 3) << 14);
+}
+
+template <int BM, int BN, int AM, int EPI, bool RES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void igemm_fast_kernel(GemmParams p) {
+  // Persistent-style grid: workgroup (bx, by) owns N-tile bx and M-tiles by, by + gy, by + 2gy, ...;
+  // the (m-tile, k-tile) steps form one software pipeline, so tile i+1's loads are in flight while
+  // tile i finishes its MFMAs and its epilogue. Workgroups are dealt round-robin to the 8 XCDs by
+  // linear id, so when gy % 8 == 0 the linear id is decoded such that all N-tiles of an M-tile
+  // row run on the same XCD at the same time and the A rows are fetched from HBM once (L2 hits).
+  // The bias lives in registers for the whole kernel (loaded before the pipeline starts) and the
+  // epilogue (RES = false) loads nothing: a VGPR-destination global load inside the loop, or an LDS
+  // object the compiler cannot tell apart from the DMA target, makes hipcc drain the in-flight
+  // LDS-DMA prefetch with vmcnt(0) at every tile boundary. Conv (EPI_STATS) GEMMs carry no bias.
+  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int AE = BM * FBK, BE = BN * FBK;  // elements per stage
+  constexpr int NLD = BM / 32 + BN / 32;       // LDS-DMA instructions per thread per step
+  __shared__ __attribute__((aligned(1024))) char smem[2 * (AE + BE) * 2 + 4 * BN * 4];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Bs = As + 2 * AE;
+  float* red = reinterpret_cast<float*>(smem + 2 * (AE + BE) * 2);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nx = (p.N + BN - 1) / BN, gy = gridDim.x / nx;
+  int bx, by;
+  if ((gy & 7) == 0) {
+    const int sidx = blockIdx.x >> 3;
+    bx = sidx % nx;
+    by = (sidx / nx) * 8 + (blockIdx.x & 7);
+  } else {
+    bx = blockIdx.x % nx;
+    by = blockIdx.x / nx;
+  }
+  const int n0 = bx * BN;
+  long long aoff = 0, boff = 0;
+  bf16_t* Cout = reinterpret_cast<bf16_t*>(p.C);
+  const bf16_t* Res = RES ? reinterpret_cast<const bf16_t*>(p.residual) : nullptr;
+  if (p.batch_inner > 0) {
+    const int zo = blockIdx.z / p.batch_inner, zi = blockIdx.z - zo * p.batch_inner;
+    aoff = zo * p.a_so + zi * p.a_si;
+    boff = zo * p.b_so + zi * p.b_si;
+    Cout += zo * p.c_so + zi * p.c_si;
+    if (Res) Res += zo * p.c_so + zi * p.c_si;
+  }
+  const int mtiles = (p.M + BM - 1) / BM;
+  const int my_tiles = by < mtiles ? (mtiles - 1 - by) / gy + 1 : 0;
+  const int ntiles = (p.K + FBK - 1) / FBK;
+  const int steps = my_tiles * ntiles;
+  if (steps == 0) return;
+
+  float bv[NT][4];
+  if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bv[j][0] = bv[j][1] = bv[j][2] = bv[j][3] = 0.f;
+  } else {
+    load_bias<BN>(bv, p.bias, n0, wn, lane, p.N);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) asm volatile("" ::"v"(bv[j][0]), "v"(bv[j][1]), "v"(bv[j][2]), "v"(bv[j][3]));
+  }
+
+  FastLoader<BM, AM> la;
+  FastLoader<BN, OP_DENSE_K> lb;
+  la.init(p.a, aoff, by * BM, wave, lane);
+  lb.init(p.b, boff, n0, wave, lane);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  la.issue(p.a, 0, p.K, As, wave);
+  lb.issue(p.b, 0, p.K, Bs, wave);
+  int kt = 0, tile = 0;
+  for (int s = 0; s < steps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < steps) {
+      int nkt = kt + 1;
+      if (nkt == ntiles) {  // next step starts the next M-tile of this workgroup
+        nkt = 0;
+        la.init(p.a, aoff, (by + (tile + 1) * gy) * BM, wave, lane);
+      }
+      la.issue(p.a, nkt * FBK, p.K, As + (cur ^ 1) * AE, wave);
+      lb.issue(p.b, nkt * FBK, p.K, Bs + (cur ^ 1) * BE, wave);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(NLD));  // step s landed (step s+1 may stay in flight)
+    } else {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    }
+    __builtin_amdgcn_s_barrier();
+    const bf16_t* Ac = As + cur * AE;
+    const bf16_t* Bc = Bs + cur * BE;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      s16x8 af[MT], bfr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[i] = fast_frag(Ac, wm * (BM / 2) + i * 16, lane, s2);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bfr[j] = fast_frag(Bc, wn * (BN / 2) + j * 16, lane, s2);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    // every wave's ds_reads of this stage have returned before any wave refills it (WAR)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+    __builtin_amdgcn_s_barrier();
+    if (++kt == ntiles) {
+      const int mt = by + tile * gy;
+      gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      kt = 0;
+      ++tile;
+    }
+  }
+}
+
+template <int BM, int BN, int AM, int EPI, bool RES>
+static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
+  // One resident round of workgroups (LDS allows 2 per CU at BN = 128, 3 at BN = 64); each walks
+  // ceil(mtiles / gy) M-tiles. gy is a multiple of 8 whenever possible (XCD-aware decode).
+  const int nx = (p.N + BN - 1) / BN, mtiles = (p.M + BM - 1) / BM;
+  const int resident = (BN == 128 ? 2 : 3) * 256;
+  int gy = resident / (nx * z);
+  if (gy >= 8) gy &= ~7;
+  if (gy > mtiles) gy = mtiles >= 8 ? (mtiles & ~7) : mtiles;
+  if (gy < 1) gy = 1;
+  dim3 grid(nx * gy, 1, z);
+  hipLaunchKernelGGL((igemm_fast_kernel<BM, BN, AM, EPI, RES>), grid, dim3(256), 0, s, p);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+template <int AM, int EPI, bool RES = false>
+static int fast_bn(const GemmParams& p, int z, hipStream_t s) {
+  if (p.N % 128 == 0 || p.N > 64 * 3) return launch_fast<128, 128, AM, EPI, RES>(p, z, s);
+  return launch_fast<128, 64, AM, EPI, RES>(p, z, s);
+}
+
+// Entry from igemm.hip's dispatcher (bf16, K-contiguous A and B, no split-K).
+int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
+  if (epi == EPI_STATS) {
+    if (amode == OP_IM2COL) return fast_bn<OP_IM2COL, EPI_STATS>(p, z, s);
+    if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_STATS>(p, z, s);
+    return fast_bn<OP_DENSE_K, EPI_STATS>(p, z, s);
+  }
+  if (p.residual) return fast_bn<OP_DENSE_K, EPI_STORE, true>(p, z, s);  // dense layers only (BERT bwd)
+  if (amode == OP_IM2COL) return fast_bn<OP_IM2COL, EPI_STORE>(p, z, s);
+  if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_STORE>(p, z, s);
+  return fast_bn<OP_DENSE_K, EPI_STORE>(p, z, s);
+}
+
+}  // namespace vcg

@@ -15,7 +15,7 @@ namespace {
 template <typename T> struct V { static constexpr int N = 16 / sizeof(T); };
 
 constexpr int EW_ITER = 8;
-constexpr int RED_ITER = 64;
+constexpr int RED_ITER = 256;
 
 template <int VN>
 __device__ __forceinline__ void load_params(const float* __restrict__ p, int c0, float (&out)[VN]) {
