@@ -14,6 +14,8 @@
 // Replaces the ATen conv / addmm kernels reached from torchvision ResNet-50
 // (reference video_chapter_generation/model/vision/resnet50_tsm.py:15) and HF BertModel
 // (model/lang/bert_hugface.py:20) on the TwoStream hot path (model/fusion/two_stream.py:172-194).
+#include <cstdio>
+
 #include "igemm.h"
 
 namespace vcg {
@@ -376,8 +378,29 @@ static int launch_bn(const GemmParams& p, int splits, hipStream_t s) {
 
 static int mtiles_of(int M) { return (M + 127) / 128; }
 
+// VCG_GEMM_LOG=<path>: append one line per GEMM dispatch (profiling aid: matches the kernel
+// trace's igemm launches in order).
+static FILE* gemm_log() {
+  static FILE* f = nullptr;
+  static bool init = false;
+  if (!init) {
+    init = true;
+    const char* e = getenv("VCG_GEMM_LOG");
+    if (e && e[0]) f = fopen(e, "a");
+  }
+  return f;
+}
+
 template <typename T, int AM, int BMD>
 static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
+  if (FILE* f = gemm_log()) {
+    const bool fast = sizeof(T) == 2 && is_kcontig(AM) && BMD == OP_DENSE_K && fast_gemm_enabled() &&
+                      epi != EPI_SPLITK && (splits == 1 || p.batch_inner > 0) && p.K % 8 == 0 &&
+                      (!p.residual || AM == OP_DENSE_K) && !(epi == EPI_STATS && p.bias);
+    fprintf(f, "a=%d b=%d epi=%d M=%d N=%d K=%d z=%d fast=%d conv=%dx%d/%d C=%d\n", AM, BMD, epi, p.M, p.N, p.K, splits,
+            (int)fast, p.a.KH, p.a.KW, p.a.stride, p.a.C);
+    fflush(f);
+  }
   if constexpr (sizeof(T) == 2 && is_kcontig(AM) && BMD == OP_DENSE_K) {
     const bool single = splits == 1 || p.batch_inner > 0;
     if (fast_gemm_enabled() && epi != EPI_SPLITK && single && p.K % 8 == 0 && p.a.bytes < 0xFFFFFF00LL &&
