@@ -17,6 +17,7 @@
 #ifndef VCG_HIP_H
 #define VCG_HIP_H
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -67,6 +68,11 @@ VCG_API int vcg_avgpool_fwd(int dtype, const void* x, float* y, int N, int HW, i
 VCG_API int vcg_avgpool_bwd(int dtype, const float* dy, void* dx, int N, int HW, int C, hipStream_t s);
 /* rearrange 'b t c h w -> (b t) c h w' (two_stream.py:183) + NCHW->NHWC staging */
 VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cpad, hipStream_t s);
+/* Frame ingest (§8f rank 2): u8 RGB frames [F][H][W][3] gathered by a window frame table idx[n_rows] (int64,
+   0-based; youtube_dataset.py:180-190 offsets applied by the caller, see data/clip_windows.py:frame_index_table) and
+   normalised like ToTensor+Normalize (train_video_segment_point.py:383-386) into NHWC [n_rows][H][W][8]. mean3/std3
+   are HOST pointers to 3 floats. */
+VCG_API int vcg_window_frames_u8(int dtype, const uint8_t* frames, const long long* idx, void* dst, long long n_rows, int F, int H, int W, const float* mean3, const float* std3, hipStream_t s);
 VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int KH, int KW, int Cpad, int transposed, hipStream_t s);
 VCG_API int vcg_cast_from_f32(int dtype, const float* in, void* out, long long n, hipStream_t s);
 VCG_API int vcg_cast_to_f32(int dtype, const void* in, float* out, long long n, hipStream_t s);

@@ -266,3 +266,22 @@ def test_avgpool(K):
     x = torch.randn(4, 49, 256)
     y = K.avgpool_fwd(x.to(DEV), 4, 49, 256)
     _close(y, x.double().mean(1), torch.float32, "avgpool")
+
+
+def test_window_frames_u8_bitexact(K):
+    """Frame ingest: u8 frames gathered by the window frame table (data/clip_windows.py) and
+    normalised like ToTensor + Normalize in fp32 — bit-exact in fp32, one rounding in bf16."""
+    from data import clip_windows as cw
+    g = torch.Generator().manual_seed(31)
+    F_, H, W, T = 40, 12, 10, 16
+    frames = torch.randint(0, 256, (F_, H, W, 3), generator=g, dtype=torch.uint8)
+    win = cw.clip_windows(F_, T)
+    idx = torch.from_numpy(cw.frame_index_table(win, F_))
+    mean = torch.tensor(K.IMAGENET_MEAN, dtype=torch.float32)
+    std = torch.tensor(K.IMAGENET_STD, dtype=torch.float32)
+    ref = (frames[idx.reshape(-1)].float() / 255.0 - mean) / std          # [n,H,W,3] fp32
+    for dt in (torch.float32, torch.bfloat16):
+        y = K.window_frames_u8(frames.to(DEV), idx.to(DEV), dt).cpu()
+        assert y.shape == (idx.numel(), H, W, 8)
+        assert torch.equal(y[..., 3:], torch.zeros_like(y[..., 3:]))
+        assert torch.equal(y[..., :3], ref.to(dt)), dt

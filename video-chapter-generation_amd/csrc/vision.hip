@@ -113,6 +113,42 @@ __global__ void frames_to_nhwc_kernel(const float* __restrict__ src, T* __restri
   }
 }
 
+// Frame ingest: decoded u8 RGB frames of one video [F][H][W][3] -> the stem's
+// NHWC input [n_rows][H][W][8] (channels 3..7 zero) for the window frame table idx[n_rows]
+// (window-major, frame-minor: row = w*T + t), normalised as torchvision ToTensor + Normalize
+// (`train_video_segment_point.py:383-386`): (u / 255 - mean_c) / std_c in fp32 with IEEE division.
+template <typename T>
+__global__ void window_frames_u8_kernel(const uint8_t* __restrict__ frames, const long long* __restrict__ idx,
+                                        T* __restrict__ dst, long long n_rows, int F, int HW, float m0, float m1,
+                                        float m2, float s0, float s1, float s2) {
+  const long long total = n_rows * HW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / HW;
+    const long long px = i - row * HW;
+    const long long f = idx[row];
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (f >= 0 && f < F) {
+      const uint8_t* q = frames + (f * HW + px) * 3;
+      v[0] = ((float)q[0] / 255.f - m0) / s0;
+      v[1] = ((float)q[1] / 255.f - m1) / s1;
+      v[2] = ((float)q[2] / 255.f - m2) / s2;
+    }
+    T* d = dst + i * 8;
+    if constexpr (sizeof(T) == 2) {
+      uint4 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]);
+      o.z = 0u;
+      o.w = 0u;
+      *reinterpret_cast<uint4*>(d) = o;
+    } else {
+      *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], 0.f);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
 // OIHW fp32 -> [Cout][KH][KW][Cpad] (transposed = 0) or [Cin][KH][KW][Cout] (transposed = 1)
 template <typename T>
 __global__ void weight_prep_kernel(const float* __restrict__ w, T* __restrict__ out, int Cout, int Cin, int KH, int KW,
@@ -235,6 +271,22 @@ VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, in
   else
     hipLaunchKernelGGL(frames_to_nhwc_kernel<float>, dim3(grid_for(tot)), dim3(256), 0, s, src, (float*)dst, N, C, H,
                        W, Cpad);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_window_frames_u8(int dtype, const uint8_t* frames, const long long* idx, void* dst, long long n_rows,
+                                 int F, int H, int W, const float* mean3, const float* std3, hipStream_t s) {
+  VCG_REQUIRE(mean3 && std3, "mean/std required");
+  VCG_REQUIRE(n_rows >= 0 && F > 0 && H > 0 && W > 0, "bad shape");
+  const long long tot = n_rows * H * W;
+  if (tot == 0) return VCG_OK;
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(window_frames_u8_kernel<bf16_t>, dim3(grid_for(tot)), dim3(256), 0, s, frames, idx,
+                       (bf16_t*)dst, n_rows, F, H * W, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2]);
+  else
+    hipLaunchKernelGGL(window_frames_u8_kernel<float>, dim3(grid_for(tot)), dim3(256), 0, s, frames, idx, (float*)dst,
+                       n_rows, F, H * W, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2]);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

@@ -1,0 +1,135 @@
+"""Data-parallel training of the clip scorer: one process per GPU, RCCL all-reduce over xGMI.
+
+This replaces the reference's `train_video_segment_ddp.py`. The reference wraps the model in
+`DDP(model)` with NCCL and 25 MB buckets, all-reducing on every backward (`:131-148`); it draws
+data with a DistributedSampler (`:210-243`), broadcasts the rank-0 parameters (`:261-263`) and
+averages the validation metric with `all_gather_object` (`:276-281`). Here:
+- `vcg_hip.ddp.GradAllReducer` reduces the flat fp32 gradient buffer in 64 MB contiguous
+  buckets. Each bucket is sent as an async RCCL all_reduce(SUM) as soon as the native backward
+  reports its parameters final, so the exchange overlaps the rest of the backward.
+- The 1/world average is folded into the fused AdamW (`grad_scale`).
+- Gradient accumulation reduces only on the last micro-step (`reducer.enabled`). The sum of the
+  micro-step gradients is linear, so the result equals DDP's reduce-every-backward.
+- Parameters start identical through one broadcast of the flat parameter buffer.
+
+Launch: `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 train_video_segment_ddp.py`.
+"""
+import argparse
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+from train_video_segment_point import TrainerConfig, lr_multiplier  # noqa: E402
+
+
+class DDPTrainer:
+    def __init__(self, model, train_dataset, test_dataset, config, rank, world_size, device):
+        from vcg_hip.ddp import GradAllReducer, broadcast_parameters
+        self.model, self.train_dataset, self.test_dataset = model, train_dataset, test_dataset
+        self.config, self.rank, self.world, self.device = config, rank, world_size, device
+        self.optimizer = model.configure_optimizers(config)
+        self.optimizer.grad_scale = 1.0 / world_size
+        broadcast_parameters(model)
+        self.reducer = GradAllReducer(model.native_flat())
+        model.set_grad_hooks(self.reducer)
+        self.history = []
+
+    def run_epoch(self, split, epoch):
+        from vcg_hip.ddp import all_gather_object
+        from vcg_hip.functions import cross_entropy
+        from eval_utils.video_metrics import trainer_video_auc_map
+        is_train = split == "train"
+        ds = self.train_dataset if is_train else self.test_dataset
+        self.model.train(is_train)
+        sampler = torch.utils.data.distributed.DistributedSampler(ds, num_replicas=self.world, rank=self.rank,
+                                                                  shuffle=is_train)
+        sampler.set_epoch(epoch)
+        bs = self.config.batch_size if is_train else self.config.val_batch_size
+        loader = torch.utils.data.DataLoader(ds, batch_size=bs, sampler=sampler, num_workers=self.config.num_workers)
+        accum = self.config.gradient_accumulation_steps
+        scored = []
+        order = list(sampler)
+        for it, (img, ids, mask, label) in enumerate(loader):
+            img, ids, mask, label = (img.float().to(self.device), ids.to(self.device), mask.to(self.device),
+                                     label.to(self.device))
+            last_micro = (it + 1) % accum == 0
+            self.reducer.enabled = is_train and self.world > 1 and last_micro
+            with torch.set_grad_enabled(is_train):
+                logits, prob = self.model(img, ids, mask)
+                loss = cross_entropy(logits, label)
+            if not is_train:
+                idx = order[it * bs:it * bs + len(label)]
+                for k, s in zip(idx, prob[:, 1].float().cpu().tolist()):
+                    scored.append((k, s))
+                continue
+            (loss / accum).backward()
+            if last_micro:
+                self.reducer.finish()
+                self.optimizer.clip_and_step(self.config.grad_norm_clip)
+                self.model.zero_grad()
+                if self.config.lr_decay:
+                    for g in self.optimizer.param_groups:
+                        g["lr"] = self.config.learning_rate * lr_multiplier(self.config, epoch)
+                self.history.append({"epoch": epoch, "it": it, "loss": loss.item()})
+        self.reducer.enabled = self.world > 1
+        if is_train:
+            return None
+        for part in all_gather_object(scored):  # every rank gets every clip's score (clip order restored)
+            for k, s in part:
+                ds.all_clip_infos[k]["pred_score"] = s
+        return trainer_video_auc_map(ds.all_clip_infos)[1]
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description="video chapter model, data parallel (MI355X, RCCL)")
+    p.add_argument("--epoch", default=2, type=int)
+    p.add_argument("--batch_size", default=4, type=int)
+    p.add_argument("--clip_frame_num", default=16, type=int)
+    p.add_argument("--max_text_len", default=100, type=int)
+    p.add_argument("--resolution", default=224, type=int)
+    p.add_argument("--videos", default=16, type=int)
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--seed", default=123, type=int)
+    args = p.parse_args(argv)
+
+    from common_utils import set_random_seed
+    from data.synthetic_dataset import HashTokenizer, InferYoutubeClipDataset, SyntheticVideoCorpus, YoutubeClipDataset
+    from vcg_hip.build import build_two_stream
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    set_random_seed.use_fix_random_seed(args.seed + rank)
+    tok = HashTokenizer()
+    train_ds = YoutubeClipDataset(SyntheticVideoCorpus(args.videos, H=args.resolution, W=args.resolution, seed=args.seed),
+                                  tok, args.clip_frame_num, args.max_text_len)
+    test_ds = InferYoutubeClipDataset(SyntheticVideoCorpus(2, H=args.resolution, W=args.resolution, seed=args.seed + 1),
+                                      tok, args.clip_frame_num, args.max_text_len)
+    model = build_two_stream(clip_frame_num=args.clip_frame_num, seed=args.seed, device=device, precision=args.precision)
+    conf = TrainerConfig(max_epochs=args.epoch, batch_size=args.batch_size, val_batch_size=args.batch_size * 8,
+                         gradient_accumulation_steps=4, num_workers=0, lr_decay=True,
+                         warmup_epochs=args.epoch // 100, final_epochs=args.epoch // 100 * 90)
+    tr = DDPTrainer(model, train_ds, test_ds, conf, rank, world, device)
+    result = None
+    for epoch in range(1, args.epoch + 1):
+        tr.run_epoch("train", epoch)
+        result = tr.run_epoch("infer_test", epoch)
+        if rank == 0:
+            print(f"epoch {epoch}: val m_ap {result}")
+    if world > 1:
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -38,3 +38,37 @@ def build_two_stream(clip_frame_num=16, hidden_size=128, head_type="mlp", dropou
         synth.load_bn_stats(model, bn_stats)
     model.precision = precision
     return model
+
+
+def build_model(data_mode="all", clip_frame_num=16, hidden_size=128, head_type="mlp", model_type="r50tsm", seed=None,
+                device=None, precision="bf16", dropout=None):
+    """The driver's model by `--data_mode` (`train_video_segment_point.py:330-363`): "text" ->
+    BertHugface + head, "image" -> Resnet50TSM (or Resnet50) + head, "all" -> TwoStream."""
+    if data_mode == "all":
+        return build_two_stream(clip_frame_num, hidden_size, head_type, dropout, seed, device, precision)
+    if data_mode == "text":
+        from model.lang.bert_hugface import BertHugface
+        from vcg_hip.nn import BertConfig
+        cfg = BertConfig(output_attentions=True)
+        if dropout is not None:
+            cfg.hidden_dropout_prob = cfg.attention_probs_dropout_prob = dropout
+        with contextlib.redirect_stdout(io.StringIO()):
+            model = BertHugface(pretrain_stage=False, config=cfg)
+    elif data_mode == "image":
+        if model_type == "r50tsm":
+            from model.vision.resnet50_tsm import Resnet50TSM
+            model = Resnet50TSM(segments_size=clip_frame_num, shift_div=8, pretrain_stage=False)
+        elif model_type == "r50":
+            from model.vision.resnet50 import Resnet50
+            model = Resnet50(segments_size=clip_frame_num, pretrain_stage=False)
+        else:
+            raise RuntimeError(f"Unknown model_type {model_type}")
+    else:
+        raise RuntimeError(f"Unknown data mode {data_mode}")
+    model.build_chapter_head()
+    if device is not None:
+        model = model.to(device)
+    if seed is not None:
+        synth.init_params(model, seed)
+    model.precision = precision
+    return model

@@ -193,6 +193,29 @@ def avgpool_bwd(dy, N, HW, C, dtype):
     return dx
 
 
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def window_frames_u8(frames, idx, dtype, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+    """u8 RGB frames [F,H,W,3] gathered by an int64 frame table `idx` (any shape, 0-based) ->
+    normalised NHWC stem input [idx.numel(),H,W,8] (channels 3..7 zero)."""
+    import ctypes
+
+    _chk(frames, torch.uint8, "frames")
+    _chk(idx, torch.int64, "idx")
+    F, H, W, C = frames.shape
+    if C != 3:
+        raise ValueError("frames must be [F,H,W,3] RGB")
+    n = idx.numel()
+    dst = torch.empty((n, H, W, 8), dtype=dtype, device=frames.device)
+    m = (ctypes.c_float * 3)(*mean)
+    sd = (ctypes.c_float * 3)(*std)
+    _lib.call("vcg_window_frames_u8", dt_code(dtype), P(frames), P(idx), P(dst), n, F, H, W,
+              ctypes.addressof(m), ctypes.addressof(sd), stream())
+    return dst
+
+
 def frames_to_nhwc(src, N, C, H, W, Cpad, dtype):
     _chk(src, torch.float32, "frames")
     dst = torch.empty((N, H, W, Cpad), dtype=dtype, device=src.device)
