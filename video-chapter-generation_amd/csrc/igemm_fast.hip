@@ -106,16 +106,14 @@ template <int ROWS, int MODE> struct FastLoader {
   }
 };
 
-// 16x16x32 bf16 fragment of rows r0..r0+15, k-step s2 (0/1) of a swizzled [rows][64] tile.
-// Element j of lane 16g+i is k = 32*s2 + 4g + 16*(j>>2) + (j&3) (same map on both operands).
+// 16x16x32 bf16 fragment of rows r0..r0+15, k-step s2 (0/1) of a swizzled [rows][64] tile: ONE
+// ds_read_b128 per lane. Element j of lane 16g+i is k = 32*s2 + 8g + j (same map on both operands).
+// A 16-lane group reads chunk 4*s2+g of 16 consecutive rows: with the (row>>1)&7 swizzle these are
+// 16 distinct 16-B slots of the 256-B bank row (conflict-free).
 __device__ __forceinline__ s16x8 fast_frag(const bf16_t* lds, int r0, int lane, int s2) {
   const int g = lane >> 4, i = lane & 15;
   const int row = r0 + i;
-  const int c1 = 4 * s2 + (g >> 1);
-  const bf16_t* rp = lds + row * 64 + 4 * (g & 1);
-  const s16x4 lo = *reinterpret_cast<const s16x4*>(rp + 8 * fswz(row, c1));
-  const s16x4 hi = *reinterpret_cast<const s16x4*>(rp + 8 * fswz(row, c1 + 2));
-  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return *reinterpret_cast<const s16x8*>(lds + row * 64 + 8 * fswz(row, 4 * s2 + g));
 }
 
 __device__ __forceinline__ constexpr int waitcnt_vm(int n) {

@@ -15,7 +15,7 @@ namespace {
 template <typename T> struct V { static constexpr int N = 16 / sizeof(T); };
 
 constexpr int EW_ITER = 8;
-constexpr int RED_ITER = 256;
+constexpr int RED_ITER_MAX = 256;  // vectors per thread of bn_bwd_reduce (adaptive: >= ~1024 blocks)
 
 template <int VN>
 __device__ __forceinline__ void load_params(const float* __restrict__ p, int c0, float (&out)[VN]) {
@@ -93,12 +93,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ mask,
                                                             const T* __restrict__ y, const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long long TV, int cpr,
-                                                            int C, float* __restrict__ partial) {
+                                                            int C, int red_iter, float* __restrict__ partial) {
   constexpr int VN = V<T>::N;
   __shared__ float red[2 * 2048];
   for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.f;
   __syncthreads();
-  const long long base = (long long)blockIdx.x * (256 * RED_ITER) + threadIdx.x;
+  const long long base = (long long)blockIdx.x * (256LL * red_iter) + threadIdx.x;
   if (cpr <= 256) {
     const int c0 = (int)(base & (cpr - 1)) * VN;
     float mu[VN], is[VN], sg[VN], sx[VN];
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
 #pragma unroll
     for (int e = 0; e < VN; ++e) { sg[e] = 0.f; sx[e] = 0.f; }
 #pragma unroll 4
-    for (int it = 0; it < RED_ITER; ++it) {
+    for (int it = 0; it < red_iter; ++it) {
       const long long v = base + it * 256;
       if (v >= TV) break;
       float d[VN], yv[VN];
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
       atomicAdd(&red[C + c0 + e], sx[e]);
     }
   } else {
-    for (int it = 0; it < RED_ITER; ++it) {
+    for (int it = 0; it < red_iter; ++it) {
       const long long v = base + it * 256;
       if (v >= TV) break;
       const int c0 = (int)(v & (cpr - 1)) * VN;
@@ -156,27 +156,36 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   for (int i = threadIdx.x; i < 2 * C; i += 256) partial[(long long)blockIdx.x * 2 * C + i] = red[i];
 }
 
-// Column sums of partial[nb][2C] -> sum_g, sum_gx (+ dgamma/dbeta): 64 channels x 4 row-stripes per block,
-// coalesced across channels, fixed summation order (deterministic).
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nb, int C,
-                                                              float* sum_g, float* sum_gx, float* dgamma,
-                                                              float* dbeta, int accumulate) {
-  __shared__ double sa[4][64], sb[4][64];
+// Column sums of partial[nb][2C] -> sum_g, sum_gx (+ dgamma/dbeta): 64 channels x 16 row-stripes per
+// block (1024 threads), loads coalesced across channels and unrolled across rows; fixed summation
+// order (deterministic).
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nb, int C,
+                                                               float* sum_g, float* sum_gx, float* dgamma,
+                                                               float* dbeta, int accumulate) {
+  __shared__ double sa[16][64], sb[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   double a = 0, b = 0;
   if (c < C) {
-    for (int i = ty; i < nb; i += 4) {
-      a += partial[(long long)i * 2 * C + c];
-      b += partial[(long long)i * 2 * C + C + c];
+    const float* p = partial + c;
+    const long long ld = 2LL * C;
+#pragma unroll 4
+    for (int i = ty; i < nb; i += 16) {
+      a += p[i * ld];
+      b += p[i * ld + C];
     }
   }
   sa[ty][tx] = a;
   sb[ty][tx] = b;
   __syncthreads();
   if (ty == 0 && c < C) {
-    a = sa[0][tx] + sa[1][tx] + sa[2][tx] + sa[3][tx];
-    b = sb[0][tx] + sb[1][tx] + sb[2][tx] + sb[3][tx];
+    a = 0;
+    b = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      a += sa[k][tx];
+      b += sb[k][tx];
+    }
     sum_g[c] = (float)a;
     sum_gx[c] = (float)b;
     if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)a;
@@ -385,14 +394,25 @@ VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const flo
   return VCG_OK;
 }
 
+// vectors per thread: enough blocks to fill the chip (~1024) but at most RED_ITER_MAX per thread
+// (the per-block partials then stay small next to the streamed tensors)
+static int bn_bwd_iter(long long P, int C, int VN) {
+  const long long TV = P * C / VN;
+  long long it = (TV + 256LL * 1024 - 1) / (256LL * 1024);
+  if (it < 4) it = 4;
+  if (it > RED_ITER_MAX) it = RED_ITER_MAX;
+  return (int)it;
+}
 static long long bn_bwd_blocks(long long P, int C, int VN) {
   const long long TV = P * C / VN;
-  return (TV + 256 * RED_ITER - 1) / (256 * RED_ITER);
+  const long long per = 256LL * bn_bwd_iter(P, C, VN);
+  return (TV + per - 1) / per;
 }
 
 VCG_API long long vcg_bn_bwd_ws_bytes(long long P, int C) {
-  // sized for the smaller vector width (fp32) so one query serves both dtypes
-  return bn_bwd_blocks(P, C, 4) * 2 * C * 4 + 64;
+  // one query serves both dtypes (vector width 4 for fp32, 8 for bf16)
+  const long long nb = bn_bwd_blocks(P, C, 4) > bn_bwd_blocks(P, C, 8) ? bn_bwd_blocks(P, C, 4) : bn_bwd_blocks(P, C, 8);
+  return nb * 2 * C * 4 + 64;
 }
 
 VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
@@ -404,14 +424,15 @@ VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, const void* mask, con
   const long long TV = P * C / VN;
   const int cpr = C / VN;
   const long long nb = bn_bwd_blocks(P, C, VN);
+  const int it = bn_bwd_iter(P, C, VN);
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, dim3((unsigned)nb), dim3(256), 0, s, (const bf16_t*)dout,
-                       (const bf16_t*)mask, (const bf16_t*)y, mean, invstd, TV, cpr, C, ws);
+                       (const bf16_t*)mask, (const bf16_t*)y, mean, invstd, TV, cpr, C, it, ws);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, (const float*)dout,
-                       (const float*)mask, (const float*)y, mean, invstd, TV, cpr, C, ws);
+                       (const float*)mask, (const float*)y, mean, invstd, TV, cpr, C, it, ws);
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, ws, (int)nb, C, sum_g, sum_gx,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, sum_g, sum_gx,
                      dgamma, dbeta, accumulate);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
