@@ -25,7 +25,8 @@ template <int ROWS, int MODE> struct FastLoader {
   static constexpr int PER_WAVE = ROWS / 32;  // 1-KiB (8-row) slices per wave per tile
   __amdgpu_buffer_rsrc_t rsrc;
   uint32_t oob;
-  long long off[PER_WAVE];  // element offset of the row's base (-1 = invalid row)
+  // element offsets fit in 31 bits: the dispatcher routes only tensors < 4 GB here (32-bit buffer range)
+  int off[PER_WAVE];  // element offset of the row's base (-1 = invalid row)
   int ra[PER_WAVE], rb[PER_WAVE], rc[PER_WAVE], kc[PER_WAVE];
 
   __device__ __forceinline__ void init(const OpArgs& a, long long batch_off, int row0, int wave, int lane) {
@@ -39,13 +40,13 @@ template <int ROWS, int MODE> struct FastLoader {
       const int gr = row0 + r;
       const bool valid = gr < a.rows;
       if constexpr (MODE == OP_DENSE_K) {
-        off[q] = valid ? batch_off + (long long)gr * a.ld : -1;
+        off[q] = valid ? (int)(batch_off + (long long)gr * a.ld) : -1;
       } else {
         const int n = gr / (a.GH * a.GW);
         const int rem = gr - n * a.GH * a.GW;
         const int y = rem / a.GW;
         const int x = rem - y * a.GW;
-        off[q] = valid ? (long long)n * a.H * a.W * a.C : -1;
+        off[q] = valid ? n * a.H * a.W * a.C : -1;
         if constexpr (MODE == OP_IM2COL) {
           ra[q] = y * a.stride - a.pad;
           rb[q] = x * a.stride - a.pad;
@@ -59,47 +60,65 @@ template <int ROWS, int MODE> struct FastLoader {
     }
   }
 
+  // offset of gathered element (row q, channel c) at tap (kh, kw); -1 if it is padding
+  __device__ __forceinline__ int gather(const OpArgs& a, int q, int kh, int kw, int c) const {
+    if constexpr (MODE == OP_IM2COL) {
+      const int ih = ra[q] + kh, iw = rb[q] + kw;
+      if (off[q] < 0 || ih < 0 || ih >= a.H || iw < 0 || iw >= a.W) return -1;
+      int o = off[q] + ((ih * a.W + iw) << a.logC) + c;
+      if (a.tsm_fold > 0) {
+        const int dt = c < a.tsm_fold ? 1 : (c < 2 * a.tsm_fold ? -1 : 0);
+        const int t2 = rc[q] + dt;
+        if (t2 < 0 || t2 >= a.tsm_T) return -1;
+        o += dt * a.H * a.W * a.C;
+      }
+      return o;
+    } else {  // OP_DGRAD: transposed gather of dy
+      int yy = ra[q] - kh, xx = rb[q] - kw;
+      bool ok = off[q] >= 0 && yy >= 0 && xx >= 0;
+      if (a.stride == 2) {
+        ok = ok && ((yy | xx) & 1) == 0;
+        yy >>= 1;
+        xx >>= 1;
+      }
+      ok = ok && yy < a.H && xx < a.W;
+      return ok ? off[q] + ((yy * a.W + xx) << a.logC) + c : -1;
+    }
+  }
+
   // issue the LDS-DMA loads of one 64-wide k tile into `lds` (tile base, [ROWS][64] bf16)
   __device__ __forceinline__ void issue(const OpArgs& a, int k0, int kend, bf16_t* lds, int wave) {
+    if constexpr (MODE != OP_DENSE_K) {
+      if (a.C >= FBK) {
+        // the whole k tile lies in one filter tap: tap / kh / kw are wave-uniform (scalar unit)
+        const int tap = k0 >> a.logC;
+        const int kh = tap / a.KW;
+        const int kw = tap - kh * a.KW;
+        const int cb = k0 & (a.C - 1);
+        const bool tap_ok = k0 < kend && kh < a.KH;
+#pragma unroll
+        for (int q = 0; q < PER_WAVE; ++q) {
+          const int e = tap_ok ? gather(a, q, kh, kw, cb + kc[q]) : -1;
+          const uint32_t voff = e >= 0 ? (uint32_t)e * 2u : oob;
+          bf16_t* slice = lds + (wave * PER_WAVE + q) * 512;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)slice, 16, voff, 0, 0, 0);
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < PER_WAVE; ++q) {
       const int k = k0 + kc[q];
-      long long e = -1;
+      int e = -1;
       if constexpr (MODE == OP_DENSE_K) {
         if (off[q] >= 0 && k < kend) e = off[q] + k;
-      } else if constexpr (MODE == OP_IM2COL) {
+      } else {
         const int tap = k >> a.logC;
-        const int c = k & (a.C - 1);
         const int kh = tap / a.KW;
         const int kw = tap - kh * a.KW;
-        const int ih = ra[q] + kh, iw = rb[q] + kw;
-        if (off[q] >= 0 && k < kend && kh < a.KH && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
-          long long o = off[q] + ((long long)(ih * a.W + iw) << a.logC) + c;
-          bool ok = true;
-          if (a.tsm_fold > 0) {
-            const int dt = c < a.tsm_fold ? 1 : (c < 2 * a.tsm_fold ? -1 : 0);
-            const int t2 = rc[q] + dt;
-            ok = t2 >= 0 && t2 < a.tsm_T;
-            o += (long long)dt * a.H * a.W * a.C;
-          }
-          if (ok) e = o;
-        }
-      } else {  // OP_DGRAD
-        const int tap = k >> a.logC;
-        const int c = k & (a.C - 1);
-        const int kh = tap / a.KW;
-        const int kw = tap - kh * a.KW;
-        int yy = ra[q] - kh, xx = rb[q] - kw;
-        bool ok = off[q] >= 0 && k < kend && kh < a.KH && yy >= 0 && xx >= 0;
-        if (a.stride == 2) {
-          ok = ok && ((yy | xx) & 1) == 0;
-          yy >>= 1;
-          xx >>= 1;
-        }
-        ok = ok && yy < a.H && xx < a.W;
-        if (ok) e = off[q] + (((long long)(yy * a.W + xx)) << a.logC) + c;
+        if (k < kend && kh < a.KH) e = gather(a, q, kh, kw, k & (a.C - 1));
       }
-      const uint32_t voff = e >= 0 ? (uint32_t)(e * 2) : oob;
+      const uint32_t voff = e >= 0 ? (uint32_t)e * 2u : oob;
       bf16_t* slice = lds + (wave * PER_WAVE + q) * 512;  // 1 KiB per slice
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)slice, 16, voff, 0, 0, 0);
     }
