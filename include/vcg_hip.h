@@ -37,7 +37,9 @@ VCG_API int vcg_sync(hipStream_t stream);
 /* ---- MFMA implicit-GEMM engine (igemm.hip) ---------------------------------------------- */
 /* torchvision conv2d inside Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15,68-77), with
  * TemporalShift.shift (ops/temporal_shift.py:33-51, inserted by make_temporal_shift :133-144)
- * fused into the input gather; optional BatchNorm partial statistics from the epilogue. */
+ * fused into the input gather; optional BatchNorm partial statistics from the epilogue.
+ * stats (optional): float2 [Cout + 1][vcg_conv_stats_tiles(M)] — per column and slot (mean, M2) of
+ * the slot's rows, then the count row (rows per slot, 0 = unused slot); merged by vcg_bn_finalize. */
 VCG_API int vcg_conv_stats_tiles(int M);
 VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
 /* autograd of conv2d: input gradient (transposed-conv gather) */

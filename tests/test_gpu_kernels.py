@@ -96,7 +96,7 @@ def test_conv_fwd_and_stats(K, dtype, case):
     OH, OW = ref.shape[2], ref.shape[3]
     M = N * OH * OW
     mt = K.stats_tiles(M)
-    stats = torch.empty((Cout, mt, 2), dtype=torch.float32, device=DEV)
+    stats = K.stats_buffer(Cout, M, DEV)
     y = K.conv_fwd(xs, wd, N, H, W, cpad, Cout, KH, KH, s, p, T, fold, stats=stats)
     _close(y.permute(0, 3, 1, 2), ref, dtype, "conv fwd")
     # BN statistics of the stored output
@@ -116,6 +116,33 @@ def test_conv_fwd_and_stats(K, dtype, case):
     assert torch.allclose(mean.double().cpu(), mu, atol=1e-5 * (1 + mu.abs().max().item()))
     assert torch.allclose(invstd.double().cpu(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4)
     assert torch.allclose(rv.double().cpu(), 0.9 + 0.1 * yref.var(0, unbiased=True), rtol=1e-4)
+
+
+@pytest.mark.parametrize("case", [(16, 56, 56, 64, 256, 1, 1, 0, 0, 2.0), (8, 28, 28, 128, 128, 3, 1, 1, 0, 0.0),
+                                  (8, 29, 27, 64, 64, 3, 1, 1, 4, 3.0)])
+def test_conv_stats_multitile(K, case):
+    """BN statistics when persistent workgroups walk several M-tiles (one stats slot per workgroup
+    row, count row), M not a multiple of 128, and outputs with |mean| >> std (shifted sums)."""
+    N, H, W, Cin, Cout, KH, s, p, T, off = case
+    dtype = torch.bfloat16
+    x = (_rand((N, Cin, H, W), dtype, 5).double() + off).to(dtype).double()
+    w = (_rand((Cout, Cin, KH, KH), torch.float32, 6, 0.05) + 0.02).to(dtype)
+    fold = Cin // 8 if T else 0
+    xs, cpad = _prep(K, x, w, dtype, T, fold)
+    wd = K.weight_prep(w.float().to(DEV), cpad, dtype)
+    OH, OW = K.conv_out_hw(H, W, KH, KH, s, p)
+    M = N * OH * OW
+    stats = K.stats_buffer(Cout, M, DEV)
+    y = K.conv_fwd(xs, wd, N, H, W, cpad, Cout, KH, KH, s, p, T, fold, stats=stats)
+    z = torch.empty(Cout, device=DEV)
+    mean, invstd, scale, shift = (torch.empty_like(z) for _ in range(4))
+    K.bn_finalize(stats, K.stats_tiles(M), M, Cout, None, None, mean, invstd, scale, shift, None, None, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    yref = y.double().cpu().reshape(M, Cout)
+    mu, var = yref.mean(0), yref.var(0, unbiased=False)
+    assert float(stats[Cout, :, 0].sum()) == M                      # slot row counts cover every row
+    assert torch.allclose(mean.double().cpu(), mu, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(invstd.double().cpu(), 1 / torch.sqrt(var + 1e-5), rtol=2e-4)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -149,6 +176,30 @@ def test_conv_wgrad(K, dtype, case):
     dw = torch.full((Cout, Cin, KH, KH), 0.5, dtype=torch.float32, device=DEV)  # accumulate onto 0.5
     K.conv_wgrad(xs, dys, dw, N, H, W, cpad, Cin, Cout, KH, KH, s, p, T, fold, accumulate=True)
     _close(dw - 0.5, ref, dtype, "conv wgrad")
+
+
+@pytest.mark.parametrize("case", [(16, 28, 28, 64, 64, 3, 1, 1, 4), (8, 30, 30, 64, 256, 1, 2, 0, 0),
+                                  (4, 64, 64, 3, 64, 7, 2, 3, 0), (4, 14, 14, 256, 128, 3, 2, 1, 0),
+                                  (8, 20, 20, 512, 192, 1, 1, 0, 8)])
+def test_conv_wgrad_split(K, case):
+    """bf16 weight gradient over many pixels: split-K slabs, M = 64 / N = 64 tiles, partial N tiles
+    (stem: N = 7*7*8 = 392), stride 2, TSM-shifted gather."""
+    dtype = torch.bfloat16
+    N, H, W, Cin, Cout, KH, s, p, T = case
+    x = _rand((N, Cin, H, W), dtype, 16).double()
+    fold = Cin // 8 if T else 0
+    w = _rand((Cout, Cin, KH, KH), torch.float32, 17, 0.1).double().requires_grad_()
+    xin = tsm_ref(x, T, fold) if T else x
+    y = F.conv2d(xin, w, stride=s, padding=p)
+    dy = _rand(y.shape, dtype, 18).double()
+    (ref,) = torch.autograd.grad(y, w, dy)
+    xs, cpad = _prep(K, x, None, dtype, T, fold)
+    dys = dy.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV)
+    dw = torch.zeros((Cout, Cin, KH, KH), dtype=torch.float32, device=DEV)
+    K.conv_wgrad(xs, dys, dw, N, H, W, cpad, Cin, Cout, KH, KH, s, p, T, fold, accumulate=False)
+    # inputs are exact bf16 values, accumulation fp32: only summation-order error
+    err = (dw.double().cpu() - ref).abs().max().item()
+    assert err <= 1e-4 * ref.abs().max().item() + 1e-6, f"max err {err}"
 
 
 @pytest.mark.parametrize("dtype", DTYPES)

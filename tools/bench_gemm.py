@@ -47,7 +47,7 @@ def main():
         w = torch.randn(Co, k, k, C, device=dev).to(dt) * 0.05
         OH, OW = ops.conv_out_hw(H, W, k, k, s, p)
         M = N * OH * OW
-        stats = torch.empty((Co, ops.stats_tiles(M), 2), device=dev) if st else None
+        stats = ops.stats_buffer(Co, M, dev) if st else None
         y = torch.empty((N, OH, OW, Co), dtype=dt, device=dev)
         fold = C // 8 if tsm else 0
         us = timeit(lambda: ops.conv_fwd(x, w, N, H, W, C, Co, k, k, s, p, tsm, fold, stats=stats, out=y))

@@ -130,7 +130,8 @@ __device__ __forceinline__ void ep_barrier() {
 // m = m0 + wm*(BM/2) + i*16 + (lane&15), n = n0 + wn*(BN/2) + j*16 + 4*(lane>>4) + r.
 // bv[j][r] is the bias of column nbase + j*16 + r (zeros when there is none; see load_bias).
 // EPI_STATS: `red` holds 4*BN floats that no other wave touches until the caller's next barrier;
-// the per-column (mean, M2) of this tile goes to stats[col][mtile] (float2, mtiles per column).
+// the per-column (mean, M2) of this tile goes to stats[col][mtile] (float2, mtiles per column) and
+// the tile's row count to the count row stats[N][mtile].
 // Each wave reduces its 64 rows in registers (two passes, DPP row sums), the two row-halves are
 // merged with Chan's formula after one barrier, and only then are the values stored, so the
 // barrier never waits on outstanding HBM writes.
@@ -224,6 +225,9 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
           reinterpret_cast<float2*>(p.stats)[(long long)col * mtiles + mtile] = make_float2(mean, m2);
         }
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0)  // count row: stats[N][mtile] = (rows of this tile, 0)
+      reinterpret_cast<float2*>(p.stats)[(long long)p.N * mtiles + mtile] =
+          make_float2((float)min(BM, p.M - m0), 0.f);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int n = nbase + j * 16;
@@ -239,5 +243,8 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
 }
 
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
+int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s);
+int wgrad_fast_tile_m(int M);
+int wgrad_fast_tile_n(int N);
 
 }  // namespace vcg

@@ -533,20 +533,44 @@ VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
                : run_gemm<float, OP_DGRAD, OP_DENSE_K>(p, EPI_STORE, 1, stream);
 }
 
+// The bf16 LDS-DMA wgrad kernel (igemm_wgrad.hip) takes x / dy below 4 GB (32-bit buffer range)
+// and C >= 8 (a 16-B chunk of x never straddles two filter taps).
+static bool wgrad_fast_ok(int dtype, int N, int H, int W, int C, int Cout, int K) {
+  return dtype == VCG_BF16 && fast_gemm_enabled() && C >= 8 && (long long)N * H * W * C * 2 < 0xFFFFFF00LL &&
+         (long long)K * Cout * 2 < 0xFFFFFF00LL;
+}
+
 static void wgrad_geometry(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad,
-                           int* M, int* Nn, int* K, int* splits) {
+                           int* M, int* Nn, int* K, int* splits, int* kps, bool* fast) {
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   *M = Cout;
   *Nn = KH * KW * C;
   *K = N * OH * OW;
-  const int BK = dtype == VCG_BF16 ? 32 : 16;
-  *splits = choose_splits(*M, *Nn, *K, BK);
+  *fast = wgrad_fast_ok(dtype, N, H, W, C, Cout, *K);
+  int BK, sp;
+  if (*fast) {
+    BK = 64;
+    const int tiles = ((*Nn + wgrad_fast_tile_n(*Nn) - 1) / wgrad_fast_tile_n(*Nn)) *
+                      ((*M + wgrad_fast_tile_m(*M) - 1) / wgrad_fast_tile_m(*M));
+    sp = (1024 + tiles - 1) / tiles;
+    const int max_sp = (*K + 8 * BK - 1) / (8 * BK);  // at least 8 k-steps (512 pixels) per split
+    sp = sp > max_sp ? max_sp : sp;
+    sp = sp < 1 ? 1 : sp;
+  } else {
+    BK = dtype == VCG_BF16 ? 32 : 16;
+    sp = choose_splits(*M, *Nn, *K, BK);
+  }
+  int k = (*K + sp - 1) / sp;
+  k = (k + BK - 1) / BK * BK;
+  *kps = k;
+  *splits = (*K + k - 1) / k;
 }
 
 VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW,
                                           int stride, int pad) {
-  int M, Nn, K, splits;
-  wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits);
+  int M, Nn, K, splits, kps;
+  bool fast;
+  wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits, &kps, &fast);
   return (long long)splits * M * Nn * 4;
 }
 
@@ -557,30 +581,36 @@ VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, 
   const int logC = ilog2_exact(C);
   VCG_REQUIRE(logC >= 0, "C must be a power of two");
   VCG_REQUIRE(Cout % 64 == 0, "Cout must be a multiple of 64");
-  int M, Nn, K, splits;
-  wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits);
+  int M, Nn, K, splits, kps;
+  bool fast;
+  wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits, &kps, &fast);
   VCG_REQUIRE(ws_bytes >= (long long)splits * M * Nn * 4, "workspace too small");
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
-  const int BK = dtype == VCG_BF16 ? 32 : 16;
   GemmParams p{};
   p.M = M;
   p.N = Nn;
   p.K = K;
-  int kps = (K + splits - 1) / splits;
-  kps = (kps + BK - 1) / BK * BK;
-  splits = (K + kps - 1) / kps;
   p.k_per_split = kps;
   p.a = dense_op(dy, Cout, Cout);  // A[m=cout][k=pixel] = dy[pixel][cout]
+  p.a.bytes = (long long)K * Cout * (dtype == VCG_BF16 ? 2 : 4);
   OpArgs b{};
   b.ptr = x; b.rows = Nn; b.N = N; b.H = H; b.W = W; b.C = C; b.logC = logC;
+  b.bytes = (long long)N * H * W * C * (dtype == VCG_BF16 ? 2 : 4);
   b.GH = OH; b.GW = OW; b.KH = KH; b.KW = KW; b.stride = stride; b.pad = pad;
   b.tsm_T = tsm_T > 0 ? tsm_T : 1; b.tsm_fold = tsm_fold;
   b.fd_ghw = make_fastdiv(OH * OW); b.fd_gw = make_fastdiv(OW); b.fd_T = make_fastdiv(b.tsm_T);
   p.b = b;
   p.ws = ws;
   p.alpha = 1.f;
-  int rc = dtype == VCG_BF16 ? run_gemm<bf16_t, OP_DENSE_MN, OP_IM2COL_T>(p, EPI_SPLITK, splits, stream)
-                             : run_gemm<float, OP_DENSE_MN, OP_IM2COL_T>(p, EPI_SPLITK, splits, stream);
+  FILE* f = fast ? gemm_log() : nullptr;  // the generic path logs in run_gemm
+  if (f)
+    fprintf(f, "a=3 b=4 epi=2 M=%d N=%d K=%d z=%d fast=2 conv=%dx%d/%d C=%d\n", M, Nn, K, splits, KH, KW, stride, C);
+  int rc;
+  if (fast)
+    rc = run_fast_wgrad(p, splits, stream);
+  else
+    rc = dtype == VCG_BF16 ? run_gemm<bf16_t, OP_DENSE_MN, OP_IM2COL_T>(p, EPI_SPLITK, splits, stream)
+                           : run_gemm<float, OP_DENSE_MN, OP_IM2COL_T>(p, EPI_SPLITK, splits, stream);
   if (rc) return rc;
   const long long MN = (long long)M * Nn;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, splits,

@@ -140,6 +140,99 @@ __device__ __forceinline__ constexpr int waitcnt_vm(int n) {
   return (n & 0xF) | (0x7 << 4) | (0xF << 8) | (((n >> 4) & 3) << 14);
 }
 
+// EPI_STATS epilogue of the fast kernel: store the tile (bf16) and fold its rounded values into the
+// running shifted sums. No barriers, no LDS: nothing waits on the in-flight prefetch or the stores.
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue_accstats(f32x4 (&acc)[BM / 32][BN / 32], const GemmParams& p,
+                                                  const float (&bv)[BN / 32][4], bf16_t* Cout, int m0, int n0, int wm,
+                                                  int wn, int lane, bool first, float (&ks)[BN / 32][4],
+                                                  float (&s1)[BN / 32][4], float (&s2)[BN / 32][4], int& nrows) {
+  constexpr int MT = BM / 32, NT = BN / 32;
+  const int g = lane >> 4, ci = lane & 15;
+  const int mbase = m0 + wm * (BM / 2) + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
+  nrows += min(BM / 2, max(0, p.M - (m0 + wm * (BM / 2))));
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = nbase + j * 16;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int m = mbase + i * 16;
+      const bool ok = m < p.M && n < p.N;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = acc[i][j][r] * p.alpha + bv[j][r];
+        if (p.act != ACT_NONE) t = apply_act(t, p.act);
+        v[r] = bf2f(f2bf(t));  // statistics of the stored (rounded) values
+      }
+      if (first && i == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ks[j][r] = __shfl(v[r], lane & 48, 64);  // row mbase - ci of column
+      }
+      if (ok) {
+        store4<bf16_t>(Cout + (long long)m * p.ldc + n, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = v[r] - ks[j][r];
+          s1[j][r] += d;
+          s2[j][r] = fmaf(d, d, s2[j][r]);
+        }
+      }
+    }
+  }
+}
+
+// Reduce the shifted sums across the 16 row-lanes (DPP) and the two row-halves (LDS, Chan), then write
+// (mean, M2) to stats[col][by] and the slot's row count to the count row stats[N][by] (slots by + k*gy,
+// k >= 1, are marked empty).
+template <int BN>
+__device__ __forceinline__ void stats_finish(const GemmParams& p, float* red, const float (&ks)[BN / 32][4],
+                                             float (&s1)[BN / 32][4], float (&s2)[BN / 32][4], int nrows, int n0,
+                                             int by, int bx, int gy, int mtiles, int wm, int wn, int lane) {
+  constexpr int NT = BN / 32;
+  const int g = lane >> 4, ci = lane & 15;
+  const float n = (float)nrows;
+  const float inv = nrows > 0 ? 1.f / n : 0.f;
+  __syncthreads();  // all LDS-DMA retired (last step waited vmcnt(0)); stage buffers and `red` are free
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a = row16_sum(s1[j][r]);
+      const float b = row16_sum(s2[j][r]);
+      if (ci == 0) {
+        const int lc = wn * (BN / 2) + j * 16 + 4 * g + r;
+        red[wm * 2 * BN + lc] = ks[j][r] + a * inv;            // mean of this row-half
+        red[wm * 2 * BN + BN + lc] = fmaxf(b - a * a * inv, 0.f);  // M2 of this row-half
+      }
+    }
+  if (lane == 0 && wn == 0) red[4 * BN + wm] = n;
+  __syncthreads();
+  if (wm == 0 && ci == 0) {
+    const float n1 = red[4 * BN], n2 = red[4 * BN + 1], nt = n1 + n2;
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lc = wn * (BN / 2) + j * 16 + 4 * g + r;
+        const int col = n0 + lc;
+        if (col >= p.N) continue;
+        float mean = red[lc], m2 = red[BN + lc];
+        if (n2 > 0.f) {
+          const float d = red[2 * BN + lc] - mean;
+          mean += d * (n2 / nt);
+          m2 += red[3 * BN + lc] + d * d * (n1 * n2 / nt);
+        }
+        reinterpret_cast<float2*>(p.stats)[(long long)col * mtiles + by] = make_float2(mean, m2);
+      }
+  }
+  if (bx == 0 && threadIdx.x == 0) {
+    float2* cnt = reinterpret_cast<float2*>(p.stats) + (long long)p.N * mtiles;
+    cnt[by] = make_float2(red[4 * BN] + red[4 * BN + 1], 0.f);
+    for (int t = by + gy; t < mtiles; t += gy) cnt[t] = make_float2(0.f, 0.f);
+  }
+}
+
 template <int BM, int BN, int AM, int EPI, bool RES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void igemm_fast_kernel(GemmParams p) {
   // Persistent-style grid: workgroup (bx, by) owns N-tile bx and M-tiles by, by + gy, by + 2gy, ...;
@@ -154,7 +247,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
   constexpr int MT = BM / 32, NT = BN / 32;
   constexpr int AE = BM * FBK, BE = BN * FBK;  // elements per stage
   constexpr int NLD = BM / 32 + BN / 32;       // LDS-DMA instructions per thread per step
-  __shared__ __attribute__((aligned(1024))) char smem[2 * (AE + BE) * 2 + 4 * BN * 4];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * (AE + BE) * 2 + (4 * BN + 4) * 4];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
   bf16_t* Bs = As + 2 * AE;
   float* red = reinterpret_cast<float*>(smem + 2 * (AE + BE) * 2);
@@ -209,6 +302,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // EPI_STATS: per-column sums of (v - shift) and (v - shift)^2 over every row this wave stores, across
+  // all of the workgroup's M-tiles (shift = the column's first value: no cancellation); reduced across
+  // lanes and waves once at the end -> one (mean, M2) slot per workgroup row `by`.
+  float ks[NT][4], s1[NT][4], s2[NT][4];
+  int nrows = 0;
+  if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ks[j][r] = s1[j][r] = s2[j][r] = 0.f;
+  }
+
   la.issue(p.a, 0, p.K, As, wave);
   lb.issue(p.b, 0, p.K, Bs, wave);
   int kt = 0, tile = 0;
@@ -247,7 +352,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
     __builtin_amdgcn_s_barrier();
     if (++kt == ntiles) {
       const int mt = by + tile * gy;
-      gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);
+      if constexpr (EPI == EPI_STATS)
+        epilogue_accstats<BM, BN>(acc, p, bv, Cout, mt * BM, n0, wm, wn, lane, tile == 0, ks, s1, s2, nrows);
+      else
+        gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -256,6 +364,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
       ++tile;
     }
   }
+  if constexpr (EPI == EPI_STATS) stats_finish<BN>(p, red, ks, s1, s2, nrows, n0, by, bx, gy, mtiles, wm, wn, lane);
 }
 
 template <int BM, int BN, int AM, int EPI, bool RES>

@@ -1,0 +1,237 @@
+// bf16 weight-gradient GEMM of the conv engine (the backward of torchvision conv2d inside
+// Resnet50TSM.base_model, model/vision/resnet50_tsm.py:15; TSM shift of ops/temporal_shift.py:33-51
+// folded into the gather):
+//
+//   dW[m = cout][n = (kh, kw, ci)] = sum_{pixel k} dy[k][cout] * x[im2col(k, n)]
+//
+// Both operands are "MN-contiguous": for a fixed pixel k the tile's BM couts (dy row) and its BN
+// (tap, channel) columns (one NHWC pixel of x per 8-channel chunk) are contiguous 16-B chunks.
+// They go global -> LDS with LDS-DMA (buffer_load ... lds, 16 B per lane, 1 KiB per wave
+// instruction) into [64 k][COLS] tiles whose 16-B chunks are XOR-swizzled per k-row; fragments are
+// read with ds_read_b64_tr_b16 (the transpose read gives each lane 4 consecutive k of one column),
+// 16 distinct 16-B bank slots per 32 lanes. Two LDS stages, counted vmcnt, raw s_barrier (the
+// pipeline of igemm_fast.hip). K (pixels) is split across workgroups; every split writes an fp32
+// slab [split][M][N] that splitk_reduce_kernel sums in a fixed order (deterministic).
+#include "igemm.h"
+
+namespace vcg {
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int WBK = 64;  // pixels per k-step
+
+// swizzled 16-B slot of chunk c in k-row `row` of a [64][COLS] bf16 tile (an involution in c):
+// COLS = 128 (256-B rows): rows 0..7 XOR 0,2,..,14 -> the 8 rows x 32 B read by two 16-lane groups
+// of a transpose read cover all 16 slots of the 256-B bank row; COLS = 64 (128-B rows, two rows per
+// bank row): XOR 0,2,4,6 over row pairs.
+template <int COLS> __device__ __forceinline__ int wswz(int row, int c) {
+  if constexpr (COLS == 128) return c ^ (2 * (row & 7));
+  else return c ^ (2 * ((row >> 1) & 3));
+}
+
+template <int COLS, bool GATHER> struct MNLoader {
+  static constexpr int CPR = COLS / 8;          // 16-B chunks per k-row
+  static constexpr int RPI = 64 / CPR;          // k-rows per 1-KiB wave instruction (4 or 8)
+  static constexpr int NI = WBK / RPI / 4;      // instructions per wave per stage (4 or 2)
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t oob;
+  int row[NI];   // k-row of the tile this lane fills
+  int col[NI];   // dense: element column (m0 + 8c), gather: channel ci; -1 = outside N
+  int kh[NI], kw[NI], dt[NI];
+
+  __device__ __forceinline__ void init(const OpArgs& a, int col0, int ncols, int wave, int lane) {
+    const uint32_t nbytes = (uint32_t)min(a.bytes, (long long)0xFFFFFF00LL);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr), 0, nbytes, 0x00020000);
+    oob = nbytes;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const int inst = wave * NI + q;
+      const int r = inst * RPI + lane / CPR;
+      const int c = wswz<COLS>(r, lane % CPR);  // logical chunk whose data lands in this lane's slot
+      const int cc = col0 + 8 * c;
+      row[q] = r;
+      if constexpr (!GATHER) {
+        col[q] = cc < ncols ? cc : -1;
+      } else {
+        const int tap = cc >> a.logC;
+        const int ci = cc & (a.C - 1);
+        const int h = tap / a.KW;
+        col[q] = (cc < ncols && tap < a.KH * a.KW) ? ci : -1;
+        kh[q] = h - a.pad;
+        kw[q] = tap - h * a.KW - a.pad;
+        dt[q] = a.tsm_fold > 0 ? (ci < a.tsm_fold ? 1 : (ci < 2 * a.tsm_fold ? -1 : 0)) : 0;
+      }
+    }
+  }
+
+  // pixels k0 .. k0+63 (< kend) into `lds` ([64][COLS] bf16)
+  __device__ __forceinline__ void issue(const OpArgs& a, int k0, int kend, bf16_t* lds, int wave) {
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const int k = k0 + row[q];
+      int e = -1;
+      if (col[q] >= 0 && k < kend) {
+        if constexpr (!GATHER) {
+          e = k * (int)a.ld + col[q];
+        } else {
+          const int n = (int)fdiv((uint32_t)k, a.fd_ghw);
+          const int rem = k - n * a.GH * a.GW;
+          const int y = (int)fdiv((uint32_t)rem, a.fd_gw);
+          const int x = rem - y * a.GW;
+          const int ih = y * a.stride + kh[q], iw = x * a.stride + kw[q];
+          bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+          int n2 = n;
+          if (dt[q] != 0) {
+            const int t = n - (int)fdiv((uint32_t)n, a.fd_T) * a.tsm_T + dt[q];
+            ok = ok && t >= 0 && t < a.tsm_T;
+            n2 += dt[q];
+          }
+          if (ok) e = (((n2 * a.H + ih) * a.W + iw) << a.logC) + col[q];
+        }
+      }
+      const uint32_t voff = e >= 0 ? (uint32_t)e * 2u : oob;
+      bf16_t* slice = lds + (wave * NI + q) * 512;  // 1 KiB per instruction
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)slice, 16, voff, 0, 0, 0);
+    }
+  }
+};
+
+// 16x16x32 fragment of columns r0..r0+15 (of the [64][COLS] tile), k-substep s2: two transpose reads.
+// Element j of lane 16g+i is k = 32*s2 + 4g + 16*(j>>2) + (j&3) (same map on both operands).
+// The reads are inline asm: hipcc treats the ds_read_tr intrinsic as aliasing the in-flight LDS-DMA
+// and drains it (vmcnt(0)) before every read. Ordering is explicit instead: the counted vmcnt +
+// barrier before the reads (RAW), lgkmcnt(0) + sched_barrier before the MFMAs use them, lgkmcnt(0) +
+// barrier before the stage is refilled (WAR).
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ uint32_t lds_addr(const bf16_t* p) { return (uint32_t)(uintptr_t)(const lds_char*)p; }
+
+template <int COLS> __device__ __forceinline__ void wfrag_issue(s16x4& lo, s16x4& hi, const bf16_t* lds, int r0,
+                                                                int lane, int s2) {
+  const int g = lane >> 4, i = lane & 15;
+  const int q = i >> 2, pp = i & 3;
+  const int cl = r0 + 4 * pp;
+  const int k0 = 32 * s2 + 4 * g + q, k1 = k0 + 16;
+  const uint32_t a0 = lds_addr(lds + k0 * COLS + 8 * wswz<COLS>(k0, cl >> 3) + (cl & 7));
+  const uint32_t a1 = lds_addr(lds + k1 * COLS + 8 * wswz<COLS>(k1, cl >> 3) + (cl & 7));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
+}
+__device__ __forceinline__ s16x8 cat8(const s16x4& lo, const s16x4& hi) {
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+__device__ __forceinline__ void lgkm0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ constexpr int wvm(int n) { return (n & 0xF) | (0x7 << 4) | (0xF << 8) | (((n >> 4) & 3) << 14); }
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_fast_kernel(GemmParams p) {
+  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int AE = WBK * BM, BE = WBK * BN;
+  constexpr int NLD = MNLoader<BM, false>::NI + MNLoader<BN, true>::NI;
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[2 * (AE + BE)];
+  bf16_t* As = smem;
+  bf16_t* Bs = smem + 2 * AE;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nx = (p.N + BN - 1) / BN;
+  const int bx = blockIdx.x % nx, bym = blockIdx.x / nx;  // n-tiles of one (m-tile, split) adjacent
+  const int n0 = bx * BN, m0 = bym * BM;
+  const int kb = blockIdx.z * p.k_per_split;
+  const int ke = min(p.K, kb + p.k_per_split);
+  const int ntiles = (ke - kb + WBK - 1) / WBK;
+
+  MNLoader<BM, false> la;
+  MNLoader<BN, true> lb;
+  la.init(p.a, m0, p.M, wave, lane);
+  lb.init(p.b, n0, p.N, wave, lane);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (ntiles > 0) {
+    la.issue(p.a, kb, ke, As, wave);
+    lb.issue(p.b, kb, ke, Bs, wave);
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) {
+      la.issue(p.a, kb + (t + 1) * WBK, ke, As + (cur ^ 1) * AE, wave);
+      lb.issue(p.b, kb + (t + 1) * WBK, ke, Bs + (cur ^ 1) * BE, wave);
+      __builtin_amdgcn_s_waitcnt(wvm(NLD));
+    } else {
+      __builtin_amdgcn_s_waitcnt(wvm(0));
+    }
+    __builtin_amdgcn_s_barrier();
+    const bf16_t* Ac = As + cur * AE;
+    const bf16_t* Bc = Bs + cur * BE;
+    s16x4 al[2][MT], ah[2][MT], bl[2][NT], bh[2][NT];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) wfrag_issue<BM>(al[s2][i], ah[s2][i], Ac, wm * (BM / 2) + i * 16, lane, s2);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) wfrag_issue<BN>(bl[s2][j], bh[s2][j], Bc, wn * (BN / 2) + j * 16, lane, s2);
+      if (s2 == 0) lgkm0();  // substep 0 landed; substep 1's reads stay in flight under its MFMAs
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (s2 == 1) lgkm0();
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat8(bl[s2][j], bh[s2][j]), cat8(al[s2][i], ah[s2][i]),
+                                                              acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of the stage are done
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // acc[i][j][r] = dW[m = mbase + i*16][n = nbase + j*16 + r] -> fp32 slab of this split
+  const int g = lane >> 4, ci = lane & 15;
+  const int mbase = m0 + wm * (BM / 2) + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
+  float* ws = p.ws + (long long)blockIdx.z * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = mbase + i * 16;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = nbase + j * 16;
+      if (n < p.N) *reinterpret_cast<f32x4*>(ws + (long long)m * p.N + n) = acc[i][j];
+    }
+  }
+}
+
+template <int BM, int BN> int launch_wgrad(const GemmParams& p, int splits, hipStream_t s) {
+  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN>), dim3(tiles, 1, splits), dim3(256), 0, s, p);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+}  // namespace
+
+int wgrad_fast_tile_m(int M) { return M >= 128 ? 128 : 64; }
+int wgrad_fast_tile_n(int N) { return N > 64 ? 128 : 64; }
+
+// p.a: dy as a dense [K][M] operand (ld = M), p.b: x with IM2COL_T geometry; p.ws slabs.
+int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s) {
+  const int bm = wgrad_fast_tile_m(p.M), bn = wgrad_fast_tile_n(p.N);
+  if (bm == 128 && bn == 128) return launch_wgrad<128, 128>(p, splits, s);
+  if (bm == 128) return launch_wgrad<128, 64>(p, splits, s);
+  if (bn == 128) return launch_wgrad<64, 128>(p, splits, s);
+  return launch_wgrad<64, 64>(p, splits, s);
+}
+
+}  // namespace vcg

@@ -21,9 +21,11 @@ __global__ void bn_finalize_kernel(const float2* __restrict__ stats, int mtiles,
   const int c = blockIdx.x;
   __shared__ double sn[256], sm[256], s2[256];
   double n = 0, mean = 0, m2 = 0;
+  const float2* cnt = stats + (long long)gridDim.x * mtiles;  // count row (slot row counts; 0 = empty)
   for (int t = threadIdx.x; t < mtiles; t += blockDim.x) {
     const float2 st = stats[(long long)c * mtiles + t];
-    const double nb = (double)min(tile_rows, M - t * tile_rows);
+    const double nb = (double)cnt[t].x;
+    if (nb <= 0.0) continue;
     const double delta = (double)st.x - mean;
     const double nn = n + nb;
     mean += delta * nb / nn;

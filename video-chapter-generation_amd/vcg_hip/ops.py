@@ -60,9 +60,20 @@ def stats_tiles(M):
     return _lib.query("vcg_conv_stats_tiles", M)
 
 
+def stats_buffer(Cout, M, device):
+    """BN statistics buffer of vcg_conv_fwd: float2 [Cout + 1][slots] — (mean, M2) per column and
+    slot, then the count row (rows per slot; 0 = unused slot)."""
+    return torch.empty((Cout + 1, stats_tiles(M), 2), dtype=torch.float32, device=device)
+
+
 def conv_fwd(x, w, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, stats=None, out=None):
-    """x: NHWC [N,H,W,C]; w: [Cout,KH,KW,C] (same storage dtype). Returns y [N,OH,OW,Cout]."""
+    """x: NHWC [N,H,W,C]; w: [Cout,KH,KW,C] (same storage dtype). Returns y [N,OH,OW,Cout].
+    stats: None or a stats_buffer(Cout, N*OH*OW)."""
     _chk(x, name="x")
+    if stats is not None:
+        OH_, OW_ = conv_out_hw(H, W, KH, KW, stride, pad)
+        if stats.numel() < (Cout + 1) * stats_tiles(N * OH_ * OW_) * 2:
+            raise ValueError("stats buffer too small: use ops.stats_buffer(Cout, M)")
     _chk(w, x.dtype, "w")
     OH, OW = conv_out_hw(H, W, KH, KW, stride, pad)
     y = out if out is not None else torch.empty((N, OH, OW, Cout), dtype=x.dtype, device=x.device)

@@ -66,7 +66,7 @@ class ResNetTrunk:
                                st.scale, st.shift)
         else:
             mt = ops.stats_tiles(M)
-            stats = torch.empty((Cout, mt, 2), dtype=torch.float32, device=x.device)
+            stats = ops.stats_buffer(Cout, M, x.device)
             y = ops.conv_fwd(x, w, N, H, W, C, Cout, KH, KW, s, p, tsm_T, tsm_fold, stats=stats)
             upd = mode == "train"
             mom = bn.momentum if bn.momentum is not None else 0.1
