@@ -59,10 +59,13 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
  * batch-stat eval test_video_segment_point.py:116-122) */
 VCG_API int vcg_bn_finalize(const float* stats, int mtiles, int M, int C, const float* gamma, const float* beta, float* mean_out, float* invstd_out, float* scale_out, float* shift_out, float* running_mean, float* running_var, float momentum, float eps, hipStream_t s);
 VCG_API int vcg_bn_eval_params(const float* gamma, const float* beta, const float* rm, const float* rv, float eps, int C, float* mean_out, float* invstd_out, float* scale, float* shift, hipStream_t s);
-VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const void* res, const float* rscale, const float* rshift, int relu, void* out, long long P, int C, hipStream_t s);
+/* bits (optional): ReLU mask of out, one byte per 16-byte vector (bit e = element e), for VCG_MASK_BITS. */
+VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const void* res, const float* rscale, const float* rshift, int relu, void* out, unsigned char* bits, long long P, int C, hipStream_t s);
 VCG_API long long vcg_bn_bwd_ws_bytes(long long P, int C);
-VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean, const float* invstd, long long P, int C, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, int accumulate, hipStream_t s);
-VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, long long count, int train_stats, void* dy, void* gout, long long P, int C, hipStream_t s);
+/* ReLU mask of the upstream gradient (mask_mode): 0 none, 1 tensor (mask > 0), 2 bits from vcg_bn_apply,
+   3 affine (fma(y, mscale[c], mshift[c]) > 0: the forward BN+ReLU decision recomputed from y). */
+VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, int mask_mode, const void* mask, const unsigned char* mbits, const float* mscale, const float* mshift, const void* y, const float* mean, const float* invstd, long long P, int C, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, int accumulate, hipStream_t s);
+VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, int mask_mode, const void* mask, const unsigned char* mbits, const float* mscale, const float* mshift, const void* y, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, long long count, int train_stats, void* dy, void* gout, long long P, int C, hipStream_t s);
 /* torchvision stem maxpool 3x3/2 and avgpool + fc=Identity (resnet50_tsm.py:19) */
 VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* idx, int N, int H, int W, int C, hipStream_t s);
 VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C, hipStream_t s);
@@ -80,7 +83,7 @@ VCG_API int vcg_cast_from_f32(int dtype, const float* in, void* out, long long n
 VCG_API int vcg_cast_to_f32(int dtype, const void* in, float* out, long long n, hipStream_t s);
 /* TemporalShift.shift (ops/temporal_shift.py:33-51) on NCHW; direction 1 = its adjoint */
 VCG_API int vcg_tsm_shift(int dtype, const void* x, void* y, long long n_batch, int T, int C, long long HW, int fold_div, int direction, hipStream_t s);
-VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other, void* dx, long long NT, int T, long long HW, int C, int fold, hipStream_t s);
+VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other, const unsigned char* other_bits, void* dx, long long NT, int T, long long HW, int C, int fold, hipStream_t s);
 
 /* ---- BERT support (bert.hip) ------------------------------------------------------------- */
 VCG_API int vcg_embed_ln_fwd(int dtype, const long long* ids, const float* word, const float* pos, const float* type, const float* gamma, const float* beta, void* out, float* mean, float* rstd, int B, int L, int H, float eps, float dropout_p, unsigned long long seed, hipStream_t s);

@@ -283,6 +283,33 @@ def test_bn_apply_and_bwd(K, dtype):
     _close(dy.permute(0, 3, 1, 2), gy, dtype, "bn bwd dx")
     _close(dgam, gg, dtype, "bn dgamma")
     _close(dbet, gb, dtype, "bn dbeta")
+    # the mask recomputed from y (mode 3) and the forward's mask bits (mode 2) give the same bits
+    a2, bits = K.bn_apply(ys, scale, shift, C, relu=True, bits=True)
+    assert torch.equal(a2, a)
+    ref_bits = (a.reshape(-1, 16 // a.element_size()) > 0).to(torch.int32)
+    weights = 2 ** torch.arange(ref_bits.shape[1], device=DEV, dtype=torch.int32)
+    assert torch.equal(bits.to(torch.int32), (ref_bits * weights).sum(1))
+    for kw in ({"mscale": scale, "mshift": shift}, {"mbits": bits}):
+        sg2, sgx2 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        K.bn_bwd_reduce(douts, None, ys, mean, invstd, C, sg2, sgx2, **kw)
+        dy2 = K.bn_bwd_apply(douts, None, ys, mean, invstd, g32, sg2, sgx2, C, train_stats=True, **kw)
+        assert torch.equal(sg2, sg) and torch.equal(sgx2, sgx), kw.keys()
+        assert torch.equal(dy2, dy), kw.keys()
+
+
+def test_tsm_unshift_masked_residual(K):
+    """dx = unshift(dshift) + other * mask(bits) == unshift(dshift) + (other where out > 0)."""
+    dtype = torch.bfloat16
+    NT, T, HW, C, fold = 16, 8, 9, 64, 8
+    dsh = _rand((NT, HW, C), dtype, 41).to(DEV)
+    oth = _rand((NT, HW, C), dtype, 42).to(DEV)
+    y = _rand((NT, HW, C), dtype, 43).to(DEV)
+    one = torch.ones(C, device=DEV)
+    zero = torch.zeros(C, device=DEV)
+    a, bits = K.bn_apply(y, one, zero, C, relu=True, bits=True)
+    dx = K.tsm_unshift_add(dsh, oth, NT, T, HW, C, fold, other_bits=bits)
+    ref = K.tsm_unshift_add(dsh, torch.where(a > 0, oth, torch.zeros_like(oth)), NT, T, HW, C, fold)
+    assert torch.equal(dx, ref)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)

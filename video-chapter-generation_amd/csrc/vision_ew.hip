@@ -26,6 +26,35 @@ __device__ __forceinline__ void load_params(const float* __restrict__ p, int c0,
   }
 }
 
+// Which elements of the upstream gradient pass the ReLU (vcg_hip.h VCG_MASK_*):
+//   0 none; 1 tensor (mask[v] > 0); 2 bits (one byte per 16-B vector, bit e = element e);
+//   3 affine (fma(y, mscale[c], mshift[c]) > 0: the forward's BN+ReLU decision recomputed from y).
+struct MaskArgs {
+  int mode;
+  const void* t;
+  const uint8_t* bits;
+  const float* sc;
+  const float* sh;
+};
+
+template <typename T, int VN>
+__device__ __forceinline__ void apply_mask(float (&d)[VN], const MaskArgs& m, long long v, const float (&yv)[VN],
+                                           const float (&msc)[VN], const float (&msh)[VN]) {
+  if (m.mode == 1) {
+    float mk[VN];
+    load16<T>(reinterpret_cast<const T*>(m.t) + v * VN, mk);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) d[e] = mk[e] > 0.f ? d[e] : 0.f;
+  } else if (m.mode == 2) {
+    const unsigned b = m.bits[v];
+#pragma unroll
+    for (int e = 0; e < VN; ++e) d[e] = ((b >> e) & 1u) ? d[e] : 0.f;
+  } else if (m.mode == 3) {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) d[e] = fmaf(yv[e], msc[e], msh[e]) > 0.f ? d[e] : 0.f;
+  }
+}
+
 __host__ __device__ inline int ilog2i(int x) {
   int l = 0;
   while ((1 << l) < x) ++l;
@@ -33,13 +62,15 @@ __host__ __device__ inline int ilog2i(int x) {
 }
 
 // ------------------------------------------------------------------ BN apply
-// out = act(y*scale + shift + [res*rscale + rshift | res])
+// out = act(fma(y, scale, shift) + [fma(res, rscale, rshift) | res]); bits (optional): ReLU mask of
+// out, one byte per 16-B vector (the backward's VCG_MASK_BITS)
 template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const T* __restrict__ res,
                                                        const float* __restrict__ rscale,
                                                        const float* __restrict__ rshift, int relu,
-                                                       T* __restrict__ out, long long TV, int cpr) {
+                                                       T* __restrict__ out, uint8_t* __restrict__ bits, long long TV,
+                                                       int cpr) {
   constexpr int VN = V<T>::N;
   const long long base = (long long)blockIdx.x * (256 * EW_ITER) + threadIdx.x;
   const bool fixed = cpr <= 256;
@@ -67,13 +98,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, 
     float a[VN];
     load16<T>(y + v * VN, a);
 #pragma unroll
-    for (int e = 0; e < VN; ++e) a[e] = a[e] * sc[e] + sh[e];
+    for (int e = 0; e < VN; ++e) a[e] = fmaf(a[e], sc[e], sh[e]);
     if (res) {
       float r[VN];
       load16<T>(res + v * VN, r);
       if (rscale) {
 #pragma unroll
-        for (int e = 0; e < VN; ++e) a[e] += r[e] * rs[e] + rb[e];
+        for (int e = 0; e < VN; ++e) a[e] += fmaf(r[e], rs[e], rb[e]);
       } else {
 #pragma unroll
         for (int e = 0; e < VN; ++e) a[e] += r[e];
@@ -83,77 +114,79 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, 
 #pragma unroll
       for (int e = 0; e < VN; ++e) a[e] = fmaxf(a[e], 0.f);
     }
+    if (bits) {
+      unsigned b = 0;
+#pragma unroll
+      for (int e = 0; e < VN; ++e) b |= (a[e] > 0.f ? 1u : 0u) << e;
+      bits[v] = (uint8_t)b;
+    }
     store16<T>(out + v * VN, a);
   }
 }
 
 // ------------------------------------------------------------------ BN backward
-// partial[block][2C]: per-channel sums of g and g*xhat over the block's vectors, g = dout*[mask>0]
+// partial[bx][2C]: per-channel sums of g and g*xhat over the block's rows, g = dout * mask.
+// Each thread owns one 16-B channel chunk for the whole block (cpr <= 256: 256/cpr threads share a
+// chunk and walk interleaved rows; cpr > 256: blockIdx.y selects 256 chunks, threads walk all rows),
+// and threads sharing a chunk are combined through LDS in a fixed order: deterministic.
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ mask,
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dout, MaskArgs mk,
                                                             const T* __restrict__ y, const float* __restrict__ mean,
-                                                            const float* __restrict__ invstd, long long TV, int cpr,
-                                                            int C, int red_iter, float* __restrict__ partial) {
+                                                            const float* __restrict__ invstd, long long P, int cpr,
+                                                            int C, int rows_per_block, float* __restrict__ partial) {
   constexpr int VN = V<T>::N;
-  __shared__ float red[2 * 2048];
-  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i] = 0.f;
-  __syncthreads();
-  const long long base = (long long)blockIdx.x * (256LL * red_iter) + threadIdx.x;
-  if (cpr <= 256) {
-    const int c0 = (int)(base & (cpr - 1)) * VN;
-    float mu[VN], is[VN], sg[VN], sx[VN];
-    load_params<VN>(mean, c0, mu);
-    load_params<VN>(invstd, c0, is);
+  __shared__ float part[2][256][VN];
+  const int tid = threadIdx.x;
+  const bool narrow = cpr <= 256;
+  const int chunk = narrow ? (tid & (cpr - 1)) : (blockIdx.y * 256 + tid);
+  const int rstep = narrow ? 256 / cpr : 1;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = min(P, r0 + rows_per_block);
+  const int c0 = chunk * VN;
+  float mu[VN], is[VN], sg[VN], sx[VN], msc[VN], msh[VN];
+  load_params<VN>(mean, c0, mu);
+  load_params<VN>(invstd, c0, is);
+  if (mk.mode == 3) {
+    load_params<VN>(mk.sc, c0, msc);
+    load_params<VN>(mk.sh, c0, msh);
+  }
 #pragma unroll
-    for (int e = 0; e < VN; ++e) { sg[e] = 0.f; sx[e] = 0.f; }
+  for (int e = 0; e < VN; ++e) { sg[e] = 0.f; sx[e] = 0.f; }
 #pragma unroll 4
-    for (int it = 0; it < red_iter; ++it) {
-      const long long v = base + it * 256;
-      if (v >= TV) break;
-      float d[VN], yv[VN];
-      load16<T>(dout + v * VN, d);
-      load16<T>(y + v * VN, yv);
-      if (mask) {
-        float m[VN];
-        load16<T>(mask + v * VN, m);
-#pragma unroll
-        for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < VN; ++e) {
-        sg[e] += d[e];
-        sx[e] += d[e] * (yv[e] - mu[e]) * is[e];
-      }
-    }
-    // threads with the same chunk: t, t + cpr, ... -> LDS atomics (256/cpr adders per address)
+  for (long long r = r0 + (narrow ? tid / cpr : 0); r < r1; r += rstep) {
+    const long long v = r * cpr + chunk;
+    float d[VN], yv[VN];
+    load16<T>(dout + v * VN, d);
+    load16<T>(y + v * VN, yv);
+    apply_mask<T, VN>(d, mk, v, yv, msc, msh);
 #pragma unroll
     for (int e = 0; e < VN; ++e) {
-      atomicAdd(&red[c0 + e], sg[e]);
-      atomicAdd(&red[C + c0 + e], sx[e]);
-    }
-  } else {
-    for (int it = 0; it < red_iter; ++it) {
-      const long long v = base + it * 256;
-      if (v >= TV) break;
-      const int c0 = (int)(v & (cpr - 1)) * VN;
-      float d[VN], yv[VN];
-      load16<T>(dout + v * VN, d);
-      load16<T>(y + v * VN, yv);
-      if (mask) {
-        float m[VN];
-        load16<T>(mask + v * VN, m);
-#pragma unroll
-        for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < VN; ++e) {
-        atomicAdd(&red[c0 + e], d[e]);
-        atomicAdd(&red[C + c0 + e], d[e] * (yv[e] - mean[c0 + e]) * invstd[c0 + e]);
-      }
+      sg[e] += d[e];
+      sx[e] += d[e] * (yv[e] - mu[e]) * is[e];
     }
   }
+  float* out = partial + (long long)blockIdx.x * 2 * C;
+  if (!narrow) {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      out[c0 + e] = sg[e];
+      out[C + c0 + e] = sx[e];
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < VN; ++e) {
+    part[0][tid][e] = sg[e];
+    part[1][tid][e] = sx[e];
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * C; i += 256) partial[(long long)blockIdx.x * 2 * C + i] = red[i];
+  for (int i = tid; i < 2 * C; i += 256) {
+    const int which = i >= C, c = i - which * C;
+    const int ch = c / VN, e = c - ch * VN;
+    float acc = 0.f;
+    for (int k = ch; k < 256; k += cpr) acc += part[which][k][e];
+    out[i] = acc;
+  }
 }
 
 // Column sums of partial[nb][2C] -> sum_g, sum_gx (+ dgamma/dbeta): 64 channels x 16 row-stripes per
@@ -197,7 +230,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
 //   A = gamma*invstd, B = -A*invstd*sum_gx/N, Cc = -A*sum_g/N - B*mean ; running mode: dy = A*g.
 // optionally gout = g (masked upstream gradient: the residual path)
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ mask,
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dout, MaskArgs mk,
                                                            const T* __restrict__ y, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ gamma,
@@ -207,8 +240,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            long long TV, int cpr) {
   constexpr int VN = V<T>::N;
   const long long base = (long long)blockIdx.x * (256 * EW_ITER) + threadIdx.x;
-  float A[VN], Bc[VN], Cc[VN];
+  float A[VN], Bc[VN], Cc[VN], msc[VN], msh[VN];
   int c_loaded = -1;
+  const bool need_y = train_stats || mk.mode == 3;
 #pragma unroll 4
   for (int it = 0; it < EW_ITER; ++it) {
     const long long v = base + it * 256;
@@ -229,19 +263,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
           Cc[e] = 0.f;
         }
       }
+      if (mk.mode == 3) {
+        load_params<VN>(mk.sc, c0, msc);
+        load_params<VN>(mk.sh, c0, msh);
+      }
       c_loaded = c0;
     }
     float d[VN], yv[VN], o[VN];
     load16<T>(dout + v * VN, d);
-    if (mask) {
-      float m[VN];
-      load16<T>(mask + v * VN, m);
-#pragma unroll
-      for (int e = 0; e < VN; ++e) d[e] = m[e] > 0.f ? d[e] : 0.f;
-    }
+    if (need_y) load16<T>(y + v * VN, yv);
+    apply_mask<T, VN>(d, mk, v, yv, msc, msh);
     if (gout) store16<T>(gout + v * VN, d);
     if (train_stats) {
-      load16<T>(y + v * VN, yv);
 #pragma unroll
       for (int e = 0; e < VN; ++e) o[e] = A[e] * d[e] + Bc[e] * yv[e] + Cc[e];
     } else {
@@ -334,6 +367,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
 // dx = unshift(dshift) + other over NHWC [N*T][H][W][C] (adjoint of ops/temporal_shift.py:45-47)
 template <typename T>
 __global__ __launch_bounds__(256) void tsm_unshift_add_kernel(const T* __restrict__ dshift, const T* __restrict__ other,
+                                                              const uint8_t* __restrict__ other_bits,
                                                               T* __restrict__ dx, long long TV, int lcpr, int HW,
                                                               int Tn, int fold_chunks) {
   constexpr int VN = V<T>::N;
@@ -362,8 +396,9 @@ __global__ __launch_bounds__(256) void tsm_unshift_add_kernel(const T* __restric
     if (other) {
       float b[VN];
       load16<T>(other + v * VN, b);
+      const unsigned m = other_bits ? other_bits[v] : 0xFFu;  // residual gradient through the ReLU mask
 #pragma unroll
-      for (int e = 0; e < VN; ++e) a[e] += b[e];
+      for (int e = 0; e < VN; ++e) a[e] += ((m >> e) & 1u) ? b[e] : 0.f;
     }
     store16<T>(dx + v * VN, a);
   }
@@ -376,8 +411,8 @@ inline unsigned blocks_for(long long TV, int per_block) { return (unsigned)((TV 
 // ==================================================================== C ABI
 
 VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const void* res,
-                         const float* rscale, const float* rshift, int relu, void* out, long long P, int C,
-                         hipStream_t s) {
+                         const float* rscale, const float* rshift, int relu, void* out, unsigned char* bits,
+                         long long P, int C, hipStream_t s) {
   const int VN = dtype == VCG_BF16 ? 8 : 4;
   VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
   const long long TV = P * C / VN;
@@ -386,27 +421,27 @@ VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const flo
   const unsigned g = blocks_for(TV, 256 * EW_ITER);
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
-                       (const bf16_t*)res, rscale, rshift, relu, (bf16_t*)out, TV, cpr);
+                       (const bf16_t*)res, rscale, rshift, relu, (bf16_t*)out, bits, TV, cpr);
   else
     hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)y, scale, shift,
-                       (const float*)res, rscale, rshift, relu, (float*)out, TV, cpr);
+                       (const float*)res, rscale, rshift, relu, (float*)out, bits, TV, cpr);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
 
-// vectors per thread: enough blocks to fill the chip (~1024) but at most RED_ITER_MAX per thread
-// (the per-block partials then stay small next to the streamed tensors)
-static int bn_bwd_iter(long long P, int C, int VN) {
-  const long long TV = P * C / VN;
+// rows per block: enough blocks to fill the chip (~1024 in total) but at most RED_ITER_MAX vectors
+// per thread (the per-block partials then stay small next to the streamed tensors)
+static long long bn_bwd_rows(long long P, int C, int VN) {
+  const int cpr = C / VN;
+  const long long TV = P * cpr;
   long long it = (TV + 256LL * 1024 - 1) / (256LL * 1024);
   if (it < 4) it = 4;
   if (it > RED_ITER_MAX) it = RED_ITER_MAX;
-  return (int)it;
+  return cpr <= 256 ? it * (256 / cpr) : it;
 }
 static long long bn_bwd_blocks(long long P, int C, int VN) {
-  const long long TV = P * C / VN;
-  const long long per = 256LL * bn_bwd_iter(P, C, VN);
-  return (TV + per - 1) / per;
+  const long long rows = bn_bwd_rows(P, C, VN);
+  return (P + rows - 1) / rows;
 }
 
 VCG_API long long vcg_bn_bwd_ws_bytes(long long P, int C) {
@@ -415,22 +450,44 @@ VCG_API long long vcg_bn_bwd_ws_bytes(long long P, int C) {
   return nb * 2 * C * 4 + 64;
 }
 
-VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
+static MaskArgs mask_args(int mode, const void* mask, const unsigned char* bits, const float* msc, const float* msh) {
+  MaskArgs m;
+  m.mode = mode;
+  m.t = mask;
+  m.bits = bits;
+  m.sc = msc;
+  m.sh = msh;
+  return m;
+}
+
+static int check_mask(int mode, const void* mask, const unsigned char* bits, const float* msc, const float* msh) {
+  VCG_REQUIRE(mode >= 0 && mode <= 3, "mask_mode must be 0..3");
+  VCG_REQUIRE(mode != 1 || mask, "mask_mode 1 needs the mask tensor");
+  VCG_REQUIRE(mode != 2 || bits, "mask_mode 2 needs the mask bits");
+  VCG_REQUIRE(mode != 3 || (msc && msh), "mask_mode 3 needs mscale/mshift");
+  return VCG_OK;
+}
+
+VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, int mask_mode, const void* mask, const unsigned char* mbits,
+                              const float* mscale, const float* mshift, const void* y, const float* mean,
                               const float* invstd, long long P, int C, float* ws, long long ws_bytes, float* sum_g,
                               float* sum_gx, float* dgamma, float* dbeta, int accumulate, hipStream_t s) {
+  if (int rc = check_mask(mask_mode, mask, mbits, mscale, mshift)) return rc;
+  const MaskArgs mk = mask_args(mask_mode, mask, mbits, mscale, mshift);
   const int VN = dtype == VCG_BF16 ? 8 : 4;
   VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && C <= 2048, "C must be a power of two <= 2048");
   VCG_REQUIRE(ws_bytes >= vcg_bn_bwd_ws_bytes(P, C), "workspace too small");
   const long long TV = P * C / VN;
   const int cpr = C / VN;
   const long long nb = bn_bwd_blocks(P, C, VN);
-  const int it = bn_bwd_iter(P, C, VN);
+  const int rows = (int)bn_bwd_rows(P, C, VN);
+  const dim3 grid((unsigned)nb, cpr > 256 ? cpr / 256 : 1);
   if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, dim3((unsigned)nb), dim3(256), 0, s, (const bf16_t*)dout,
-                       (const bf16_t*)mask, (const bf16_t*)y, mean, invstd, TV, cpr, C, it, ws);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dout, mk,
+                       (const bf16_t*)y, mean, invstd, P, cpr, C, rows, ws);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, (const float*)dout,
-                       (const float*)mask, (const float*)y, mean, invstd, TV, cpr, C, it, ws);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, grid, dim3(256), 0, s, (const float*)dout, mk,
+                       (const float*)y, mean, invstd, P, cpr, C, rows, ws);
   VCG_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, sum_g, sum_gx,
                      dgamma, dbeta, accumulate);
@@ -438,23 +495,26 @@ VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, const void* mask, con
   return VCG_OK;
 }
 
-VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
+VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, int mask_mode, const void* mask, const unsigned char* mbits,
+                             const float* mscale, const float* mshift, const void* y, const float* mean,
                              const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx,
                              long long count, int train_stats, void* dy, void* gout, long long P, int C,
                              hipStream_t s) {
+  if (int rc = check_mask(mask_mode, mask, mbits, mscale, mshift)) return rc;
+  const MaskArgs mk = mask_args(mask_mode, mask, mbits, mscale, mshift);
   const int VN = dtype == VCG_BF16 ? 8 : 4;
   VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
   const long long TV = P * C / VN;
   const float ic = 1.f / (float)count;
   const unsigned g = blocks_for(TV, 256 * EW_ITER);
   if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)dout,
-                       (const bf16_t*)mask, (const bf16_t*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats,
-                       (bf16_t*)dy, (bf16_t*)gout, TV, C / VN);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)dout, mk,
+                       (const bf16_t*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats, (bf16_t*)dy,
+                       (bf16_t*)gout, TV, C / VN);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)dout,
-                       (const float*)mask, (const float*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats,
-                       (float*)dy, (float*)gout, TV, C / VN);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)dout, mk,
+                       (const float*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats, (float*)dy,
+                       (float*)gout, TV, C / VN);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -495,8 +555,8 @@ VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx,
   return VCG_OK;
 }
 
-VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other, void* dx, long long NT, int T,
-                                long long HW, int C, int fold, hipStream_t s) {
+VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other, const unsigned char* other_bits,
+                                void* dx, long long NT, int T, long long HW, int C, int fold, hipStream_t s) {
   const int VN = dtype == VCG_BF16 ? 8 : 4;
   VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && fold % VN == 0, "C / fold must be multiples of the vector width");
   const long long TV = NT * HW * C / VN;
@@ -504,10 +564,10 @@ VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other
   const unsigned g = blocks_for(TV, 256 * EW_ITER);
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(tsm_unshift_add_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)dshift,
-                       (const bf16_t*)other, (bf16_t*)dx, TV, lcpr, (int)HW, T, fold / VN);
+                       (const bf16_t*)other, other_bits, (bf16_t*)dx, TV, lcpr, (int)HW, T, fold / VN);
   else
     hipLaunchKernelGGL(tsm_unshift_add_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)dshift,
-                       (const float*)other, (float*)dx, TV, lcpr, (int)HW, T, fold / VN);
+                       (const float*)other, other_bits, (float*)dx, TV, lcpr, (int)HW, T, fold / VN);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

@@ -153,28 +153,45 @@ def bn_eval_params(gamma, beta, rm, rv, eps, C, mean, invstd, scale, shift):
               P(shift), stream())
 
 
-def bn_apply(y, scale, shift, C, relu, res=None, rscale=None, rshift=None, out=None):
+def bn_apply(y, scale, shift, C, relu, res=None, rscale=None, rshift=None, out=None, bits=False):
+    """act(y*scale + shift [+ res*rscale + rshift | + res]). bits=True also returns the ReLU mask
+    bits of the output (one byte per 16-B vector) for the backward (mask mode 2)."""
     out = out if out is not None else torch.empty_like(y)
+    b = torch.empty(y.numel() * y.element_size() // 16, dtype=torch.uint8, device=y.device) if bits else None
     _lib.call("vcg_bn_apply", dt_code(y.dtype), P(y), P(scale), P(shift), P(res), P(rscale), P(rshift), int(relu),
-              P(out), y.numel() // C, C, stream())
-    return out
+              P(out), P(b), y.numel() // C, C, stream())
+    return (out, b) if bits else out
 
 
-def bn_bwd_reduce(dout, mask, y, mean, invstd, C, sum_g, sum_gx, dgamma=None, dbeta=None, workspace=None):
+def _mask_mode(mask, mbits, mscale):
+    if mbits is not None:
+        return 2
+    if mscale is not None:
+        return 3
+    return 1 if mask is not None else 0
+
+
+def bn_bwd_reduce(dout, mask, y, mean, invstd, C, sum_g, sum_gx, dgamma=None, dbeta=None, workspace=None,
+                  mbits=None, mscale=None, mshift=None):
+    """Per-channel sums of g and g*xhat, g = dout masked by the ReLU: `mask` tensor (> 0), `mbits`
+    (from bn_apply(bits=True)) or the affine recompute fma(y, mscale, mshift) > 0."""
     Pn = y.numel() // C
     nbytes = _lib.query("vcg_bn_bwd_ws_bytes", Pn, C)
     if workspace is None or workspace.numel() * 4 < nbytes:
         workspace = ws(nbytes, y.device)
-    _lib.call("vcg_bn_bwd_reduce", dt_code(y.dtype), P(dout), P(mask), P(y), P(mean), P(invstd), Pn, C, P(workspace),
-              workspace.numel() * 4, P(sum_g), P(sum_gx), P(dgamma), P(dbeta), 1, stream())
+    _lib.call("vcg_bn_bwd_reduce", dt_code(y.dtype), P(dout), _mask_mode(mask, mbits, mscale), P(mask), P(mbits),
+              P(mscale), P(mshift), P(y), P(mean), P(invstd), Pn, C, P(workspace), workspace.numel() * 4, P(sum_g),
+              P(sum_gx), P(dgamma), P(dbeta), 1, stream())
     return workspace
 
 
-def bn_bwd_apply(dout, mask, y, mean, invstd, gamma, sum_g, sum_gx, C, train_stats, gout=None, out=None):
+def bn_bwd_apply(dout, mask, y, mean, invstd, gamma, sum_g, sum_gx, C, train_stats, gout=None, out=None,
+                 mbits=None, mscale=None, mshift=None):
     Pn = y.numel() // C
     dy = out if out is not None else torch.empty_like(y)
-    _lib.call("vcg_bn_bwd_apply", dt_code(y.dtype), P(dout), P(mask), P(y), P(mean), P(invstd), P(gamma), P(sum_g),
-              P(sum_gx), Pn, int(train_stats), P(dy), P(gout), Pn, C, stream())
+    _lib.call("vcg_bn_bwd_apply", dt_code(y.dtype), P(dout), _mask_mode(mask, mbits, mscale), P(mask), P(mbits),
+              P(mscale), P(mshift), P(y), P(mean), P(invstd), P(gamma), P(sum_g), P(sum_gx), Pn, int(train_stats),
+              P(dy), P(gout), Pn, C, stream())
     return dy
 
 
@@ -266,9 +283,11 @@ def tsm_shift(x, n_segment, fold_div, direction=0):
     return y
 
 
-def tsm_unshift_add(dshift, other, NT, T, HW, C, fold):
+def tsm_unshift_add(dshift, other, NT, T, HW, C, fold, other_bits=None):
+    """dx = unshift(dshift) + other (other masked by `other_bits` when given)."""
     dx = torch.empty_like(dshift)
-    _lib.call("vcg_tsm_unshift_add", dt_code(dshift.dtype), P(dshift), P(other), P(dx), NT, T, HW, C, fold, stream())
+    _lib.call("vcg_tsm_unshift_add", dt_code(dshift.dtype), P(dshift), P(other), P(other_bits), P(dx), NT, T, HW, C,
+              fold, stream())
     return dx
 
 

@@ -85,7 +85,8 @@ class ResNetTrunk:
         a0 = ops.bn_apply(y0, b0.scale, b0.shift, 64, relu=True)
         mp, idx = ops.maxpool_fwd(a0, N, H1, W1, 64)
         Hm, Wm = mp.shape[1], mp.shape[2]
-        saved = {"stem": (xs, y0, a0, idx, b0, N, H, W, cpad, H1, W1)} if need_grad else None
+        # a0 is not kept: the backward recomputes the ReLU decision from y0 (mask mode 3)
+        saved = {"stem": (xs, y0, None, idx, b0, N, H, W, cpad, H1, W1)} if need_grad else None
         if not need_grad:
             del y0, a0, idx
         h, Hc, Wc = mp, Hm, Wm
@@ -114,25 +115,32 @@ class ResNetTrunk:
         yd = bd = None
         if blk.downsample is not None:
             yd, bd, _, _ = self._conv_bn(x, blk.downsample[0], blk.downsample[1], N, H, W, Cin)
-            out = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale, rshift=bd.shift)
+            out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale,
+                                      rshift=bd.shift, bits=True)
         else:
-            out = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=x)
+            out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=x, bits=True)
         rec = None
         if need_grad:
-            rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, y3=y3, yd=yd, out=out, b1=b1, b2=b2, b3=b3, bd=bd,
-                       N=N, H=H, W=W, H2=H2, W2=W2, Cin=Cin, planes=planes, C3=C3, T=T, fold=fold, conv1=conv1)
+            rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, y3=y3, yd=yd, obits=obits, b1=b1, b2=b2, b3=b3,
+                       bd=bd, N=N, H=H, W=W, H2=H2, W2=W2, Cin=Cin, planes=planes, C3=C3, T=T, fold=fold,
+                       conv1=conv1)
         return out, rec, H2, W2
 
     # ---------------------------------------------------------------- backward
-    def _bn_bwd(self, dout, mask, y, st, C, gout=None):
+    def _bn_bwd(self, dout, y, st, C, mbits=None, affine=False):
+        """BN backward of conv output y. The upstream gradient is masked by the ReLU that followed the BN:
+        affine=True recomputes the decision fma(y, scale, shift) > 0 exactly as the forward made it;
+        mbits are the forward's mask bits (bn3, where the residual joins before the ReLU)."""
         bn = st.bn
         dev = y.device
         sums = torch.empty((2, C), dtype=torch.float32, device=dev)
         need_affine = bn.weight is not None and bn.weight.requires_grad
-        ops.bn_bwd_reduce(dout, mask, y, st.mean, st.invstd, C, sums[0], sums[1],
-                          bn.weight.grad if need_affine else None, bn.bias.grad if need_affine else None)
-        return ops.bn_bwd_apply(dout, mask, y, st.mean, st.invstd, bn.weight, sums[0], sums[1], C,
-                                train_stats=st.mode != "running", gout=gout)
+        msc, msh = (st.scale, st.shift) if affine else (None, None)
+        ops.bn_bwd_reduce(dout, None, y, st.mean, st.invstd, C, sums[0], sums[1],
+                          bn.weight.grad if need_affine else None, bn.bias.grad if need_affine else None,
+                          mbits=mbits, mscale=msc, mshift=msh)
+        return ops.bn_bwd_apply(dout, None, y, st.mean, st.invstd, bn.weight, sums[0], sums[1], C,
+                                train_stats=st.mode != "running", mbits=mbits, mscale=msc, mshift=msh)
 
     def _wgrad(self, conv, x, dy, N, H, W, Cpad, T=0, fold=0):
         if not conv.weight.requires_grad:
@@ -159,7 +167,7 @@ class ResNetTrunk:
             del rec
         xs, y0, a0, idx, b0, N, H, W, cpad, H1, W1 = saved["stem"]
         da0 = ops.maxpool_bwd(dout, idx, N, H1, W1, 64)
-        dy0 = self._bn_bwd(da0, a0, y0, b0, 64)
+        dy0 = self._bn_bwd(da0, y0, b0, 64, affine=True)
         self._wgrad(self.net.conv1, xs, dy0, N, H, W, cpad)
         if hooks is not None:
             hooks(list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
@@ -168,25 +176,24 @@ class ResNetTrunk:
         blk = r["blk"]
         N, H, W, H2, W2 = r["N"], r["H"], r["W"], r["H2"], r["W2"]
         Cin, planes, C3, T, fold = r["Cin"], r["planes"], r["C3"], r["T"], r["fold"]
-        gout = torch.empty_like(dout)
-        dy3 = self._bn_bwd(dout, r["out"], r["y3"], r["b3"], C3, gout=gout)
+        obits = r["obits"]
+        dy3 = self._bn_bwd(dout, r["y3"], r["b3"], C3, mbits=obits)
         self._wgrad(blk.conv3, r["a2"], dy3, N, H2, W2, planes)
         da2 = self._dgrad(blk.conv3, dy3, N, H2, W2)
         del dy3
-        dy2 = self._bn_bwd(da2, r["a2"], r["y2"], r["b2"], planes)
+        dy2 = self._bn_bwd(da2, r["y2"], r["b2"], planes, affine=True)
         del da2
         self._wgrad(blk.conv2, r["a1"], dy2, N, H, W, planes)
         da1 = self._dgrad(blk.conv2, dy2, N, H, W)
         del dy2
-        dy1 = self._bn_bwd(da1, r["a1"], r["y1"], r["b1"], planes)
+        dy1 = self._bn_bwd(da1, r["y1"], r["b1"], planes, affine=True)
         del da1
         self._wgrad(r["conv1"], r["x"], dy1, N, H, W, Cin, T, fold)
         dxs = self._dgrad(r["conv1"], dy1, N, H, W)
         del dy1
         if blk.downsample is not None:
-            dyd = self._bn_bwd(gout, None, r["yd"], r["bd"], C3)
+            dyd = self._bn_bwd(dout, r["yd"], r["bd"], C3, mbits=obits)  # the residual gradient: dout * mask
             self._wgrad(blk.downsample[0], r["x"], dyd, N, H, W, Cin)
             other = self._dgrad(blk.downsample[0], dyd, N, H, W)
-        else:
-            other = gout
-        return ops.tsm_unshift_add(dxs, other, N, T if T else 1, H * W, Cin, fold)
+            return ops.tsm_unshift_add(dxs, other, N, T if T else 1, H * W, Cin, fold)
+        return ops.tsm_unshift_add(dxs, dout, N, T if T else 1, H * W, Cin, fold, other_bits=obits)
