@@ -23,6 +23,15 @@ def timeit(fn, iters=10):
 
 
 def main():
+    if os.environ.get("VCG_BENCH_AB"):  # A/B of the output staging threshold in one process
+        for name, fn in _ab_cases():
+            res = []
+            for kt in ("0", "4", "1000"):
+                os.environ["VCG_STAGE_KT"] = kt
+                res.append(f"stage_kt={kt}: {timeit(fn, 20):8.1f}us")
+            print(f"{name:32s} " + "  ".join(res))
+        return
+
     dt = torch.bfloat16
     dev = "cuda"
     a = torch.empty(800 * 1024 * 1024, dtype=torch.uint8, device=dev)
@@ -69,6 +78,26 @@ def main():
         C = torch.empty(M, Nn, device=dev, dtype=dt)
         us = timeit(lambda: ops.gemm(A, B, M, Nn, K, K, K, out=C))
         print(f"gemm {M}x{Nn}x{K:<20d} {us:8.1f} us  {2.0 * M * Nn * K / us / 1e6:7.1f} TF/s")
+
+
+def _ab_cases():
+    dt = torch.bfloat16
+    dev = "cuda"
+    out = []
+    for name, N, H, W, C, Co, k, s, p, st in (("l1 conv3 64->256 stats", 1024, 56, 56, 64, 256, 1, 1, 0, True),
+                                              ("l1 conv3 64->256", 1024, 56, 56, 64, 256, 1, 1, 0, False),
+                                              ("l2 conv3 128->512 stats", 1024, 28, 28, 128, 512, 1, 1, 0, True),
+                                              ("l3 conv1 1024->256 stats", 1024, 14, 14, 1024, 256, 1, 1, 0, True),
+                                              ("l2 conv2 3x3 128 stats", 1024, 28, 28, 128, 128, 3, 1, 1, True),
+                                              ("l3 conv2 3x3 256 stats", 1024, 14, 14, 256, 256, 3, 1, 1, True)):
+        x = torch.randn(N, H, W, C, device=dev).to(dt)
+        w = torch.randn(Co, k, k, C, device=dev).to(dt) * 0.05
+        OH, OW = ops.conv_out_hw(H, W, k, k, s, p)
+        stats = ops.stats_buffer(Co, N * OH * OW, dev) if st else None
+        y = torch.empty((N, OH, OW, Co), dtype=dt, device=dev)
+        out.append((name, (lambda x=x, w=w, y=y, stats=stats, N=N, H=H, W=W, C=C, Co=Co, k=k, s=s, p=p:
+                           ops.conv_fwd(x, w, N, H, W, C, Co, k, k, s, p, 0, 0, stats=stats, out=y))))
+    return out
 
 
 if __name__ == "__main__":

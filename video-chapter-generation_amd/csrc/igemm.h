@@ -66,6 +66,7 @@ struct GemmParams {
   // batched mode (batch_inner > 0): blockIdx.z = zo * batch_inner + zi selects element offsets
   int batch_inner;
   long long a_so, a_si, b_so, b_si, c_so, c_si;
+  int stage_kt;  // fast kernel: stage the output tile through LDS when the tile has <= stage_kt k-steps
 };
 
 

@@ -140,13 +140,93 @@ __device__ __forceinline__ constexpr int waitcnt_vm(int n) {
   return (n & 0xF) | (0x7 << 4) | (0xF << 8) | (((n >> 4) & 3) << 14);
 }
 
+// ---- output staging through LDS: full-row 16-B stores instead of 8-B row fragments ----------------
+// The finished stage `cur` (A part: BM x 64, B part: BN x 64 bf16) holds the bf16 output tile: BN = 128
+// -> rows 0..63 in the A part and rows 64..127 in the B part ([64][128] each); BN = 64 -> the whole
+// [128][64] tile in the A part. 16-B chunks are XOR-swizzled per row (conflict-free 8-B writes of a
+// 16-row fragment and 16-B reads of a row). LDS accesses are inline asm with explicit lgkmcnt waits.
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)(const lds_char*)p; }
+
+template <int BN> __device__ __forceinline__ int st_slot(int row, int chunk) {
+  if constexpr (BN == 128) return chunk ^ (row & 15);
+  else return chunk ^ ((row >> 1) & 7);
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void stage_put(bf16_t* stA, bf16_t* stB, int wm, int wn, int lane, int i, int j,
+                                          const float (&v)[4]) {
+  const int g = lane >> 4, ci = lane & 15;
+  const int trow = wm * (BM / 2) + i * 16 + ci;        // row in the tile
+  const int tcol = wn * (BN / 2) + j * 16 + 4 * g;     // first of 4 columns
+  bf16_t* reg = (BN == 128 && trow >= 64) ? stB : stA;
+  const int row = BN == 128 ? (trow & 63) : trow;
+  const uint32_t addr = lds_u32(reg + row * BN + 8 * st_slot<BN>(row, tcol >> 3) + (tcol & 7));
+  uint2 q;
+  q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(q) : "memory");
+}
+
+// all waves' stage_put done -> 16-B row chunks to global (rows >= M / cols >= N skipped)
+template <int BM, int BN>
+__device__ __forceinline__ void stage_flush(const bf16_t* stA, const bf16_t* stB, const GemmParams& p, bf16_t* Cout,
+                                            int m0, int n0) {
+  constexpr int CPR = BN / 8, NCH = BM * BN / 8;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  uint4 q[NCH / 256];
+#pragma unroll
+  for (int k = 0; k < NCH / 256; ++k) {
+    const int id = threadIdx.x + 256 * k;
+    const int trow = id / CPR, c = id - trow * CPR;
+    const bf16_t* reg = (BN == 128 && trow >= 64) ? stB : stA;
+    const int row = BN == 128 ? (trow & 63) : trow;
+    const uint32_t addr = lds_u32(reg + row * BN + 8 * st_slot<BN>(row, c));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(q[k]) : "v"(addr) : "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < NCH / 256; ++k) {
+    const int id = threadIdx.x + 256 * k;
+    const int trow = id / CPR, c = id - trow * CPR;
+    const int m = m0 + trow, n = n0 + 8 * c;
+    if (m < p.M && n < p.N) *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + n) = q[k];
+  }
+  __builtin_amdgcn_s_barrier();  // every wave has read the stage before the next step's DMA refills it
+}
+
+// EPI_STORE (no residual / aux) through the stage
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue_staged(f32x4 (&acc)[BM / 32][BN / 32], const GemmParams& p,
+                                                const float (&bv)[BN / 32][4], bf16_t* Cout, bf16_t* stA,
+                                                bf16_t* stB, int m0, int n0, int wm, int wn, int lane) {
+  constexpr int MT = BM / 32, NT = BN / 32;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = acc[i][j][r] * p.alpha + bv[j][r];
+        if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) t = apply_act(t, p.act);
+        v[r] = t;
+      }
+      stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
+    }
+  stage_flush<BM, BN>(stA, stB, p, Cout, m0, n0);
+}
+
 // EPI_STATS epilogue of the fast kernel: store the tile (bf16) and fold its rounded values into the
 // running shifted sums. No barriers, no LDS: nothing waits on the in-flight prefetch or the stores.
 template <int BM, int BN>
 __device__ __forceinline__ void epilogue_accstats(f32x4 (&acc)[BM / 32][BN / 32], const GemmParams& p,
-                                                  const float (&bv)[BN / 32][4], bf16_t* Cout, int m0, int n0, int wm,
-                                                  int wn, int lane, bool first, float (&ks)[BN / 32][4],
-                                                  float (&s1)[BN / 32][4], float (&s2)[BN / 32][4], int& nrows) {
+                                                  const float (&bv)[BN / 32][4], bf16_t* Cout, bf16_t* stA,
+                                                  bf16_t* stB, bool staged, int m0, int n0, int wm, int wn, int lane,
+                                                  bool first, float (&ks)[BN / 32][4], float (&s1)[BN / 32][4],
+                                                  float (&s2)[BN / 32][4], int& nrows) {
   constexpr int MT = BM / 32, NT = BN / 32;
   const int g = lane >> 4, ci = lane & 15;
   const int mbase = m0 + wm * (BM / 2) + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
@@ -169,8 +249,11 @@ __device__ __forceinline__ void epilogue_accstats(f32x4 (&acc)[BM / 32][BN / 32]
 #pragma unroll
         for (int r = 0; r < 4; ++r) ks[j][r] = __shfl(v[r], lane & 48, 64);  // row mbase - ci of column
       }
-      if (ok) {
+      if (staged)
+        stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
+      else if (ok)
         store4<bf16_t>(Cout + (long long)m * p.ldc + n, v);
+      if (ok) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float d = v[r] - ks[j][r];
@@ -180,6 +263,7 @@ __device__ __forceinline__ void epilogue_accstats(f32x4 (&acc)[BM / 32][BN / 32]
       }
     }
   }
+  if (staged) stage_flush<BM, BN>(stA, stB, p, Cout, m0, n0);
 }
 
 // Reduce the shifted sums across the 16 row-lanes (DPP) and the two row-halves (LDS, Chan), then write
@@ -352,10 +436,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
     __builtin_amdgcn_s_barrier();
     if (++kt == ntiles) {
       const int mt = by + tile * gy;
-      if constexpr (EPI == EPI_STATS)
-        epilogue_accstats<BM, BN>(acc, p, bv, Cout, mt * BM, n0, wm, wn, lane, tile == 0, ks, s1, s2, nrows);
-      else
+      // output tiles go through the LDS stage for full-row 16-B stores (VCG_STAGE_KT can limit it)
+      const bool staged = ntiles <= p.stage_kt;
+      if constexpr (EPI == EPI_STATS) {
+        epilogue_accstats<BM, BN>(acc, p, bv, Cout, As + cur * AE, Bs + cur * BE, staged, mt * BM, n0, wm, wn,
+                                  lane, tile == 0, ks, s1, s2, nrows);
+      } else if (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0) {
+        epilogue_staged<BM, BN>(acc, p, bv, Cout, As + cur * AE, Bs + cur * BE, mt * BM, n0, wm, wn, lane);
+      } else {
         gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -390,7 +480,11 @@ static int fast_bn(const GemmParams& p, int z, hipStream_t s) {
 }
 
 // Entry from igemm.hip's dispatcher (bf16, K-contiguous A and B, no split-K).
+// VCG_STAGE_KT (default: all): largest k-step count per tile whose output goes through the LDS stage
+// (A/B in one process, tools/bench_gemm.py with VCG_BENCH_AB=1: staging never loses).
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
+  const char* e = getenv("VCG_STAGE_KT");
+  p.stage_kt = e && e[0] ? atoi(e) : 1 << 30;
   if (epi == EPI_STATS) {
     if (amode == OP_IM2COL) return fast_bn<OP_IM2COL, EPI_STATS>(p, z, s);
     if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_STATS>(p, z, s);
