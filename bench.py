@@ -3,9 +3,13 @@
 16 frames x 224^2 + 128 tokens per window, B=64 windows per GPU, bf16, fused clip+AdamW) on 1..8
 MI355X, one process per GPU (torchrun), RCCL all-reduce overlapped with the backward.
 
-Prints ONE JSON line (rank 0). `roofline` prices the step against HBM with SURVEY Appendix A's
-algorithmic bytes per window; `cpu_baseline` times the CPU oracle (oracle/, test infrastructure)
-on a bounded sample on this host's cores.
+Prints ONE JSON line (rank 0).
+- `roofline`: the dominant kernel (igemm_fast_kernel, the bf16 conv/linear GEMM engine): algorithmic
+  FLOPs (2*M*N*K per launch) over its launch durations, timed live with HIP events on the launch
+  stream during one extra instrumented step after the timed region (vcg_timing_*), against the bf16
+  dense MFMA peak; `traffic` = its HBM bytes per launch from the committed PMC pass, if any.
+- `roofline_step`: the whole step priced against HBM with SURVEY Appendix A's fused-minimum bytes.
+- `cpu_baseline`: the CPU oracle (oracle/, test infrastructure) on a bounded sample on this host.
 """
 import argparse
 import json
@@ -128,7 +132,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from vcg_hip import _lib, synth
+    from vcg_hip import _lib, ops, synth
     from vcg_hip.build import build_two_stream
     from vcg_hip.ddp import GradAllReducer, broadcast_parameters
     from vcg_hip.functions import cross_entropy
@@ -184,6 +188,13 @@ def main():
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / args.steps
     ms = max(ms, wall * 1000.0 / args.steps)
+    # one extra (untimed) step with every fast-GEMM launch bracketed by HIP events
+    ops.timing_enable(True)
+    step()
+    torch.cuda.synchronize()
+    k_ms, k_n, k_fl = ops.timing_query(ops.TIMING_FAST_GEMM)
+    ops.timing_enable(False)
+    kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
     if world > 1:
         t = torch.tensor([ms], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -196,11 +207,23 @@ def main():
         nbytes, nflops = window_costs(T, HW, L, B, s_bytes, args.mode == "train")
         achieved = nbytes * B / (ms / 1000.0) / 1e9  # per GPU
         tflops = nflops * B / (ms / 1000.0) / 1e12
-        traffic = None
+        traffic = kern_traffic = None
         tf = os.path.join(REPO, "profiles", f"traffic_{args.mode}_{args.precision}_b{B}.json")
         if os.path.exists(tf):
             with open(tf) as f:
-                traffic = json.load(f).get("hbm_bytes_per_step")
+                tj = json.load(f)
+            traffic = tj.get("hbm_bytes_per_step")
+            kern_traffic = tj.get("igemm_fast_kernel", {}).get("hbm_bytes_per_launch")
+        dom = None
+        if kern["launches"]:
+            k_tf = kern["flops"] / (kern["ms"] / 1e3) / 1e12
+            dom = {"kernel": "igemm_fast_kernel", "bound": "mfma", "achieved": round(k_tf, 2),
+                   "peak": MFMA_PEAK_TFLOPS[args.precision], "unit": "TFLOP/s",
+                   "frac": round(k_tf / MFMA_PEAK_TFLOPS[args.precision], 4), "traffic": kern_traffic,
+                   "launches_per_step": kern["launches"], "avg_launch_us": round(kern["ms"] * 1e3 / kern["launches"], 2),
+                   "gflop_per_launch": round(kern["flops"] / kern["launches"] / 1e9, 3),
+                   "share_of_step": round(kern["ms"] / ms, 4),
+                   "timing": "HIP events around each launch on its stream, one instrumented step"}
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "clip-windows/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
@@ -211,7 +234,8 @@ def main():
                                    + (", fused clip+AdamW" if args.mode == "train" else ""),
                        "global_batch": windows, "seq_len": L, "frames": T, "resolution": HW,
                        "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": dom,
+            "roofline_step": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "scope": "whole step (all kernels) vs SURVEY App. A fused-minimum bytes "
                                   f"({nbytes / 1e9:.3f} GB/window)",

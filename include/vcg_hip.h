@@ -33,6 +33,11 @@ VCG_API int vcg_version(void);
 VCG_API int vcg_init(int device);      /* per-device handle; fails unless the device is gfx950 */
 VCG_API int vcg_finalize(void);
 VCG_API int vcg_sync(hipStream_t stream);
+/* Live launch timing (bench.py's dominant-kernel roofline): while enabled, every fast-GEMM / wgrad launch is
+   bracketed with HIP events on its stream; query sums durations (ms), launches and algorithmic FLOPs per kernel
+   id (0 igemm_fast_kernel, 1 wgrad_fast_kernel). Enabling (or disabling) clears the records. */
+VCG_API int vcg_timing_enable(int on);
+VCG_API int vcg_timing_query(int kernel_id, double* ms_total, long long* launches, double* flops);
 
 /* ---- MFMA implicit-GEMM engine (igemm.hip) ---------------------------------------------- */
 /* torchvision conv2d inside Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15,68-77), with

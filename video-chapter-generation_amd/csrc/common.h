@@ -15,6 +15,13 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 #define VCG_API extern "C" __attribute__((visibility("default")))
 
+namespace vcg {
+// kernel ids of vcg_timing_query
+enum { TIMING_FAST_GEMM = 0, TIMING_WGRAD = 1, TIMING_GENERIC_GEMM = 2 };
+int timing_begin(hipStream_t s);
+void timing_end(int idx, hipStream_t s, int id, double flops);
+}  // namespace vcg
+
 enum vcg_dtype { VCG_F32 = 0, VCG_BF16 = 1 };
 enum vcg_status {
   VCG_OK = 0,

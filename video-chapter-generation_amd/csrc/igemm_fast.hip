@@ -468,7 +468,9 @@ static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   if (gy > mtiles) gy = mtiles >= 8 ? (mtiles & ~7) : mtiles;
   if (gy < 1) gy = 1;
   dim3 grid(nx * gy, 1, z);
+  const int tk = timing_begin(s);
   hipLaunchKernelGGL((igemm_fast_kernel<BM, BN, AM, EPI, RES>), grid, dim3(256), 0, s, p);
+  timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K * z);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

@@ -140,10 +140,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int nx = (p.N + BN - 1) / BN;
-  const int bx = blockIdx.x % nx, bym = blockIdx.x / nx;  // n-tiles of one (m-tile, split) adjacent
+  // XCD-aware decode of the 1-D grid: all (m-tile, n-tile) workgroups of one K split read the same dy
+  // rows and x pixels (each n-tile a few filter taps of the same pixels, each m-tile other couts of the
+  // same dy rows). Workgroups are dealt to the 8 XCDs round-robin by linear id, so split S runs on XCD
+  // S % 8 with its tiles back to back and the re-reads hit that XCD's L2 instead of HBM. The grid is
+  // padded to a multiple of 8 splits; padding workgroups exit at once.
+  const int nx = (p.N + BN - 1) / BN, mtiles = (p.M + BM - 1) / BM, per = nx * mtiles;
+  const int sidx = blockIdx.x >> 3;
+  const int split = (sidx / per) * 8 + (blockIdx.x & 7);
+  if (split >= p.batch_inner) return;  // batch_inner carries the split count here
+  const int t = sidx % per;
+  const int bx = t % nx, bym = t / nx;
   const int n0 = bx * BN, m0 = bym * BM;
-  const int kb = blockIdx.z * p.k_per_split;
+  const int kb = split * p.k_per_split;
   const int ke = min(p.K, kb + p.k_per_split);
   const int ntiles = (ke - kb + WBK - 1) / WBK;
 
@@ -200,7 +209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   // acc[i][j][r] = dW[m = mbase + i*16][n = nbase + j*16 + r] -> fp32 slab of this split
   const int g = lane >> 4, ci = lane & 15;
   const int mbase = m0 + wm * (BM / 2) + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
-  float* ws = p.ws + (long long)blockIdx.z * p.M * p.N;
+  float* ws = p.ws + (long long)split * p.M * p.N;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int m = mbase + i * 16;
@@ -213,9 +222,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   }
 }
 
-template <int BM, int BN> int launch_wgrad(const GemmParams& p, int splits, hipStream_t s) {
-  const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN>), dim3(tiles, 1, splits), dim3(256), 0, s, p);
+template <int BM, int BN> int launch_wgrad(const GemmParams& p0, int splits, hipStream_t s) {
+  GemmParams p = p0;
+  p.batch_inner = splits;
+  const long long per = (long long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+  const long long wgs = (splits + 7) / 8 * 8 * per;
+  VCG_REQUIRE(wgs < (1LL << 31), "wgrad grid too large");
+  const int tk = timing_begin(s);
+  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN>), dim3((unsigned)wgs), dim3(256), 0, s, p);
+  timing_end(tk, s, TIMING_WGRAD, 2.0 * p.M * p.N * (double)p.K);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

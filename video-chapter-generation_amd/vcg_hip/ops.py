@@ -56,6 +56,22 @@ def conv_out_hw(H, W, KH, KW, stride, pad):
     return (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
 
 
+TIMING_FAST_GEMM, TIMING_WGRAD = 0, 1
+
+
+def timing_enable(on):
+    """Bracket every fast-GEMM / wgrad launch with HIP events (clears earlier records)."""
+    _lib.call("vcg_timing_enable", int(bool(on)))
+
+
+def timing_query(kernel_id):
+    """(total ms, launches, algorithmic FLOPs) of the recorded launches of one kernel."""
+    import ctypes
+    ms, n, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+    _lib.call("vcg_timing_query", int(kernel_id), ctypes.addressof(ms), ctypes.addressof(n), ctypes.addressof(fl))
+    return ms.value, n.value, fl.value
+
+
 def stats_tiles(M):
     return _lib.query("vcg_conv_stats_tiles", M)
 
