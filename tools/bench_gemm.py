@@ -71,6 +71,18 @@ def main():
     us = timeit(lambda: ops.conv_dgrad(dy, wt, 1024, 56, 56, 256, 64, 1, 1, 1, 0, out=dx))
     print(f"{'l1 dgrad 1x1 64->256':32s} {us:8.1f} us  {2.0 * dx.numel() * 64 / us / 1e6:7.1f} TF/s  "
           f"{(dy.numel() + dx.numel()) * 2 / us / 1e3:7.1f} GB/s")
+    # BERT attention (B=64, 12 heads, L=128, dh=64) as the encoder calls it
+    Bb, nh, L, dh = 64, 12, 128, 64
+    H = nh * dh
+    qkv = torch.randn(Bb * L, 3 * H, device=dev).to(dt)
+    S = torch.empty((Bb * nh, L, L), dtype=dt, device=dev)
+    us = timeit(lambda: ops.gemm_batched(qkv, qkv[:, H:], S, L, L, dh, 3 * H, 3 * H, L, L * 3 * H, dh, L * 3 * H, dh,
+                                         nh * L * L, L * L, Bb, nh))
+    print(f"{'attn QK^T batched':32s} {us:8.1f} us  {2.0 * Bb * nh * L * L * dh / us / 1e6:7.1f} TF/s")
+    ctx = torch.empty((Bb * L, H), dtype=dt, device=dev)
+    us = timeit(lambda: ops.gemm_batched(S, qkv[:, 2 * H:], ctx, L, dh, L, L, 3 * H, H, nh * L * L, L * L, L * 3 * H,
+                                         dh, L * H, dh, Bb, nh, transB=True))
+    print(f"{'attn PV batched (transB)':32s} {us:8.1f} us  {2.0 * Bb * nh * L * L * dh / us / 1e6:7.1f} TF/s")
     # BERT FFN1 / FFN2 / QKV
     for M, Nn, K in ((8192, 3072, 768), (8192, 768, 3072), (8192, 2304, 768)):
         A = torch.randn(M, K, device=dev).to(dt)
