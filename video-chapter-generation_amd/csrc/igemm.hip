@@ -396,7 +396,9 @@ static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
   if (FILE* f = gemm_log()) {
     const bool fast = sizeof(T) == 2 && is_kcontig(AM) && BMD == OP_DENSE_K && fast_gemm_enabled() &&
                       epi != EPI_SPLITK && (splits == 1 || p.batch_inner > 0) && p.K % 8 == 0 &&
-                      (!p.residual || AM == OP_DENSE_K) && !(epi == EPI_STATS && p.bias);
+                      (!p.residual || AM == OP_DENSE_K) && !(epi == EPI_STATS && p.bias) &&
+                      (AM == OP_DENSE_K || (p.a.C >= 64 && p.a.KH * p.a.KW <= 32) ||
+                       (AM == OP_IM2COL && p.a.tsm_fold == 0));
     fprintf(f, "a=%d b=%d epi=%d M=%d N=%d K=%d z=%d fast=%d conv=%dx%d/%d C=%d\n", AM, BMD, epi, p.M, p.N, p.K, splits,
             (int)fast, p.a.KH, p.a.KW, p.a.stride, p.a.C);
     fflush(f);
@@ -405,7 +407,8 @@ static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
     const bool single = splits == 1 || p.batch_inner > 0;
     if (fast_gemm_enabled() && epi != EPI_SPLITK && single && p.K % 8 == 0 && p.a.bytes < 0xFFFFFF00LL &&
         p.b.bytes < 0xFFFFFF00LL && (!p.residual || AM == OP_DENSE_K) &&
-        !(epi == EPI_STATS && p.bias))
+        !(epi == EPI_STATS && p.bias) &&
+        (AM == OP_DENSE_K || (p.a.C >= 64 && p.a.KH * p.a.KW <= 32) || (AM == OP_IM2COL && p.a.tsm_fold == 0)))
       return run_fast_gemm(p, AM, epi, splits, s);
   }
   if (epi == EPI_STORE) return launch_bn<T, AM, BMD, EPI_STORE>(p, splits, s);

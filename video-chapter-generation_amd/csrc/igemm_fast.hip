@@ -21,104 +21,164 @@ constexpr int FBK = 64;
 
 __device__ __forceinline__ int fswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// A-operand gather modes of the fast kernel: OP_IM2COL / OP_DGRAD (C >= 64: one filter tap per 64-wide
+// k tile), OP_IM2COL_TSM (the same with the TSM shift fused), OP_IM2COL_SMALLC (C < 64: the stem)
+constexpr int OP_IM2COL_TSM = 5;
+constexpr int OP_IM2COL_SMALLC = 6;
+
 template <int ROWS, int MODE> struct FastLoader {
   static constexpr int PER_WAVE = ROWS / 32;  // 1-KiB (8-row) slices per wave per tile
+  static constexpr bool GATHER = MODE != OP_DENSE_K;
+  static constexpr bool IM2COL = MODE == OP_IM2COL || MODE == OP_IM2COL_TSM || MODE == OP_IM2COL_SMALLC;
+  static constexpr bool TSM = MODE == OP_IM2COL_TSM;
+  static constexpr bool SMALLC = MODE == OP_IM2COL_SMALLC;
+  static constexpr int BAD = -(1 << 28);  // spatial base of rows beyond M: every bounds test fails
   __amdgpu_buffer_rsrc_t rsrc;
   uint32_t oob;
   // element offsets fit in 31 bits: the dispatcher routes only tensors < 4 GB here (32-bit buffer range)
-  int off[PER_WAVE];  // element offset of the row's base (-1 = invalid row)
+  // Gathers with C >= 64 (one filter tap per 64-wide k tile) keep per row: pb = element offset of the
+  // tap (0,0) source pixel, tm = bit mask of the taps that land inside the image (and, for stride-2
+  // dgrad, on a stride-2 site); the tap's own offset is then a wave-uniform scalar. Other gathers
+  // (the stem, C = 8) keep the pixel coordinates ra/rb and test per lane.
+  int off[PER_WAVE];  // dense: element offset of the row (-1 = invalid row); gather: image base
   int ra[PER_WAVE], rb[PER_WAVE], rc[PER_WAVE], kc[PER_WAVE];
 
   __device__ __forceinline__ void init(const OpArgs& a, long long batch_off, int row0, int wave, int lane) {
     const uint32_t nbytes = (uint32_t)min(a.bytes, (long long)0xFFFFFF00LL);
     rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr), 0, nbytes, 0x00020000);
     oob = nbytes;  // offset + 16 > num_records -> the load returns zeros
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int q = 0; q < PER_WAVE; ++q) {
       const int r = (wave * PER_WAVE + q) * 8 + (lane >> 3);
       kc[q] = 8 * fswz(r, lane & 7);
       const int gr = row0 + r;
       const bool valid = gr < a.rows;
-      if constexpr (MODE == OP_DENSE_K) {
+      if constexpr (!GATHER) {
         off[q] = valid ? (int)(batch_off + (long long)gr * a.ld) : -1;
       } else {
         const int n = gr / (a.GH * a.GW);
         const int rem = gr - n * a.GH * a.GW;
         const int y = rem / a.GW;
         const int x = rem - y * a.GW;
-        off[q] = valid ? n * a.H * a.W * a.C : -1;
-        if constexpr (MODE == OP_IM2COL) {
-          ra[q] = y * a.stride - a.pad;
-          rb[q] = x * a.stride - a.pad;
-          rc[q] = a.tsm_fold > 0 ? (n % a.tsm_T) : 0;
+        off[q] = n * a.H * a.W * a.C;
+        rc[q] = TSM ? (n % a.tsm_T) : 0;
+        int py, px;  // source pixel of tap (0, 0)
+        if constexpr (IM2COL) {
+          py = y * a.stride - a.pad;
+          px = x * a.stride - a.pad;
         } else {
-          ra[q] = y + a.pad;
-          rb[q] = x + a.pad;
-          rc[q] = 0;
+          py = y + a.pad;
+          px = x + a.pad;
+        }
+        if constexpr (!SMALLC) {
+          // valid taps = [kh range (x parity)] x [kw range (x parity)], closed form (no loops: a runtime
+          // loop here makes hipcc move the per-row arrays to scratch)
+          int kh_lo, kh_hi, kw_lo, kw_hi;
+          uint32_t hpar = 0xFFFFFFFFu, wpar = 0xFFFFFFFFu;  // parity filters (stride-2 dgrad)
+          if constexpr (IM2COL) {
+            kh_lo = max(0, -py); kh_hi = min(a.KH, a.H - py);
+            kw_lo = max(0, -px); kw_hi = min(a.KW, a.W - px);
+          } else if (a.stride == 2) {
+            kh_lo = max(0, py - 2 * a.H + 2); kh_hi = min(a.KH, py + 1);
+            kw_lo = max(0, px - 2 * a.W + 2); kw_hi = min(a.KW, px + 1);
+            hpar = (py & 1) ? 0xAAAAAAAAu : 0x55555555u;  // kh = py (mod 2)
+            wpar = (px & 1) ? 0xAAAAAAAAu : 0x55555555u;
+          } else {
+            kh_lo = max(0, py - a.H + 1); kh_hi = min(a.KH, py + 1);
+            kw_lo = max(0, px - a.W + 1); kw_hi = min(a.KW, px + 1);
+          }
+          const int khi = min(max(kw_hi, 0), 31), klo = min(kw_lo, 31);
+          const uint32_t cols = kw_hi > kw_lo ? (((1u << khi) - 1u) & ~((1u << klo) - 1u) & wpar) : 0u;
+          uint32_t rows = 0;  // bit kh*KW for each allowed kh
+#pragma unroll
+          for (int kh = 0; kh < 8; ++kh)
+            rows |= (kh >= kh_lo && kh < kh_hi && ((hpar >> kh) & 1u)) ? (1u << ((kh * a.KW) & 31)) : 0u;
+          rb[q] = valid ? (int)(cols * rows) : 0;
+          // (the source pixel may lie outside the image: multiply, a negative value must not be shifted)
+          if constexpr (IM2COL)
+            ra[q] = off[q] + (py * a.W + px) * a.C;
+          else
+            ra[q] = off[q] + (((a.stride == 2) ? (py >> 1) : py) * a.W + ((a.stride == 2) ? (px >> 1) : px)) * a.C;
+        } else {
+          ra[q] = valid ? py : BAD;
+          rb[q] = px;
         }
       }
     }
   }
 
-  // offset of gathered element (row q, channel c) at tap (kh, kw); -1 if it is padding
-  __device__ __forceinline__ int gather(const OpArgs& a, int q, int kh, int kw, int c) const {
-    if constexpr (MODE == OP_IM2COL) {
-      const int ih = ra[q] + kh, iw = rb[q] + kw;
-      if (off[q] < 0 || ih < 0 || ih >= a.H || iw < 0 || iw >= a.W) return -1;
-      int o = off[q] + ((ih * a.W + iw) << a.logC) + c;
-      if (a.tsm_fold > 0) {
-        const int dt = c < a.tsm_fold ? 1 : (c < 2 * a.tsm_fold ? -1 : 0);
-        const int t2 = rc[q] + dt;
-        if (t2 < 0 || t2 >= a.tsm_T) return -1;
-        o += dt * a.H * a.W * a.C;
-      }
-      return o;
-    } else {  // OP_DGRAD: transposed gather of dy
-      int yy = ra[q] - kh, xx = rb[q] - kw;
-      bool ok = off[q] >= 0 && yy >= 0 && xx >= 0;
+  // general per-lane gather (C < 64): element offset of row q's tap (kh, kw), channel c
+  __device__ __forceinline__ int gather(const OpArgs& a, int q, int kh, int kw, int c, bool& ok) const {
+    int yy, xx;
+    if constexpr (IM2COL) {
+      yy = ra[q] + kh;
+      xx = rb[q] + kw;
+    } else {
+      yy = ra[q] - kh;
+      xx = rb[q] - kw;
       if (a.stride == 2) {
         ok = ok && ((yy | xx) & 1) == 0;
         yy >>= 1;
         xx >>= 1;
       }
-      ok = ok && yy < a.H && xx < a.W;
-      return ok ? off[q] + ((yy * a.W + xx) << a.logC) + c : -1;
     }
+    ok = ok && ((unsigned)yy < (unsigned)a.H) && ((unsigned)xx < (unsigned)a.W);
+    int e = off[q] + ((yy * a.W + xx) << a.logC) + c;
+    if constexpr (TSM) {
+      const int dt = c < a.tsm_fold ? 1 : (c < 2 * a.tsm_fold ? -1 : 0);
+      ok = ok && ((unsigned)(rc[q] + dt) < (unsigned)a.tsm_T);
+      e += dt * (a.H * a.W * a.C);
+    }
+    return e;
   }
 
   // issue the LDS-DMA loads of one 64-wide k tile into `lds` (tile base, [ROWS][64] bf16)
   __device__ __forceinline__ void issue(const OpArgs& a, int k0, int kend, bf16_t* lds, int wave) {
-    if constexpr (MODE != OP_DENSE_K) {
-      if (a.C >= FBK) {
-        // the whole k tile lies in one filter tap: tap / kh / kw are wave-uniform (scalar unit)
+    if constexpr (GATHER && !SMALLC) {
+      {
+        // one filter tap per k tile: tap, its pixel offset and the channel base are scalars
         const int tap = k0 >> a.logC;
         const int kh = tap / a.KW;
         const int kw = tap - kh * a.KW;
         const int cb = k0 & (a.C - 1);
-        const bool tap_ok = k0 < kend && kh < a.KH;
-#pragma unroll
+        int toff;
+        if constexpr (IM2COL) {
+          toff = (kh * a.W + kw) << a.logC;
+        } else {
+          toff = a.stride == 2 ? -((((kh >> 1) * a.W) + (kw >> 1)) << a.logC) : -((kh * a.W + kw) << a.logC);
+        }
+        const uint32_t tbit = k0 < kend ? (1u << tap) : 0u;
+#pragma clang loop unroll(full)
         for (int q = 0; q < PER_WAVE; ++q) {
-          const int e = tap_ok ? gather(a, q, kh, kw, cb + kc[q]) : -1;
-          const uint32_t voff = e >= 0 ? (uint32_t)e * 2u : oob;
+          const int c = cb + kc[q];
+          bool ok = ((uint32_t)rb[q] & tbit) != 0u;
+          int e = ra[q] + toff + c;
+          if constexpr (TSM) {
+            const int dt = c < a.tsm_fold ? 1 : (c < 2 * a.tsm_fold ? -1 : 0);
+            ok = ok && ((unsigned)(rc[q] + dt) < (unsigned)a.tsm_T);
+            e += dt * (a.H * a.W * a.C);
+          }
+          const uint32_t voff = ok ? (uint32_t)e * 2u : oob;
           bf16_t* slice = lds + (wave * PER_WAVE + q) * 512;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)slice, 16, voff, 0, 0, 0);
         }
         return;
       }
     }
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int q = 0; q < PER_WAVE; ++q) {
       const int k = k0 + kc[q];
-      int e = -1;
-      if constexpr (MODE == OP_DENSE_K) {
-        if (off[q] >= 0 && k < kend) e = off[q] + k;
-      } else {
+      uint32_t voff = oob;
+      if constexpr (!GATHER) {
+        if (off[q] >= 0 && k < kend) voff = (uint32_t)(off[q] + k) * 2u;
+      } else {  // C < 64 (stem): per-lane tap
         const int tap = k >> a.logC;
         const int kh = tap / a.KW;
         const int kw = tap - kh * a.KW;
-        if (k < kend && kh < a.KH) e = gather(a, q, kh, kw, k & (a.C - 1));
+        bool ok = k < kend && kh < a.KH;
+        const int e = gather(a, q, kh, kw, k & (a.C - 1), ok);
+        if (ok) voff = (uint32_t)e * 2u;
       }
-      const uint32_t voff = e >= 0 ? (uint32_t)e * 2u : oob;
       bf16_t* slice = lds + (wave * PER_WAVE + q) * 512;  // 1 KiB per slice
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)slice, 16, voff, 0, 0, 0);
     }
@@ -336,7 +396,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
   bf16_t* Bs = As + 2 * AE;
   float* red = reinterpret_cast<float*>(smem + 2 * (AE + BE) * 2);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int nx = (p.N + BN - 1) / BN, gy = gridDim.x / nx;
   int bx, by;
@@ -487,12 +547,20 @@ static int fast_bn(const GemmParams& p, int z, hipStream_t s) {
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   const char* e = getenv("VCG_STAGE_KT");
   p.stage_kt = e && e[0] ? atoi(e) : 1 << 30;
+  if (amode == OP_IM2COL && p.a.tsm_fold > 0) amode = OP_IM2COL_TSM;
+  if (amode == OP_IM2COL && p.a.C < FBK) amode = OP_IM2COL_SMALLC;
+  if (amode == OP_IM2COL_TSM && p.a.C < FBK) return -1;  // (dispatcher keeps these off the fast path)
+  if (amode == OP_DGRAD && p.a.C < FBK) return -1;
   if (epi == EPI_STATS) {
+    if (amode == OP_IM2COL_SMALLC) return fast_bn<OP_IM2COL_SMALLC, EPI_STATS>(p, z, s);
+    if (amode == OP_IM2COL_TSM) return fast_bn<OP_IM2COL_TSM, EPI_STATS>(p, z, s);
     if (amode == OP_IM2COL) return fast_bn<OP_IM2COL, EPI_STATS>(p, z, s);
     if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_STATS>(p, z, s);
     return fast_bn<OP_DENSE_K, EPI_STATS>(p, z, s);
   }
   if (p.residual) return fast_bn<OP_DENSE_K, EPI_STORE, true>(p, z, s);  // dense layers only (BERT bwd)
+  if (amode == OP_IM2COL_SMALLC) return fast_bn<OP_IM2COL_SMALLC, EPI_STORE>(p, z, s);
+  if (amode == OP_IM2COL_TSM) return fast_bn<OP_IM2COL_TSM, EPI_STORE>(p, z, s);
   if (amode == OP_IM2COL) return fast_bn<OP_IM2COL, EPI_STORE>(p, z, s);
   if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_STORE>(p, z, s);
   return fast_bn<OP_DENSE_K, EPI_STORE>(p, z, s);
