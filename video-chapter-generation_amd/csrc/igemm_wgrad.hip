@@ -32,6 +32,10 @@ template <int COLS> __device__ __forceinline__ int wswz(int row, int c) {
   else return c ^ (2 * ((row >> 1) & 3));
 }
 
+// Per lane: one k-row (pixel offset `row` within the 64-pixel step) and one 16-B chunk per instruction.
+// The loader is issued for pixels k0 = kb, kb + 64, kb + 128, ... in order, so the gather keeps each
+// row's pixel coordinates (n, oh, ow, t = n mod T) and advances them by 64 pixels per step with
+// carries (no divisions in the loop); everything is straight-line selects.
 template <int COLS, bool GATHER> struct MNLoader {
   static constexpr int CPR = COLS / 8;          // 16-B chunks per k-row
   static constexpr int RPI = 64 / CPR;          // k-rows per 1-KiB wave instruction (4 or 8)
@@ -39,14 +43,23 @@ template <int COLS, bool GATHER> struct MNLoader {
   __amdgpu_buffer_rsrc_t rsrc;
   uint32_t oob;
   int row[NI];   // k-row of the tile this lane fills
-  int col[NI];   // dense: element column (m0 + 8c), gather: channel ci; -1 = outside N
+  int col[NI];   // dense: element column (m0 + 8c) or -1; gather: channel ci or -1
   int kh[NI], kw[NI], dt[NI];
+  int n[NI], oh[NI], ow[NI], t[NI];  // gather: coordinates of the row's current pixel
+  int dn, doh, dow, dtt;             // gather: a 64-pixel step in (n, oh, ow, t) units (uniform)
 
-  __device__ __forceinline__ void init(const OpArgs& a, int col0, int ncols, int wave, int lane) {
+  __device__ __forceinline__ void init(const OpArgs& a, int col0, int ncols, int kb, int wave, int lane) {
     const uint32_t nbytes = (uint32_t)min(a.bytes, (long long)0xFFFFFF00LL);
     rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr), 0, nbytes, 0x00020000);
     oob = nbytes;
-#pragma unroll
+    if constexpr (GATHER) {
+      const int ohw = a.GH * a.GW;
+      dn = WBK / ohw;
+      doh = (WBK - dn * ohw) / a.GW;
+      dow = WBK - dn * ohw - doh * a.GW;
+      dtt = dn % a.tsm_T;
+    }
+#pragma clang loop unroll(full)
     for (int q = 0; q < NI; ++q) {
       const int inst = wave * NI + q;
       const int r = inst * RPI + lane / CPR;
@@ -63,36 +76,47 @@ template <int COLS, bool GATHER> struct MNLoader {
         kh[q] = h - a.pad;
         kw[q] = tap - h * a.KW - a.pad;
         dt[q] = a.tsm_fold > 0 ? (ci < a.tsm_fold ? 1 : (ci < 2 * a.tsm_fold ? -1 : 0)) : 0;
+        const int k = kb + r;
+        const int nn = (int)fdiv((uint32_t)k, a.fd_ghw);
+        const int rem = k - nn * a.GH * a.GW;
+        const int y = (int)fdiv((uint32_t)rem, a.fd_gw);
+        n[q] = nn;
+        oh[q] = y;
+        ow[q] = rem - y * a.GW;
+        t[q] = nn - (int)fdiv((uint32_t)nn, a.fd_T) * a.tsm_T;
       }
     }
   }
 
-  // pixels k0 .. k0+63 (< kend) into `lds` ([64][COLS] bf16)
+  // pixels k0 .. k0+63 (< kend) into `lds` ([64][COLS] bf16); k0 = kb + 64 * (calls so far)
   __device__ __forceinline__ void issue(const OpArgs& a, int k0, int kend, bf16_t* lds, int wave) {
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int q = 0; q < NI; ++q) {
-      const int k = k0 + row[q];
-      int e = -1;
-      if (col[q] >= 0 && k < kend) {
-        if constexpr (!GATHER) {
-          e = k * (int)a.ld + col[q];
-        } else {
-          const int n = (int)fdiv((uint32_t)k, a.fd_ghw);
-          const int rem = k - n * a.GH * a.GW;
-          const int y = (int)fdiv((uint32_t)rem, a.fd_gw);
-          const int x = rem - y * a.GW;
-          const int ih = y * a.stride + kh[q], iw = x * a.stride + kw[q];
-          bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-          int n2 = n;
-          if (dt[q] != 0) {
-            const int t = n - (int)fdiv((uint32_t)n, a.fd_T) * a.tsm_T + dt[q];
-            ok = ok && t >= 0 && t < a.tsm_T;
-            n2 += dt[q];
-          }
-          if (ok) e = (((n2 * a.H + ih) * a.W + iw) << a.logC) + col[q];
-        }
+      bool ok = col[q] >= 0 && k0 + row[q] < kend;
+      int e;
+      if constexpr (!GATHER) {
+        e = (k0 + row[q]) * (int)a.ld + col[q];
+      } else {
+        const int ih = oh[q] * a.stride + kh[q], iw = ow[q] * a.stride + kw[q];
+        ok = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        ok = ok && (unsigned)(t[q] + dt[q]) < (unsigned)a.tsm_T;
+        e = (((n[q] + dt[q]) * a.H + ih) * a.W + iw) * a.C + col[q];
+        // advance the pixel by 64 (carry ow -> oh -> n, and t = n mod T)
+        int w2 = ow[q] + dow, h2 = oh[q] + doh, n2 = n[q] + dn, t2 = t[q] + dtt;
+        const bool cw = w2 >= a.GW;
+        w2 = cw ? w2 - a.GW : w2;
+        h2 = cw ? h2 + 1 : h2;
+        const bool ch = h2 >= a.GH;
+        h2 = ch ? h2 - a.GH : h2;
+        n2 = ch ? n2 + 1 : n2;
+        t2 = ch ? t2 + 1 : t2;
+        t2 = t2 >= a.tsm_T ? t2 - a.tsm_T : t2;
+        ow[q] = w2;
+        oh[q] = h2;
+        n[q] = n2;
+        t[q] = t2;
       }
-      const uint32_t voff = e >= 0 ? (uint32_t)e * 2u : oob;
+      const uint32_t voff = ok ? (uint32_t)e * 2u : oob;
       bf16_t* slice = lds + (wave * NI + q) * 512;  // 1 KiB per instruction
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)slice, 16, voff, 0, 0, 0);
     }
@@ -138,7 +162,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   bf16_t* As = smem;
   bf16_t* Bs = smem + 2 * AE;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   // XCD-aware decode of the 1-D grid: all (m-tile, n-tile) workgroups of one K split read the same dy
   // rows and x pixels (each n-tile a few filter taps of the same pixels, each m-tile other couts of the
@@ -158,8 +182,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
 
   MNLoader<BM, false> la;
   MNLoader<BN, true> lb;
-  la.init(p.a, m0, p.M, wave, lane);
-  lb.init(p.b, n0, p.N, wave, lane);
+  la.init(p.a, m0, p.M, kb, wave, lane);
+  lb.init(p.b, n0, p.N, kb, wave, lane);
 
   f32x4 acc[MT][NT];
 #pragma unroll
