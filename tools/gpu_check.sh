@@ -6,7 +6,7 @@ TAG=${1:-run}
 SEL=${2:-tests/test_gpu_kernels.py tests/test_gpu_parity.py}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest $SEL -q -m gpu -x > gpurun_out/${TAG}_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest $SEL -q -m gpu -x --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -2 gpurun_out/${TAG}_tests.log
 timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/${TAG}_bench.log; exit 2; }
 tail -1 gpurun_out/${TAG}_bench.log

@@ -14,7 +14,9 @@ namespace {
 
 template <typename T> struct V { static constexpr int N = 16 / sizeof(T); };
 
-constexpr int EW_ITER = 8;
+constexpr int SU = 4;                // 16-B vectors per thread per batch (all loads issued before use)
+constexpr int SB = 256 * SU;         // vectors per block per batch
+constexpr long long GRID_MAX = 2048;  // streaming grids: 8 blocks per CU, grid-stride beyond
 constexpr int RED_ITER_MAX = 256;  // vectors per thread of bn_bwd_reduce (adaptive: >= ~1024 blocks)
 
 template <int VN>
@@ -63,8 +65,9 @@ __host__ __device__ inline int ilog2i(int x) {
 
 // ------------------------------------------------------------------ BN apply
 // out = act(fma(y, scale, shift) + [fma(res, rscale, rshift) | res]); bits (optional): ReLU mask of
-// out, one byte per 16-B vector (the backward's VCG_MASK_BITS)
-template <typename T>
+// out, one byte per 16-B vector (the backward's VCG_MASK_BITS). Grid-stride over batches of SU
+// vectors per thread; every load of a batch is issued before the first use.
+template <typename T, bool RES, bool RAFF>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const T* __restrict__ res,
                                                        const float* __restrict__ rscale,
@@ -72,55 +75,49 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, 
                                                        T* __restrict__ out, uint8_t* __restrict__ bits, long long TV,
                                                        int cpr) {
   constexpr int VN = V<T>::N;
-  const long long base = (long long)blockIdx.x * (256 * EW_ITER) + threadIdx.x;
+  const long long stride = (long long)gridDim.x * SB;
+  long long base = (long long)blockIdx.x * SB + threadIdx.x;
   const bool fixed = cpr <= 256;
-  int c0 = (int)(base & (cpr - 1)) * VN;
   float sc[VN], sh[VN], rs[VN], rb[VN];
-  load_params<VN>(scale, c0, sc);
-  load_params<VN>(shift, c0, sh);
-  if (rscale) {
-    load_params<VN>(rscale, c0, rs);
-    load_params<VN>(rshift, c0, rb);
-  }
-#pragma unroll 4
-  for (int it = 0; it < EW_ITER; ++it) {
-    const long long v = base + it * 256;
-    if (v >= TV) break;
-    if (!fixed && it > 0) {
-      c0 = (int)(v & (cpr - 1)) * VN;
-      load_params<VN>(scale, c0, sc);
-      load_params<VN>(shift, c0, sh);
-      if (rscale) {
-        load_params<VN>(rscale, c0, rs);
-        load_params<VN>(rshift, c0, rb);
+  auto params = [&](long long v) {
+    const int c0 = (int)(v & (cpr - 1)) * VN;
+    load_params<VN>(scale, c0, sc);
+    load_params<VN>(shift, c0, sh);
+    if (RAFF) {
+      load_params<VN>(rscale, c0, rs);
+      load_params<VN>(rshift, c0, rb);
+    }
+  };
+  params(base);
+  for (; base < TV; base += stride) {
+    float a[SU][VN], r[SU][VN];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const long long v = base + u * 256;
+      if (v < TV) {
+        load16<T>(y + v * VN, a[u]);
+        if (RES) load16<T>(res + v * VN, r[u]);
       }
     }
-    float a[VN];
-    load16<T>(y + v * VN, a);
 #pragma unroll
-    for (int e = 0; e < VN; ++e) a[e] = fmaf(a[e], sc[e], sh[e]);
-    if (res) {
-      float r[VN];
-      load16<T>(res + v * VN, r);
-      if (rscale) {
+    for (int u = 0; u < SU; ++u) {
+      const long long v = base + u * 256;
+      if (v >= TV) break;
+      if (!fixed) params(v);
 #pragma unroll
-        for (int e = 0; e < VN; ++e) a[e] += fmaf(r[e], rs[e], rb[e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < VN; ++e) a[e] += r[e];
+      for (int e = 0; e < VN; ++e) {
+        float o = fmaf(a[u][e], sc[e], sh[e]);
+        if (RES) o += RAFF ? fmaf(r[u][e], rs[e], rb[e]) : r[u][e];
+        a[u][e] = relu ? fmaxf(o, 0.f) : o;
       }
-    }
-    if (relu) {
+      if (bits) {
+        unsigned b = 0;
 #pragma unroll
-      for (int e = 0; e < VN; ++e) a[e] = fmaxf(a[e], 0.f);
+        for (int e = 0; e < VN; ++e) b |= (a[u][e] > 0.f ? 1u : 0u) << e;
+        bits[v] = (uint8_t)b;
+      }
+      store16<T>(out + v * VN, a[u]);
     }
-    if (bits) {
-      unsigned b = 0;
-#pragma unroll
-      for (int e = 0; e < VN; ++e) b |= (a[e] > 0.f ? 1u : 0u) << e;
-      bits[v] = (uint8_t)b;
-    }
-    store16<T>(out + v * VN, a);
   }
 }
 
@@ -129,7 +126,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, 
 // Each thread owns one 16-B channel chunk for the whole block (cpr <= 256: 256/cpr threads share a
 // chunk and walk interleaved rows; cpr > 256: blockIdx.y selects 256 chunks, threads walk all rows),
 // and threads sharing a chunk are combined through LDS in a fixed order: deterministic.
-template <typename T>
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dout, MaskArgs mk,
                                                             const T* __restrict__ y, const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long long P, int cpr,
@@ -146,23 +143,38 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   float mu[VN], is[VN], sg[VN], sx[VN], msc[VN], msh[VN];
   load_params<VN>(mean, c0, mu);
   load_params<VN>(invstd, c0, is);
-  if (mk.mode == 3) {
+  if (MODE == 3) {
     load_params<VN>(mk.sc, c0, msc);
     load_params<VN>(mk.sh, c0, msh);
   }
 #pragma unroll
   for (int e = 0; e < VN; ++e) { sg[e] = 0.f; sx[e] = 0.f; }
-#pragma unroll 4
-  for (long long r = r0 + (narrow ? tid / cpr : 0); r < r1; r += rstep) {
-    const long long v = r * cpr + chunk;
-    float d[VN], yv[VN];
-    load16<T>(dout + v * VN, d);
-    load16<T>(y + v * VN, yv);
-    apply_mask<T, VN>(d, mk, v, yv, msc, msh);
+  for (long long r = r0 + (narrow ? tid / cpr : 0); r < r1; r += (long long)rstep * SU) {
+    float d[SU][VN], yv[SU][VN];
 #pragma unroll
-    for (int e = 0; e < VN; ++e) {
-      sg[e] += d[e];
-      sx[e] += d[e] * (yv[e] - mu[e]) * is[e];
+    for (int u = 0; u < SU; ++u) {
+      const long long rr = r + (long long)u * rstep;
+      if (rr < r1) {
+        const long long v = rr * cpr + chunk;
+        load16<T>(dout + v * VN, d[u]);
+        load16<T>(y + v * VN, yv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const long long rr = r + (long long)u * rstep;
+      if (rr >= r1) break;
+      const long long v = rr * cpr + chunk;
+      if (MODE != 0) {
+        MaskArgs m = mk;
+        m.mode = MODE;
+        apply_mask<T, VN>(d[u], m, v, yv[u], msc, msh);
+      }
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        sg[e] += d[u][e];
+        sx[e] += d[u][e] * (yv[u][e] - mu[e]) * is[e];
+      }
     }
   }
   float* out = partial + (long long)blockIdx.x * 2 * C;
@@ -229,59 +241,70 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
 // dy = A*g + B*y + Cc per channel (batch-stat BN backward folded to an affine map of (g, y)):
 //   A = gamma*invstd, B = -A*invstd*sum_gx/N, Cc = -A*sum_g/N - B*mean ; running mode: dy = A*g.
 // optionally gout = g (masked upstream gradient: the residual path)
-template <typename T>
+template <typename T, int MODE, bool TRAIN>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dout, MaskArgs mk,
                                                            const T* __restrict__ y, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ sum_g,
                                                            const float* __restrict__ sum_gx, float inv_count,
-                                                           int train_stats, T* __restrict__ dy, T* __restrict__ gout,
-                                                           long long TV, int cpr) {
+                                                           T* __restrict__ dy, T* __restrict__ gout, long long TV,
+                                                           int cpr) {
   constexpr int VN = V<T>::N;
-  const long long base = (long long)blockIdx.x * (256 * EW_ITER) + threadIdx.x;
+  constexpr bool NEED_Y = TRAIN || MODE == 3;
+  const long long stride = (long long)gridDim.x * SB;
+  long long base = (long long)blockIdx.x * SB + threadIdx.x;
+  const bool fixed = cpr <= 256;
   float A[VN], Bc[VN], Cc[VN], msc[VN], msh[VN];
-  int c_loaded = -1;
-  const bool need_y = train_stats || mk.mode == 3;
-#pragma unroll 4
-  for (int it = 0; it < EW_ITER; ++it) {
-    const long long v = base + it * 256;
-    if (v >= TV) break;
+  auto params = [&](long long v) {
     const int c0 = (int)(v & (cpr - 1)) * VN;
-    if (c0 != c_loaded) {
+    float is[VN];
+    load_params<VN>(invstd, c0, is);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) A[e] = (gamma ? gamma[c0 + e] : 1.f) * is[e];
+    if (TRAIN) {
+      float sgx[VN], sgg[VN], mu[VN];
+      load_params<VN>(sum_gx, c0, sgx);
+      load_params<VN>(sum_g, c0, sgg);
+      load_params<VN>(mean, c0, mu);
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
-        const int c = c0 + e;
-        const float is = invstd[c];
-        const float a = (gamma ? gamma[c] : 1.f) * is;
-        A[e] = a;
-        if (train_stats) {
-          Bc[e] = -a * is * sum_gx[c] * inv_count;
-          Cc[e] = -a * sum_g[c] * inv_count - Bc[e] * mean[c];
-        } else {
-          Bc[e] = 0.f;
-          Cc[e] = 0.f;
-        }
+        Bc[e] = -A[e] * is[e] * sgx[e] * inv_count;
+        Cc[e] = -A[e] * sgg[e] * inv_count - Bc[e] * mu[e];
       }
-      if (mk.mode == 3) {
-        load_params<VN>(mk.sc, c0, msc);
-        load_params<VN>(mk.sh, c0, msh);
+    }
+    if (MODE == 3) {
+      load_params<VN>(mk.sc, c0, msc);
+      load_params<VN>(mk.sh, c0, msh);
+    }
+  };
+  params(base);
+  for (; base < TV; base += stride) {
+    float d[SU][VN], yv[SU][VN];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const long long v = base + u * 256;
+      if (v < TV) {
+        load16<T>(dout + v * VN, d[u]);
+        if (NEED_Y) load16<T>(y + v * VN, yv[u]);
       }
-      c_loaded = c0;
     }
-    float d[VN], yv[VN], o[VN];
-    load16<T>(dout + v * VN, d);
-    if (need_y) load16<T>(y + v * VN, yv);
-    apply_mask<T, VN>(d, mk, v, yv, msc, msh);
-    if (gout) store16<T>(gout + v * VN, d);
-    if (train_stats) {
 #pragma unroll
-      for (int e = 0; e < VN; ++e) o[e] = A[e] * d[e] + Bc[e] * yv[e] + Cc[e];
-    } else {
+    for (int u = 0; u < SU; ++u) {
+      const long long v = base + u * 256;
+      if (v >= TV) break;
+      if (!fixed) params(v);
+      if (MODE != 0) {
+        MaskArgs m = mk;
+        m.mode = MODE;
+        apply_mask<T, VN>(d[u], m, v, yv[u], msc, msh);
+      }
+      if (gout) store16<T>(gout + v * VN, d[u]);
+      float o[VN];
 #pragma unroll
-      for (int e = 0; e < VN; ++e) o[e] = A[e] * d[e];
+      for (int e = 0; e < VN; ++e) o[e] = TRAIN ? A[e] * d[u][e] + Bc[e] * yv[u][e] + Cc[e] : A[e] * d[u][e];
+      store16<T>(dy + v * VN, o);
     }
-    store16<T>(dy + v * VN, o);
   }
 }
 
@@ -365,46 +388,56 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
 
 // ------------------------------------------------------------------ TSM gradient combine
 // dx = unshift(dshift) + other over NHWC [N*T][H][W][C] (adjoint of ops/temporal_shift.py:45-47)
-template <typename T>
+template <typename T, bool OTHER, bool BITS>
 __global__ __launch_bounds__(256) void tsm_unshift_add_kernel(const T* __restrict__ dshift, const T* __restrict__ other,
                                                               const uint8_t* __restrict__ other_bits,
-                                                              T* __restrict__ dx, long long TV, int lcpr, int HW,
-                                                              int Tn, int fold_chunks) {
+                                                              T* __restrict__ dx, unsigned TV, int lcpr,
+                                                              unsigned row_vecs, int Tn, int fold_chunks) {
   constexpr int VN = V<T>::N;
-  const long long base = (long long)blockIdx.x * (256 * EW_ITER) + threadIdx.x;
-  const long long row_vecs = (long long)HW << lcpr;  // vectors per frame
-#pragma unroll 4
-  for (int it = 0; it < EW_ITER; ++it) {
-    const long long v = base + it * 256;
-    if (v >= TV) break;
-    const int chunk = (int)(v & ((1 << lcpr) - 1));
-    int dt = 0;
-    if (chunk < fold_chunks) dt = -1;
-    else if (chunk < 2 * fold_chunks) dt = 1;
-    float a[VN];
-    bool have = true;
-    if (dt != 0) {
-      const int frame = (int)(v / row_vecs);
-      const int t = frame % Tn;
-      have = (t + dt >= 0) && (t + dt < Tn);
-    }
-    if (have) load16<T>(dshift + (v + dt * row_vecs) * VN, a);
-    else {
+  const unsigned stride = gridDim.x * SB;
+  const int cmask = (1 << lcpr) - 1;
+  for (unsigned base = blockIdx.x * SB + threadIdx.x; base < TV; base += stride) {
+    float a[SU][VN], b[SU][VN];
+    unsigned m[SU];
 #pragma unroll
-      for (int e = 0; e < VN; ++e) a[e] = 0.f;
-    }
-    if (other) {
-      float b[VN];
-      load16<T>(other + v * VN, b);
-      const unsigned m = other_bits ? other_bits[v] : 0xFFu;  // residual gradient through the ReLU mask
+    for (int u = 0; u < SU; ++u) {
+      const unsigned v = base + u * 256;
+      if (v >= TV) continue;
+      const int chunk = (int)(v & cmask);
+      int dt = 0;
+      if (chunk < fold_chunks) dt = -1;
+      else if (chunk < 2 * fold_chunks) dt = 1;
+      bool have = true;
+      if (dt != 0) {
+        const int t = (int)((v / row_vecs) % (unsigned)Tn);
+        have = (t + dt >= 0) && (t + dt < Tn);
+      }
+      if (have) load16<T>(dshift + ((long long)v + dt * (long long)row_vecs) * VN, a[u]);
+      else {
 #pragma unroll
-      for (int e = 0; e < VN; ++e) a[e] += ((m >> e) & 1u) ? b[e] : 0.f;
+        for (int e = 0; e < VN; ++e) a[u][e] = 0.f;
+      }
+      if (OTHER) load16<T>(other + (long long)v * VN, b[u]);
+      m[u] = BITS ? other_bits[v] : 0xFFu;  // residual gradient through the ReLU mask
     }
-    store16<T>(dx + v * VN, a);
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const unsigned v = base + u * 256;
+      if (v >= TV) break;
+      if (OTHER) {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) a[u][e] += ((m[u] >> e) & 1u) ? b[u][e] : 0.f;
+      }
+      store16<T>(dx + (long long)v * VN, a[u]);
+    }
   }
 }
 
 inline unsigned blocks_for(long long TV, int per_block) { return (unsigned)((TV + per_block - 1) / per_block); }
+inline unsigned stream_grid(long long TV) {
+  const long long b = (TV + SB - 1) / SB;
+  return (unsigned)(b < GRID_MAX ? b : GRID_MAX);
+}
 
 }  // namespace
 
@@ -418,13 +451,23 @@ VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const flo
   const long long TV = P * C / VN;
   const int cpr = C / VN;
   if (TV == 0) return VCG_OK;
-  const unsigned g = blocks_for(TV, 256 * EW_ITER);
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
-                       (const bf16_t*)res, rscale, rshift, relu, (bf16_t*)out, bits, TV, cpr);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)y, scale, shift,
-                       (const float*)res, rscale, rshift, relu, (float*)out, bits, TV, cpr);
+  const unsigned g = stream_grid(TV);
+  const bool raff = rscale != nullptr;
+  VCG_REQUIRE(!raff || (res && rshift), "rscale needs res and rshift");
+#define VCG_BN_APPLY(T, R, A)                                                                                     \
+  hipLaunchKernelGGL((bn_apply_kernel<T, R, A>), dim3(g), dim3(256), 0, s, (const T*)y, scale, shift, (const T*)res, \
+                     rscale, rshift, relu, (T*)out, bits, TV, cpr)
+#define VCG_BN_APPLY_T(T)                     \
+  if (!res) VCG_BN_APPLY(T, false, false);    \
+  else if (!raff) VCG_BN_APPLY(T, true, false); \
+  else VCG_BN_APPLY(T, true, true);
+  if (dtype == VCG_BF16) {
+    VCG_BN_APPLY_T(bf16_t)
+  } else {
+    VCG_BN_APPLY_T(float)
+  }
+#undef VCG_BN_APPLY_T
+#undef VCG_BN_APPLY
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -482,12 +525,23 @@ VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, int mask_mode, const 
   const long long nb = bn_bwd_blocks(P, C, VN);
   const int rows = (int)bn_bwd_rows(P, C, VN);
   const dim3 grid((unsigned)nb, cpr > 256 ? cpr / 256 : 1);
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dout, mk,
-                       (const bf16_t*)y, mean, invstd, P, cpr, C, rows, ws);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, grid, dim3(256), 0, s, (const float*)dout, mk,
-                       (const float*)y, mean, invstd, P, cpr, C, rows, ws);
+#define VCG_BN_RED(T, M)                                                                                  \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, M>), grid, dim3(256), 0, s, (const T*)dout, mk, (const T*)y, mean, \
+                     invstd, P, cpr, C, rows, ws)
+#define VCG_BN_RED_T(T)                \
+  switch (mask_mode) {                 \
+    case 0: VCG_BN_RED(T, 0); break;   \
+    case 1: VCG_BN_RED(T, 1); break;   \
+    case 2: VCG_BN_RED(T, 2); break;   \
+    default: VCG_BN_RED(T, 3); break;  \
+  }
+  if (dtype == VCG_BF16) {
+    VCG_BN_RED_T(bf16_t)
+  } else {
+    VCG_BN_RED_T(float)
+  }
+#undef VCG_BN_RED_T
+#undef VCG_BN_RED
   VCG_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, sum_g, sum_gx,
                      dgamma, dbeta, accumulate);
@@ -506,15 +560,25 @@ VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, int mask_mode, const v
   VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
   const long long TV = P * C / VN;
   const float ic = 1.f / (float)count;
-  const unsigned g = blocks_for(TV, 256 * EW_ITER);
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)dout, mk,
-                       (const bf16_t*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats, (bf16_t*)dy,
-                       (bf16_t*)gout, TV, C / VN);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)dout, mk,
-                       (const float*)y, mean, invstd, gamma, sum_g, sum_gx, ic, train_stats, (float*)dy,
-                       (float*)gout, TV, C / VN);
+  const unsigned g = stream_grid(TV);
+  const int cpr = C / VN;
+#define VCG_BN_BAPP(T, M, TR)                                                                                    \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, M, TR>), dim3(g), dim3(256), 0, s, (const T*)dout, mk, (const T*)y, \
+                     mean, invstd, gamma, sum_g, sum_gx, ic, (T*)dy, (T*)gout, TV, cpr)
+#define VCG_BN_BAPP_M(T, TR)               \
+  switch (mask_mode) {                     \
+    case 0: VCG_BN_BAPP(T, 0, TR); break;  \
+    case 1: VCG_BN_BAPP(T, 1, TR); break;  \
+    case 2: VCG_BN_BAPP(T, 2, TR); break;  \
+    default: VCG_BN_BAPP(T, 3, TR); break; \
+  }
+  if (dtype == VCG_BF16) {
+    if (train_stats) { VCG_BN_BAPP_M(bf16_t, true) } else { VCG_BN_BAPP_M(bf16_t, false) }
+  } else {
+    if (train_stats) { VCG_BN_BAPP_M(float, true) } else { VCG_BN_BAPP_M(float, false) }
+  }
+#undef VCG_BN_BAPP_M
+#undef VCG_BN_BAPP
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -560,14 +624,25 @@ VCG_API int vcg_tsm_unshift_add(int dtype, const void* dshift, const void* other
   const int VN = dtype == VCG_BF16 ? 8 : 4;
   VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && fold % VN == 0, "C / fold must be multiples of the vector width");
   const long long TV = NT * HW * C / VN;
+  VCG_REQUIRE(TV < (1LL << 31), "tensor too large for 32-bit vector indices");
   const int lcpr = ilog2i(C / VN);
-  const unsigned g = blocks_for(TV, 256 * EW_ITER);
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(tsm_unshift_add_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)dshift,
-                       (const bf16_t*)other, other_bits, (bf16_t*)dx, TV, lcpr, (int)HW, T, fold / VN);
-  else
-    hipLaunchKernelGGL(tsm_unshift_add_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)dshift,
-                       (const float*)other, other_bits, (float*)dx, TV, lcpr, (int)HW, T, fold / VN);
+  const unsigned g = stream_grid(TV);
+  const unsigned row_vecs = (unsigned)(HW * C / VN);
+#define VCG_TSM(T, O, B)                                                                                           \
+  hipLaunchKernelGGL((tsm_unshift_add_kernel<T, O, B>), dim3(g), dim3(256), 0, s, (const T*)dshift, (const T*)other, \
+                     other_bits, (T*)dx, (unsigned)TV, lcpr, row_vecs, T_, fold / VN)
+#define VCG_TSM_T(T)                         \
+  if (!other) VCG_TSM(T, false, false);      \
+  else if (!other_bits) VCG_TSM(T, true, false); \
+  else VCG_TSM(T, true, true);
+  const int T_ = T;
+  if (dtype == VCG_BF16) {
+    VCG_TSM_T(bf16_t)
+  } else {
+    VCG_TSM_T(float)
+  }
+#undef VCG_TSM_T
+#undef VCG_TSM
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
