@@ -49,6 +49,12 @@ VCG_API int vcg_conv_stats_tiles(int M);
 VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
 /* autograd of conv2d: input gradient (transposed-conv gather) */
 VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, hipStream_t stream);
+/* vcg_conv_dgrad fused with the trunk backward's next steps (igemm.h BwdEpi): TSM adjoint (tsm_fold > 0:
+   ops/temporal_shift.py:33-51 autograd), + res, ReLU mask (bits or fma(y, mscale, mshift) > 0), stored as g, and
+   the BatchNorm backward reductions against y (and y2) -> sum_g / sum_gx (/ sum_gx2), dgamma / dbeta
+   (/ dgamma2 / dbeta2) accumulated. bf16 fast engine only; VCG_ERR_UNSUPPORTED elsewhere. */
+VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C);
+VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, const void* res, const unsigned char* bits, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, const void* y2, const float* mean2, const float* invstd2, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, float* sum_gx2, float* dgamma2, float* dbeta2, hipStream_t s);
 /* autograd of conv2d: weight gradient, split-K over pixels, written in OIHW (state-dict layout) */
 VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad);
 VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
@@ -84,6 +90,8 @@ VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, in
    are HOST pointers to 3 floats. */
 VCG_API int vcg_window_frames_u8(int dtype, const uint8_t* frames, const long long* idx, void* dst, long long n_rows, int F, int H, int W, const float* mean3, const float* std3, hipStream_t s);
 VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int KH, int KW, int Cpad, int transposed, hipStream_t s);
+/* out[c][r] = in[r][c] ([rows][cols], leading dims ld_in / ld_out): W^T for the BERT input-gradient GEMMs */
+VCG_API int vcg_transpose(int dtype, const void* in, void* out, int rows, int cols, long long ld_in, long long ld_out, hipStream_t s);
 VCG_API int vcg_cast_from_f32(int dtype, const float* in, void* out, long long n, hipStream_t s);
 VCG_API int vcg_cast_to_f32(int dtype, const void* in, float* out, long long n, hipStream_t s);
 /* TemporalShift.shift (ops/temporal_shift.py:33-51) on NCHW; direction 1 = its adjoint */

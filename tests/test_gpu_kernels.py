@@ -229,13 +229,15 @@ def test_gemm(K, dtype, tA, tB):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-def test_gemm_splitk(K, dtype):
-    M, N, Kd = 64, 768, 5000
-    A = _rand((Kd, M), dtype, 12)
-    B = _rand((Kd, N), dtype, 13)
+@pytest.mark.parametrize("shape", [(64, 768, 5000, 64, 768), (200, 136, 1000, 256, 144), (768, 3072, 8192, 768, 3072)])
+def test_gemm_splitk(K, dtype, shape):
+    # transA = transB = 1 (dW = dY^T X of the linear layers)
+    M, N, Kd, lda, ldb = shape
+    A = _rand((Kd, lda), dtype, 12)
+    B = _rand((Kd, ldb), dtype, 13)
     out = torch.ones((M, N), dtype=torch.float32, device=DEV)
-    K.gemm_splitk(A.to(DEV), B.to(DEV), out, M, N, Kd, M, N, transA=True, transB=True, accumulate=True)
-    _close(out - 1, A.double().t() @ B.double(), dtype, "gemm splitk")
+    K.gemm_splitk(A.to(DEV), B.to(DEV), out, M, N, Kd, lda, ldb, transA=True, transB=True, accumulate=True)
+    _close(out - 1, A[:, :M].double().t() @ B[:, :N].double(), dtype, "gemm splitk")
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -363,3 +365,83 @@ def test_window_frames_u8_bitexact(K):
         assert y.shape == (idx.numel(), H, W, 8)
         assert torch.equal(y[..., 3:], torch.zeros_like(y[..., 3:]))
         assert torch.equal(y[..., :3], ref.to(dt)), dt
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(2304, 768), (70, 129), (1, 64)])
+def test_transpose(K, dtype, shape):
+    x = _rand(shape, dtype, 21)
+    y = K.transpose(x.to(DEV))
+    assert torch.equal(y.cpu(), x.t().contiguous()), "transpose must be an exact copy"
+
+
+# (N, H, W, C = dgrad output channels, Cout, k, stride, pad, T) of the fused trunk-backward dgrad
+DGRAD_BWD_CASES = [
+    (8, 9, 9, 64, 64, 3, 1, 1, 4),     # conv2 3x3
+    (8, 10, 10, 64, 128, 3, 2, 1, 4),  # conv2 3x3 / 2 (block 0 of a stage)
+    (8, 7, 7, 64, 256, 1, 1, 0, 4),    # conv3 / conv1 1x1 (dense)
+    (8, 6, 6, 128, 64, 1, 1, 0, 8),    # wider C: BN = 128 tiles
+]
+
+
+@pytest.mark.parametrize("case", DGRAD_BWD_CASES)
+@pytest.mark.parametrize("mode", ["affine", "tsm_bits_two", "tsm_plain"])
+def test_conv_dgrad_bwd(K, case, mode):
+    """Fused dgrad epilogue == the unfused ops (dgrad, TSM combine, masks) bit for bit; its BN sums == a
+    float64 reduction of the same g."""
+    dtype = torch.bfloat16
+    N, H, W, C, Cout, k, s, p, T = case
+    OH, OW = K.conv_out_hw(H, W, k, k, s, p)
+    dy = _rand((N, OH, OW, Cout), dtype, 61).to(DEV)
+    w = _rand((Cout, C, k, k), torch.float32, 62, 0.1).to(DEV)
+    wt = K.weight_prep(w, C, dtype, transposed=True)
+    y = _rand((N, H, W, C), dtype, 63).to(DEV)
+    y2 = _rand((N, H, W, C), dtype, 64).to(DEV)
+    res = _rand((N, H, W, C), dtype, 65).to(DEV)
+    g0 = torch.Generator().manual_seed(66)
+    mean = (torch.randn(C, generator=g0) * 0.1).to(DEV)
+    inv = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    # dyadic mask parameters: y * msc + msh is exact in f32, so torch's unfused test == the kernel's fma
+    msc = (torch.tensor([0.5, 1.0, 2.0, -0.5, -1.0, -2.0])[torch.randint(0, 6, (C,), generator=g0)]).to(DEV)
+    msh = (torch.randint(-16, 17, (C,), generator=g0).float() / 64).to(DEV)
+    mean2 = (torch.randn(C, generator=g0) * 0.1).to(DEV)
+    inv2 = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    dx = K.conv_dgrad(dy, wt, N, H, W, C, Cout, k, k, s, p)
+    sums = torch.zeros((2, C), device=DEV)
+    sgx2 = torch.zeros(C, device=DEV)
+    dgam, dbet = torch.full((C,), 0.5, device=DEV), torch.full((C,), 0.25, device=DEV)
+    dgam2, dbet2 = torch.full((C,), 0.5, device=DEV), torch.full((C,), 0.25, device=DEV)
+    if mode == "affine":
+        g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, k, k, s, p, y=y, mean=mean, invstd=inv, mscale=msc,
+                             mshift=msh, sums=sums, dgamma=dgam, dbeta=dbet)
+        keep = y.float() * msc + msh > 0
+        ref = torch.where(keep, dx, torch.zeros_like(dx))
+    else:
+        fold = C // 8
+        _, bits = K.bn_apply(y2, torch.ones(C, device=DEV), torch.zeros(C, device=DEV), C, relu=True, bits=True)
+        comb = K.tsm_unshift_add(dx, res, N, T, H * W, C, fold)
+        if mode == "tsm_plain":
+            g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, k, k, s, p, tsm_T=T, tsm_fold=fold, res=res)
+            ref = comb
+        else:
+            g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, k, k, s, p, tsm_T=T, tsm_fold=fold, res=res, bits=bits,
+                                 y=y, mean=mean, invstd=inv, y2=y2, mean2=mean2, invstd2=inv2, sums=sums,
+                                 sum_gx2=sgx2, dgamma=dgam, dbeta=dbet, dgamma2=dgam2, dbeta2=dbet2)
+            ref = torch.where(y2 > 0, comb, torch.zeros_like(comb))
+    assert g is not None, "the fused bf16 engine must take this shape"
+    assert torch.equal(g, ref), f"g differs: max {(g.float() - ref.float()).abs().max().item():.3e}"
+    if mode == "tsm_plain":
+        return
+    gd = g.double().reshape(-1, C)
+    sg = gd.sum(0)
+    sx = (gd * (y.double().reshape(-1, C) - mean.double()) * inv.double()).sum(0)
+    tol = lambda r: 1e-4 * (r.abs().max().item() + 1.0)  # noqa: E731
+    assert (sums[0].double() - sg).abs().max().item() <= tol(sg)
+    assert (sums[1].double() - sx).abs().max().item() <= tol(sx)
+    assert (dbet.double() - 0.25 - sg).abs().max().item() <= tol(sg)
+    assert (dgam.double() - 0.5 - sx).abs().max().item() <= tol(sx)
+    if mode == "tsm_bits_two":
+        sx2 = (gd * (y2.double().reshape(-1, C) - mean2.double()) * inv2.double()).sum(0)
+        assert (sgx2.double() - sx2).abs().max().item() <= tol(sx2)
+        assert (dgam2.double() - 0.5 - sx2).abs().max().item() <= tol(sx2)
+        assert (dbet2.double() - 0.25 - sg).abs().max().item() <= tol(sg)

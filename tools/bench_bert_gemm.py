@@ -1,0 +1,59 @@
+"""Micro-benchmark of the BERT-base GEMMs at B=64 x L=128 (8192 token rows), bf16, HIP events:
+forward projections (with / without the GELU + pre-activation epilogue), input-gradient GEMMs
+(W^T materialised vs the transposed-B generic path) and weight-gradient split-K GEMMs.
+Usage: python tools/bench_bert_gemm.py"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "video-chapter-generation_amd"))
+from vcg_hip import ops  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3  # us
+
+
+def main():
+    dt, dev = torch.bfloat16, "cuda"
+    R, H, I = 8192, 768, 3072
+    x = torch.randn(R, H, device=dev).to(dt)
+    xi = torch.randn(R, I, device=dev).to(dt)
+    for (N, K, name) in ((3 * H, H, "qkv"), (H, H, "out-proj"), (I, H, "ffn1"), (H, I, "ffn2")):
+        W = (torch.randn(N, K, device=dev) * 0.02).to(dt)
+        b = torch.zeros(N, device=dev)
+        A = x if K == H else xi
+        fl = 2.0 * R * N * K
+        t = timeit(lambda: ops.gemm(A, W, R, N, K, K, K, bias=b))
+        line = [f"{name:9s} fwd {t:7.1f}us {fl / t / 1e6:6.0f}TF/s"]
+        if name == "ffn1":
+            pre = torch.empty(R, N, dtype=dt, device=dev)
+            t = timeit(lambda: ops.gemm(A, W, R, N, K, K, K, bias=b, act=ops.ACT_GELU, aux=pre))
+            line.append(f"gelu+aux {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
+        # input gradient: dA [R, K] = dY [R, N] @ W [N, K]
+        dY = torch.randn(R, N, device=dev).to(dt)
+        t = timeit(lambda: ops.gemm(dY, W, R, K, N, N, K, transB=True))
+        line.append(f"dX transB {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
+        t = timeit(lambda: ops.gemm(dY, ops.transpose(W), R, K, N, N, N))
+        line.append(f"dX W^T {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
+        t = timeit(lambda: ops.transpose(W))
+        line.append(f"(transpose {t:5.1f}us)")
+        gW = torch.zeros(N, K, device=dev)
+        wsb = ops.gemm_splitk(dY, A, gW, N, K, R, N, K, transA=True, transB=True)
+        t = timeit(lambda: ops.gemm_splitk(dY, A, gW, N, K, R, N, K, transA=True, transB=True, workspace=wsb))
+        line.append(f"dW {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
+        print("  ".join(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

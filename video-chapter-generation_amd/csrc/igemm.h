@@ -5,7 +5,7 @@
 namespace vcg {
 
 enum { OP_DENSE_K = 0, OP_IM2COL = 1, OP_DGRAD = 2, OP_DENSE_MN = 3, OP_IM2COL_T = 4 };
-enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2 };
+enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
 
 template <typename T> struct Cfg;
@@ -49,6 +49,31 @@ struct OpArgs {
   FastDiv fd_ghw, fd_gw, fd_T;
 };
 
+// EPI_BWD (fast kernel, conv dgrad): the epilogue of a conv input gradient inside the trunk backward.
+// Per output element (row m, column n), in this order:
+//   * TSM adjoint (tsm_T > 0): the value moves to row m + hw (n < fold) / m - hw (fold <= n < 2 fold), i.e. one
+//     frame later / earlier inside its clip of tsm_T frames; at the clip edge it is dropped and the
+//     destination row of the wrap (frame 0 / tsm_T - 1) receives zero -- every element is written once;
+//   * + res[dst] (residual gradient);
+//   * mask: bits[dst / 8] bit (dst % 8) (ReLU mask bytes of vcg_bn_apply) or fma(y, msc, msh) > 0 (the
+//     forward's BN + ReLU decision recomputed from the saved pre-BN y);
+//   * stored (bf16) as g, and reduced per column: part[slot][0][n] = sum g, part[slot][1][n] = sum
+//     g * (y - mean) * invstd, part[slot][2][n] = sum g * (y2 - mean2) * invstd2 (second BatchNorm fed by the
+//     same gradient: the downsample branch), slot = the workgroup's grid row (bwd_slots rows in all).
+struct BwdEpi {
+  int tsm_T, tsm_fold;
+  FastDiv fd_hw, fd_T;
+  int hw;
+  const void* res;
+  const uint8_t* bits;
+  const void* y;
+  const float *mean, *invstd, *msc, *msh;
+  const void* y2;
+  const float *mean2, *invstd2;
+  float* part;  // [slots][nred][N]
+  int nred;     // 0 (no reduction), 2 or 3
+};
+
 struct GemmParams {
   int M, N, K;
   int k_per_split;  // multiple of BK
@@ -67,6 +92,7 @@ struct GemmParams {
   int batch_inner;
   long long a_so, a_si, b_so, b_si, c_so, c_si;
   int stage_kt;  // fast kernel: stage the output tile through LDS when the tile has <= stage_kt k-steps
+  BwdEpi bwd;    // EPI_BWD
 };
 
 
@@ -244,6 +270,9 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
 }
 
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
+int fast_grid_rows(int M, int N, int z, int epi);
+int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
+                           float* dgamma, float* dbeta, int accumulate, hipStream_t s);  // grid rows (slots of EPI_BWD partials) of a fast-kernel launch
 int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s);
 int wgrad_fast_tile_m(int M);
 int wgrad_fast_tile_n(int N);

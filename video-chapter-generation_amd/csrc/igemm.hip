@@ -536,6 +536,87 @@ VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
                : run_gemm<float, OP_DGRAD, OP_DENSE_K>(p, EPI_STORE, 1, stream);
 }
 
+// Workspace of vcg_conv_dgrad_bwd: partial sums [slots <= 768][3][C] floats.
+VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C) { return 768LL * 3 * C * 4 + 256; }
+
+// Conv input gradient of the trunk backward with the fused EPI_BWD epilogue (igemm.h BwdEpi): the dgrad value
+// (moved by the TSM adjoint when tsm_fold > 0) plus `res`, masked by `bits` (VCG_MASK_BITS bytes) or by
+// fma(y, mscale, mshift) > 0, is stored as g, and the BatchNorm backward reductions of g against y (and y2)
+// are finalized into sum_g / sum_gx (/ sum_gx2) with dgamma / dbeta (dgamma2 / dbeta2) accumulated: the
+// input of vcg_bn_bwd_apply with mask_mode 0. y == NULL: no reduction. Fast bf16 engine only:
+// returns VCG_ERR_UNSUPPORTED where it does not apply (the caller then runs the unfused ops).
+VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C,
+                               int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold,
+                               const void* res, const unsigned char* bits, const void* y, const float* mean,
+                               const float* invstd, const float* mscale, const float* mshift, const void* y2,
+                               const float* mean2, const float* invstd2, float* ws, long long ws_bytes,
+                               float* sum_g, float* sum_gx, float* dgamma, float* dbeta, float* sum_gx2,
+                               float* dgamma2, float* dbeta2, hipStream_t stream) {
+  const int logCo = ilog2_exact(Cout);
+  VCG_REQUIRE(logCo >= 0 && Cout >= 8, "Cout must be a power of two >= 8");
+  VCG_REQUIRE(C % 64 == 0, "C must be a multiple of 64");
+  VCG_REQUIRE(stride == 1 || stride == 2, "stride must be 1 or 2");
+  VCG_REQUIRE(!(bits && mscale), "one ReLU mask (bits or mscale/mshift)");
+  VCG_REQUIRE(!mscale || (mshift && y), "mscale needs mshift and y");
+  VCG_REQUIRE(!y || (mean && invstd && sum_g && sum_gx), "the reduction needs mean/invstd/sum_g/sum_gx");
+  VCG_REQUIRE(!y2 || (y && mean2 && invstd2 && sum_gx2), "the second reduction needs y, mean2/invstd2/sum_gx2");
+  VCG_REQUIRE(tsm_fold == 0 || (tsm_T > 0 && N % tsm_T == 0 && tsm_fold % 8 == 0 && 2 * tsm_fold <= C),
+              "bad TSM geometry");
+  VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C), "workspace too small");
+  const long long nelem = (long long)N * H * W * C;
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  if (dtype != VCG_BF16 || !fast_gemm_enabled() || nelem * 2 >= 0xFFFFFF00LL ||
+      (long long)N * OH * OW * Cout * 2 >= 0xFFFFFF00LL || (long long)N * H * W >= (1LL << 31))
+    return VCG_ERR_UNSUPPORTED;
+  const bool dense = (KH == 1 && KW == 1 && stride == 1 && pad == 0);
+  if (!dense && (Cout < 64 || KH * KW > 32)) return VCG_ERR_UNSUPPORTED;  // fast dgrad gather: one tap per k tile
+  GemmParams p{};
+  p.M = N * H * W;
+  p.N = C;
+  p.K = KH * KW * Cout;
+  p.k_per_split = p.K + 64;
+  if (dense) {
+    p.a = dense_op(dy, Cout, p.M, Cout, 2);
+  } else {
+    OpArgs a{};
+    a.ptr = dy; a.rows = p.M; a.N = N; a.H = OH; a.W = OW; a.C = Cout; a.logC = logCo;
+    a.GH = H; a.GW = W; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+    a.bytes = (long long)N * OH * OW * Cout * 2;
+    p.a = a;
+  }
+  p.b = dense_op(wt, p.K, C, p.K, 2);
+  p.C = g;
+  p.ldc = C;
+  p.alpha = 1.f;
+  BwdEpi& e = p.bwd;
+  e.tsm_T = tsm_fold > 0 ? tsm_T : 0;
+  e.tsm_fold = tsm_fold;
+  e.hw = H * W;
+  e.fd_hw = make_fastdiv((uint32_t)(H * W));
+  e.fd_T = make_fastdiv((uint32_t)(tsm_T > 0 ? tsm_T : 1));
+  e.res = res; e.bits = bits; e.y = y; e.mean = mean; e.invstd = invstd; e.msc = mscale; e.msh = mshift;
+  e.y2 = y2; e.mean2 = mean2; e.invstd2 = invstd2;
+  e.part = ws;
+  e.nred = y ? (y2 ? 3 : 2) : 0;
+  if (FILE* f = gemm_log()) {
+    fprintf(f, "a=%d b=0 epi=3 M=%d N=%d K=%d z=1 fast=1 conv=%dx%d/%d C=%d\n", dense ? 0 : 2, p.M, p.N, p.K, KH, KW,
+            stride, Cout);
+    fflush(f);
+  }
+  int rc = run_fast_gemm(p, dense ? OP_DENSE_K : OP_DGRAD, EPI_BWD, 1, stream);
+  if (rc) return rc;
+  if (e.nred > 0) {
+    const int slots = fast_grid_rows(p.M, p.N, 1, EPI_BWD);
+    rc = bn_bwd_finalize_launch(ws, slots, C, (long long)e.nred * C, C, sum_g, sum_gx, dgamma, dbeta, 1, stream);
+    if (rc) return rc;
+    if (e.nred > 2) {
+      rc = bn_bwd_finalize_launch(ws, slots, C, 3LL * C, 2 * C, sum_g, sum_gx2, dgamma2, dbeta2, 1, stream);
+      if (rc) return rc;
+    }
+  }
+  return VCG_OK;
+}
+
 // The bf16 LDS-DMA wgrad kernel (igemm_wgrad.hip) takes x / dy below 4 GB (32-bit buffer range)
 // and C >= 8 (a 16-B chunk of x never straddles two filter taps).
 static bool wgrad_fast_ok(int dtype, int N, int H, int W, int C, int Cout, int K) {

@@ -279,6 +279,164 @@ __device__ __forceinline__ void epilogue_staged(f32x4 (&acc)[BM / 32][BN / 32], 
   stage_flush<BM, BN>(stA, stB, p, Cout, m0, n0);
 }
 
+// ---- EPI_BWD (igemm.h BwdEpi): conv-dgrad epilogue of the trunk backward ------------------------------
+// Per-column parameters live in LDS (cpar[4][BN]: mean, msc, msh, mean2 of the workgroup's BN columns);
+// a thread of the flush always owns the same 8-column chunk c = tid % (BN / 8), so its per-column sums stay
+// in registers for the whole kernel and are combined across threads once at the end (bwd_finish).
+__device__ __forceinline__ void unpack8(const uint4& u, float (&v)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t* stB, const GemmParams& p,
+                                                bf16_t* Cout, int m0, int n0, const float* cpar, float (&s1)[8],
+                                                float (&s2)[8], float (&s3)[8]) {
+  constexpr int CPR = BN / 8, NCH = BM * BN / 8, KC = NCH / 256, KB = KC < 4 ? KC : 4;
+  const BwdEpi& e = p.bwd;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  uint4 q[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int id = threadIdx.x + 256 * k;
+    const int trow = id / CPR, c = id - trow * CPR;
+    const bf16_t* reg = (BN == 128 && trow >= 64) ? stB : stA;
+    const int row = BN == 128 ? (trow & 63) : trow;
+    const uint32_t addr = lds_u32(reg + row * BN + 8 * st_slot<BN>(row, c));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(q[k]) : "v"(addr) : "memory");
+  }
+  const int c = threadIdx.x % CPR;
+  const int lc = 8 * c, n = n0 + lc;
+  float mu[8], sc[8], sh[8], mu2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = cpar[lc + i];
+    sc[i] = cpar[BN + lc + i];
+    sh[i] = cpar[2 * BN + lc + i];
+    mu2[i] = cpar[3 * BN + lc + i];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  int shift = 0;  // TSM adjoint: this column group's values move one frame later (+1) / earlier (-1)
+  if (e.tsm_T > 0) shift = n < e.tsm_fold ? 1 : (n < 2 * e.tsm_fold ? -1 : 0);
+  const bf16_t* res = reinterpret_cast<const bf16_t*>(e.res);
+  const bf16_t* yp = reinterpret_cast<const bf16_t*>(e.y);
+  const bf16_t* y2p = reinterpret_cast<const bf16_t*>(e.y2);
+#pragma unroll
+  for (int k0 = 0; k0 < KC; k0 += KB) {
+    long long off[KB];
+    bool ok[KB], src[KB];
+    uint4 rv[KB], yv[KB], y2v[KB];
+    uint32_t bv[KB];
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {  // all loads of the batch first
+      const int id = threadIdx.x + 256 * (k0 + kk);
+      const int m = m0 + id / CPR;
+      ok[kk] = m < p.M && n < p.N;
+      src[kk] = true;
+      int dst = m;
+      if (shift != 0 && ok[kk]) {
+        const int f = (int)fdiv((uint32_t)m, e.fd_hw);
+        const int t = f - (int)fdiv((uint32_t)f, e.fd_T) * e.tsm_T;
+        const bool edge = shift > 0 ? t == e.tsm_T - 1 : t == 0;
+        src[kk] = !edge;
+        dst = edge ? m - shift * (e.tsm_T - 1) * e.hw : m + shift * e.hw;
+      }
+      off[kk] = (long long)dst * p.ldc + n;
+      if (ok[kk]) {
+        if (res) rv[kk] = *reinterpret_cast<const uint4*>(res + off[kk]);
+        if (e.bits) bv[kk] = e.bits[off[kk] >> 3];
+        if (yp) yv[kk] = *reinterpret_cast<const uint4*>(yp + off[kk]);
+        if (y2p) y2v[kk] = *reinterpret_cast<const uint4*>(y2p + off[kk]);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      if (!ok[kk]) continue;
+      float v[8];
+      unpack8(q[k0 + kk], v);
+      if (!src[kk]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 0.f;
+      }
+      if (res) {
+        float r[8];
+        unpack8(rv[kk], r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += r[i];
+      }
+      if (e.bits) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = ((bv[kk] >> i) & 1u) ? v[i] : 0.f;
+      }
+      float yy[8];
+      if (yp) {
+        unpack8(yv[kk], yy);
+        if (e.msc) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = fmaf(yy[i], sc[i], sh[i]) > 0.f ? v[i] : 0.f;
+        }
+      }
+      uint4 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+      o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+      *reinterpret_cast<uint4*>(Cout + off[kk]) = o;
+      if (e.nred > 0) {
+        unpack8(o, v);  // statistics of the stored (rounded) gradient
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s1[i] += v[i];
+          s2[i] = fmaf(v[i], yy[i] - mu[i], s2[i]);
+        }
+        if (y2p) {
+          float y2[8];
+          unpack8(y2v[kk], y2);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s3[i] = fmaf(v[i], y2[i] - mu2[i], s3[i]);
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_s_barrier();  // every wave has read the stage before the next step's DMA refills it
+}
+
+// Combine the per-thread column sums of EPI_BWD (threads tid = c (mod BN/8) share columns 8c..8c+7) in a
+// fixed order and write this workgroup's partial slot; scratch = the (idle) stage buffers.
+template <int BN>
+__device__ __forceinline__ void bwd_finish(const GemmParams& p, float* scratch, const float* cpar_invstd,
+                                           const float (&s1)[8], const float (&s2)[8], const float (&s3)[8], int n0,
+                                           int slot) {
+  constexpr int CPR = BN / 8;
+  const int nred = p.bwd.nred;
+  __syncthreads();
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    scratch[(0 * 256 + tid) * 8 + i] = s1[i];
+    scratch[(1 * 256 + tid) * 8 + i] = s2[i];
+    scratch[(2 * 256 + tid) * 8 + i] = s3[i];
+  }
+  __syncthreads();
+  if (tid < BN && n0 + tid < p.N) {
+    const int c = tid >> 3, i = tid & 7;
+    float a[3] = {0.f, 0.f, 0.f};
+    for (int t = c; t < 256; t += CPR)
+#pragma unroll
+      for (int r = 0; r < 3; ++r) a[r] += scratch[(r * 256 + t) * 8 + i];
+    float* out = p.bwd.part + (long long)slot * nred * p.N + n0 + tid;
+    out[0] = a[0];
+    out[p.N] = a[1] * cpar_invstd[tid];
+    if (nred > 2) out[2 * p.N] = a[2] * cpar_invstd[BN + tid];
+  }
+}
+
 // EPI_STATS epilogue of the fast kernel: store the tile (bf16) and fold its rounded values into the
 // running shifted sums. No barriers, no LDS: nothing waits on the in-flight prefetch or the stores.
 template <int BM, int BN>
@@ -391,10 +549,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
   constexpr int MT = BM / 32, NT = BN / 32;
   constexpr int AE = BM * FBK, BE = BN * FBK;  // elements per stage
   constexpr int NLD = BM / 32 + BN / 32;       // LDS-DMA instructions per thread per step
-  __shared__ __attribute__((aligned(1024))) char smem[2 * (AE + BE) * 2 + (4 * BN + 4) * 4];
+  constexpr int CPAR = EPI == EPI_BWD ? 6 * BN : 0;  // EPI_BWD per-column parameters
+  __shared__ __attribute__((aligned(1024))) char smem[2 * (AE + BE) * 2 + (4 * BN + 4 + CPAR) * 4];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
   bf16_t* Bs = As + 2 * AE;
   float* red = reinterpret_cast<float*>(smem + 2 * (AE + BE) * 2);
+  float* cpar = red + 4 * BN + 4;  // [mean, msc, msh, mean2, invstd, invstd2][BN]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -423,6 +583,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
   const int my_tiles = by < mtiles ? (mtiles - 1 - by) / gy + 1 : 0;
   const int ntiles = (p.K + FBK - 1) / FBK;
   const int steps = my_tiles * ntiles;
+  if constexpr (EPI == EPI_BWD) {
+    if (steps == 0) {  // no rows: an all-zero partial slot
+      if (p.bwd.nred > 0 && tid < BN && n0 + tid < p.N)
+        for (int r = 0; r < p.bwd.nred; ++r) p.bwd.part[((long long)by * p.bwd.nred + r) * p.N + n0 + tid] = 0.f;
+      return;
+    }
+    if (tid < BN) {
+      const int n = min(n0 + tid, p.N - 1);
+      const BwdEpi& e = p.bwd;
+      cpar[tid] = e.mean ? e.mean[n] : 0.f;
+      cpar[BN + tid] = e.msc ? e.msc[n] : 0.f;
+      cpar[2 * BN + tid] = e.msh ? e.msh[n] : 0.f;
+      cpar[3 * BN + tid] = e.mean2 ? e.mean2[n] : 0.f;
+      cpar[4 * BN + tid] = e.invstd ? e.invstd[n] : 0.f;
+      cpar[5 * BN + tid] = e.invstd2 ? e.invstd2[n] : 0.f;
+    }
+  }
   if (steps == 0) return;
 
   float bv[NT][4];
@@ -451,6 +628,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
   // lanes and waves once at the end -> one (mean, M2) slot per workgroup row `by`.
   float ks[NT][4], s1[NT][4], s2[NT][4];
   int nrows = 0;
+  float b1[8], b2[8], b3[8];  // EPI_BWD column sums of this thread's chunk
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b1[i] = b2[i] = b3[i] = 0.f;
   if constexpr (EPI == EPI_STATS) {
 #pragma unroll
     for (int j = 0; j < NT; ++j)
@@ -498,7 +678,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
       const int mt = by + tile * gy;
       // output tiles go through the LDS stage for full-row 16-B stores (VCG_STAGE_KT can limit it)
       const bool staged = ntiles <= p.stage_kt;
-      if constexpr (EPI == EPI_STATS) {
+      if constexpr (EPI == EPI_BWD) {
+        constexpr int MT_ = BM / 32, NT_ = BN / 32;
+#pragma unroll
+        for (int j = 0; j < NT_; ++j)
+#pragma unroll
+          for (int i = 0; i < MT_; ++i) {
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            stage_put<BM, BN>(As + cur * AE, Bs + cur * BE, wm, wn, lane, i, j, v);
+          }
+        stage_flush_bwd<BM, BN>(As + cur * AE, Bs + cur * BE, p, Cout, mt * BM, n0, cpar, b1, b2, b3);
+      } else if constexpr (EPI == EPI_STATS) {
         epilogue_accstats<BM, BN>(acc, p, bv, Cout, As + cur * AE, Bs + cur * BE, staged, mt * BM, n0, wm, wn,
                                   lane, tile == 0, ks, s1, s2, nrows);
       } else if (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0) {
@@ -515,18 +705,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
     }
   }
   if constexpr (EPI == EPI_STATS) stats_finish<BN>(p, red, ks, s1, s2, nrows, n0, by, bx, gy, mtiles, wm, wn, lane);
+  if constexpr (EPI == EPI_BWD) {
+    if (p.bwd.nred > 0) bwd_finish<BN>(p, reinterpret_cast<float*>(smem), cpar + 4 * BN, b1, b2, b3, n0, by);
+  }
 }
 
-template <int BM, int BN, int AM, int EPI, bool RES>
-static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
-  // One resident round of workgroups (LDS allows 2 per CU at BN = 128, 3 at BN = 64); each walks
-  // ceil(mtiles / gy) M-tiles. gy is a multiple of 8 whenever possible (XCD-aware decode).
-  const int nx = (p.N + BN - 1) / BN, mtiles = (p.M + BM - 1) / BM;
-  const int resident = (BN == 128 ? 2 : 3) * 256;
+// One resident round of workgroups (LDS allows 2 per CU at BN = 128, 3 at BN = 64); each walks
+// ceil(mtiles / gy) M-tiles. gy is a multiple of 8 whenever possible (XCD-aware decode).
+// (EPI_BWD's BN = 64 kernel needs > 170 VGPRs: 2 workgroups per CU there too)
+static int grid_rows(int M, int N, int z, int BM, int BN, int epi) {
+  const int nx = (N + BN - 1) / BN, mtiles = (M + BM - 1) / BM;
+  const int resident = (BN == 128 || epi == EPI_BWD ? 2 : 3) * 256;
   int gy = resident / (nx * z);
   if (gy >= 8) gy &= ~7;
   if (gy > mtiles) gy = mtiles >= 8 ? (mtiles & ~7) : mtiles;
   if (gy < 1) gy = 1;
+  return gy;
+}
+
+static int fast_bn_cols(int N) { return (N % 128 == 0 || N > 64 * 3) ? 128 : 64; }
+
+int fast_grid_rows(int M, int N, int z, int epi) { return grid_rows(M, N, z, 128, fast_bn_cols(N), epi); }
+
+template <int BM, int BN, int AM, int EPI, bool RES>
+static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
+  const int nx = (p.N + BN - 1) / BN;
+  const int gy = grid_rows(p.M, p.N, z, BM, BN, EPI);
   dim3 grid(nx * gy, 1, z);
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((igemm_fast_kernel<BM, BN, AM, EPI, RES>), grid, dim3(256), 0, s, p);
@@ -537,7 +741,7 @@ static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
 
 template <int AM, int EPI, bool RES = false>
 static int fast_bn(const GemmParams& p, int z, hipStream_t s) {
-  if (p.N % 128 == 0 || p.N > 64 * 3) return launch_fast<128, 128, AM, EPI, RES>(p, z, s);
+  if (fast_bn_cols(p.N) == 128) return launch_fast<128, 128, AM, EPI, RES>(p, z, s);
   return launch_fast<128, 64, AM, EPI, RES>(p, z, s);
 }
 
@@ -551,6 +755,11 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   if (amode == OP_IM2COL && p.a.C < FBK) amode = OP_IM2COL_SMALLC;
   if (amode == OP_IM2COL_TSM && p.a.C < FBK) return -1;  // (dispatcher keeps these off the fast path)
   if (amode == OP_DGRAD && p.a.C < FBK) return -1;
+  if (epi == EPI_BWD) {
+    if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_BWD>(p, z, s);
+    if (amode == OP_DENSE_K) return fast_bn<OP_DENSE_K, EPI_BWD>(p, z, s);
+    return -1;
+  }
   if (epi == EPI_STATS) {
     if (amode == OP_IM2COL_SMALLC) return fast_bn<OP_IM2COL_SMALLC, EPI_STATS>(p, z, s);
     if (amode == OP_IM2COL_TSM) return fast_bn<OP_IM2COL_TSM, EPI_STATS>(p, z, s);

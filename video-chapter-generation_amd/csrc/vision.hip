@@ -178,6 +178,27 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, T* __restrict__ 
   }
 }
 
+// out[c][r] = in[r][c] for a [rows][cols] matrix (leading dims ld_in / ld_out): 64x64 tiles through
+// LDS (odd row pitch: conflict-free column reads), coalesced reads and writes.
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ in, T* __restrict__ out, int rows,
+                                                        int cols, long long ld_in, long long ld_out) {
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int r = r0 + ty + 4 * k, c = c0 + tx;
+    if (r < rows && c < cols) tile[ty + 4 * k][tx] = to_f<T>(in[(long long)r * ld_in + c]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = c0 + ty + 4 * k, r = r0 + tx;
+    if (r < rows && c < cols) out[(long long)c * ld_out + r] = from_f<T>(tile[tx][ty + 4 * k]);
+  }
+}
+
 template <typename TO>
 __global__ void cast_kernel(const float* __restrict__ in, TO* __restrict__ out, long long n) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
@@ -302,6 +323,20 @@ VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int 
   else
     hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(grid_for(tot)), dim3(256), 0, s, w, (float*)out, Cout, Cin, KH,
                        KW, Cpad, transposed);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_transpose(int dtype, const void* in, void* out, int rows, int cols, long long ld_in, long long ld_out,
+                          hipStream_t s) {
+  VCG_REQUIRE(rows > 0 && cols > 0 && ld_in >= cols && ld_out >= rows, "bad transpose shape");
+  const dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(transpose_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)in, (bf16_t*)out, rows, cols,
+                       ld_in, ld_out);
+  else
+    hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, s, (const float*)in, (float*)out, rows, cols,
+                       ld_in, ld_out);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

@@ -204,20 +204,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
 // Column sums of partial[nb][2C] -> sum_g, sum_gx (+ dgamma/dbeta): 64 channels x 16 row-stripes per
 // block (1024 threads), loads coalesced across channels and unrolled across rows; fixed summation
 // order (deterministic).
+// (row i of partial: sum_g at [i * ld + c], sum_gx at [i * ld + gx_off + c]; ld = 2C / gx_off = C for
+// bn_bwd_reduce's partials)
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nb, int C,
-                                                               float* sum_g, float* sum_gx, float* dgamma,
-                                                               float* dbeta, int accumulate) {
+                                                               long long ld, int gx_off, float* sum_g, float* sum_gx,
+                                                               float* dgamma, float* dbeta, int accumulate) {
   __shared__ double sa[16][64], sb[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   double a = 0, b = 0;
   if (c < C) {
     const float* p = partial + c;
-    const long long ld = 2LL * C;
 #pragma unroll 4
     for (int i = ty; i < nb; i += 16) {
       a += p[i * ld];
-      b += p[i * ld + C];
+      b += p[i * ld + gx_off];
     }
   }
   sa[ty][tx] = a;
@@ -441,6 +442,17 @@ inline unsigned stream_grid(long long TV) {
 
 }  // namespace
 
+namespace vcg {
+// column sums of EPI_BWD partials (igemm_fast.hip) -> sum_g / sum_gx (+ dgamma / dbeta, accumulated)
+int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
+                           float* dgamma, float* dbeta, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, partial, nb, C, ld, gx_off, sum_g,
+                     sum_gx, dgamma, dbeta, accumulate);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+}  // namespace vcg
+
 // ==================================================================== C ABI
 
 VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const void* res,
@@ -543,8 +555,8 @@ VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, int mask_mode, const 
 #undef VCG_BN_RED_T
 #undef VCG_BN_RED
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, sum_g, sum_gx,
-                     dgamma, dbeta, accumulate);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
+                     sum_g, sum_gx, dgamma, dbeta, accumulate);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

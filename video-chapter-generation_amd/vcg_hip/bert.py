@@ -27,6 +27,15 @@ class BertEncoderEngine:
     def _w(self, p):
         return self.flat.compute_view(p, self.dtype)
 
+    def _gemm_dx(self, A, W, M, N, K, **kw):
+        """A [M, K] @ W [K, N] (W = a Linear weight [out=K, in=N]: the input gradient). bf16 with a long K
+        (QKV, FFN1 input gradients: K = 2304 / 3072, N = 768): W^T is materialised (tiled transpose) so the
+        LDS-DMA GEMM reads both operands K-contiguous (measured 87 -> 61 us at K = 3072, 67 -> 53 us at
+        K = 2304; no gain at K = 768, tools/bench_bert_gemm.py)."""
+        if self.dtype == torch.bfloat16 and K >= 2 * N:
+            return ops.gemm(A, ops.transpose(W), M, N, K, K, K, **kw)
+        return ops.gemm(A, W, M, N, K, K, N, transB=True, **kw)
+
     def forward(self, ids, mask, need_grad, seed):
         m, dt, flat = self.m, self.dtype, self.flat
         cfg = m.config
@@ -128,12 +137,11 @@ class BertEncoderEngine:
                                       ln2.bias.grad, rows, H, p_h, s["s2"])
             ops.gemm_splitk(dfo, s["ff"], out.weight.grad, H, I, rows, H, I, transA=True, transB=True)
             ops.colsum(dfo, H, rows, H, out.bias.grad)
-            dpre = ops.gemm(dfo, self._w(out.weight), rows, I, H, H, I, transB=True, act=ops.ACT_GELU_BWD,
-                            residual=s["pre"], ldr=I)
+            dpre = self._gemm_dx(dfo, self._w(out.weight), rows, I, H, act=ops.ACT_GELU_BWD, residual=s["pre"], ldr=I)
             del dfo
             ops.gemm_splitk(dpre, s["h1"], inter.weight.grad, I, H, rows, I, H, transA=True, transB=True)
             ops.colsum(dpre, I, rows, I, inter.bias.grad)
-            dh1 = ops.gemm(dpre, self._w(inter.weight), rows, H, I, I, H, transB=True, residual=dh1_res, ldr=H)
+            dh1 = self._gemm_dx(dpre, self._w(inter.weight), rows, H, I, residual=dh1_res, ldr=H)
             del dpre, dh1_res
             ln1 = at.output.LayerNorm
             dao, dh_res = ops.ln_bwd(dh1, s["ao"], s["h"], ln1.weight, s["m1"], s["r1"], ln1.weight.grad,
@@ -141,7 +149,7 @@ class BertEncoderEngine:
             od = at.output.dense
             ops.gemm_splitk(dao, s["ctx"], od.weight.grad, H, H, rows, H, H, transA=True, transB=True)
             ops.colsum(dao, H, rows, H, od.bias.grad)
-            dctx = ops.gemm(dao, self._w(od.weight), rows, H, H, H, H, transB=True)
+            dctx = self._gemm_dx(dao, self._w(od.weight), rows, H, H)
             del dao
             # ---- attention backward
             qkv_buf = s["qkv_buf"]
@@ -170,7 +178,7 @@ class BertEncoderEngine:
                 ops.gemm_splitk(dqkv, s["h"], gW, 3 * H, H, rows, 3 * H, H, transA=True, transB=True)
                 ops.colsum(dqkv, 3 * H, rows, 3 * H, gb)
             Wqkv = flat.compute_contiguous([sq.weight, sk.weight, svv.weight], (3 * H, H), dt)
-            dh_ = ops.gemm(dqkv, Wqkv, rows, H, 3 * H, 3 * H, H, transB=True, residual=dh_res, ldr=H)
+            dh_ = self._gemm_dx(dqkv, Wqkv, rows, H, 3 * H, residual=dh_res, ldr=H)
             del dqkv, dh_res, s
             if hooks is not None:
                 hooks(list(layer.parameters()))

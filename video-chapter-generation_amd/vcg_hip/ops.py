@@ -108,6 +108,36 @@ def conv_dgrad(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, out=None):
     return dx
 
 
+def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, res=None, bits=None, y=None,
+                   mean=None, invstd=None, mscale=None, mshift=None, y2=None, mean2=None, invstd2=None, sums=None,
+                   sum_gx2=None, dgamma=None, dbeta=None, dgamma2=None, dbeta2=None, out=None, workspace=None):
+    """Conv input gradient fused with the trunk backward's next steps (vcg_conv_dgrad_bwd, igemm.h BwdEpi):
+    g = mask(tsm_adjoint(dgrad) + res) and the BN-backward sums of g against y (sums [2, C] = sum_g,
+    sum_gx) and y2 (sum_gx2 [C]); dgamma/dbeta (dgamma2/dbeta2) accumulate. Returns g, or None where the
+    fused engine does not apply (fp32 / unsupported shape): the caller then runs the unfused ops."""
+    OH, OW = conv_out_hw(H, W, KH, KW, stride, pad)
+    _chk(dy, None, "dy")
+    assert dy.numel() == N * OH * OW * Cout and wt.numel() == C * KH * KW * Cout
+    g = out if out is not None else torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    nbytes = _lib.query("vcg_conv_dgrad_bwd_ws_bytes", C)
+    if workspace is None or workspace.numel() * 4 < nbytes:
+        workspace = ws(nbytes, dy.device)
+    for t in (res, y, y2):
+        if t is not None:
+            _chk(t, dy.dtype)
+            assert t.numel() == N * H * W * C
+    rc = _lib.query("vcg_conv_dgrad_bwd", dt_code(dy.dtype), P(dy), P(wt), P(g), N, H, W, C, Cout, KH, KW, stride,
+                    pad, tsm_T, tsm_fold, P(res), P(bits), P(y), P(mean), P(invstd), P(mscale), P(mshift), P(y2),
+                    P(mean2), P(invstd2), P(workspace), workspace.numel() * 4,
+                    P(sums[0]) if sums is not None else None, P(sums[1]) if sums is not None else None, P(dgamma),
+                    P(dbeta), P(sum_gx2), P(dgamma2), P(dbeta2), stream())
+    if rc == -2:  # VCG_ERR_UNSUPPORTED
+        return None
+    if rc != 0:
+        raise _lib.VcgError(f"vcg_conv_dgrad_bwd failed ({rc}): {_lib.last_error()}")
+    return g
+
+
 def conv_wgrad(x, dy, dw, N, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, accumulate=True,
                workspace=None):
     """dw (fp32 OIHW [Cout,Cin,KH,KW]) += wgrad. x: NHWC with C (padded) channels."""
@@ -273,6 +303,15 @@ def weight_prep(w, Cpad, dtype, transposed=False, out=None):
     shape = (Cin, KH, KW, Cout) if transposed else (Cout, KH, KW, Cpad)
     out = out if out is not None else torch.empty(shape, dtype=dtype, device=w.device)
     _lib.call("vcg_weight_prep", dt_code(dtype), P(w), P(out), Cout, Cin, KH, KW, Cpad, int(transposed), stream())
+    return out
+
+
+def transpose(x, out=None):
+    """[rows, cols] -> [cols, rows] (contiguous)."""
+    _chk(x, None, "x")
+    rows, cols = x.shape
+    out = out if out is not None else torch.empty((cols, rows), dtype=x.dtype, device=x.device)
+    _lib.call("vcg_transpose", dt_code(x.dtype), P(x), P(out), rows, cols, cols, rows, stream())
     return out
 
 

@@ -155,13 +155,22 @@ class ResNetTrunk:
 
     def backward(self, d_emb, saved, hooks=None):
         """d_emb: [N, 2048] fp32. Accumulates all trunk parameter grads; `hooks(params)` is told
-        when a block's gradients are final (DDP bucket all-reduce)."""
+        when a block's gradients are final (DDP bucket all-reduce).
+
+        bf16 (fast engine): every conv input gradient carries the next steps of the backward in its
+        epilogue (ops.conv_dgrad_bwd): conv3 / conv2 dgrads emit the ReLU-masked gradient of bn2 / bn1
+        and their BN-backward sums; conv1's dgrad applies the TSM adjoint, adds the residual-branch
+        gradient and emits the previous block's masked output gradient g with the sums of its bn3 (and
+        downsample BN). The separate reduce / TSM-combine passes remain only where the fused engine
+        does not apply (fp32 parity mode)."""
         N, Hc, Wc, C = saved["final"]
         dout = ops.avgpool_bwd(d_emb.contiguous(), N, Hc * Wc, C, self.dtype).view(N, Hc, Wc, C)
         blocks = saved["blocks"]
+        gin = None  # (g, sums3, sumsd): masked output gradient of the block + its BN sums (fused path)
         while blocks:
             rec = blocks.pop()  # frees the block's activations as soon as its backward is done
-            dout = self._block_bwd(rec, dout)
+            prev = blocks[-1] if blocks else None
+            dout, gin = self._block_bwd(rec, dout, gin, prev)
             if hooks is not None:
                 hooks(list(rec["blk"].parameters()))
             del rec
@@ -172,28 +181,92 @@ class ResNetTrunk:
         if hooks is not None:
             hooks(list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
 
-    def _block_bwd(self, r, dout):
+    def _bn_grads(self, st):
+        bn = st.bn
+        if bn.weight is not None and bn.weight.requires_grad:
+            return bn.weight.grad, bn.bias.grad
+        return None, None
+
+    def _bn_apply_bwd(self, g, y, st, C, sums):
+        """BN backward apply on an already-masked gradient g with precomputed sums (mask mode 0)."""
+        return ops.bn_bwd_apply(g, None, y, st.mean, st.invstd, st.bn.weight, sums[0], sums[1], C,
+                                train_stats=st.mode != "running")
+
+    def _dgrad_bn(self, conv, dy, N, H, W, y, st, C):
+        """Input gradient of `conv` followed by the backward of the BN (+ReLU) that produced its input:
+        returns the gradient of that BN's conv output y."""
+        Cout, Cin, KH, KW, s, p = _conv_shape(conv)
+        wt = ops.weight_prep(conv.weight.data, Cin, self.dtype, transposed=True)
+        sums = torch.empty((2, C), dtype=torch.float32, device=y.device)
+        dg, db = self._bn_grads(st)
+        g = ops.conv_dgrad_bwd(dy, wt, N, H, W, Cin, Cout, KH, KW, s, p, y=y, mean=st.mean, invstd=st.invstd,
+                               mscale=st.scale, mshift=st.shift, sums=sums, dgamma=dg, dbeta=db)
+        if g is None:
+            da = ops.conv_dgrad(dy, wt, N, H, W, Cin, Cout, KH, KW, s, p)
+            return self._bn_bwd(da, y, st, C, affine=True)
+        return self._bn_apply_bwd(g, y, st, C, sums)
+
+    def _block_bwd(self, r, dout, gin, prev):
+        """Backward of one bottleneck. `gin` (fused path): (g, sums3, sumsd) = this block's ReLU-masked output
+        gradient and its BN sums; else `dout` is the raw output gradient. `prev`: the record of the block
+        whose output is this block's input (None: the max-pool). Returns (dout, gin) for `prev`."""
         blk = r["blk"]
         N, H, W, H2, W2 = r["N"], r["H"], r["W"], r["H2"], r["W2"]
         Cin, planes, C3, T, fold = r["Cin"], r["planes"], r["C3"], r["T"], r["fold"]
         obits = r["obits"]
-        dy3 = self._bn_bwd(dout, r["y3"], r["b3"], C3, mbits=obits)
+        ds = blk.downsample is not None
+        if gin is not None:
+            g, sums3, sumsd = gin
+            dy3 = self._bn_apply_bwd(g, r["y3"], r["b3"], C3, sums3)
+            dyd = self._bn_apply_bwd(g, r["yd"], r["bd"], C3, sumsd) if ds else None
+        else:
+            g = torch.empty_like(dout)
+            dy3 = self._bn_bwd_g(dout, r["y3"], r["b3"], C3, obits, g)
+            dyd = self._bn_bwd(dout, r["yd"], r["bd"], C3, mbits=obits) if ds else None
         self._wgrad(blk.conv3, r["a2"], dy3, N, H2, W2, planes)
-        da2 = self._dgrad(blk.conv3, dy3, N, H2, W2)
+        dy2 = self._dgrad_bn(blk.conv3, dy3, N, H2, W2, r["y2"], r["b2"], planes)
         del dy3
-        dy2 = self._bn_bwd(da2, r["y2"], r["b2"], planes, affine=True)
-        del da2
         self._wgrad(blk.conv2, r["a1"], dy2, N, H, W, planes)
-        da1 = self._dgrad(blk.conv2, dy2, N, H, W)
+        dy1 = self._dgrad_bn(blk.conv2, dy2, N, H, W, r["y1"], r["b1"], planes)
         del dy2
-        dy1 = self._bn_bwd(da1, r["y1"], r["b1"], planes, affine=True)
-        del da1
         self._wgrad(r["conv1"], r["x"], dy1, N, H, W, Cin, T, fold)
-        dxs = self._dgrad(r["conv1"], dy1, N, H, W)
-        del dy1
-        if blk.downsample is not None:
-            dyd = self._bn_bwd(dout, r["yd"], r["bd"], C3, mbits=obits)  # the residual gradient: dout * mask
+        if ds:
             self._wgrad(blk.downsample[0], r["x"], dyd, N, H, W, Cin)
-            other = self._dgrad(blk.downsample[0], dyd, N, H, W)
-            return ops.tsm_unshift_add(dxs, other, N, T if T else 1, H * W, Cin, fold)
-        return ops.tsm_unshift_add(dxs, dout, N, T if T else 1, H * W, Cin, fold, other_bits=obits)
+            res = self._dgrad(blk.downsample[0], dyd, N, H, W)  # the downsample branch's input gradient
+            del dyd
+        else:
+            res = g  # the identity branch: the block's masked output gradient
+        # conv1 input gradient + TSM adjoint + residual branch; fused: also the previous block's mask and sums
+        conv1 = r["conv1"]
+        Cout1, Cin1, KH, KW, s, p = _conv_shape(conv1)
+        wt = ops.weight_prep(conv1.weight.data, Cin1, self.dtype, transposed=True)
+        kw = dict(tsm_T=T if fold else 0, tsm_fold=fold, res=res)
+        sums3 = sumsd = None
+        if prev is not None:
+            sums3 = torch.empty((2, Cin), dtype=torch.float32, device=dy1.device)
+            dg, db = self._bn_grads(prev["b3"])
+            kw.update(bits=prev["obits"], y=prev["y3"], mean=prev["b3"].mean, invstd=prev["b3"].invstd, sums=sums3,
+                      dgamma=dg, dbeta=db)
+            if prev["blk"].downsample is not None:
+                sumsd = torch.empty((2, Cin), dtype=torch.float32, device=dy1.device)
+                dg2, db2 = self._bn_grads(prev["bd"])
+                kw.update(y2=prev["yd"], mean2=prev["bd"].mean, invstd2=prev["bd"].invstd, sum_gx2=sumsd[1],
+                          dgamma2=dg2, dbeta2=db2)
+        out = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, **kw)
+        if out is not None:
+            if prev is None:
+                return out, None  # the max-pool's output gradient (no mask, no BN)
+            if sumsd is not None:
+                sumsd[0].copy_(sums3[0])
+            return None, (out, sums3, sumsd)
+        dxs = ops.conv_dgrad(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p)
+        return ops.tsm_unshift_add(dxs, res, N, T if T else 1, H * W, Cin, fold), None
+
+    def _bn_bwd_g(self, dout, y, st, C, mbits, gout):
+        """bn3 backward from the raw output gradient (mask bits), also writing the masked gradient g."""
+        bn = st.bn
+        sums = torch.empty((2, C), dtype=torch.float32, device=y.device)
+        dg, db = self._bn_grads(st)
+        ops.bn_bwd_reduce(dout, None, y, st.mean, st.invstd, C, sums[0], sums[1], dg, db, mbits=mbits)
+        return ops.bn_bwd_apply(dout, None, y, st.mean, st.invstd, bn.weight, sums[0], sums[1], C,
+                                train_stats=st.mode != "running", mbits=mbits, gout=gout)
