@@ -103,7 +103,7 @@ VCG_API int vcg_embed_ln_fwd(int dtype, const long long* ids, const float* word,
 VCG_API long long vcg_ln_bwd_ws_bytes(int rows, int H);
 VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, const float* word, const float* pos, const float* type, const float* gamma, const float* mean, const float* rstd, float* word_grad, float* pos_grad, float* type_grad, float* gamma_grad, float* beta_grad, float* ws, long long ws_bytes, int B, int L, int H, float dropout_p, unsigned long long seed, long long pad_idx, hipStream_t s);
 VCG_API int vcg_ln_fwd(int dtype, const void* x, const void* res, const float* gamma, const float* beta, void* out, float* mean, float* rstd, int rows, int H, float eps, float dropout_p, unsigned long long seed, hipStream_t s);
-VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* res, const float* gamma, const float* mean, const float* rstd, void* dx, void* dres, float* gamma_grad, float* beta_grad, float* ws, long long ws_bytes, int rows, int H, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* res, const float* gamma, const float* mean, const float* rstd, void* dx, void* dres, float* gamma_grad, float* beta_grad, float* bias_grad, float* ws, long long ws_bytes, int rows, int H, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API long long vcg_colsum_ws_bytes(int rows, int N);
 VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, float* out, int accumulate, float* ws, long long ws_bytes, hipStream_t s);
 VCG_API int vcg_attn_softmax_fwd(int dtype, const void* S, const long long* mask, void* P, void* Pd, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);

@@ -445,3 +445,38 @@ def test_conv_dgrad_bwd(K, case, mode):
         assert (sgx2.double() - sx2).abs().max().item() <= tol(sx2)
         assert (dgam2.double() - 0.5 - sx2).abs().max().item() <= tol(sx2)
         assert (dbet2.double() - 0.25 - sg).abs().max().item() <= tol(sg)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("H", [768, 200])
+def test_layernorm_fwd_bwd(K, dtype, H):
+    """LN(x + res) forward / backward (row-wise wave kernels at H = 768, block kernels at H = 200) against
+    torch autograd in float64; the fused bias gradient = column sums of dx."""
+    rows = 37
+    x = _rand((rows, H), dtype, 71)
+    r = _rand((rows, H), dtype, 72)
+    g0 = torch.Generator().manual_seed(73)
+    gamma = torch.rand(H, generator=g0) + 0.5
+    beta = torch.randn(H, generator=g0) * 0.1
+    dout = _rand((rows, H), dtype, 74)
+    xd = x.double().requires_grad_()
+    rd = r.double().requires_grad_()
+    gd = gamma.double().requires_grad_()
+    bd = beta.double().requires_grad_()
+    y = F.layer_norm(xd + rd, (H,), gd, bd, eps=1e-12)
+    dx_ref, dr_ref, dg_ref, db_ref = torch.autograd.grad(y, (xd, rd, gd, bd), dout.double())
+    out, mean, rstd = K.ln_fwd(x.to(DEV), r.to(DEV), gamma.to(DEV), beta.to(DEV), rows, H, 1e-12)
+    _close(out, y, dtype, "ln fwd")
+    gg = torch.zeros(H, device=DEV)
+    gb = torch.zeros(H, device=DEV)
+    gbias = torch.full((H,), 0.5, device=DEV)
+    dx, dres = K.ln_bwd(dout.to(DEV), x.to(DEV), r.to(DEV), gamma.to(DEV), mean, rstd, gg, gb, rows, H,
+                        bias_grad=gbias)
+    _close(dx, dx_ref, dtype, "ln bwd dx")
+    _close(dres, dr_ref, dtype, "ln bwd dres")
+    _close(gg, dg_ref, dtype, "ln dgamma")
+    _close(gb, db_ref, dtype, "ln dbeta")
+    _close(gbias - 0.5, dx.double().sum(0), torch.float32, "ln fused bias grad")
+    cs = torch.full((H,), 0.25, device=DEV)
+    K.colsum(dx, H, rows, H, cs)
+    _close(cs - 0.25, dx.double().sum(0), torch.float32, "colsum")

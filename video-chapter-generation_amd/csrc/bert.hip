@@ -18,6 +18,9 @@ __device__ __forceinline__ bool keep(uint64_t seed, uint64_t idx, float p) {
   return u >= p;
 }
 
+// value as stored in T (bias-gradient sums use the gradient the GEMM will read)
+template <typename T> __device__ __forceinline__ float bf_round(float v) { return to_f<T>(from_f<T>(v)); }
+
 inline int grid_for(long long n, int bs = 256) {
   long long g = (n + bs - 1) / bs;
   if (g > 8192) g = 8192;
@@ -364,6 +367,234 @@ __global__ void attn_softmax_bwd_kernel(const T* __restrict__ dPd, const T* __re
   }
 }
 
+// ---------------------------------------------------------------- row-wise (one wave per row) kernels
+// H = 256 * NQ: lane l owns the NQ 4-element chunks at columns 4 * (l + 64 q); loads are 8 B (bf16) /
+// 16 B (fp32) per lane, row statistics are wave reductions (no LDS, no barriers).
+template <typename T> __device__ __forceinline__ void ld4(const T* p, float (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    const uint2 q = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+}
+template <typename T> __device__ __forceinline__ void st4(T* p, const float (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    uint2 q;
+    q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = q;
+  }
+}
+__device__ __forceinline__ void ldf4(const float* p, float (&v)[4]) {
+  const float4 q = *reinterpret_cast<const float4*>(p);
+  v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+}
+
+// out = LN(dropout(x) + res), one row per wave
+template <typename T, int NQ>
+__global__ __launch_bounds__(256) void ln_fwd_rw_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        T* __restrict__ out, float* __restrict__ mean_out,
+                                                        float* __restrict__ rstd_out, int rows, float eps, float p,
+                                                        uint64_t seed) {
+  constexpr int H = 256 * NQ;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const long long rb = (long long)row * H;
+  float v[NQ][4], r[NQ][4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int c = 4 * (lane + 64 * q);
+    ld4<T>(x + rb + c, v[q]);
+    if (res) ld4<T>(res + rb + c, r[q]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int c = 4 * (lane + 64 * q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float a = v[q][i];
+      if (p > 0.f) a = keep(seed, rb + c + i, p) ? a / (1.f - p) : 0.f;
+      if (res) a += r[q][i];
+      v[q][i] = a;
+      s += a;
+    }
+  }
+  const float mean = warp_sum(s) * (1.f / H);
+  float s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = v[q][i] - mean;
+      s2 += d * d;
+    }
+  const float rstd = rsqrtf(warp_sum(s2) * (1.f / H) + eps);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int c = 4 * (lane + 64 * q);
+    float g[4], b[4], o[4];
+    ldf4(gamma + c, g);
+    ldf4(beta + c, b);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (v[q][i] - mean) * rstd * g[i] + b[i];
+    st4<T>(out + rb + c, o);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// LN backward, rows strided over the grid's waves; per-block column partials part[block][NRED][H]:
+// dgamma (sum dout * xhat), dbeta (sum dout) and (NRED = 3) the column sums of dx (the bias gradient of the
+// dense layer in front of the LayerNorm).
+template <typename T, int NQ, int NRED>
+__global__ __launch_bounds__(256) void ln_bwd_rw_kernel(const T* __restrict__ dout, const T* __restrict__ x,
+                                                        const T* __restrict__ res, const float* __restrict__ gamma,
+                                                        const float* __restrict__ mean_in,
+                                                        const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                        T* __restrict__ dres, float* __restrict__ part, int rows,
+                                                        float p, uint64_t seed) {
+  constexpr int H = 256 * NQ;
+  __shared__ float red[4][NRED][H];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pg[NQ][4], pb[NQ][4], pd[NQ][4], gm[NQ][4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    ldf4(gamma + 4 * (lane + 64 * q), gm[q]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pg[q][i] = pb[q][i] = pd[q][i] = 0.f;
+  }
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+    const long long rb = (long long)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xv[NQ][4], rv[NQ][4], dv[NQ][4];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = 4 * (lane + 64 * q);
+      ld4<T>(x + rb + c, xv[q]);
+      if (res) ld4<T>(res + rb + c, rv[q]);
+      ld4<T>(dout + rb + c, dv[q]);
+    }
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = 4 * (lane + 64 * q);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = xv[q][i];
+        if (p > 0.f) v = keep(seed, rb + c + i, p) ? v / (1.f - p) : 0.f;
+        if (res) v += rv[q][i];
+        const float xh = (v - mean) * rstd;
+        const float d = dv[q][i];
+        pg[q][i] += d * xh;
+        pb[q][i] += d;
+        const float dxh = d * gm[q][i];
+        xv[q][i] = xh;
+        dv[q][i] = dxh;
+        a += dxh;
+        b += dxh * xh;
+      }
+    }
+    a = warp_sum(a) * (1.f / H);
+    b = warp_sum(b) * (1.f / H);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = 4 * (lane + 64 * q);
+      float o[4], od[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[i] = rstd * (dv[q][i] - a - xv[q][i] * b);
+        od[i] = (p > 0.f) ? (keep(seed, rb + c + i, p) ? o[i] / (1.f - p) : 0.f) : o[i];
+        if (NRED > 2) pd[q][i] += bf_round<T>(od[i]);
+      }
+      if (dres) st4<T>(dres + rb + c, o);
+      if (dx) st4<T>(dx + rb + c, od);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 4 * (lane + 64 * q) + i;
+      red[wave][0][c] = pg[q][i];
+      red[wave][1][c] = pb[q][i];
+      if (NRED > 2) red[wave][NRED - 1][c] = pd[q][i];
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NRED * H; i += 256) {
+    const int r = i / H, c = i - r * H;
+    part[(long long)blockIdx.x * NRED * H + i] = red[0][r][c] + red[1][r][c] + red[2][r][c] + red[3][r][c];
+  }
+}
+
+// column sums of x [rows][ld] (first N columns): lane = 8 consecutive columns, waves stride the rows;
+// per-block partials part[block][N]
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_rw_kernel(const T* __restrict__ x, long long ld, int rows, int N,
+                                                        float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.y * 512 + 8 * lane;
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  if (c0 < N) {
+    for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+      float a[4], b[4];
+      ld4<T>(x + (long long)row * ld + c0, a);
+      ld4<T>(x + (long long)row * ld + c0 + 4, b);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i] += a[i];
+        acc[4 + i] += b[i];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[wave][8 * lane + i] = acc[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int c = blockIdx.y * 512 + i;
+    if (c < N) part[(long long)blockIdx.x * N + c] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
+}
+
+// Column sums of partial rows, 64 columns x 16 row-stripes per block (1024 threads), fixed order:
+//   out_k[c] (+)= sum_i part[i * stride + k * N + c], k < nout
+__global__ __launch_bounds__(1024) void colred16_kernel(const float* __restrict__ part, int nblocks, long long stride,
+                                                        int N, int nout, float* out0, float* out1, float* out2,
+                                                        int accumulate) {
+  __shared__ double sa[3][16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  double a[3] = {0, 0, 0};
+  if (c < N) {
+    for (int i = ty; i < nblocks; i += 16)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (k < nout) a[k] += part[(long long)i * stride + (long long)k * N + c];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) sa[k][ty][tx] = a[k];
+  __syncthreads();
+  if (ty < 3 && ty < nout && c < N) {
+    double t = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t += sa[ty][j][tx];
+    float* o = ty == 0 ? out0 : (ty == 1 ? out1 : out2);
+    if (o) o[c] = (accumulate ? o[c] : 0.f) + (float)t;
+  }
+}
+
 // y = dy * (1 - t^2) where t = tanh output (pooler backward); all [rows][N] with given lds
 template <typename T>
 __global__ void tanh_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ t, T* __restrict__ dx, long long n) {
@@ -445,6 +676,25 @@ VCG_API int vcg_ln_fwd(int dtype, const void* x, const void* res, const float* g
                        float* mean, float* rstd, int rows, int H, float eps, float dropout_p, unsigned long long seed,
                        hipStream_t s) {
   VCG_REQUIRE(H <= 256 * LN_MAXE, "hidden size too large");
+  const int nq = H % 256 == 0 ? H / 256 : 0;
+  if (nq >= 1 && nq <= 4 && rows > 0) {  // one wave per row
+    const dim3 g((rows + 3) / 4);
+#define VCG_LNF(T, NQ)                                                                                               \
+  hipLaunchKernelGGL((ln_fwd_rw_kernel<T, NQ>), g, dim3(256), 0, s, (const T*)x, (const T*)res, gamma, beta, (T*)out, \
+                     mean, rstd, rows, eps, dropout_p, (uint64_t)seed)
+#define VCG_LNF_T(T)                          \
+  switch (nq) {                               \
+    case 1: VCG_LNF(T, 1); break;             \
+    case 2: VCG_LNF(T, 2); break;             \
+    case 3: VCG_LNF(T, 3); break;             \
+    default: VCG_LNF(T, 4); break;            \
+  }
+    if (dtype == VCG_BF16) { VCG_LNF_T(bf16_t) } else { VCG_LNF_T(float) }
+#undef VCG_LNF_T
+#undef VCG_LNF
+    VCG_LAUNCH_CHECK();
+    return VCG_OK;
+  }
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(rows), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)res, gamma,
                        beta, (bf16_t*)out, mean, rstd, H, eps, dropout_p, (uint64_t)seed);
@@ -457,11 +707,39 @@ VCG_API int vcg_ln_fwd(int dtype, const void* x, const void* res, const float* g
 
 VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* res, const float* gamma,
                        const float* mean, const float* rstd, void* dx, void* dres, float* gamma_grad,
-                       float* beta_grad, float* ws, long long ws_bytes, int rows, int H, float dropout_p,
-                       unsigned long long seed, hipStream_t s) {
+                       float* beta_grad, float* bias_grad, float* ws, long long ws_bytes, int rows, int H,
+                       float dropout_p, unsigned long long seed, hipStream_t s) {
   int rpb;
   const int nb = row_blocks(rows, &rpb);
   VCG_REQUIRE(ws_bytes >= (long long)nb * 2 * H * 4, "workspace too small");
+  VCG_REQUIRE(!bias_grad || dx, "bias_grad is the column sum of dx");
+  const int nq = H % 256 == 0 ? H / 256 : 0;
+  const int nbr = (rows + 3) / 4 < 256 ? (rows + 3) / 4 : 256;  // one wave per row, <= 8 rows per wave at 8192
+  if (nq >= 1 && nq <= 4 && rows > 0 && (long long)nbr * 3 * H <= (long long)nb * 2 * H) {
+    const int nred = bias_grad ? 3 : 2;
+#define VCG_LNB(T, NQ, NR)                                                                                        \
+  hipLaunchKernelGGL((ln_bwd_rw_kernel<T, NQ, NR>), dim3(nbr), dim3(256), 0, s, (const T*)dout, (const T*)x,         \
+                     (const T*)res, gamma, mean, rstd, (T*)dx, (T*)dres, ws, rows, dropout_p, (uint64_t)seed)
+#define VCG_LNB_Q(T, NR)                     \
+  switch (nq) {                              \
+    case 1: VCG_LNB(T, 1, NR); break;        \
+    case 2: VCG_LNB(T, 2, NR); break;        \
+    case 3: VCG_LNB(T, 3, NR); break;        \
+    default: VCG_LNB(T, 4, NR); break;       \
+  }
+    if (dtype == VCG_BF16) {
+      if (nred == 3) { VCG_LNB_Q(bf16_t, 3) } else { VCG_LNB_Q(bf16_t, 2) }
+    } else {
+      if (nred == 3) { VCG_LNB_Q(float, 3) } else { VCG_LNB_Q(float, 2) }
+    }
+#undef VCG_LNB_Q
+#undef VCG_LNB
+    VCG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colred16_kernel, dim3((H + 63) / 64), dim3(1024), 0, s, ws, nbr, (long long)nred * H, H, nred,
+                       gamma_grad, beta_grad, bias_grad, 1);
+    VCG_LAUNCH_CHECK();
+    return VCG_OK;
+  }
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dout, (const bf16_t*)x,
                        (const bf16_t*)res, gamma, mean, rstd, (bf16_t*)dx, (bf16_t*)dres, ws, H, rpb, rows, dropout_p,
@@ -474,6 +752,18 @@ VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* r
   hipLaunchKernelGGL(colred_kernel, dim3((H + 63) / 64), dim3(256), 0, s, ws, nb, (long long)2 * H, H, (long long)H,
                      gamma_grad, beta_grad, 1);
   VCG_LAUNCH_CHECK();
+  if (bias_grad) {  // column sums of dx (generic path: the partial buffer is free again)
+    if (dtype == VCG_BF16)
+      hipLaunchKernelGGL(colsum_part_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dx, (long long)H,
+                         rows, H, rpb, ws);
+    else
+      hipLaunchKernelGGL(colsum_part_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dx, (long long)H, rows,
+                         H, rpb, ws);
+    VCG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colred_kernel, dim3((H + 63) / 64), dim3(256), 0, s, ws, nb, (long long)H, H, 0LL, bias_grad,
+                       (float*)nullptr, 1);
+    VCG_LAUNCH_CHECK();
+  }
   return VCG_OK;
 }
 
@@ -489,6 +779,21 @@ VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, 
   int rpb;
   const int nb = row_blocks(rows, &rpb);
   VCG_REQUIRE(ws_bytes >= (long long)nb * N * 4, "workspace too small");
+  if (N % 8 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15) == 0 && rows > 0) {
+    int nbx = (rows + 3) / 4;
+    nbx = nbx < 128 ? nbx : 128;
+    if (nbx > nb) nbx = nb;
+    const dim3 g(nbx, (N + 511) / 512);
+    if (dtype == VCG_BF16)
+      hipLaunchKernelGGL(colsum_rw_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, ld, rows, N, ws);
+    else
+      hipLaunchKernelGGL(colsum_rw_kernel<float>, g, dim3(256), 0, s, (const float*)x, ld, rows, N, ws);
+    VCG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colred16_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, ws, nbx, (long long)N, N, 1, out,
+                       (float*)nullptr, (float*)nullptr, accumulate);
+    VCG_LAUNCH_CHECK();
+    return VCG_OK;
+  }
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(colsum_part_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, (const bf16_t*)x, ld, rows, N, rpb, ws);
   else

@@ -134,9 +134,8 @@ class BertEncoderEngine:
             I = inter.out_features
             ln2 = layer.output.LayerNorm
             dfo, dh1_res = ops.ln_bwd(dh_, s["fo"], s["h1"], ln2.weight, s["m2"], s["r2"], ln2.weight.grad,
-                                      ln2.bias.grad, rows, H, p_h, s["s2"])
+                                      ln2.bias.grad, rows, H, p_h, s["s2"], bias_grad=out.bias.grad)
             ops.gemm_splitk(dfo, s["ff"], out.weight.grad, H, I, rows, H, I, transA=True, transB=True)
-            ops.colsum(dfo, H, rows, H, out.bias.grad)
             dpre = self._gemm_dx(dfo, self._w(out.weight), rows, I, H, act=ops.ACT_GELU_BWD, residual=s["pre"], ldr=I)
             del dfo
             ops.gemm_splitk(dpre, s["h1"], inter.weight.grad, I, H, rows, I, H, transA=True, transB=True)
@@ -144,11 +143,10 @@ class BertEncoderEngine:
             dh1 = self._gemm_dx(dpre, self._w(inter.weight), rows, H, I, residual=dh1_res, ldr=H)
             del dpre, dh1_res
             ln1 = at.output.LayerNorm
-            dao, dh_res = ops.ln_bwd(dh1, s["ao"], s["h"], ln1.weight, s["m1"], s["r1"], ln1.weight.grad,
-                                     ln1.bias.grad, rows, H, p_h, s["s1"])
             od = at.output.dense
+            dao, dh_res = ops.ln_bwd(dh1, s["ao"], s["h"], ln1.weight, s["m1"], s["r1"], ln1.weight.grad,
+                                     ln1.bias.grad, rows, H, p_h, s["s1"], bias_grad=od.bias.grad)
             ops.gemm_splitk(dao, s["ctx"], od.weight.grad, H, H, rows, H, H, transA=True, transB=True)
-            ops.colsum(dao, H, rows, H, od.bias.grad)
             dctx = self._gemm_dx(dao, self._w(od.weight), rows, H, H)
             del dao
             # ---- attention backward

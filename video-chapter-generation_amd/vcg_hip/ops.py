@@ -375,13 +375,16 @@ def ln_fwd(x, res, gamma, beta, rows, H, eps, p=0.0, seed=0):
 
 
 def ln_bwd(dout, x, res, gamma, mean, rstd, gamma_grad, beta_grad, rows, H, p=0.0, seed=0, want_dx=True,
-           want_dres=True):
+           want_dres=True, bias_grad=None):
+    """LayerNorm(dropout(x) + res) backward. bias_grad (optional, accumulated): column sums of dx, i.e. the
+    bias gradient of the dense layer that produced x."""
     dx = torch.empty_like(dout) if want_dx else None
     dres = torch.empty_like(dout) if want_dres else None
     nbytes = _lib.query("vcg_ln_bwd_ws_bytes", rows, H)
     w = ws(nbytes, dout.device)
     _lib.call("vcg_ln_bwd", dt_code(dout.dtype), P(dout), P(x), P(res), P(gamma), P(mean), P(rstd), P(dx), P(dres),
-              P(gamma_grad), P(beta_grad), P(w), w.numel() * 4, rows, H, float(p), int(seed) & (2**64 - 1), stream())
+              P(gamma_grad), P(beta_grad), P(bias_grad), P(w), w.numel() * 4, rows, H, float(p),
+              int(seed) & (2**64 - 1), stream())
     return dx, dres
 
 
