@@ -80,6 +80,10 @@ VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, int mask_mode, const v
 /* torchvision stem maxpool 3x3/2 and avgpool + fc=Identity (resnet50_tsm.py:19) */
 VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* idx, int N, int H, int W, int C, hipStream_t s);
 VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C, hipStream_t s);
+/* maxpool backward fused with the stem BatchNorm backward reduction (BN + ReLU before the pool): g = mask(dx),
+   mask = fma(y, mscale, mshift) > 0; sum_g / sum_gx finalized, dgamma / dbeta accumulated */
+VCG_API long long vcg_maxpool_bwd_bn_ws_bytes(int C);
+VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* idx, void* g, int N, int H, int W, int C, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t s);
 VCG_API int vcg_avgpool_fwd(int dtype, const void* x, float* y, int N, int HW, int C, hipStream_t s);
 VCG_API int vcg_avgpool_bwd(int dtype, const float* dy, void* dx, int N, int HW, int C, hipStream_t s);
 /* rearrange 'b t c h w -> (b t) c h w' (two_stream.py:183) + NCHW->NHWC staging */

@@ -480,3 +480,57 @@ def test_layernorm_fwd_bwd(K, dtype, H):
     cs = torch.full((H,), 0.25, device=DEV)
     K.colsum(dx, H, rows, H, cs)
     _close(cs - 0.25, dx.double().sum(0), torch.float32, "colsum")
+
+
+def test_maxpool_bwd_bn(K):
+    """maxpool backward fused with the stem BN mask + reduction == maxpool_bwd, masked; sums in float64."""
+    dtype = torch.bfloat16
+    N, C, H, W = 3, 64, 13, 12
+    x = F.relu(_rand((N, H, W, C), dtype, 81)).to(DEV)
+    ys, idx = K.maxpool_fwd(x, N, H, W, C)
+    dys = _rand(ys.shape, dtype, 82).to(DEV)
+    y = _rand((N, H, W, C), dtype, 83).to(DEV)
+    g0 = torch.Generator().manual_seed(84)
+    msc = (torch.tensor([0.5, 1.0, 2.0, -0.5, -1.0, -2.0])[torch.randint(0, 6, (C,), generator=g0)]).to(DEV)
+    msh = (torch.randint(-16, 17, (C,), generator=g0).float() / 64).to(DEV)
+    mean = (torch.randn(C, generator=g0) * 0.1).to(DEV)
+    inv = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    sums = torch.zeros((2, C), device=DEV)
+    dg, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), 0.25, device=DEV)
+    g = K.maxpool_bwd_bn(dys, idx, N, H, W, C, y, mean, inv, msc, msh, sums, dg, db)
+    dx = K.maxpool_bwd(dys, idx, N, H, W, C)
+    ref = torch.where(y.float() * msc + msh > 0, dx, torch.zeros_like(dx))
+    assert torch.equal(g, ref)
+    gd = g.double().reshape(-1, C)
+    sg = gd.sum(0)
+    sx = (gd * (y.double().reshape(-1, C) - mean.double()) * inv.double()).sum(0)
+    assert (sums[0].double() - sg).abs().max().item() <= 1e-4 * (sg.abs().max().item() + 1)
+    assert (sums[1].double() - sx).abs().max().item() <= 1e-4 * (sx.abs().max().item() + 1)
+    assert (db.double() - 0.25 - sg).abs().max().item() <= 1e-4 * (sg.abs().max().item() + 1)
+    assert (dg.double() - 0.5 - sx).abs().max().item() <= 1e-4 * (sx.abs().max().item() + 1)
+
+
+def test_attention_softmax_dropout(K):
+    """Masked softmax + dropout: P matches torch softmax over the valid keys; Pd = P / (1 - p) on kept
+    entries and 0 on dropped ones (drop rate ~ p); the backward regenerates the same mask."""
+    B, nh, L, Lp, p = 2, 3, 40, 40, 0.1
+    Z = B * nh
+    S = torch.randn(Z, L, Lp).to(DEV)
+    mask = torch.ones(B, L, dtype=torch.int64)
+    mask[1, 30:] = 0
+    mask = mask.to(DEV)
+    Pm, Pd = torch.empty_like(S), torch.empty_like(S)
+    K.attn_softmax_fwd(S, mask, Pm, Pd, B, nh, L, Lp, 0.125, p, seed=1234)
+    add = torch.where(mask.bool(), 0.0, float("-inf")).repeat_interleave(nh, 0)[:, None, :]
+    ref = torch.softmax(S.double() * 0.125 + add.double(), -1)
+    assert (Pm.double() - ref).abs().max().item() < 1e-5
+    kept = Pd != 0
+    valid = ref > 0
+    rate = 1 - kept[valid].float().mean().item()
+    assert abs(rate - p) < 0.02, f"drop rate {rate:.3f}"
+    assert torch.allclose(Pd[kept], Pm[kept] / (1 - p), rtol=1e-6, atol=0)
+    dS = torch.empty_like(S)
+    K.attn_softmax_bwd(torch.ones_like(S), Pm, dS, Z, L, Lp, 0.125, p, seed=1234)
+    dp = kept.double() / (1 - p)
+    dot = (dp * Pm.double()).sum(-1, keepdim=True)
+    assert (dS.double() - 0.125 * Pm.double() * (dp - dot)).abs().max().item() < 1e-5

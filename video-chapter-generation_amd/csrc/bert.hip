@@ -11,11 +11,19 @@ using namespace vcg;
 
 namespace {
 
+// Dropout keep decision of element idx (a stateless counter hash, so the backward regenerates the mask):
+// 32-bit murmur3 finaliser of (idx * golden ratio) ^ seed -- two 32-bit multiplies, no 64-bit arithmetic.
+// (Tensors here stay below 2^32 elements; the seed differs per dropout site and step.)
 __device__ __forceinline__ bool keep(uint64_t seed, uint64_t idx, float p) {
   if (p <= 0.f) return true;
-  const uint64_t h = mix64(seed + 0x9E3779B97F4A7C15ULL * (idx + 1));
-  const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-  return u >= p;
+  uint32_t h = ((uint32_t)idx * 0x9E3779B1u) ^ (uint32_t)seed;
+  h += (uint32_t)(seed >> 32);
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
 }
 
 // value as stored in T (bias-gradient sums use the gradient the GEMM will read)
@@ -296,74 +304,113 @@ __global__ void colsum_part_kernel(const T* __restrict__ x, long long ld, int ro
 // Writes P (pre-dropout, needed by the backward) and Pd = dropout(P) (input of the PV GEMM).
 // HF eager attention adds finfo(f32).min to padded keys; exp() of that underflows to exactly 0,
 // which is what excluding the key gives.
+template <typename T> __device__ __forceinline__ void ld2(const T* p, float& a, float& b) {
+  if constexpr (sizeof(T) == 4) {
+    const float2 q = *reinterpret_cast<const float2*>(p);
+    a = q.x; b = q.y;
+  } else {
+    const uint32_t q = *reinterpret_cast<const uint32_t*>(p);
+    a = __uint_as_float(q << 16); b = __uint_as_float(q & 0xffff0000u);
+  }
+}
+template <typename T> __device__ __forceinline__ void st2(T* p, float a, float b) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float2*>(p) = make_float2(a, b);
+  } else {
+    *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  }
+}
+
+// One wave per score row; lane l owns key pairs j = 2l + 128e (e < 4: L <= 512, Lp even): 4-B (bf16)
+// / 8-B (fp32) loads and stores.
 template <typename T>
-__global__ void attn_softmax_fwd_kernel(const T* __restrict__ S, const long long* __restrict__ mask,
-                                        T* __restrict__ P, T* __restrict__ Pd, int nh, int L, int Lp, float scale,
-                                        float p, uint64_t seed) {
+__global__ __launch_bounds__(256) void attn_softmax_fwd_kernel(const T* __restrict__ S,
+                                                               const long long* __restrict__ mask,
+                                                               T* __restrict__ P, T* __restrict__ Pd, int nh, int L,
+                                                               int Lp, float scale, float p, uint64_t seed) {
   const int z = blockIdx.y;
   const int b = z / nh;
-  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= L) return;
   const long long base = ((long long)z * L + row) * Lp;
-  constexpr int MAXJ = 8;  // L <= 512
-  float v[MAXJ];
+  constexpr int MAXE = 4;
+  float v[MAXE][2];
   float mx = -INFINITY;
 #pragma unroll
-  for (int e = 0; e < MAXJ; ++e) {
-    const int j = lane + e * 64;
-    v[e] = -INFINITY;
-    if (j < L && (mask == nullptr || mask[(long long)b * L + j] != 0)) v[e] = to_f<T>(S[base + j]) * scale;
-    mx = fmaxf(mx, v[e]);
+  for (int e = 0; e < MAXE; ++e) {
+    const int j = 2 * lane + 128 * e;
+    v[e][0] = v[e][1] = -INFINITY;
+    if (j < L) {
+      float a, c;
+      ld2<T>(S + base + j, a, c);
+      const bool k0 = mask == nullptr || mask[(long long)b * L + j] != 0;
+      const bool k1 = j + 1 < L && (mask == nullptr || mask[(long long)b * L + j + 1] != 0);
+      v[e][0] = k0 ? a * scale : -INFINITY;
+      v[e][1] = k1 ? c * scale : -INFINITY;
+      mx = fmaxf(mx, fmaxf(v[e][0], v[e][1]));
+    }
   }
   mx = warp_max(mx);
   float sum = 0.f;
 #pragma unroll
-  for (int e = 0; e < MAXJ; ++e) {
-    v[e] = (v[e] == -INFINITY) ? 0.f : __expf(v[e] - mx);
-    sum += v[e];
-  }
+  for (int e = 0; e < MAXE; ++e)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      v[e][k] = (v[e][k] == -INFINITY) ? 0.f : __expf(v[e][k] - mx);
+      sum += v[e][k];
+    }
   sum = warp_sum(sum);
   const float inv = 1.f / sum;
 #pragma unroll
-  for (int e = 0; e < MAXJ; ++e) {
-    const int j = lane + e * 64;
+  for (int e = 0; e < MAXE; ++e) {
+    const int j = 2 * lane + 128 * e;
     if (j < Lp) {
-      const float pr = j < L ? v[e] * inv : 0.f;
-      P[base + j] = from_f<T>(pr);
-      if (Pd) Pd[base + j] = from_f<T>(keep(seed, base + j, p) ? pr / (1.f - p) : 0.f);
+      const float p0 = j < L ? v[e][0] * inv : 0.f;
+      const float p1 = j + 1 < L ? v[e][1] * inv : 0.f;
+      st2<T>(P + base + j, p0, p1);
+      if (Pd) {
+        const float d0 = keep(seed, base + j, p) ? p0 / (1.f - p) : 0.f;
+        const float d1 = keep(seed, base + j + 1, p) ? p1 / (1.f - p) : 0.f;
+        st2<T>(Pd + base + j, d0, d1);
+      }
     }
   }
 }
 
-// dS = scale * P o (dP - rowsum(dP o P)), dP = dPd o mask/(1-p)
+// dS = scale * P o (dP - rowsum(dP o P)), dP = dPd o mask/(1-p); same lane layout as the forward
 template <typename T>
-__global__ void attn_softmax_bwd_kernel(const T* __restrict__ dPd, const T* __restrict__ P, T* __restrict__ dS, int L,
-                                        int Lp, float scale, float p, uint64_t seed, int Z) {
+__global__ __launch_bounds__(256) void attn_softmax_bwd_kernel(const T* __restrict__ dPd, const T* __restrict__ P,
+                                                               T* __restrict__ dS, int L, int Lp, float scale, float p,
+                                                               uint64_t seed, int Z) {
   const int z = blockIdx.y;
-  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= L || z >= Z) return;
   const long long base = ((long long)z * L + row) * Lp;
-  constexpr int MAXJ = 8;
-  float dp[MAXJ], pr[MAXJ];
+  constexpr int MAXE = 4;
+  float dp[MAXE][2], pr[MAXE][2];
   float dot = 0.f;
 #pragma unroll
-  for (int e = 0; e < MAXJ; ++e) {
-    const int j = lane + e * 64;
-    dp[e] = 0.f; pr[e] = 0.f;
-    if (j < L) {
-      pr[e] = to_f<T>(P[base + j]);
-      const float g = to_f<T>(dPd[base + j]);
-      dp[e] = keep(seed, base + j, p) ? g / (1.f - p) : 0.f;
-      dot += dp[e] * pr[e];
+  for (int e = 0; e < MAXE; ++e) {
+    const int j = 2 * lane + 128 * e;
+    dp[e][0] = dp[e][1] = pr[e][0] = pr[e][1] = 0.f;
+    if (j < Lp) {
+      float g0, g1;
+      ld2<T>(P + base + j, pr[e][0], pr[e][1]);
+      ld2<T>(dPd + base + j, g0, g1);
+      dp[e][0] = (j < L && keep(seed, base + j, p)) ? g0 / (1.f - p) : 0.f;
+      dp[e][1] = (j + 1 < L && keep(seed, base + j + 1, p)) ? g1 / (1.f - p) : 0.f;
+      dot += dp[e][0] * pr[e][0] + dp[e][1] * pr[e][1];
     }
   }
   dot = warp_sum(dot);
 #pragma unroll
-  for (int e = 0; e < MAXJ; ++e) {
-    const int j = lane + e * 64;
-    if (j < Lp) dS[base + j] = from_f<T>(j < L ? scale * pr[e] * (dp[e] - dot) : 0.f);
+  for (int e = 0; e < MAXE; ++e) {
+    const int j = 2 * lane + 128 * e;
+    if (j < Lp)
+      st2<T>(dS + base + j, j < L ? scale * pr[e][0] * (dp[e][0] - dot) : 0.f,
+             j + 1 < L ? scale * pr[e][1] * (dp[e][1] - dot) : 0.f);
   }
 }
 
@@ -485,13 +532,18 @@ __global__ __launch_bounds__(256) void ln_bwd_rw_kernel(const T* __restrict__ do
       ld4<T>(dout + rb + c, dv[q]);
     }
     float a = 0.f, b = 0.f;
+    uint32_t kb = 0xFFFFFFFFu;  // dropout keep bits of this lane's elements (hashed once)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int c = 4 * (lane + 64 * q);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float v = xv[q][i];
-        if (p > 0.f) v = keep(seed, rb + c + i, p) ? v / (1.f - p) : 0.f;
+        if (p > 0.f) {
+          const bool k = keep(seed, rb + c + i, p);
+          kb = k ? kb : (kb & ~(1u << (4 * q + i)));
+          v = k ? v / (1.f - p) : 0.f;
+        }
         if (res) v += rv[q][i];
         const float xh = (v - mean) * rstd;
         const float d = dv[q][i];
@@ -513,7 +565,7 @@ __global__ __launch_bounds__(256) void ln_bwd_rw_kernel(const T* __restrict__ do
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         o[i] = rstd * (dv[q][i] - a - xv[q][i] * b);
-        od[i] = (p > 0.f) ? (keep(seed, rb + c + i, p) ? o[i] / (1.f - p) : 0.f) : o[i];
+        od[i] = (p > 0.f) ? (((kb >> (4 * q + i)) & 1u) ? o[i] / (1.f - p) : 0.f) : o[i];
         if (NRED > 2) pd[q][i] += bf_round<T>(od[i]);
       }
       if (dres) st4<T>(dres + rb + c, o);
@@ -807,7 +859,7 @@ VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, 
 
 VCG_API int vcg_attn_softmax_fwd(int dtype, const void* S, const long long* mask, void* P, void* Pd, int B, int nh,
                                  int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s) {
-  VCG_REQUIRE(L <= 512 && Lp >= L, "L must be <= 512");
+  VCG_REQUIRE(L <= 512 && Lp >= L && Lp % 2 == 0 && Lp <= 512, "L must be <= 512, Lp even");
   dim3 grid((L + 3) / 4, B * nh);
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(attn_softmax_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)S, mask, (bf16_t*)P,
@@ -821,6 +873,7 @@ VCG_API int vcg_attn_softmax_fwd(int dtype, const void* S, const long long* mask
 
 VCG_API int vcg_attn_softmax_bwd(int dtype, const void* dPd, const void* P, void* dS, int Z, int L, int Lp, float scale,
                                  float dropout_p, unsigned long long seed, hipStream_t s) {
+  VCG_REQUIRE(L <= 512 && Lp >= L && Lp % 2 == 0 && Lp <= 512, "L must be <= 512, Lp even");
   dim3 grid((L + 3) / 4, Z);
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(attn_softmax_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dPd, (const bf16_t*)P,

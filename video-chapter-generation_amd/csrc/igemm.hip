@@ -416,24 +416,36 @@ static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
   return launch_bn<T, AM, BMD, EPI_SPLITK>(p, splits, s);
 }
 
-// split-K reduction: out[m][n] (+)= sum_s ws[s][m][n], with optional conv-weight layout permutation
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long MN, int N,
-                                     float* __restrict__ out, int accumulate, int conv_perm, int KH, int KW,
-                                     int Cpad, int Cin, float scale) {
-  long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+// split-K reduction: out[m][n] (+)= sum_s ws[s][m][n], with optional conv-weight layout permutation.
+// The slabs are summed in split order (deterministic); 8 independent loads are in flight per thread
+// (a dependent one-load-per-iteration loop is latency-bound at 100-300 splits).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long MN,
+                                                            int N, float* __restrict__ out, int accumulate,
+                                                            int conv_perm, int KH, int KW, int Cpad, int Cin,
+                                                            float scale) {
+  const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (idx >= MN) return;
   float v = 0.f;
-  for (int s = 0; s < splits; ++s) v += ws[s * MN + idx];
+  const float* p = ws + idx;
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {
+    float a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = p[(long long)(s + k) * MN];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += a[k];
+  }
+  for (; s < splits; ++s) v += p[(long long)s * MN];
   v *= scale;
   long long dst = idx;
   if (conv_perm) {
-    // idx = m * N + n, m = cout, n = (kh*KW + kw)*Cpad + ci  ->  OIHW [cout][ci][kh][kw]
-    const int m = (int)(idx / N);
-    const int n = (int)(idx - (long long)m * N);
+    // idx = m * N + n, m = cout, n = (kh*KW + kw)*Cpad + ci  ->  OIHW [cout][ci][kh][kw]  (MN < 2^31)
+    const int m = (int)idx / N;
+    const int n = (int)idx - m * N;
     const int tap = n / Cpad;
     const int ci = n - tap * Cpad;
     if (ci >= Cin) return;
-    const int kh = tap / KW, kw = tap - (tap / KW) * KW;
+    const int kh = tap / KW, kw = tap - kh * KW;
     dst = (((long long)m * Cin + ci) * KH + kh) * KW + kw;
   }
   if (accumulate) out[dst] += v;

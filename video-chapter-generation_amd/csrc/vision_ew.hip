@@ -310,7 +310,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 }
 
 // ------------------------------------------------------------------ max pool 3x3 / 2, pad 1
-// thread = (output pixel, 16-B channel chunk); first max in (kh, kw) scan order (torch CPU semantics)
+// thread = (output pixel, 16-B channel chunk); first max in (kh, kw) scan order (torch CPU semantics);
+// the argmax bytes of a chunk are stored as one VN-byte word
+template <int VN> struct IdxWord;
+template <> struct IdxWord<8> { typedef uint2 t; };
+template <> struct IdxWord<4> { typedef uint32_t t; };
+template <int VN> __device__ __forceinline__ void idx_store(uint8_t* p, const uint8_t (&b)[VN]) {
+  if constexpr (VN == 8) {
+    uint2 q;
+    q.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+    q.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+    *reinterpret_cast<uint2*>(p) = q;
+  } else {
+    *reinterpret_cast<uint32_t*>(p) = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+  }
+}
+template <int VN> __device__ __forceinline__ uint8_t idx_byte(const typename IdxWord<VN>::t& w, int e) {
+  if constexpr (VN == 8) return (uint8_t)(((e < 4 ? w.x : w.y) >> (8 * (e & 3))) & 0xFF);
+  else return (uint8_t)((w >> (8 * e)) & 0xFF);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int H, int W, int C, int OH,
@@ -342,49 +361,93 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
     }
   }
   store16<T>(y + v * VN, best);
-  uint8_t* ip = idx + v * VN;
-#pragma unroll
-  for (int e = 0; e < VN; ++e) ip[e] = bi[e];
+  idx_store<VN>(idx + v * VN, bi);
 }
 
-// thread = (input pixel, chunk): sums dy over the <= 4 windows whose argmax is this pixel
-template <typename T>
+// thread = (input pixel, chunk): sums dy over the <= 4 windows whose argmax is this pixel. Grid-stride with
+// a fixed chunk per thread (cpr <= 256). RED: the result is the upstream gradient of the stem BN + ReLU:
+// masked by fma(y, msc, msh) > 0, stored as g, and reduced into per-block partials part[block][2C] of
+// sum g and sum g * (y - mean) * invstd (the BatchNorm backward sums; bn_bwd_finalize_kernel).
+template <typename T, bool RED>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                           T* __restrict__ dx, int H, int W, int C, int OH, int OW,
-                                                          int lcpr, long long TV) {
+                                                          int lcpr, long long TV, const T* __restrict__ yb,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ msc,
+                                                          const float* __restrict__ msh, float* __restrict__ part) {
   constexpr int VN = V<T>::N;
-  const long long v = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (v >= TV) return;
-  const int chunk = (int)(v & ((1 << lcpr) - 1));
-  const int pix = (int)(v >> lcpr);
-  const int iw = pix % W;
-  const int t = pix / W;
-  const int ih = t % H;
-  const int n = t / H;
-  float acc[VN];
+  typedef typename IdxWord<VN>::t IW;
+  __shared__ float red[RED ? 2 : 1][RED ? 256 : 1][VN];
+  const int cpr = 1 << lcpr;
+  const int chunk = threadIdx.x & (cpr - 1);
+  const int c0 = chunk * VN;
+  float mu[VN], sc[VN], sh[VN], s1[VN], s2[VN];
+  if (RED) {
+    load_params<VN>(mean, c0, mu);
+    load_params<VN>(msc, c0, sc);
+    load_params<VN>(msh, c0, sh);
 #pragma unroll
-  for (int e = 0; e < VN; ++e) acc[e] = 0.f;
-  const int oh0 = ih / 2, oh1 = (ih + 1) / 2;  // windows with 2*oh-1 <= ih <= 2*oh+1
-  const int ow0 = iw / 2, ow1 = (iw + 1) / 2;
-  for (int oh = oh0; oh <= oh1; ++oh) {
-    if (oh >= OH) continue;
-    const int kh = ih - (oh * 2 - 1);
-    if (kh < 0 || kh > 2) continue;
-    for (int ow = ow0; ow <= ow1; ++ow) {
-      if (ow >= OW) continue;
-      const int kw = iw - (ow * 2 - 1);
-      if (kw < 0 || kw > 2) continue;
-      const long long o = (((long long)n * OH + oh) * OW + ow) * C + chunk * VN;
-      const uint8_t want = (uint8_t)(kh * 3 + kw);
-      float g[VN];
-      load16<T>(dy + o, g);
-      const uint8_t* ip = idx + o;
+    for (int e = 0; e < VN; ++e) s1[e] = s2[e] = 0.f;
+  }
+  for (long long v = (long long)blockIdx.x * 256 + threadIdx.x; v < TV; v += (long long)gridDim.x * 256) {
+    const int pix = (int)(v >> lcpr);
+    const int iw = pix % W;
+    const int t = pix / W;
+    const int ih = t % H;
+    const int n = t / H;
+    float acc[VN];
 #pragma unroll
-      for (int e = 0; e < VN; ++e)
-        if (ip[e] == want) acc[e] += g[e];
+    for (int e = 0; e < VN; ++e) acc[e] = 0.f;
+    const int oh0 = ih / 2, oh1 = (ih + 1) / 2;  // windows with 2*oh-1 <= ih <= 2*oh+1
+    const int ow0 = iw / 2, ow1 = (iw + 1) / 2;
+    float yv[VN];
+    if (RED) load16<T>(yb + v * VN, yv);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      if (oh >= OH) continue;
+      const int kh = ih - (oh * 2 - 1);
+      if (kh < 0 || kh > 2) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        if (ow >= OW) continue;
+        const int kw = iw - (ow * 2 - 1);
+        if (kw < 0 || kw > 2) continue;
+        const long long o = (((long long)n * OH + oh) * OW + ow) * C + chunk * VN;
+        const uint8_t want = (uint8_t)(kh * 3 + kw);
+        float g[VN];
+        load16<T>(dy + o, g);
+        const IW w = *reinterpret_cast<const IW*>(idx + o);
+#pragma unroll
+        for (int e = 0; e < VN; ++e)
+          if (idx_byte<VN>(w, e) == want) acc[e] += g[e];
+      }
+    }
+    if (RED) {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        acc[e] = fmaf(yv[e], sc[e], sh[e]) > 0.f ? acc[e] : 0.f;
+        const float gr = to_f<T>(from_f<T>(acc[e]));  // statistics of the stored gradient
+        s1[e] += gr;
+        s2[e] = fmaf(gr, yv[e] - mu[e], s2[e]);
+      }
+    }
+    store16<T>(dx + v * VN, acc);
+  }
+  if (RED) {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      red[0][threadIdx.x][e] = s1[e];
+      red[1][threadIdx.x][e] = s2[e];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * C; i += 256) {
+      const int which = i >= C, c = i - which * C;
+      const int ch = c / VN, e = c - ch * VN;
+      float a = 0.f;
+      for (int k = ch; k < 256; k += cpr) a += red[which][k][e];
+      if (which) a *= invstd[c];
+      part[(long long)blockIdx.x * 2 * C + i] = a;
     }
   }
-  store16<T>(dx + v * VN, acc);
 }
 
 // ------------------------------------------------------------------ TSM gradient combine
@@ -616,17 +679,48 @@ VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* id
 VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C,
                             hipStream_t s) {
   const int VN = dtype == VCG_BF16 ? 8 : 4;
-  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && C / VN <= 256, "C must be a power of two multiple of the vector width");
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
   const int lcpr = ilog2i(C / VN);
   const long long TV = (long long)N * H * W * (C / VN);
   VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
+  const unsigned g = stream_grid(TV);
   if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const bf16_t*)dy, idx,
-                       (bf16_t*)dx, H, W, C, OH, OW, lcpr, TV);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16_t, false>), dim3(g), dim3(256), 0, s, (const bf16_t*)dy, idx,
+                       (bf16_t*)dx, H, W, C, OH, OW, lcpr, TV, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const float*)dy, idx,
-                       (float*)dx, H, W, C, OH, OW, lcpr, TV);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<float, false>), dim3(g), dim3(256), 0, s, (const float*)dy, idx,
+                       (float*)dx, H, W, C, OH, OW, lcpr, TV, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API long long vcg_maxpool_bwd_bn_ws_bytes(int C) { return GRID_MAX * 2 * C * 4 + 64; }
+
+// max-pool backward fused with the stem BatchNorm-backward reduction: g = maxpool_bwd(dy) masked by the
+// forward ReLU (fma(y, mscale, mshift) > 0); sum_g / sum_gx finalized, dgamma / dbeta accumulated.
+VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* idx, void* g, int N, int H, int W,
+                               int C, const void* y, const float* mean, const float* invstd, const float* mscale,
+                               const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx,
+                               float* dgamma, float* dbeta, hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && C / VN <= 256, "C must be a power of two multiple of the vector width");
+  VCG_REQUIRE(y && mean && invstd && mscale && mshift && sum_g && sum_gx, "BN arguments required");
+  VCG_REQUIRE(ws_bytes >= vcg_maxpool_bwd_bn_ws_bytes(C), "workspace too small");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int lcpr = ilog2i(C / VN);
+  const long long TV = (long long)N * H * W * (C / VN);
+  VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
+  const unsigned nb = stream_grid(TV);
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16_t, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dy, idx,
+                       (bf16_t*)g, H, W, C, OH, OW, lcpr, TV, (const bf16_t*)y, mean, invstd, mscale, mshift, ws);
+  else
+    hipLaunchKernelGGL((maxpool_bwd_kernel<float, true>), dim3(nb), dim3(256), 0, s, (const float*)dy, idx,
+                       (float*)g, H, W, C, OH, OW, lcpr, TV, (const float*)y, mean, invstd, mscale, mshift, ws);
+  VCG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
+                     sum_g, sum_gx, dgamma, dbeta, 1);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

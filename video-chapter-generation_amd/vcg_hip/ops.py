@@ -255,6 +255,15 @@ def maxpool_bwd(dy, idx, N, H, W, C):
     return dx
 
 
+def maxpool_bwd_bn(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, sums, dgamma=None, dbeta=None):
+    """maxpool backward + the stem BN + ReLU mask + BN-backward sums (sums [2, C] = sum_g, sum_gx)."""
+    g = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    w = ws(_lib.query("vcg_maxpool_bwd_bn_ws_bytes", C), dy.device)
+    _lib.call("vcg_maxpool_bwd_bn", dt_code(dy.dtype), P(dy), P(idx), P(g), N, H, W, C, P(y), P(mean), P(invstd),
+              P(mscale), P(mshift), P(w), w.numel() * 4, P(sums[0]), P(sums[1]), P(dgamma), P(dbeta), stream())
+    return g
+
+
 def avgpool_fwd(x, N, HW, C):
     y = torch.empty((N, C), dtype=torch.float32, device=x.device)
     _lib.call("vcg_avgpool_fwd", dt_code(x.dtype), P(x), P(y), N, HW, C, stream())

@@ -175,8 +175,10 @@ class ResNetTrunk:
                 hooks(list(rec["blk"].parameters()))
             del rec
         xs, y0, a0, idx, b0, N, H, W, cpad, H1, W1 = saved["stem"]
-        da0 = ops.maxpool_bwd(dout, idx, N, H1, W1, 64)
-        dy0 = self._bn_bwd(da0, y0, b0, 64, affine=True)
+        sums0 = torch.empty((2, 64), dtype=torch.float32, device=y0.device)
+        dg0, db0 = self._bn_grads(b0)
+        g0 = ops.maxpool_bwd_bn(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift, sums0, dg0, db0)
+        dy0 = self._bn_apply_bwd(g0, y0, b0, 64, sums0)
         self._wgrad(self.net.conv1, xs, dy0, N, H, W, cpad)
         if hooks is not None:
             hooks(list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
