@@ -119,7 +119,9 @@ def test_conv_fwd_and_stats(K, dtype, case):
 
 
 @pytest.mark.parametrize("case", [(16, 56, 56, 64, 256, 1, 1, 0, 0, 2.0), (8, 28, 28, 128, 128, 3, 1, 1, 0, 0.0),
-                                  (8, 29, 27, 64, 64, 3, 1, 1, 4, 3.0)])
+                                  (8, 29, 27, 64, 64, 3, 1, 1, 4, 3.0),
+                                  # >= 64 Ki rows (the 256-row kernel's shapes when VCG_BIG_TILE=1)
+                                  (24, 56, 56, 64, 256, 1, 1, 0, 0, 2.0), (16, 65, 71, 64, 128, 3, 1, 1, 4, 1.0)])
 def test_conv_stats_multitile(K, case):
     """BN statistics when persistent workgroups walk several M-tiles (one stats slot per workgroup
     row, count row), M not a multiple of 128, and outputs with |mean| >> std (shifted sums)."""
@@ -138,6 +140,10 @@ def test_conv_stats_multitile(K, case):
     mean, invstd, scale, shift = (torch.empty_like(z) for _ in range(4))
     K.bn_finalize(stats, K.stats_tiles(M), M, Cout, None, None, mean, invstd, scale, shift, None, None, 0.1, 1e-5)
     torch.cuda.synchronize()
+    if M >= 65536:  # the 256-row kernel's output values too
+        xin = tsm_ref(x, T, fold) if T else x
+        ref = F.conv2d(xin, w.double(), stride=s, padding=p)
+        _close(y.permute(0, 3, 1, 2), ref, dtype, "conv fwd (>= 64 Ki rows)")
     yref = y.double().cpu().reshape(M, Cout)
     mu, var = yref.mean(0), yref.var(0, unbiased=False)
     assert float(stats[Cout, :, 0].sum()) == M                      # slot row counts cover every row
@@ -377,6 +383,8 @@ def test_transpose(K, dtype, shape):
 
 # (N, H, W, C = dgrad output channels, Cout, k, stride, pad, T) of the fused trunk-backward dgrad
 DGRAD_BWD_CASES = [
+    (16, 65, 71, 128, 64, 3, 1, 1, 4),  # >= 64 Ki rows, 128 columns (256-row kernel with VCG_BIG_TILE=1)
+    (16, 64, 70, 256, 64, 1, 1, 0, 8),  # same, dense 1x1
     (8, 9, 9, 64, 64, 3, 1, 1, 4),     # conv2 3x3
     (8, 10, 10, 64, 128, 3, 2, 1, 4),  # conv2 3x3 / 2 (block 0 of a stage)
     (8, 7, 7, 64, 256, 1, 1, 0, 4),    # conv3 / conv1 1x1 (dense)
@@ -534,3 +542,20 @@ def test_attention_softmax_dropout(K):
     dp = kept.double() / (1 - p)
     dot = (dp * Pm.double()).sum(-1, keepdim=True)
     assert (dS.double() - 0.125 * Pm.double() * (dp - dot)).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("case", [(16, 65, 71, 128, 64, 3, 1, 1), (16, 64, 70, 256, 64, 1, 1, 0),
+                                  (8, 130, 66, 128, 64, 3, 2, 1)])
+def test_conv_dgrad_big(K, case):
+    """Input gradients with >= 64 Ki rows (the 256-row kernel's shapes with VCG_BIG_TILE=1) against torch in float64."""
+    dtype = torch.bfloat16
+    N, H, W, Cin, Cout, KH, s, p = case
+    x = torch.zeros((N, Cin, H, W), dtype=torch.float64, requires_grad=True)
+    w = _rand((Cout, Cin, KH, KH), torch.float32, 91, 0.1)
+    y = F.conv2d(x, w.to(dtype).double(), stride=s, padding=p)
+    dy = _rand(y.shape, dtype, 92).double()
+    (ref,) = torch.autograd.grad(y, x, dy)
+    dys = dy.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV)
+    wt = K.weight_prep(w.to(DEV), Cin, dtype, transposed=True)
+    dx = K.conv_dgrad(dys, wt, N, H, W, Cin, Cout, KH, KH, s, p)
+    _close(dx.permute(0, 3, 1, 2), ref, dtype, "conv dgrad (>= 64 Ki rows)")

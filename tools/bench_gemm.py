@@ -84,7 +84,8 @@ def main():
                                          dh, L * H, dh, Bb, nh, transB=True))
     print(f"{'attn PV batched (transB)':32s} {us:8.1f} us  {2.0 * Bb * nh * L * L * dh / us / 1e6:7.1f} TF/s")
     # BERT FFN1 / FFN2 / QKV
-    for M, Nn, K in ((8192, 3072, 768), (8192, 768, 3072), (8192, 2304, 768)):
+    for M, Nn, K in ((8192, 3072, 768), (8192, 768, 3072), (8192, 2304, 768), (8192, 8192, 8192),
+                     (65536, 256, 2304), (65536, 128, 1152)):
         A = torch.randn(M, K, device=dev).to(dt)
         B = torch.randn(Nn, K, device=dev).to(dt)
         C = torch.empty(M, Nn, device=dev, dtype=dt)

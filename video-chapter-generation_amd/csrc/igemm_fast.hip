@@ -26,8 +26,8 @@ __device__ __forceinline__ int fswz(int row, int chunk) { return chunk ^ ((row >
 constexpr int OP_IM2COL_TSM = 5;
 constexpr int OP_IM2COL_SMALLC = 6;
 
-template <int ROWS, int MODE> struct FastLoader {
-  static constexpr int PER_WAVE = ROWS / 32;  // 1-KiB (8-row) slices per wave per tile
+template <int ROWS, int MODE, int NW = 4> struct FastLoader {
+  static constexpr int PER_WAVE = ROWS / (8 * NW);  // 1-KiB (8-row) slices per wave per tile
   static constexpr bool GATHER = MODE != OP_DENSE_K;
   static constexpr bool IM2COL = MODE == OP_IM2COL || MODE == OP_IM2COL_TSM || MODE == OP_IM2COL_SMALLC;
   static constexpr bool TSM = MODE == OP_IM2COL_TSM;
@@ -201,10 +201,12 @@ __device__ __forceinline__ constexpr int waitcnt_vm(int n) {
 }
 
 // ---- output staging through LDS: full-row 16-B stores instead of 8-B row fragments ----------------
-// The finished stage `cur` (A part: BM x 64, B part: BN x 64 bf16) holds the bf16 output tile: BN = 128
-// -> rows 0..63 in the A part and rows 64..127 in the B part ([64][128] each); BN = 64 -> the whole
-// [128][64] tile in the A part. 16-B chunks are XOR-swizzled per row (conflict-free 8-B writes of a
-// 16-row fragment and 16-B reads of a row). LDS accesses are inline asm with explicit lgkmcnt waits.
+// The output tile goes out in rounds of 128 rows (one round at BM = 128, two at BM = 256: the waves of
+// M-rows 2h, 2h+1 put round h). A round lives in the finished stage `cur`: BN = 128 -> rows 0..63 at stA
+// and rows 64..127 at stB ([64][128] each; BM = 256 passes stB = stA + 64 * 128, its A part holds the
+// whole round); BN = 64 -> the whole [128][64] round at stA. 16-B chunks are XOR-swizzled per row
+// (conflict-free 8-B writes of a 16-row fragment and 16-B reads of a row). LDS accesses are inline asm
+// with explicit lgkmcnt waits.
 typedef __attribute__((address_space(3))) char lds_char;
 __device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)(const lds_char*)p; }
 
@@ -217,7 +219,7 @@ template <int BM, int BN>
 __device__ __forceinline__ void stage_put(bf16_t* stA, bf16_t* stB, int wm, int wn, int lane, int i, int j,
                                           const float (&v)[4]) {
   const int g = lane >> 4, ci = lane & 15;
-  const int trow = wm * (BM / 2) + i * 16 + ci;        // row in the tile
+  const int trow = (wm & 1) * 64 + i * 16 + ci;        // row in the 128-row round
   const int tcol = wn * (BN / 2) + j * 16 + 4 * g;     // first of 4 columns
   bf16_t* reg = (BN == 128 && trow >= 64) ? stB : stA;
   const int row = BN == 128 ? (trow & 63) : trow;
@@ -229,16 +231,17 @@ __device__ __forceinline__ void stage_put(bf16_t* stA, bf16_t* stB, int wm, int 
 }
 
 // all waves' stage_put done -> 16-B row chunks to global (rows >= M / cols >= N skipped)
+// (m0: first row of the round)
 template <int BM, int BN>
 __device__ __forceinline__ void stage_flush(const bf16_t* stA, const bf16_t* stB, const GemmParams& p, bf16_t* Cout,
                                             int m0, int n0) {
-  constexpr int CPR = BN / 8, NCH = BM * BN / 8;
+  constexpr int NTH = BM * 2, CPR = BN / 8, NCH = 128 * BN / 8;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  uint4 q[NCH / 256];
+  uint4 q[NCH / NTH];
 #pragma unroll
-  for (int k = 0; k < NCH / 256; ++k) {
-    const int id = threadIdx.x + 256 * k;
+  for (int k = 0; k < NCH / NTH; ++k) {
+    const int id = threadIdx.x + NTH * k;
     const int trow = id / CPR, c = id - trow * CPR;
     const bf16_t* reg = (BN == 128 && trow >= 64) ? stB : stA;
     const int row = BN == 128 ? (trow & 63) : trow;
@@ -248,8 +251,8 @@ __device__ __forceinline__ void stage_flush(const bf16_t* stA, const bf16_t* stB
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int k = 0; k < NCH / 256; ++k) {
-    const int id = threadIdx.x + 256 * k;
+  for (int k = 0; k < NCH / NTH; ++k) {
+    const int id = threadIdx.x + NTH * k;
     const int trow = id / CPR, c = id - trow * CPR;
     const int m = m0 + trow, n = n0 + 8 * c;
     if (m < p.M && n < p.N) *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + n) = q[k];
@@ -259,24 +262,29 @@ __device__ __forceinline__ void stage_flush(const bf16_t* stA, const bf16_t* stB
 
 // EPI_STORE (no residual / aux) through the stage
 template <int BM, int BN>
-__device__ __forceinline__ void epilogue_staged(f32x4 (&acc)[BM / 32][BN / 32], const GemmParams& p,
+__device__ __forceinline__ void epilogue_staged(f32x4 (&acc)[4][BN / 32], const GemmParams& p,
                                                 const float (&bv)[BN / 32][4], bf16_t* Cout, bf16_t* stA,
                                                 bf16_t* stB, int m0, int n0, int wm, int wn, int lane) {
-  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int MT = 4, NT = BN / 32;
 #pragma unroll
-  for (int j = 0; j < NT; ++j)
+  for (int h = 0; h < BM / 128; ++h) {
+    if ((wm >> 1) == h) {
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      float v[4];
+      for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = acc[i][j][r] * p.alpha + bv[j][r];
-        if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) t = apply_act(t, p.act);
-        v[r] = t;
-      }
-      stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
+        for (int i = 0; i < MT; ++i) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t = acc[i][j][r] * p.alpha + bv[j][r];
+            if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) t = apply_act(t, p.act);
+            v[r] = t;
+          }
+          stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
+        }
     }
-  stage_flush<BM, BN>(stA, stB, p, Cout, m0, n0);
+    stage_flush<BM, BN>(stA, stB, p, Cout, m0 + 128 * h, n0);
+  }
 }
 
 // ---- EPI_BWD (igemm.h BwdEpi): conv-dgrad epilogue of the trunk backward ------------------------------
@@ -296,14 +304,14 @@ template <int BM, int BN>
 __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t* stB, const GemmParams& p,
                                                 bf16_t* Cout, int m0, int n0, const float* cpar, float (&s1)[8],
                                                 float (&s2)[8], float (&s3)[8]) {
-  constexpr int CPR = BN / 8, NCH = BM * BN / 8, KC = NCH / 256, KB = KC < 4 ? KC : 4;
+  constexpr int NTH = BM * 2, CPR = BN / 8, NCH = 128 * BN / 8, KC = NCH / NTH, KB = KC < 4 ? KC : (BM == 256 ? 2 : 4);
   const BwdEpi& e = p.bwd;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   uint4 q[KC];
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
-    const int id = threadIdx.x + 256 * k;
+    const int id = threadIdx.x + NTH * k;
     const int trow = id / CPR, c = id - trow * CPR;
     const bf16_t* reg = (BN == 128 && trow >= 64) ? stB : stA;
     const int row = BN == 128 ? (trow & 63) : trow;
@@ -335,7 +343,7 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
     uint32_t bv[KB];
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk) {  // all loads of the batch first
-      const int id = threadIdx.x + 256 * (k0 + kk);
+      const int id = threadIdx.x + NTH * (k0 + kk);
       const int m = m0 + id / CPR;
       ok[kk] = m < p.M && n < p.N;
       src[kk] = true;
@@ -409,27 +417,27 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
 
 // Combine the per-thread column sums of EPI_BWD (threads tid = c (mod BN/8) share columns 8c..8c+7) in a
 // fixed order and write this workgroup's partial slot; scratch = the (idle) stage buffers.
-template <int BN>
+template <int BM, int BN>
 __device__ __forceinline__ void bwd_finish(const GemmParams& p, float* scratch, const float* cpar_invstd,
                                            const float (&s1)[8], const float (&s2)[8], const float (&s3)[8], int n0,
                                            int slot) {
-  constexpr int CPR = BN / 8;
+  constexpr int NTH = BM * 2, CPR = BN / 8;
   const int nred = p.bwd.nred;
   __syncthreads();
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    scratch[(0 * 256 + tid) * 8 + i] = s1[i];
-    scratch[(1 * 256 + tid) * 8 + i] = s2[i];
-    scratch[(2 * 256 + tid) * 8 + i] = s3[i];
+    scratch[(0 * NTH + tid) * 8 + i] = s1[i];
+    scratch[(1 * NTH + tid) * 8 + i] = s2[i];
+    scratch[(2 * NTH + tid) * 8 + i] = s3[i];
   }
   __syncthreads();
   if (tid < BN && n0 + tid < p.N) {
     const int c = tid >> 3, i = tid & 7;
     float a[3] = {0.f, 0.f, 0.f};
-    for (int t = c; t < 256; t += CPR)
+    for (int t = c; t < NTH; t += CPR)
 #pragma unroll
-      for (int r = 0; r < 3; ++r) a[r] += scratch[(r * 256 + t) * 8 + i];
+      for (int r = 0; r < 3; ++r) a[r] += scratch[(r * NTH + t) * 8 + i];
     float* out = p.bwd.part + (long long)slot * nred * p.N + n0 + tid;
     out[0] = a[0];
     out[p.N] = a[1] * cpar_invstd[tid];
@@ -440,15 +448,18 @@ __device__ __forceinline__ void bwd_finish(const GemmParams& p, float* scratch, 
 // EPI_STATS epilogue of the fast kernel: store the tile (bf16) and fold its rounded values into the
 // running shifted sums. No barriers, no LDS: nothing waits on the in-flight prefetch or the stores.
 template <int BM, int BN>
-__device__ __forceinline__ void epilogue_accstats(f32x4 (&acc)[BM / 32][BN / 32], const GemmParams& p,
+__device__ __forceinline__ void epilogue_accstats(f32x4 (&acc)[4][BN / 32], const GemmParams& p,
                                                   const float (&bv)[BN / 32][4], bf16_t* Cout, bf16_t* stA,
                                                   bf16_t* stB, bool staged, int m0, int n0, int wm, int wn, int lane,
                                                   bool first, float (&ks)[BN / 32][4], float (&s1)[BN / 32][4],
                                                   float (&s2)[BN / 32][4], int& nrows) {
-  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int MT = 4, NT = BN / 32;
   const int g = lane >> 4, ci = lane & 15;
-  const int mbase = m0 + wm * (BM / 2) + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
-  nrows += min(BM / 2, max(0, p.M - (m0 + wm * (BM / 2))));
+  const int mbase = m0 + wm * 64 + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
+  nrows += min(64, max(0, p.M - (m0 + wm * 64)));
+#pragma unroll
+  for (int h = 0; h < BM / 128; ++h) {
+  if ((wm >> 1) == h) {
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int n = nbase + j * 16;
@@ -481,13 +492,15 @@ __device__ __forceinline__ void epilogue_accstats(f32x4 (&acc)[BM / 32][BN / 32]
       }
     }
   }
-  if (staged) stage_flush<BM, BN>(stA, stB, p, Cout, m0, n0);
+  }
+  if (staged) stage_flush<BM, BN>(stA, stB, p, Cout, m0 + 128 * h, n0);
+  }
 }
 
-// Reduce the shifted sums across the 16 row-lanes (DPP) and the two row-halves (LDS, Chan), then write
-// (mean, M2) to stats[col][by] and the slot's row count to the count row stats[N][by] (slots by + k*gy,
-// k >= 1, are marked empty).
-template <int BN>
+// Reduce the shifted sums across the 16 row-lanes (DPP) and the WM row-waves (LDS, Chan, in order), then
+// write (mean, M2) to stats[col][by] and the slot's row count to the count row stats[N][by] (slots by + k*gy,
+// k >= 1, are marked empty). red: 2 * WM * BN + WM floats.
+template <int BN, int WM>
 __device__ __forceinline__ void stats_finish(const GemmParams& p, float* red, const float (&ks)[BN / 32][4],
                                              float (&s1)[BN / 32][4], float (&s2)[BN / 32][4], int nrows, int n0,
                                              int by, int bx, int gy, int mtiles, int wm, int wn, int lane) {
@@ -504,14 +517,16 @@ __device__ __forceinline__ void stats_finish(const GemmParams& p, float* red, co
       const float b = row16_sum(s2[j][r]);
       if (ci == 0) {
         const int lc = wn * (BN / 2) + j * 16 + 4 * g + r;
-        red[wm * 2 * BN + lc] = ks[j][r] + a * inv;            // mean of this row-half
-        red[wm * 2 * BN + BN + lc] = fmaxf(b - a * a * inv, 0.f);  // M2 of this row-half
+        red[wm * 2 * BN + lc] = ks[j][r] + a * inv;            // mean of this row-wave
+        red[wm * 2 * BN + BN + lc] = fmaxf(b - a * a * inv, 0.f);  // M2 of this row-wave
       }
     }
-  if (lane == 0 && wn == 0) red[4 * BN + wm] = n;
+  if (lane == 0 && wn == 0) red[2 * WM * BN + wm] = n;
   __syncthreads();
+  float ntot = 0.f;
+#pragma unroll
+  for (int w = 0; w < WM; ++w) ntot += red[2 * WM * BN + w];
   if (wm == 0 && ci == 0) {
-    const float n1 = red[4 * BN], n2 = red[4 * BN + 1], nt = n1 + n2;
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -519,42 +534,56 @@ __device__ __forceinline__ void stats_finish(const GemmParams& p, float* red, co
         const int lc = wn * (BN / 2) + j * 16 + 4 * g + r;
         const int col = n0 + lc;
         if (col >= p.N) continue;
-        float mean = red[lc], m2 = red[BN + lc];
-        if (n2 > 0.f) {
-          const float d = red[2 * BN + lc] - mean;
-          mean += d * (n2 / nt);
-          m2 += red[3 * BN + lc] + d * d * (n1 * n2 / nt);
+        float n1 = red[2 * WM * BN], mean = red[lc], m2 = red[BN + lc];
+#pragma unroll
+        for (int w = 1; w < WM; ++w) {
+          const float n2 = red[2 * WM * BN + w];
+          if (n2 > 0.f) {
+            const float nt = n1 + n2;
+            const float d = red[w * 2 * BN + lc] - mean;
+            mean += d * (n2 / nt);
+            m2 += red[w * 2 * BN + BN + lc] + d * d * (n1 * n2 / nt);
+            n1 = nt;
+          }
         }
         reinterpret_cast<float2*>(p.stats)[(long long)col * mtiles + by] = make_float2(mean, m2);
       }
   }
   if (bx == 0 && threadIdx.x == 0) {
     float2* cnt = reinterpret_cast<float2*>(p.stats) + (long long)p.N * mtiles;
-    cnt[by] = make_float2(red[4 * BN] + red[4 * BN + 1], 0.f);
+    cnt[by] = make_float2(ntot, 0.f);
     for (int t = by + gy; t < mtiles; t += gy) cnt[t] = make_float2(0.f, 0.f);
   }
 }
 
 template <int BM, int BN, int AM, int EPI, bool RES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void igemm_fast_kernel(GemmParams p) {
+__global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) void igemm_fast_kernel(GemmParams p) {
   // Persistent-style grid: workgroup (bx, by) owns N-tile bx and M-tiles by, by + gy, by + 2gy, ...;
-  // the (m-tile, k-tile) steps form one software pipeline, so tile i+1's loads are in flight while
-  // tile i finishes its MFMAs and its epilogue. Workgroups are dealt round-robin to the 8 XCDs by
+  // the (m-tile, k-tile) steps form one software pipeline, so the next tiles' loads are in flight while
+  // a tile finishes its MFMAs and its epilogue. Workgroups are dealt round-robin to the 8 XCDs by
   // linear id, so when gy % 8 == 0 the linear id is decoded such that all N-tiles of an M-tile
   // row run on the same XCD at the same time and the A rows are fetched from HBM once (L2 hits).
   // The bias lives in registers for the whole kernel (loaded before the pipeline starts) and the
   // epilogue (RES = false) loads nothing: a VGPR-destination global load inside the loop, or an LDS
   // object the compiler cannot tell apart from the DMA target, makes hipcc drain the in-flight
   // LDS-DMA prefetch with vmcnt(0) at every tile boundary. Conv (EPI_STATS) GEMMs carry no bias.
-  constexpr int MT = BM / 32, NT = BN / 32;
+  //
+  // Shapes: every wave owns a 64 x BN/2 sub-tile (4 x BN/32 fragments of 16x16); WM = BM / 64 waves
+  // along M, 2 along N. BM = 128: 4 waves, 2 LDS stages (1 step in flight), 2 workgroups per CU.
+  // BM = 256: 8 waves, 3 LDS stages (2 steps in flight across each barrier, counted vmcnt), 1 workgroup
+  // per CU (the big conv GEMMs).
+  constexpr int WM = BM / 64, NW = 2 * WM;
+  constexpr int MT = 4, NT = BN / 32;
+  constexpr int STAGES = BM == 256 ? 3 : 2;
   constexpr int AE = BM * FBK, BE = BN * FBK;  // elements per stage
-  constexpr int NLD = BM / 32 + BN / 32;       // LDS-DMA instructions per thread per step
+  constexpr int NLD = BM / (8 * NW) + BN / (8 * NW);  // LDS-DMA instructions per thread per step
   constexpr int CPAR = EPI == EPI_BWD ? 6 * BN : 0;  // EPI_BWD per-column parameters
-  __shared__ __attribute__((aligned(1024))) char smem[2 * (AE + BE) * 2 + (4 * BN + 4 + CPAR) * 4];
+  constexpr int RED = 2 * WM * BN + WM + 4;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * (AE + BE) * 2 + (RED + CPAR) * 4];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* Bs = As + 2 * AE;
-  float* red = reinterpret_cast<float*>(smem + 2 * (AE + BE) * 2);
-  float* cpar = red + 4 * BN + 4;  // [mean, msc, msh, mean2, invstd, invstd2][BN]
+  bf16_t* Bs = As + STAGES * AE;
+  float* red = reinterpret_cast<float*>(smem + STAGES * (AE + BE) * 2);
+  float* cpar = red + RED;  // [mean, msc, msh, mean2, invstd, invstd2][BN]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -612,8 +641,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
     for (int j = 0; j < NT; ++j) asm volatile("" ::"v"(bv[j][0]), "v"(bv[j][1]), "v"(bv[j][2]), "v"(bv[j][3]));
   }
 
-  FastLoader<BM, AM> la;
-  FastLoader<BN, OP_DENSE_K> lb;
+  FastLoader<BM, AM, NW> la;
+  FastLoader<BN, OP_DENSE_K, NW> lb;
   la.init(p.a, aoff, by * BM, wave, lane);
   lb.init(p.b, boff, n0, wave, lane);
 
@@ -638,23 +667,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
       for (int r = 0; r < 4; ++r) ks[j][r] = s1[j][r] = s2[j][r] = 0.f;
   }
 
-  la.issue(p.a, 0, p.K, As, wave);
-  lb.issue(p.b, 0, p.K, Bs, wave);
-  int kt = 0, tile = 0;
-  for (int s = 0; s < steps; ++s) {
-    const int cur = s & 1;
-    if (s + 1 < steps) {
-      int nkt = kt + 1;
-      if (nkt == ntiles) {  // next step starts the next M-tile of this workgroup
-        nkt = 0;
-        la.init(p.a, aoff, (by + (tile + 1) * gy) * BM, wave, lane);
-      }
-      la.issue(p.a, nkt * FBK, p.K, As + (cur ^ 1) * AE, wave);
-      lb.issue(p.b, nkt * FBK, p.K, Bs + (cur ^ 1) * BE, wave);
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(NLD));  // step s landed (step s+1 may stay in flight)
-    } else {
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  // issue side of the pipeline: the next step to load is k-tile ikt of the workgroup's local tile itile
+  int ikt = 0, itile = 0;
+  auto issue_next = [&](int stage) {
+    if (ikt == 0 && itile > 0) la.init(p.a, aoff, (by + itile * gy) * BM, wave, lane);
+    la.issue(p.a, ikt * FBK, p.K, As + stage * AE, wave);
+    lb.issue(p.b, ikt * FBK, p.K, Bs + stage * BE, wave);
+    if (++ikt == ntiles) {
+      ikt = 0;
+      ++itile;
     }
+  };
+#pragma unroll
+  for (int i = 0; i < STAGES - 1; ++i)
+    if (i < steps) issue_next(i);
+  int kt = 0, tile = 0, cur = 0;
+  for (int s = 0; s < steps; ++s) {
+    // steps issued beyond s once this step's prefetch is out; step s has landed when at most that many
+    // steps' loads are still outstanding
+    const int ahead = min(STAGES - 1, steps - 1 - s);
+    if (s + STAGES - 1 < steps) issue_next(cur == 0 ? STAGES - 1 : cur - 1);  // stage (s + STAGES - 1) % STAGES
+    if (STAGES == 3 && ahead >= 2) __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * NLD));
+    else if (ahead >= 1) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NLD));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
     __builtin_amdgcn_s_barrier();
     const bf16_t* Ac = As + cur * AE;
     const bf16_t* Bc = Bs + cur * BE;
@@ -662,7 +697,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
     for (int s2 = 0; s2 < 2; ++s2) {
       s16x8 af[MT], bfr[NT];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) af[i] = fast_frag(Ac, wm * (BM / 2) + i * 16, lane, s2);
+      for (int i = 0; i < MT; ++i) af[i] = fast_frag(Ac, wm * 64 + i * 16, lane, s2);
 #pragma unroll
       for (int j = 0; j < NT; ++j) bfr[j] = fast_frag(Bc, wn * (BN / 2) + j * 16, lane, s2);
 #pragma unroll
@@ -676,25 +711,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
     __builtin_amdgcn_s_barrier();
     if (++kt == ntiles) {
       const int mt = by + tile * gy;
+      bf16_t* stA = As + cur * AE;  // the finished stage holds the output rounds (see stage_put)
+      bf16_t* stB = BM == 256 ? stA + 64 * BN : Bs + cur * BE;
       // output tiles go through the LDS stage for full-row 16-B stores (VCG_STAGE_KT can limit it)
       const bool staged = ntiles <= p.stage_kt;
       if constexpr (EPI == EPI_BWD) {
-        constexpr int MT_ = BM / 32, NT_ = BN / 32;
 #pragma unroll
-        for (int j = 0; j < NT_; ++j)
+        for (int h = 0; h < BM / 128; ++h) {
+          if ((wm >> 1) == h) {
 #pragma unroll
-          for (int i = 0; i < MT_; ++i) {
-            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            stage_put<BM, BN>(As + cur * AE, Bs + cur * BE, wm, wn, lane, i, j, v);
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+              for (int i = 0; i < MT; ++i) {
+                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
+              }
           }
-        stage_flush_bwd<BM, BN>(As + cur * AE, Bs + cur * BE, p, Cout, mt * BM, n0, cpar, b1, b2, b3);
+          stage_flush_bwd<BM, BN>(stA, stB, p, Cout, mt * BM + 128 * h, n0, cpar, b1, b2, b3);
+        }
       } else if constexpr (EPI == EPI_STATS) {
-        epilogue_accstats<BM, BN>(acc, p, bv, Cout, As + cur * AE, Bs + cur * BE, staged, mt * BM, n0, wm, wn,
-                                  lane, tile == 0, ks, s1, s2, nrows);
-      } else if (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0) {
-        epilogue_staged<BM, BN>(acc, p, bv, Cout, As + cur * AE, Bs + cur * BE, mt * BM, n0, wm, wn, lane);
+        epilogue_accstats<BM, BN>(acc, p, bv, Cout, stA, stB, staged || BM == 256, mt * BM, n0, wm, wn, lane,
+                                  tile == 0, ks, s1, s2, nrows);
+      } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0)) {
+        epilogue_staged<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane);
       } else {
-        gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);
+        if constexpr (BM == 128)
+          gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);
       }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
@@ -703,19 +745,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void i
       kt = 0;
       ++tile;
     }
+    cur = cur == STAGES - 1 ? 0 : cur + 1;
   }
-  if constexpr (EPI == EPI_STATS) stats_finish<BN>(p, red, ks, s1, s2, nrows, n0, by, bx, gy, mtiles, wm, wn, lane);
+  if constexpr (EPI == EPI_STATS)  // the stats buffer is laid out for 128-row tiles (vcg_conv_stats_tiles)
+    stats_finish<BN, WM>(p, red, ks, s1, s2, nrows, n0, by, bx, gy, (p.M + 127) / 128, wm, wn, lane);
   if constexpr (EPI == EPI_BWD) {
-    if (p.bwd.nred > 0) bwd_finish<BN>(p, reinterpret_cast<float*>(smem), cpar + 4 * BN, b1, b2, b3, n0, by);
+    if (p.bwd.nred > 0) bwd_finish<BM, BN>(p, reinterpret_cast<float*>(smem), cpar + 4 * BN, b1, b2, b3, n0, by);
   }
 }
 
-// One resident round of workgroups (LDS allows 2 per CU at BN = 128, 3 at BN = 64); each walks
-// ceil(mtiles / gy) M-tiles. gy is a multiple of 8 whenever possible (XCD-aware decode).
+// One resident round of workgroups (LDS allows 2 per CU at BM = 128 / BN = 128, 3 at BN = 64, 1 at BM = 256);
+// each walks ceil(mtiles / gy) M-tiles. gy is a multiple of 8 whenever possible (XCD-aware decode).
 // (EPI_BWD's BN = 64 kernel needs > 170 VGPRs: 2 workgroups per CU there too)
 static int grid_rows(int M, int N, int z, int BM, int BN, int epi) {
   const int nx = (N + BN - 1) / BN, mtiles = (M + BM - 1) / BM;
-  const int resident = (BN == 128 || epi == EPI_BWD ? 2 : 3) * 256;
+  const int resident = (BM == 256 ? 1 : (BN == 128 || epi == EPI_BWD ? 2 : 3)) * 256;
   int gy = resident / (nx * z);
   if (gy >= 8) gy &= ~7;
   if (gy > mtiles) gy = mtiles >= 8 ? (mtiles & ~7) : mtiles;
@@ -725,7 +769,26 @@ static int grid_rows(int M, int N, int z, int BM, int BN, int epi) {
 
 static int fast_bn_cols(int N) { return (N % 128 == 0 || N > 64 * 3) ? 128 : 64; }
 
-int fast_grid_rows(int M, int N, int z, int epi) { return grid_rows(M, N, z, 128, fast_bn_cols(N), epi); }
+// 256-row tiles (8 waves, 3-stage ring, 1 workgroup per CU) for the big conv GEMMs (>= 64 Ki rows,
+// 128-column tiles, no residual / aux epilogue, not batched): opt-in with VCG_BIG_TILE=1. Measured
+// slower than two 4-wave 128-row workgroups per CU on every conv shape (l3 conv2 3x3: 367 vs 295 us;
+// train step 565 vs 620 windows/s): with one barrier-synchronised workgroup per CU nothing overlaps
+// the barrier stalls. Kept as the base of an 8-phase schedule.
+static bool big_tile_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VCG_BIG_TILE");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+static int fast_bm(int M, int N, int z, bool res_or_aux) {
+  return (big_tile_enabled() && M >= 65536 && fast_bn_cols(N) == 128 && z == 1 && !res_or_aux) ? 256 : 128;
+}
+
+int fast_grid_rows(int M, int N, int z, int epi) {
+  return grid_rows(M, N, z, fast_bm(M, N, z, false), fast_bn_cols(N), epi);
+}
 
 template <int BM, int BN, int AM, int EPI, bool RES>
 static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
@@ -733,7 +796,7 @@ static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   const int gy = grid_rows(p.M, p.N, z, BM, BN, EPI);
   dim3 grid(nx * gy, 1, z);
   const int tk = timing_begin(s);
-  hipLaunchKernelGGL((igemm_fast_kernel<BM, BN, AM, EPI, RES>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((igemm_fast_kernel<BM, BN, AM, EPI, RES>), grid, dim3(BM * 2), 0, s, p);
   timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K * z);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -741,6 +804,9 @@ static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
 
 template <int AM, int EPI, bool RES = false>
 static int fast_bn(const GemmParams& p, int z, hipStream_t s) {
+  if constexpr (!RES) {
+    if (fast_bm(p.M, p.N, z, p.aux != nullptr) == 256) return launch_fast<256, 128, AM, EPI, false>(p, z, s);
+  }
   if (fast_bn_cols(p.N) == 128) return launch_fast<128, 128, AM, EPI, RES>(p, z, s);
   return launch_fast<128, 64, AM, EPI, RES>(p, z, s);
 }
