@@ -445,114 +445,94 @@ __device__ __forceinline__ void bwd_finish(const GemmParams& p, float* scratch, 
   }
 }
 
-// EPI_STATS epilogue of the fast kernel: store the tile (bf16) and fold its rounded values into the
-// running shifted sums. No barriers, no LDS: nothing waits on the in-flight prefetch or the stores.
+// ---- EPI_STATS: the BatchNorm statistics of the stored (bf16) conv output, from the staged rounds ---------
+// A flush thread always owns the same 8-column chunk c = tid % (BN / 8); it keeps shifted sums of the
+// values it stores (shift = its first value per column: no cancellation when |mean| >> std) for the whole
+// kernel: count, sh[8], s1[8] = sum (v - sh), s2[8] = sum (v - sh)^2.
 template <int BM, int BN>
-__device__ __forceinline__ void epilogue_accstats(f32x4 (&acc)[4][BN / 32], const GemmParams& p,
-                                                  const float (&bv)[BN / 32][4], bf16_t* Cout, bf16_t* stA,
-                                                  bf16_t* stB, bool staged, int m0, int n0, int wm, int wn, int lane,
-                                                  bool first, float (&ks)[BN / 32][4], float (&s1)[BN / 32][4],
-                                                  float (&s2)[BN / 32][4], int& nrows) {
-  constexpr int MT = 4, NT = BN / 32;
-  const int g = lane >> 4, ci = lane & 15;
-  const int mbase = m0 + wm * 64 + ci, nbase = n0 + wn * (BN / 2) + 4 * g;
-  nrows += min(64, max(0, p.M - (m0 + wm * 64)));
+__device__ __forceinline__ void stage_flush_stats(const bf16_t* stA, const bf16_t* stB, const GemmParams& p,
+                                                  bf16_t* Cout, int m0, int n0, int& cnt, float (&sh)[8],
+                                                  float (&s1)[8], float (&s2)[8]) {
+  constexpr int NTH = BM * 2, CPR = BN / 8, NCH = 128 * BN / 8, KC = NCH / NTH;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  uint4 q[KC];
 #pragma unroll
-  for (int h = 0; h < BM / 128; ++h) {
-  if ((wm >> 1) == h) {
+  for (int k = 0; k < KC; ++k) {
+    const int id = threadIdx.x + NTH * k;
+    const int trow = id / CPR, c = id - trow * CPR;
+    const bf16_t* reg = (BN == 128 && trow >= 64) ? stB : stA;
+    const int row = BN == 128 ? (trow & 63) : trow;
+    const uint32_t addr = lds_u32(reg + row * BN + 8 * st_slot<BN>(row, c));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(q[k]) : "v"(addr) : "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  const int c = threadIdx.x % CPR;
+  const int n = n0 + 8 * c;
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int n = nbase + j * 16;
+  for (int k = 0; k < KC; ++k) {
+    const int id = threadIdx.x + NTH * k;
+    const int m = m0 + id / CPR;
+    if (m < p.M && n < p.N) {
+      *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + n) = q[k];
+      float v[8];
+      unpack8(q[k], v);
+      if (cnt == 0) {
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int m = mbase + i * 16;
-      const bool ok = m < p.M && n < p.N;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = acc[i][j][r] * p.alpha + bv[j][r];
-        if (p.act != ACT_NONE) t = apply_act(t, p.act);
-        v[r] = bf2f(f2bf(t));  // statistics of the stored (rounded) values
+        for (int i = 0; i < 8; ++i) sh[i] = v[i];
       }
-      if (first && i == 0) {
+      ++cnt;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ks[j][r] = __shfl(v[r], lane & 48, 64);  // row mbase - ci of column
-      }
-      if (staged)
-        stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
-      else if (ok)
-        store4<bf16_t>(Cout + (long long)m * p.ldc + n, v);
-      if (ok) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = v[r] - ks[j][r];
-          s1[j][r] += d;
-          s2[j][r] = fmaf(d, d, s2[j][r]);
-        }
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[i] - sh[i];
+        s1[i] += d;
+        s2[i] = fmaf(d, d, s2[i]);
       }
     }
   }
-  }
-  if (staged) stage_flush<BM, BN>(stA, stB, p, Cout, m0 + 128 * h, n0);
-  }
+  __builtin_amdgcn_s_barrier();  // every wave has read the stage before the next step's DMA refills it
 }
 
-// Reduce the shifted sums across the 16 row-lanes (DPP) and the WM row-waves (LDS, Chan, in order), then
-// write (mean, M2) to stats[col][by] and the slot's row count to the count row stats[N][by] (slots by + k*gy,
-// k >= 1, are marked empty). red: 2 * WM * BN + WM floats.
-template <int BN, int WM>
-__device__ __forceinline__ void stats_finish(const GemmParams& p, float* red, const float (&ks)[BN / 32][4],
-                                             float (&s1)[BN / 32][4], float (&s2)[BN / 32][4], int nrows, int n0,
-                                             int by, int bx, int gy, int mtiles, int wm, int wn, int lane) {
-  constexpr int NT = BN / 32;
-  const int g = lane >> 4, ci = lane & 15;
-  const float n = (float)nrows;
-  const float inv = nrows > 0 ? 1.f / n : 0.f;
-  __syncthreads();  // all LDS-DMA retired (last step waited vmcnt(0)); stage buffers and `red` are free
+// Per-thread (count, mean, M2) of every column chunk, merged across the threads that share the chunk with
+// Chan's formula in thread order (deterministic) -> stats[col][by] = (mean, M2) and the count row
+// stats[N][by]; slots by + k*gy (k >= 1) are marked empty. scratch = the idle stage buffers.
+template <int BM, int BN>
+__device__ __forceinline__ void stats_finish(const GemmParams& p, float* scratch, int cnt, const float (&sh)[8],
+                                             const float (&s1)[8], const float (&s2)[8], int n0, int by, int bx,
+                                             int gy, int mslots) {
+  constexpr int NTH = BM * 2, CPR = BN / 8;
+  __syncthreads();  // all LDS-DMA retired (the last step waited vmcnt(0)); the stage buffers are free
+  const int tid = threadIdx.x;
+  const float nf = (float)cnt, inv = cnt > 0 ? 1.f / nf : 0.f;
 #pragma unroll
-  for (int j = 0; j < NT; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float a = row16_sum(s1[j][r]);
-      const float b = row16_sum(s2[j][r]);
-      if (ci == 0) {
-        const int lc = wn * (BN / 2) + j * 16 + 4 * g + r;
-        red[wm * 2 * BN + lc] = ks[j][r] + a * inv;            // mean of this row-wave
-        red[wm * 2 * BN + BN + lc] = fmaxf(b - a * a * inv, 0.f);  // M2 of this row-wave
+  for (int i = 0; i < 8; ++i) {
+    scratch[(0 * NTH + tid) * 8 + i] = sh[i] + s1[i] * inv;                 // mean
+    scratch[(1 * NTH + tid) * 8 + i] = fmaxf(s2[i] - s1[i] * s1[i] * inv, 0.f);  // M2
+  }
+  scratch[2 * NTH * 8 + tid] = nf;
+  __syncthreads();
+  if (tid < BN && n0 + tid < p.N) {
+    const int c = tid >> 3, i = tid & 7;
+    float na = 0.f, mean = 0.f, m2 = 0.f;
+    for (int t = c; t < NTH; t += CPR) {
+      const float nb = scratch[2 * NTH * 8 + t];
+      if (nb > 0.f) {
+        const float mb = scratch[t * 8 + i], m2b = scratch[(NTH + t) * 8 + i];
+        const float nt = na + nb, d = mb - mean;
+        mean += d * (nb / nt);
+        m2 += m2b + d * d * (na * nb / nt);
+        na = nt;
       }
     }
-  if (lane == 0 && wn == 0) red[2 * WM * BN + wm] = n;
-  __syncthreads();
-  float ntot = 0.f;
-#pragma unroll
-  for (int w = 0; w < WM; ++w) ntot += red[2 * WM * BN + w];
-  if (wm == 0 && ci == 0) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int lc = wn * (BN / 2) + j * 16 + 4 * g + r;
-        const int col = n0 + lc;
-        if (col >= p.N) continue;
-        float n1 = red[2 * WM * BN], mean = red[lc], m2 = red[BN + lc];
-#pragma unroll
-        for (int w = 1; w < WM; ++w) {
-          const float n2 = red[2 * WM * BN + w];
-          if (n2 > 0.f) {
-            const float nt = n1 + n2;
-            const float d = red[w * 2 * BN + lc] - mean;
-            mean += d * (n2 / nt);
-            m2 += red[w * 2 * BN + BN + lc] + d * d * (n1 * n2 / nt);
-            n1 = nt;
-          }
-        }
-        reinterpret_cast<float2*>(p.stats)[(long long)col * mtiles + by] = make_float2(mean, m2);
-      }
+    reinterpret_cast<float2*>(p.stats)[(long long)(n0 + tid) * mslots + by] = make_float2(mean, m2);
   }
-  if (bx == 0 && threadIdx.x == 0) {
-    float2* cnt = reinterpret_cast<float2*>(p.stats) + (long long)p.N * mtiles;
-    cnt[by] = make_float2(ntot, 0.f);
-    for (int t = by + gy; t < mtiles; t += gy) cnt[t] = make_float2(0.f, 0.f);
+  if (bx == 0 && tid == 0) {
+    float rows = 0.f;  // threads 0..CPR-1 cover every row of the workgroup once (one chunk column each)
+    for (int t = 0; t < NTH; t += CPR) rows += scratch[2 * NTH * 8 + t];
+    float2* cntrow = reinterpret_cast<float2*>(p.stats) + (long long)p.N * mslots;
+    cntrow[by] = make_float2(rows, 0.f);
+    for (int t = by + gy; t < mslots; t += gy) cntrow[t] = make_float2(0.f, 0.f);
   }
 }
 
@@ -652,20 +632,12 @@ __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) voi
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // EPI_STATS: per-column sums of (v - shift) and (v - shift)^2 over every row this wave stores, across
-  // all of the workgroup's M-tiles (shift = the column's first value: no cancellation); reduced across
-  // lanes and waves once at the end -> one (mean, M2) slot per workgroup row `by`.
-  float ks[NT][4], s1[NT][4], s2[NT][4];
-  int nrows = 0;
-  float b1[8], b2[8], b3[8];  // EPI_BWD column sums of this thread's chunk
+  // EPI_STATS: shifted per-column sums over every row this workgroup stores, across all of its M-tiles,
+  // merged once at the end -> one (mean, M2) slot per workgroup row `by` (stage_flush_stats, stats_finish).
+  float b1[8], b2[8], b3[8];  // EPI_BWD column sums / EPI_STATS shift, s1, s2 of this thread's chunk
+  int scnt = 0;               // EPI_STATS rows seen by this thread
 #pragma unroll
   for (int i = 0; i < 8; ++i) b1[i] = b2[i] = b3[i] = 0.f;
-  if constexpr (EPI == EPI_STATS) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ks[j][r] = s1[j][r] = s2[j][r] = 0.f;
-  }
 
   // issue side of the pipeline: the next step to load is k-tile ikt of the workgroup's local tile itile
   int ikt = 0, itile = 0;
@@ -729,9 +701,20 @@ __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) voi
           }
           stage_flush_bwd<BM, BN>(stA, stB, p, Cout, mt * BM + 128 * h, n0, cpar, b1, b2, b3);
         }
-      } else if constexpr (EPI == EPI_STATS) {
-        epilogue_accstats<BM, BN>(acc, p, bv, Cout, stA, stB, staged || BM == 256, mt * BM, n0, wm, wn, lane,
-                                  tile == 0, ks, s1, s2, nrows);
+      } else if constexpr (EPI == EPI_STATS) {  // conv outputs: no bias / activation, alpha = 1
+#pragma unroll
+        for (int h = 0; h < BM / 128; ++h) {
+          if ((wm >> 1) == h) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+              for (int i = 0; i < MT; ++i) {
+                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
+              }
+          }
+          stage_flush_stats<BM, BN>(stA, stB, p, Cout, mt * BM + 128 * h, n0, scnt, b1, b2, b3);
+        }
       } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0)) {
         epilogue_staged<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane);
       } else {
@@ -748,7 +731,7 @@ __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) voi
     cur = cur == STAGES - 1 ? 0 : cur + 1;
   }
   if constexpr (EPI == EPI_STATS)  // the stats buffer is laid out for 128-row tiles (vcg_conv_stats_tiles)
-    stats_finish<BN, WM>(p, red, ks, s1, s2, nrows, n0, by, bx, gy, (p.M + 127) / 128, wm, wn, lane);
+    stats_finish<BM, BN>(p, reinterpret_cast<float*>(smem), scnt, b1, b2, b3, n0, by, bx, gy, (p.M + 127) / 128);
   if constexpr (EPI == EPI_BWD) {
     if (p.bwd.nred > 0) bwd_finish<BM, BN>(p, reinterpret_cast<float*>(smem), cpar + 4 * BN, b1, b2, b3, n0, by);
   }
