@@ -118,6 +118,16 @@ VCG_API int vcg_tanh_bwd(int dtype, const void* dy, const void* t, void* dx, lon
  *      F.cross_entropy (train_video_segment_point.py:165) ----------------------------------- */
 VCG_API int vcg_head_mlp_fwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* bias, float* logits, float* prob, int B, int T, int hid, int O, hipStream_t s);
 VCG_API int vcg_head_mlp_bwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* dlogits, void* dV, void* dL, float* dW, float* dbias, int B, int T, int hid, int O, int relu_mask, hipStream_t s);
+/* ChapterHead head_type "attn" (head_attn.hip): SelfAttention(hid, n_head, O) (two_stream.py:8-48) over the T+1
+ * fused tokens cat([Vout [B*T][hid], Lout [B][hid]]) of each window, output proj of token 0, softmax. Weights are
+ * the fp32 nn.Linear parameters ([out][in]). `saved` (f32, vcg_head_attn_saved_floats) keeps the state of the
+ * backward; dropout_p = attn_drop.p in training (counter-hash mask, regenerated by the backward with `seed`). */
+VCG_API long long vcg_head_attn_saved_floats(int B, int T, int hid, int nh);
+VCG_API int vcg_head_attn_fwd(int dtype, const void* Vout, const void* Lout, const float* Wq, const float* bq, const float* Wk, const float* bk, const float* Wv, const float* bv, const float* Wp, const float* bp, float* saved, long long saved_floats, float* logits, float* prob, int B, int T, int hid, int nh, int O, float dropout_p, unsigned long long seed, hipStream_t s);
+/* dVout / dLout = ReLU-masked input gradients (relu_mask: the projections' ReLU); parameter grads (nullable)
+   are accumulated (+=). ws: f32 workspace of vcg_head_attn_bwd_ws_floats. */
+VCG_API long long vcg_head_attn_bwd_ws_floats(int B, int T, int hid);
+VCG_API int vcg_head_attn_bwd(int dtype, const float* saved, const float* Wq, const float* Wk, const float* Wv, const float* Wp, const float* dlogits, void* dVout, void* dLout, float* dWq, float* dbq, float* dWk, float* dbk, float* dWv, float* dbv, float* dWp, float* dbp, float* ws, long long ws_floats, int B, int T, int hid, int nh, int O, float dropout_p, unsigned long long seed, int relu_mask, hipStream_t s);
 VCG_API int vcg_cross_entropy_fwd(const float* logits, const long long* labels, float* loss, int B, int C, hipStream_t s);
 VCG_API int vcg_cross_entropy_bwd(const float* logits, const long long* labels, const float* dloss, float* dlogits, int B, int C, hipStream_t s);
 

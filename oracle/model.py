@@ -100,13 +100,32 @@ def chapter_head_mlp(p, lang_emb, vision_emb, prefix="fusion_head."):
     return F.linear(fusion, p[prefix + "head.weight"], p[prefix + "head.bias"])
 
 
-def two_stream(p, img_clip, ids, mask, bn_mode="running", p_drop=0.0, training=False):
+def chapter_head_attn(p, lang_emb, vision_emb, n_head=4, prefix="fusion_head."):
+    """ChapterHead.forward (two_stream.py:71-95), head_type attn: SelfAttention.forward (two_stream.py:31-48)
+    over cat([vision_out, lang_out], 1) without dropout; output = proj of token 0."""
+    B, T = vision_emb.shape[:2]
+    lang_out = F.relu(F.linear(lang_emb, p[prefix + "lang_proj_head.weight"])).unsqueeze(1)
+    vision_out = F.relu(F.linear(vision_emb.reshape(B * T, -1), p[prefix + "vision_proj_head.weight"])).view(B, T, -1)
+    x = torch.cat([vision_out, lang_out], dim=1)
+    C = x.shape[-1]
+    hs = C // n_head
+
+    def heads(name):
+        y = F.linear(x, p[prefix + f"head.{name}.weight"], p[prefix + f"head.{name}.bias"])
+        return y.view(B, T + 1, n_head, hs).transpose(1, 2)
+    k, q, v = heads("key"), heads("query"), heads("value")
+    att = torch.softmax((q @ k.transpose(-2, -1)) * (1.0 / math.sqrt(hs)), dim=-1)
+    y = (att @ v).transpose(1, 2).contiguous().view(B, T + 1, C)
+    return F.linear(y[:, 0, :], p[prefix + "head.proj.weight"], p[prefix + "head.proj.bias"])
+
+
+def two_stream(p, img_clip, ids, mask, bn_mode="running", p_drop=0.0, training=False, head_type="mlp"):
     """TwoStream.forward (two_stream.py:172-194) -> logits, prob, vision_emb [B,T,2048], lang_emb."""
     B, T = img_clip.shape[:2]
     lang_emb, _ = bert(p, ids, mask, p_drop=p_drop, training=training)
     x = img_clip.reshape(B * T, *img_clip.shape[2:])
     vis = resnet50_tsm(p, x, T, bn_mode).view(B, T, -1)
-    logits = chapter_head_mlp(p, lang_emb, vis)
+    logits = (chapter_head_attn if head_type == "attn" else chapter_head_mlp)(p, lang_emb, vis)
     return logits, torch.softmax(logits, 1), vis, lang_emb
 
 
@@ -125,13 +144,14 @@ def param_groups(named, weight_decay):
             {"params": [t for _, t in no_decay], "weight_decay": 0.0}]
 
 
-def train_step(params, buffers, img, ids, mask, labels, lr, betas=(0.9, 0.95), weight_decay=0.01, max_norm=1.0):
+def train_step(params, buffers, img, ids, mask, labels, lr, betas=(0.9, 0.95), weight_decay=0.01, max_norm=1.0,
+               head_type="mlp"):
     """One reference train step (train_video_segment_point.py:161-206 with accumulation 1):
     forward (BN train mode, dropout 0) -> CE -> backward -> clip_grad_norm_ -> AdamW.step.
     params: {name: leaf tensor requiring grad}; buffers: {name: running stats} (updated in place)."""
     p = dict(buffers)
     p.update(params)
-    logits, prob, _, _ = two_stream(p, img, ids, mask, bn_mode="train")
+    logits, prob, _, _ = two_stream(p, img, ids, mask, bn_mode="train", head_type=head_type)
     loss = F.cross_entropy(logits, labels)
     loss.backward()
     total_norm = torch.nn.utils.clip_grad_norm_(list(params.values()), max_norm)

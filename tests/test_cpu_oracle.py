@@ -136,3 +136,45 @@ def test_no_cpu_fallback():
     from vcg_hip import ops
     with pytest.raises(RuntimeError):
         ops.tsm_shift(torch.zeros(8, 64, 2, 2), 4, 8)
+
+
+def _head_params(g):
+    """The reference ChapterHead(attn) parameters of head_attn.npz, regenerated by name (vcg_hip/synth.py)."""
+    from model.fusion.two_stream import ChapterHead
+    from vcg_hip import synth
+    h = ChapterHead(96, 160, 4, 128, 2, head_type="attn")
+    synth.init_params(h, 123, prefix="fusion_head.")
+    return {"fusion_head." + n: p.detach().clone().requires_grad_() for n, p in h.named_parameters()}
+
+
+def test_oracle_attn_head_matches_reference():
+    """oracle.chapter_head_attn against the reference SelfAttention head (two_stream.py:8-48): logits and the
+    gradients of sum(logits * R) w.r.t. the inputs and every head parameter."""
+    from oracle import model as om
+    g = _gold("head_attn.npz")
+    p = _head_params(g)
+    lang = torch.from_numpy(g["head_lang"]).requires_grad_()
+    vis = torch.from_numpy(g["head_vis"]).requires_grad_()
+    lg = om.chapter_head_attn(p, lang, vis)
+    assert np.abs(lg.detach().numpy() - g["head_logits"]).max() < 1e-5
+    (lg * torch.from_numpy(g["head_R"])).sum().backward()
+    assert np.abs(lang.grad.numpy() - g["head_dlang"]).max() < 1e-5
+    assert np.abs(vis.grad.numpy() - g["head_dvis"]).max() < 1e-5
+    for k in [k for k in g.files if k.startswith("head_grad::")]:
+        n = "fusion_head." + k.split("::", 1)[1]
+        ref = g[k]
+        assert np.abs(p[n].grad.numpy() - ref).max() <= 1e-5 * (1 + np.abs(ref).max()), n
+
+
+def test_oracle_c1_attn_forward_matches_reference():
+    from oracle import model as om
+    from vcg_hip.build import build_two_stream
+    from vcg_hip import synth
+    g = _gold("head_attn.npz")
+    m = build_two_stream(clip_frame_num=4, seed=123, head_type="attn", bn_stats=dict(_gold("bn_running_stats.npz")),
+                         dropout=0.0)
+    frames, ids, mask, _ = synth.clip_batch(2, 4, 112, 112, 32, seed=123)
+    with torch.no_grad():
+        lg, pr, _, _ = om.two_stream(dict(m.state_dict()), frames, ids, mask, bn_mode="running", head_type="attn")
+    assert np.abs(lg.numpy() - g["c1attn_logits_running"]).max() < 1e-5
+    assert np.abs(pr.numpy() - g["c1attn_prob_running"]).max() < 1e-5

@@ -185,3 +185,130 @@ def test_c2_forward_fp32(stats, mode):
     if mode == "batch":
         _batch_mode(model)
     _check_fwd(model, g, "c2", 64, 16, 224, 128, 1e-3, mode)
+
+
+def _head_module(dev):
+    from model.fusion.two_stream import ChapterHead
+    from vcg_hip import synth
+    h = ChapterHead(96, 160, 4, 128, 2, head_type="attn").to(dev)
+    synth.init_params(h, 123, prefix="fusion_head.")
+    for p in h.parameters():
+        p.grad = torch.zeros_like(p)
+    return h
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_attn_head_kernels_vs_reference(precision):
+    """vcg_head_attn_fwd / _bwd (+ the projection GEMMs as HeadEngine runs them) against the reference
+    ChapterHead(attn) outputs and gradients (tests/golden/head_attn.npz). fp32: 1e-4 relative to each tensor's
+    max; bf16 (activations and projection operands in bf16): 3e-2."""
+    from vcg_hip import ops
+    g = _gold("head_attn.npz")
+    h = _head_module(DEV)
+    dt = ops.torch_dtype(precision)
+    B, T, hid = 3, 4, 128
+    lang = torch.from_numpy(g["head_lang"]).to(DEV)
+    vis = torch.from_numpy(g["head_vis"]).to(DEV).reshape(B * T, -1)
+    lang_t, vis_t = lang.to(dt).contiguous(), vis.to(dt).contiguous()
+    wv = h.vision_proj_head.weight.detach().to(dt).contiguous()
+    wl = h.lang_proj_head.weight.detach().to(dt).contiguous()
+    Vout = ops.gemm(vis_t, wv, B * T, hid, 160, 160, 160, act=ops.ACT_RELU)
+    Lout = ops.gemm(lang_t, wl, B, hid, 96, 96, 96, act=ops.ACT_RELU)
+    at = h.head
+    logits, prob, saved = ops.head_attn_fwd(Vout, Lout, at.query, at.key, at.value, at.proj, B, T, hid, at.n_head)
+    tol = 1e-4 if precision == "fp32" else 3e-2
+    ref = g["head_logits"]
+    assert _maxdiff(logits.cpu(), ref) <= tol * (1 + np.abs(ref).max())
+    assert _maxdiff(prob.cpu(), torch.softmax(torch.from_numpy(ref), 1)) <= tol
+    dlogits = torch.from_numpy(g["head_R"]).to(DEV)
+    dV, dL = ops.head_attn_bwd(saved, at.query, at.key, at.value, at.proj, dlogits, Vout, Lout, B, T, hid, at.n_head)
+    # the projections' gradients through the same GEMMs HeadEngine.backward uses
+    ops.gemm_splitk(dV, vis_t, h.vision_proj_head.weight.grad, hid, 160, B * T, hid, 160, transA=True, transB=True)
+    ops.gemm_splitk(dL, lang_t, h.lang_proj_head.weight.grad, hid, 96, B, hid, 96, transA=True, transB=True)
+    dvis = ops.gemm(dV, wv, B * T, 160, hid, hid, 160, transB=True)
+    dlang = ops.gemm(dL, wl, B, 96, hid, hid, 96, transB=True)
+    torch.cuda.synchronize()
+    for got, key in ((dvis.float().reshape(B, T, -1), "head_dvis"), (dlang.float(), "head_dlang")):
+        r = g[key]
+        assert _maxdiff(got.cpu(), r) <= tol * np.abs(r).max(), key
+    for n, p in h.named_parameters():
+        r = g[f"head_grad::{n}"]
+        if precision == "fp32":
+            d = _maxdiff(p.grad.cpu(), r)
+            # key.bias: analytically zero (softmax is shift-invariant); the reference holds ~1e-9 rounding noise
+            assert d <= tol * max(np.abs(r).max(), 1e-4), f"{n}: {d:.3e}"
+        else:  # bf16 operands flip near-zero ReLU decisions of the 12-row batch: relative Frobenius error
+            d = float(np.linalg.norm(p.grad.cpu().double().numpy() - r)) / max(float(np.linalg.norm(r)), 1e-4)
+            assert d <= 5e-2, f"{n}: {d:.3e}"
+
+
+def test_attn_head_dropout_regenerated_in_backward():
+    """attn_drop in training: the backward regenerates the forward's mask from the seed. Checked through a
+    directional derivative: <dlogits, d logits/dX . U> from vcg_head_attn_bwd equals the central difference of
+    the forward along U (same seed, so the same mask)."""
+    from vcg_hip import ops
+    h = _head_module(DEV)
+    at = h.head
+    B, T, hid = 4, 4, 128
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    Vout = (torch.rand(B * T, hid, generator=gen) + 0.1).to(DEV)
+    Lout = (torch.rand(B, hid, generator=gen) + 0.1).to(DEV)
+    U = torch.randn(B * T, hid, generator=gen).to(DEV)
+    R = torch.randn(B, 2, generator=gen).to(DEV)
+    seed, p = 12345, 0.3
+    _, _, saved = ops.head_attn_fwd(Vout, Lout, at.query, at.key, at.value, at.proj, B, T, hid, at.n_head, p, seed)
+    dV, _ = ops.head_attn_bwd(saved, at.query, at.key, at.value, at.proj, R, Vout, Lout, B, T, hid, at.n_head, p, seed,
+                              relu_mask=False)
+    eps = 1e-2
+    lp, _, _ = ops.head_attn_fwd(Vout + eps * U, Lout, at.query, at.key, at.value, at.proj, B, T, hid, at.n_head, p,
+                                 seed)
+    lm, _, _ = ops.head_attn_fwd(Vout - eps * U, Lout, at.query, at.key, at.value, at.proj, B, T, hid, at.n_head, p,
+                                 seed)
+    fd = ((lp - lm) * R).sum().item() / (2 * eps)
+    an = (dV * U).sum().item()
+    assert abs(fd - an) <= 2e-3 * (1 + abs(an)), (fd, an)
+    l0, _, _ = ops.head_attn_fwd(Vout, Lout, at.query, at.key, at.value, at.proj, B, T, hid, at.n_head, 0.0, seed)
+    l1, _, _ = ops.head_attn_fwd(Vout, Lout, at.query, at.key, at.value, at.proj, B, T, hid, at.n_head, p, seed)
+    assert _maxdiff(l0.cpu(), l1.cpu()) > 0  # the mask is applied
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c1_attn_forward(stats, precision):
+    """Full TwoStream C1 with head_type='attn' (running-stats eval) vs the reference golden."""
+    from vcg_hip.build import build_two_stream
+    g = _gold("head_attn.npz")
+    model = build_two_stream(clip_frame_num=4, seed=123, device=DEV, precision=precision, bn_stats=stats,
+                             dropout=0.0, head_type="attn").eval()
+    frames, ids, mask, labels = _inputs(2, 4, 112, 32)
+    with torch.no_grad():
+        lg, pr = model(frames, ids, mask)
+    tol = 1e-3 if precision == "fp32" else 5e-2
+    assert _maxdiff(lg.cpu(), g["c1attn_logits_running"]) <= tol
+    assert _maxdiff(pr.cpu(), g["c1attn_prob_running"]) <= tol
+
+
+def test_c1_attn_train_step_runs(stats):
+    """head_type='attn' through the whole native train step (fwd, bwd, clip + AdamW) in bf16 with dropout on:
+    finite loss, every head parameter receives a gradient and moves."""
+    from vcg_hip.build import build_two_stream
+    from vcg_hip.functions import cross_entropy
+    model = build_two_stream(clip_frame_num=4, seed=123, device=DEV, precision="bf16", bn_stats=stats,
+                             dropout=0.1, head_type="attn").train()
+
+    class Cfg:
+        weight_decay = 0.01
+        learning_rate = 1e-4
+        betas = (0.9, 0.95)
+    opt = model.configure_optimizers(Cfg)
+    frames, ids, mask, labels = _inputs(2, 4, 112, 32)
+    before = {n: p.detach().clone() for n, p in model.fusion_head.named_parameters()}
+    opt.zero_grad()
+    loss = cross_entropy(model(frames, ids, mask)[0], labels)
+    loss.backward()
+    for n, p in model.fusion_head.named_parameters():
+        assert torch.isfinite(p.grad).all() and p.grad.abs().sum() > 0, n
+    opt.clip_and_step(1.0)
+    torch.cuda.synchronize()
+    assert np.isfinite(loss.item())
+    for n, p in model.fusion_head.named_parameters():
+        assert not torch.equal(p.detach(), before[n]), n

@@ -64,7 +64,7 @@ def sample_idx(n, k=256):
     return np.unique(np.linspace(0, n - 1, num=min(k, n)).astype(np.int64))
 
 
-def build_reference(T, dropout=0.0):
+def build_reference(T, dropout=0.0, head_type="mlp"):
     from transformers import BertConfig, BertModel
     cfg = BertConfig(output_attentions=True, hidden_dropout_prob=dropout, attention_probs_dropout_prob=dropout)
     cfg._attn_implementation = "eager"
@@ -75,7 +75,7 @@ def build_reference(T, dropout=0.0):
             b.conv1 = TemporalShift(b.conv1, n_segment=T, n_div=8)
     vis.fc = torch.nn.Identity()
     m = ref_two_stream.TwoStream(lang, vis, 768, 2048, T, 128)
-    m.build_chapter_head(output_size=2, head_type="mlp")
+    m.build_chapter_head(output_size=2, head_type=head_type)
     synth.init_params(m, SEED)
     return m
 

@@ -11,20 +11,7 @@ using namespace vcg;
 
 namespace {
 
-// Dropout keep decision of element idx (a stateless counter hash, so the backward regenerates the mask):
-// 32-bit murmur3 finaliser of (idx * golden ratio) ^ seed -- two 32-bit multiplies, no 64-bit arithmetic.
-// (Tensors here stay below 2^32 elements; the seed differs per dropout site and step.)
-__device__ __forceinline__ bool keep(uint64_t seed, uint64_t idx, float p) {
-  if (p <= 0.f) return true;
-  uint32_t h = ((uint32_t)idx * 0x9E3779B1u) ^ (uint32_t)seed;
-  h += (uint32_t)(seed >> 32);
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
-  return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
-}
+__device__ __forceinline__ bool keep(uint64_t seed, uint64_t idx, float p) { return dropout_keep(seed, idx, p); }
 
 // value as stored in T (bias-gradient sums use the gradient the GEMM will read)
 template <typename T> __device__ __forceinline__ float bf_round(float v) { return to_f<T>(from_f<T>(v)); }

@@ -130,6 +130,21 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// Dropout keep decision of element idx (a stateless counter hash, so the backward regenerates the mask):
+// 32-bit murmur3 finaliser of (idx * golden ratio) ^ seed -- two 32-bit multiplies, no 64-bit arithmetic.
+// (Tensors stay below 2^32 elements; the seed differs per dropout site and step.)
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, float p) {
+  if (p <= 0.f) return true;
+  uint32_t h = ((uint32_t)idx * 0x9E3779B1u) ^ (uint32_t)seed;
+  h += (uint32_t)(seed >> 32);
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
 }  // namespace vcg
 
 #define VCG_CHECK_HIP(expr)                                                     \

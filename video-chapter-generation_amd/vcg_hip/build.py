@@ -30,6 +30,8 @@ def build_two_stream(clip_frame_num=16, hidden_size=128, head_type="mlp", dropou
     model = TwoStream(lang_model.base_model, vision_model.base_model, lang_model.embed_size, vision_model.feature_dim,
                       clip_frame_num, hidden_size)
     model.build_chapter_head(output_size=2, head_type=head_type)
+    if dropout is not None and head_type == "attn":
+        model.fusion_head.head.attn_drop.p = dropout
     if device is not None:
         model = model.to(device)
     if seed is not None:

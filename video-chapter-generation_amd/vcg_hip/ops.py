@@ -437,6 +437,43 @@ def head_mlp_bwd(Vout, Lout, W, dlogits, dW, dbias, B, T, hid, O, relu_mask=True
     return dV, dL
 
 
+def head_attn_fwd(Vout, Lout, query, key, value, proj, B, T, hid, n_head, p=0.0, seed=0):
+    """SelfAttention head (two_stream.py:31-48) over cat([Vout [B*T,hid], Lout [B,hid]]) per window:
+    logits / prob [B, O] fp32 and the f32 state the backward needs (vcg_head_attn_saved_floats)."""
+    _chk(Vout, name="Vout")
+    _chk(Lout, Vout.dtype, "Lout")
+    assert Vout.numel() == B * T * hid and Lout.numel() == B * hid
+    O = proj.weight.shape[0]
+    for lin in (query, key, value, proj):
+        _chk(lin.weight, torch.float32, "head weight")
+    saved = torch.empty(_lib.query("vcg_head_attn_saved_floats", B, T, hid, n_head), dtype=torch.float32,
+                        device=Vout.device)
+    logits = torch.empty((B, O), dtype=torch.float32, device=Vout.device)
+    prob = torch.empty((B, O), dtype=torch.float32, device=Vout.device)
+    _lib.call("vcg_head_attn_fwd", dt_code(Vout.dtype), P(Vout), P(Lout), P(query.weight), P(query.bias),
+              P(key.weight), P(key.bias), P(value.weight), P(value.bias), P(proj.weight), P(proj.bias), P(saved),
+              saved.numel(), P(logits), P(prob), B, T, hid, n_head, O, float(p), int(seed) & (2**64 - 1), stream())
+    return logits, prob, saved
+
+
+def head_attn_bwd(saved, query, key, value, proj, dlogits, Vout, Lout, B, T, hid, n_head, p=0.0, seed=0,
+                  relu_mask=True):
+    """Backward of head_attn_fwd: returns the ReLU-masked gradients of Vout / Lout; accumulates the
+    query / key / value / proj parameter gradients into their .grad (when they require grad)."""
+    O = proj.weight.shape[0]
+    dV = torch.empty_like(Vout)
+    dL = torch.empty_like(Lout)
+    w = torch.empty(_lib.query("vcg_head_attn_bwd_ws_floats", B, T, hid), dtype=torch.float32, device=Vout.device)
+
+    def g(t):
+        return P(t.grad) if t.requires_grad else None
+    _lib.call("vcg_head_attn_bwd", dt_code(Vout.dtype), P(saved), P(query.weight), P(key.weight), P(value.weight),
+              P(proj.weight), P(dlogits), P(dV), P(dL), g(query.weight), g(query.bias), g(key.weight), g(key.bias),
+              g(value.weight), g(value.bias), g(proj.weight), g(proj.bias), P(w), w.numel(), B, T, hid, n_head, O,
+              float(p), int(seed) & (2**64 - 1), int(relu_mask), stream())
+    return dV, dL
+
+
 def cross_entropy_fwd(logits, labels):
     B, C = logits.shape
     loss = torch.empty((), dtype=torch.float32, device=logits.device)
