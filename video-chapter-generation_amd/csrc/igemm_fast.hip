@@ -304,7 +304,12 @@ template <int BM, int BN>
 __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t* stB, const GemmParams& p,
                                                 bf16_t* Cout, int m0, int n0, const float* cpar, float (&s1)[8],
                                                 float (&s2)[8], float (&s3)[8]) {
-  constexpr int NTH = BM * 2, CPR = BN / 8, NCH = 128 * BN / 8, KC = NCH / NTH, KB = KC < 4 ? KC : (BM == 256 ? 2 : 4);
+  constexpr int NTH = BM * 2, CPR = BN / 8, NCH = 128 * BN / 8, KC = NCH / NTH;
+#ifdef VCG_EPI_KB
+  constexpr int KB = KC < VCG_EPI_KB ? KC : VCG_EPI_KB;
+#else
+  constexpr int KB = KC < 4 ? KC : (BM == 256 ? 2 : 4);
+#endif
   const BwdEpi& e = p.bwd;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();

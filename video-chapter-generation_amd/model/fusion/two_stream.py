@@ -7,6 +7,7 @@ return_emb=False) -> (logits [B,2], prob [B,2]) (+ vision_emb [B,T,2048], lang_e
 accumulation and statistics); the default "fp32" is the parity mode.
 """
 import math
+import os
 
 import torch
 from torch import nn
@@ -72,6 +73,18 @@ class TwoStream(NativeRoot, nn.Module):
     def configure_optimizers(self, train_config):
         return configure_adamw(self, train_config)
 
+    overlap_streams = os.environ.get("VCG_OVERLAP", "1") != "0"
+
+    def _side_stream(self, dev):
+        """The BERT side stream (None: one stream), created once per device."""
+        if not self.overlap_streams or dev.type != "cuda":
+            return None
+        s = getattr(self, "_vcg_side", None)
+        if s is None or s.device != dev:
+            s = torch.cuda.Stream(device=dev)
+            object.__setattr__(self, "_vcg_side", s)
+        return s
+
     def set_grad_hooks(self, hooks):
         """hooks(tag) is called from the backward when a branch's gradients are final."""
         object.__setattr__(self, "_vcg_hooks", hooks)
@@ -94,12 +107,29 @@ class TwoStream(NativeRoot, nn.Module):
         if attention_mask is None:
             attention_mask = torch.ones_like(text_ids)
         bert = BertEncoderEngine(self.lang_model, f, dt)
-        lang_emb, _ = BertFn.apply(text_ids, attention_mask, anchor, bert, need_grad, new_seed(), hooks)
+        side = self._side_stream(dev)
+        if side is None:
+            lang_emb, _ = BertFn.apply(text_ids, attention_mask, anchor, bert, need_grad, new_seed(), hooks)
+        else:
+            # The encoders are independent until the head: BERT runs on a side stream concurrently with the
+            # trunk, so its compute-bound GEMMs fill the MFMA while the trunk's HBM-bound passes stream
+            # (autograd replays the same split in the backward, see BertFn).
+            main = torch.cuda.current_stream(dev)
+            side.wait_stream(main)
+            text_ids = text_ids.contiguous()
+            attention_mask = attention_mask.contiguous()
+            for t in (text_ids, attention_mask):
+                t.record_stream(side)
+            with torch.cuda.stream(side):
+                lang_emb, _ = BertFn.apply(text_ids, attention_mask, anchor, bert, need_grad, new_seed(), hooks, main)
         # vision: rearrange 'b t c h w -> (b t) c h w' (two_stream.py:183) is a view of a contiguous clip
         batch_size = img_clip.shape[0]
         img = img_clip.float().contiguous()
         img = img.view(batch_size * img.shape[1], *img.shape[2:])
         vision_emb = TrunkFn.apply(img, anchor, ResNetTrunk(self.vision_model, dt), need_grad, hooks)
+        if side is not None:
+            main.wait_stream(side)
+            lang_emb.record_stream(main)
         # fusion
         head = HeadEngine(self.fusion_head, f, dt)
         binary_logits, binary_prob = HeadFn.apply(lang_emb, vision_emb, anchor, head, need_grad, hooks)

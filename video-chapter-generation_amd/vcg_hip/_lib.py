@@ -13,7 +13,7 @@ import threading
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvcg_hip.so")
+LIB_PATH = os.environ.get("VCG_LIB_PATH") or os.path.join(_HERE, "libvcg_hip.so")  # override: A/B builds
 
 
 def _find_header():

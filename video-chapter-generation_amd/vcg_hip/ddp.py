@@ -23,6 +23,7 @@ class GradAllReducer:
         self._lo = self._hi = None
         self._works = []
         self._done_lo = None
+        self._stream = None  # stream the open bucket's gradients were produced on
 
     # called by the engines (autograd backward thread) with parameters whose grads are final
     def __call__(self, params):
@@ -34,6 +35,10 @@ class GradAllReducer:
         lo = min(f.offset_of(p) for p in params)
         hi = max(f.offset_of(p) + p.numel() for p in params)
         hi = (hi + 255) // 256 * 256
+        stream = torch.cuda.current_stream() if torch.cuda.is_available() and f.grad.is_cuda else None
+        if stream != self._stream:  # the encoders' backwards run on two streams: a bucket never spans both
+            self._flush()
+            self._stream = stream
         if self._lo is not None and (hi == self._lo or lo == self._hi):
             self._lo, self._hi = min(lo, self._lo), max(hi, self._hi)
         else:
@@ -46,7 +51,11 @@ class GradAllReducer:
         if self._lo is None:
             return
         buf = self.flat.grad[self._lo:min(self._hi, self.flat.total)]
-        self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        if self._stream is not None and self._stream != torch.cuda.current_stream():
+            with torch.cuda.stream(self._stream):  # the collective waits on the stream that made the bucket
+                self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        else:
+            self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         self._lo = self._hi = None
 
     def finish(self):

@@ -28,11 +28,16 @@ class TrunkFn(torch.autograd.Function):
 
 
 class BertFn(torch.autograd.Function):
+    """BERT encoder. `join` (optional): the stream that consumes the outputs when the encoder runs on a side
+    stream concurrently with the trunk (TwoStream.forward). Autograd runs the backward on the forward's stream
+    (the side stream); it ends by making `join` wait for it, so the gradients are complete on the caller's
+    stream when backward() returns."""
+
     @staticmethod
-    def forward(ctx, ids, mask, anchor, engine, need_grad, seed, hooks):
+    def forward(ctx, ids, mask, anchor, engine, need_grad, seed, hooks, join=None):
         ctx.set_materialize_grads(False)
         pooled, last, saved = engine.forward(ids, mask, need_grad, seed)
-        ctx.engine, ctx.saved, ctx.hooks = engine, saved, hooks
+        ctx.engine, ctx.saved, ctx.hooks, ctx.join = engine, saved, hooks, join
         if pooled is None:
             pooled = torch.zeros(0, device=ids.device)
         return pooled, last
@@ -41,11 +46,18 @@ class BertFn(torch.autograd.Function):
     def backward(ctx, d_pooled, d_last):
         if ctx.saved is None:
             raise RuntimeError("BertFn: forward ran without saving activations (need_grad=False)")
+        if ctx.join is not None:  # incoming grads were made on the joining stream: keep their memory alive here
+            cur = torch.cuda.current_stream()
+            for t in (d_pooled, d_last):
+                if t is not None and t.is_cuda:
+                    t.record_stream(cur)
         if d_pooled is not None or d_last is not None:
             ctx.engine.backward(d_pooled if d_pooled is not None and d_pooled.numel() else None, d_last, ctx.saved,
                                 hooks=ctx.hooks)
         ctx.saved = None
-        return None, None, None, None, None, None, None
+        if ctx.join is not None:
+            ctx.join.wait_stream(torch.cuda.current_stream())
+        return None, None, None, None, None, None, None, None
 
 
 class HeadFn(torch.autograd.Function):
