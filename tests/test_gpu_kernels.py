@@ -393,7 +393,7 @@ DGRAD_BWD_CASES = [
 
 
 @pytest.mark.parametrize("case", DGRAD_BWD_CASES)
-@pytest.mark.parametrize("mode", ["affine", "tsm_bits_two", "tsm_plain"])
+@pytest.mark.parametrize("mode", ["affine", "tsm_bits_two", "tsm_plain", "tsm_strided_res"])
 def test_conv_dgrad_bwd(K, case, mode):
     """Fused dgrad epilogue == the unfused ops (dgrad, TSM combine, masks) bit for bit; its BN sums == a
     float64 reduction of the same g."""
@@ -431,6 +431,13 @@ def test_conv_dgrad_bwd(K, case, mode):
         if mode == "tsm_plain":
             g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, k, k, s, p, tsm_T=T, tsm_fold=fold, res=res)
             ref = comb
+        elif mode == "tsm_strided_res":
+            # compact residual of a 1x1 / stride-2 downsample: only even (h, w) rows receive it
+            rc = _rand((N, (H + 1) // 2, (W + 1) // 2, C), dtype, 67).to(DEV)
+            full = torch.zeros_like(res)
+            full[:, ::2, ::2, :] = rc
+            g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, k, k, s, p, tsm_T=T, tsm_fold=fold, res=rc, res_stride=2)
+            ref = K.tsm_unshift_add(dx, full, N, T, H * W, C, fold)
         else:
             g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, k, k, s, p, tsm_T=T, tsm_fold=fold, res=res, bits=bits,
                                  y=y, mean=mean, invstd=inv, y2=y2, mean2=mean2, invstd2=inv2, sums=sums,
@@ -438,7 +445,7 @@ def test_conv_dgrad_bwd(K, case, mode):
             ref = torch.where(y2 > 0, comb, torch.zeros_like(comb))
     assert g is not None, "the fused bf16 engine must take this shape"
     assert torch.equal(g, ref), f"g differs: max {(g.float() - ref.float()).abs().max().item():.3e}"
-    if mode == "tsm_plain":
+    if mode in ("tsm_plain", "tsm_strided_res"):
         return
     gd = g.double().reshape(-1, C)
     sg = gd.sum(0)

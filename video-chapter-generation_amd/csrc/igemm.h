@@ -54,7 +54,7 @@ struct OpArgs {
 //   * TSM adjoint (tsm_T > 0): the value moves to row m + hw (n < fold) / m - hw (fold <= n < 2 fold), i.e. one
 //     frame later / earlier inside its clip of tsm_T frames; at the clip edge it is dropped and the
 //     destination row of the wrap (frame 0 / tsm_T - 1) receives zero -- every element is written once;
-//   * + res[dst] (residual gradient);
+//   * + res[dst] (residual gradient; res_s > 1: compact strided residual, see res_s);
 //   * mask: bits[dst / 8] bit (dst % 8) (ReLU mask bytes of vcg_bn_apply) or fma(y, msc, msh) > 0 (the
 //     forward's BN + ReLU decision recomputed from the saved pre-BN y);
 //   * stored (bf16) as g, and reduced per column: part[slot][0][n] = sum g, part[slot][1][n] = sum
@@ -65,6 +65,9 @@ struct BwdEpi {
   FastDiv fd_hw, fd_T;
   int hw;
   const void* res;
+  int res_s;       // > 1: res is the compact [N][H/res_s][W/res_s][C] input gradient of a 1x1 stride-res_s conv
+  int rH, rW;      //      (rows whose h or w is not a multiple of res_s get no residual); rH, rW its grid
+  FastDiv fd_w;    //      and the row decode h = (m % hw) / W
   const uint8_t* bits;
   const void* y;
   const float *mean, *invstd, *msc, *msh;

@@ -559,7 +559,7 @@ VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C) { return 768LL * 3 * C * 4 
 // returns VCG_ERR_UNSUPPORTED where it does not apply (the caller then runs the unfused ops).
 VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C,
                                int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold,
-                               const void* res, const unsigned char* bits, const void* y, const float* mean,
+                               const void* res, int res_stride, const unsigned char* bits, const void* y, const float* mean,
                                const float* invstd, const float* mscale, const float* mshift, const void* y2,
                                const float* mean2, const float* invstd2, float* ws, long long ws_bytes,
                                float* sum_g, float* sum_gx, float* dgamma, float* dbeta, float* sum_gx2,
@@ -575,6 +575,7 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   VCG_REQUIRE(tsm_fold == 0 || (tsm_T > 0 && N % tsm_T == 0 && tsm_fold % 8 == 0 && 2 * tsm_fold <= C),
               "bad TSM geometry");
   VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C), "workspace too small");
+  VCG_REQUIRE(res_stride == 1 || (res_stride == 2 && res), "res_stride must be 1, or 2 with a residual");
   const long long nelem = (long long)N * H * W * C;
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   if (dtype != VCG_BF16 || !fast_gemm_enabled() || nelem * 2 >= 0xFFFFFF00LL ||
@@ -606,7 +607,10 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   e.hw = H * W;
   e.fd_hw = make_fastdiv((uint32_t)(H * W));
   e.fd_T = make_fastdiv((uint32_t)(tsm_T > 0 ? tsm_T : 1));
-  e.res = res; e.bits = bits; e.y = y; e.mean = mean; e.invstd = invstd; e.msc = mscale; e.msh = mshift;
+  e.res = res; e.bits = bits;
+  e.res_s = res_stride;
+  e.rH = (H + 1) / 2; e.rW = (W + 1) / 2;
+  e.fd_w = make_fastdiv((uint32_t)W); e.y = y; e.mean = mean; e.invstd = invstd; e.msc = mscale; e.msh = mshift;
   e.y2 = y2; e.mean2 = mean2; e.invstd2 = invstd2;
   e.part = ws;
   e.nred = y ? (y2 ? 3 : 2) : 0;

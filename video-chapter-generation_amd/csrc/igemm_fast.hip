@@ -362,7 +362,17 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
       }
       off[kk] = (long long)dst * p.ldc + n;
       if (ok[kk]) {
-        if (res) rv[kk] = *reinterpret_cast<const uint4*>(res + off[kk]);
+        if (res) {
+          long long roff = off[kk];
+          bool rok = true;
+          if (e.res_s > 1) {  // compact residual of a 1x1 / stride-2 conv: only even (h, w) rows carry one
+            const uint32_t f = fdiv((uint32_t)dst, e.fd_hw), r = (uint32_t)dst - f * (uint32_t)e.hw;
+            const uint32_t h = fdiv(r, e.fd_w), w = r - h * e.fd_w.d;
+            rok = ((h | w) & 1u) == 0;
+            roff = ((long long)(f * e.rH + (h >> 1)) * e.rW + (w >> 1)) * p.ldc + n;
+          }
+          rv[kk] = rok ? *reinterpret_cast<const uint4*>(res + roff) : make_uint4(0u, 0u, 0u, 0u);
+        }
         if (e.bits) bv[kk] = e.bits[off[kk] >> 3];
         if (yp) yv[kk] = *reinterpret_cast<const uint4*>(yp + off[kk]);
         if (y2p) y2v[kk] = *reinterpret_cast<const uint4*>(y2p + off[kk]);

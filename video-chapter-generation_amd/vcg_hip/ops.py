@@ -108,12 +108,12 @@ def conv_dgrad(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, out=None):
     return dx
 
 
-def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, res=None, bits=None, y=None,
-                   mean=None, invstd=None, mscale=None, mshift=None, y2=None, mean2=None, invstd2=None, sums=None,
+def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, res=None, res_stride=1,
+                   bits=None, y=None, mean=None, invstd=None, mscale=None, mshift=None, y2=None, mean2=None, invstd2=None, sums=None,
                    sum_gx2=None, dgamma=None, dbeta=None, dgamma2=None, dbeta2=None, out=None, workspace=None):
     """Conv input gradient fused with the trunk backward's next steps (vcg_conv_dgrad_bwd, igemm.h BwdEpi):
     g = mask(tsm_adjoint(dgrad) + res) and the BN-backward sums of g against y (sums [2, C] = sum_g,
-    sum_gx) and y2 (sum_gx2 [C]); dgamma/dbeta (dgamma2/dbeta2) accumulate. Returns g, or None where the
+    sum_gx) and y2 (res_stride 2: res is the compact [N, H/2, W/2, C] gradient of a 1x1 / stride-2 conv) (sum_gx2 [C]); dgamma/dbeta (dgamma2/dbeta2) accumulate. Returns g, or None where the
     fused engine does not apply (fp32 / unsupported shape): the caller then runs the unfused ops."""
     OH, OW = conv_out_hw(H, W, KH, KW, stride, pad)
     _chk(dy, None, "dy")
@@ -125,10 +125,11 @@ def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_f
     for t in (res, y, y2):
         if t is not None:
             _chk(t, dy.dtype)
-            assert t.numel() == N * H * W * C
+            assert t.numel() == (N * ((H + 1) // 2) * ((W + 1) // 2) * C if t is res and res_stride == 2
+                                 else N * H * W * C)
     rc = _lib.query("vcg_conv_dgrad_bwd", dt_code(dy.dtype), P(dy), P(wt), P(g), N, H, W, C, Cout, KH, KW, stride,
-                    pad, tsm_T, tsm_fold, P(res), P(bits), P(y), P(mean), P(invstd), P(mscale), P(mshift), P(y2),
-                    P(mean2), P(invstd2), P(workspace), workspace.numel() * 4,
+                    pad, tsm_T, tsm_fold, P(res), int(res_stride), P(bits), P(y), P(mean), P(invstd), P(mscale),
+                    P(mshift), P(y2), P(mean2), P(invstd2), P(workspace), workspace.numel() * 4,
                     P(sums[0]) if sums is not None else None, P(sums[1]) if sums is not None else None, P(dgamma),
                     P(dbeta), P(sum_gx2), P(dgamma2), P(dbeta2), stream())
     if rc == -2:  # VCG_ERR_UNSUPPORTED

@@ -232,17 +232,26 @@ class ResNetTrunk:
         dy1 = self._dgrad_bn(blk.conv2, dy2, N, H, W, r["y1"], r["b1"], planes)
         del dy2
         self._wgrad(r["conv1"], r["x"], dy1, N, H, W, Cin, T, fold)
+        res_stride = 1
         if ds:
-            self._wgrad(blk.downsample[0], r["x"], dyd, N, H, W, Cin)
-            res = self._dgrad(blk.downsample[0], dyd, N, H, W)  # the downsample branch's input gradient
-            del dyd
+            cds = blk.downsample[0]
+            self._wgrad(cds, r["x"], dyd, N, H, W, Cin)
+            if cds.stride[0] == 2 and self.dtype == torch.bfloat16:
+                # 1x1 / stride 2: only the even (h, w) inputs receive a gradient, so it is ONE dense GEMM over the
+                # output pixels (no 3/4-zero rows), added by the conv1 dgrad epilogue at those rows (res_stride 2)
+                wt_ds = ops.weight_prep(cds.weight.data, Cin, self.dtype, transposed=True)
+                Mo = dyd.numel() // C3
+                res = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3)
+                res_stride = 2
+            else:
+                res = self._dgrad(cds, dyd, N, H, W)  # the downsample branch's input gradient
         else:
             res = g  # the identity branch: the block's masked output gradient
         # conv1 input gradient + TSM adjoint + residual branch; fused: also the previous block's mask and sums
         conv1 = r["conv1"]
         Cout1, Cin1, KH, KW, s, p = _conv_shape(conv1)
         wt = ops.weight_prep(conv1.weight.data, Cin1, self.dtype, transposed=True)
-        kw = dict(tsm_T=T if fold else 0, tsm_fold=fold, res=res)
+        kw = dict(tsm_T=T if fold else 0, tsm_fold=fold, res=res, res_stride=res_stride)
         sums3 = sumsd = None
         if prev is not None:
             sums3 = torch.empty((2, Cin), dtype=torch.float32, device=dy1.device)
@@ -255,6 +264,10 @@ class ResNetTrunk:
                 kw.update(y2=prev["yd"], mean2=prev["bd"].mean, invstd2=prev["bd"].invstd, sum_gx2=sumsd[1],
                           dgamma2=dg2, dbeta2=db2)
         out = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, **kw)
+        if ds:
+            if out is None and res_stride == 2:  # unfused fallback: the full-grid downsample input gradient
+                res = self._dgrad(blk.downsample[0], dyd, N, H, W)
+            del dyd
         if out is not None:
             if prev is None:
                 return out, None  # the max-pool's output gradient (no mask, no BN)
