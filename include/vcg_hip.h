@@ -53,9 +53,10 @@ VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
    ops/temporal_shift.py:33-51 autograd), + res, ReLU mask (bits or fma(y, mscale, mshift) > 0), stored as g, and
    the BatchNorm backward reductions against y (and y2) -> sum_g / sum_gx (/ sum_gx2), dgamma / dbeta
    (/ dgamma2 / dbeta2) accumulated. res_stride 2: `res` is the compact [N][ceil(H/2)][ceil(W/2)][C] input
-   gradient of a 1x1 stride-2 conv (the downsample branch), added at the even (h, w) rows only.
+   gradient of a 1x1 stride-2 conv (the downsample branch), added at the even (h, w) rows only. A 3x3 / stride-2
+   dgrad runs as four sub-pixel classes (dx pixels of one (h, w) parity) over only the taps reaching each.
    bf16 fast engine only; VCG_ERR_UNSUPPORTED elsewhere. */
-VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C);
+VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C, int Cout, int KH, int KW);
 VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, const void* res, int res_stride, const unsigned char* bits, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, const void* y2, const float* mean2, const float* invstd2, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, float* sum_gx2, float* dgamma2, float* dbeta2, hipStream_t s);
 /* autograd of conv2d: weight gradient, split-K over pixels, written in OIHW (state-dict layout) */
 VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad);

@@ -386,7 +386,8 @@ DGRAD_BWD_CASES = [
     (16, 65, 71, 128, 64, 3, 1, 1, 4),  # >= 64 Ki rows, 128 columns (256-row kernel with VCG_BIG_TILE=1)
     (16, 64, 70, 256, 64, 1, 1, 0, 8),  # same, dense 1x1
     (8, 9, 9, 64, 64, 3, 1, 1, 4),     # conv2 3x3
-    (8, 10, 10, 64, 128, 3, 2, 1, 4),  # conv2 3x3 / 2 (block 0 of a stage)
+    (8, 10, 10, 64, 128, 3, 2, 1, 4),  # conv2 3x3 / 2 (block 0 of a stage): four sub-pixel class GEMMs
+    (16, 28, 28, 128, 128, 3, 2, 1, 4),  # same, several tiles per class
     (8, 7, 7, 64, 256, 1, 1, 0, 4),    # conv3 / conv1 1x1 (dense)
     (8, 6, 6, 128, 64, 1, 1, 0, 8),    # wider C: BN = 128 tiles
 ]

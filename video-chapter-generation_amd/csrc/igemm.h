@@ -47,6 +47,10 @@ struct OpArgs {
   int KH, KW, stride, pad;
   int tsm_T, tsm_fold;   // TSM temporal shift fused into the gather (fold = 0: off)
   FastDiv fd_ghw, fd_gw, fd_T;
+  // sub-pixel class of a stride-2 dgrad (fast kernel, tKW > 0): the GH x GW row grid is the pixels
+  // (2i + ry, 2j + rx) of the dx image, and the k tiles walk only the taps that reach them,
+  // kh = tkh0 + 2a (a < tKH), kw = tkw0 + 2b (b < tKW) -- 1, 2 or 4 of the 9 taps of a 3x3 kernel
+  int tKH, tKW, tkh0, tkw0, ry, rx;
 };
 
 // EPI_BWD (fast kernel, conv dgrad): the epilogue of a conv input gradient inside the trunk backward.
@@ -75,6 +79,10 @@ struct BwdEpi {
   const float *mean2, *invstd2;
   float* part;  // [slots][nred][N]
   int nred;     // 0 (no reduction), 2 or 3
+  // sub-pixel class rows (sub != 0): GEMM row m = (f, i, j) of the cH x cW class grid is dx row
+  // f * fH * fW + (2i + ry) * fW + (2j + rx)
+  int sub, cW, ry, rx, fH, fW;
+  FastDiv fd_chw, fd_cw;
 };
 
 struct GemmParams {

@@ -352,6 +352,11 @@ static OpArgs dense_op(const void* ptr, long long ld, int rows, long long K = 0,
   return a;
 }
 
+static bool getenv_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+
 static bool fast_gemm_enabled() {
   static int v = -1;
   if (v < 0) {
@@ -548,8 +553,29 @@ VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
                : run_gemm<float, OP_DGRAD, OP_DENSE_K>(p, EPI_STORE, 1, stream);
 }
 
-// Workspace of vcg_conv_dgrad_bwd: partial sums [slots <= 768][3][C] floats.
-VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C) { return 768LL * 3 * C * 4 + 256; }
+// Workspace of vcg_conv_dgrad_bwd: partial sums [slots][3][C] floats (slots <= 768 per launch, 4 launches for
+// the sub-pixel classes of a stride-2 dgrad), then the class-packed weights (KH * KW * C * Cout bf16).
+static long long dgrad_bwd_part_bytes(int C) { return 4LL * 768 * 3 * C * 4; }
+VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C, int Cout, int KH, int KW) {
+  return dgrad_bwd_part_bytes(C) + (long long)KH * KW * C * Cout * 2 + 256;
+}
+
+namespace {
+// wt [C][KH][KW][Cout] -> the taps of one sub-pixel class, [C][tKH][tKW][Cout] (kh = kh0 + 2a, kw = kw0 + 2b)
+__global__ void pack_class_taps_kernel(const bf16_t* __restrict__ wt, bf16_t* __restrict__ out, int C, int KH, int KW,
+                                       int Cout, int tKH, int tKW, int kh0, int kw0) {
+  const long long n = (long long)C * tKH * tKW * Cout;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Cout);
+    long long t = i / Cout;
+    const int b = (int)(t % tKW);
+    t /= tKW;
+    const int a = (int)(t % tKH);
+    const int c = (int)(t / tKH);
+    out[i] = wt[(((long long)c * KH + kh0 + 2 * a) * KW + kw0 + 2 * b) * Cout + co];
+  }
+}
+}  // namespace
 
 // Conv input gradient of the trunk backward with the fused EPI_BWD epilogue (igemm.h BwdEpi): the dgrad value
 // (moved by the TSM adjoint when tsm_fold > 0) plus `res`, masked by `bits` (VCG_MASK_BITS bytes) or by
@@ -574,7 +600,7 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   VCG_REQUIRE(!y2 || (y && mean2 && invstd2 && sum_gx2), "the second reduction needs y, mean2/invstd2/sum_gx2");
   VCG_REQUIRE(tsm_fold == 0 || (tsm_T > 0 && N % tsm_T == 0 && tsm_fold % 8 == 0 && 2 * tsm_fold <= C),
               "bad TSM geometry");
-  VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C), "workspace too small");
+  VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C, Cout, KH, KW), "workspace too small");
   VCG_REQUIRE(res_stride == 1 || (res_stride == 2 && res), "res_stride must be 1, or 2 with a residual");
   const long long nelem = (long long)N * H * W * C;
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
@@ -583,6 +609,10 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
     return VCG_ERR_UNSUPPORTED;
   const bool dense = (KH == 1 && KW == 1 && stride == 1 && pad == 0);
   if (!dense && (Cout < 64 || KH * KW > 32)) return VCG_ERR_UNSUPPORTED;  // fast dgrad gather: one tap per k tile
+  // stride-2 3x3: four sub-pixel classes (dx pixels of one (h, w) parity), each a GEMM over only the taps that
+  // reach it (4 / 2 / 2 / 1 of 9) instead of one GEMM over all 9 with 3/4 of the tap rows masked to zero
+  const bool subpix = stride == 2 && KH == 3 && KW == 3 && pad == 1 && tsm_fold == 0 && res_stride == 1 &&
+                      H % 2 == 0 && W % 2 == 0 && !getenv_flag("VCG_NO_SUBPIXEL");
   GemmParams p{};
   p.M = N * H * W;
   p.N = C;
@@ -614,6 +644,51 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   e.y2 = y2; e.mean2 = mean2; e.invstd2 = invstd2;
   e.part = ws;
   e.nred = y ? (y2 ? 3 : 2) : 0;
+  if (subpix) {
+    bf16_t* wpk = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(ws) + dgrad_bwd_part_bytes(C));
+    const int cH = H / 2, cW = W / 2;
+    int slots = 0;
+    for (int ry = 0; ry < 2; ++ry)
+      for (int rx = 0; rx < 2; ++rx) {
+        // dx row 2i + ry sits at py = 2i + ry + pad; the taps that reach it have kh = py (mod 2)
+        const int kh0 = (ry + pad) & 1, kw0 = (rx + pad) & 1;
+        const int tKH = (KH - kh0 + 1) / 2, tKW = (KW - kw0 + 1) / 2;
+        GemmParams q = p;
+        q.M = N * cH * cW;
+        q.K = tKH * tKW * Cout;
+        q.k_per_split = q.K + 64;
+        q.a.rows = q.M;
+        q.a.GH = cH; q.a.GW = cW;
+        q.a.tKH = tKH; q.a.tKW = tKW; q.a.tkh0 = kh0; q.a.tkw0 = kw0; q.a.ry = ry; q.a.rx = rx;
+        bf16_t* wc = wpk;  // reused by each class: its pack runs after the previous class's GEMM (stream order)
+        hipLaunchKernelGGL(pack_class_taps_kernel, dim3(256), dim3(256), 0, stream, (const bf16_t*)wt, wc, C, KH, KW,
+                           Cout, tKH, tKW, kh0, kw0);
+        VCG_LAUNCH_CHECK();
+        q.b = dense_op(wc, q.K, C, q.K, 2);
+        BwdEpi& qe = q.bwd;
+        qe.sub = 1; qe.cW = cW; qe.ry = ry; qe.rx = rx; qe.fH = H; qe.fW = W;
+        qe.fd_chw = make_fastdiv((uint32_t)(cH * cW));
+        qe.fd_cw = make_fastdiv((uint32_t)cW);
+        qe.part = ws + (long long)slots * (e.nred > 0 ? e.nred : 1) * C;
+        if (FILE* f = gemm_log()) {
+          fprintf(f, "a=2 b=0 epi=3 M=%d N=%d K=%d z=1 fast=1 conv=%dx%d/%d C=%d\n", q.M, q.N, q.K, KH, KW, stride,
+                  Cout);
+          fflush(f);
+        }
+        int rc = run_fast_gemm(q, OP_DGRAD, EPI_BWD, 1, stream);
+        if (rc) return rc;
+        slots += fast_grid_rows(q.M, q.N, 1, EPI_BWD);
+      }
+    if (e.nred > 0) {
+      int rc = bn_bwd_finalize_launch(ws, slots, C, (long long)e.nred * C, C, sum_g, sum_gx, dgamma, dbeta, 1, stream);
+      if (rc) return rc;
+      if (e.nred > 2) {
+        rc = bn_bwd_finalize_launch(ws, slots, C, 3LL * C, 2 * C, sum_g, sum_gx2, dgamma2, dbeta2, 1, stream);
+        if (rc) return rc;
+      }
+    }
+    return VCG_OK;
+  }
   if (FILE* f = gemm_log()) {
     fprintf(f, "a=%d b=0 epi=3 M=%d N=%d K=%d z=1 fast=1 conv=%dx%d/%d C=%d\n", dense ? 0 : 2, p.M, p.N, p.K, KH, KW,
             stride, Cout);

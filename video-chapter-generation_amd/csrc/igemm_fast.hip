@@ -58,8 +58,12 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
       } else {
         const int n = gr / (a.GH * a.GW);
         const int rem = gr - n * a.GH * a.GW;
-        const int y = rem / a.GW;
-        const int x = rem - y * a.GW;
+        int y = rem / a.GW;
+        int x = rem - y * a.GW;
+        if (!IM2COL && a.tKW > 0) {  // sub-pixel class of a stride-2 dgrad
+          y = 2 * y + a.ry;
+          x = 2 * x + a.rx;
+        }
         off[q] = n * a.H * a.W * a.C;
         rc[q] = TSM ? (n % a.tsm_T) : 0;
         int py, px;  // source pixel of tap (0, 0)
@@ -93,7 +97,19 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
 #pragma unroll
           for (int kh = 0; kh < 8; ++kh)
             rows |= (kh >= kh_lo && kh < kh_hi && ((hpar >> kh) & 1u)) ? (1u << ((kh * a.KW) & 31)) : 0u;
-          rb[q] = valid ? (int)(cols * rows) : 0;
+          uint32_t m = cols * rows;
+          if (!IM2COL && a.tKW > 0) {  // class taps: local bit a * tKW + b for kh = tkh0 + 2a, kw = tkw0 + 2b
+            m = 0u;
+#pragma unroll
+            for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+              for (int tb = 0; tb < 2; ++tb) {
+                const int kh = a.tkh0 + 2 * ta, kw = a.tkw0 + 2 * tb;
+                const bool okt = ta < a.tKH && tb < a.tKW && kh >= kh_lo && kh < kh_hi && kw >= kw_lo && kw < kw_hi;
+                m |= okt ? (1u << (ta * a.tKW + tb)) : 0u;
+              }
+          }
+          rb[q] = valid ? (int)m : 0;
           // (the source pixel may lie outside the image: multiply, a negative value must not be shifted)
           if constexpr (IM2COL)
             ra[q] = off[q] + (py * a.W + px) * a.C;
@@ -138,8 +154,13 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
       {
         // one filter tap per k tile: tap, its pixel offset and the channel base are scalars
         const int tap = k0 >> a.logC;
-        const int kh = tap / a.KW;
-        const int kw = tap - kh * a.KW;
+        int kh = tap / a.KW;
+        int kw = tap - kh * a.KW;
+        if (!IM2COL && a.tKW > 0) {  // class-local tap
+          const int ta = tap / a.tKW;
+          kh = a.tkh0 + 2 * ta;
+          kw = a.tkw0 + 2 * (tap - ta * a.tKW);
+        }
         const int cb = k0 & (a.C - 1);
         int toff;
         if constexpr (IM2COL) {
@@ -353,6 +374,11 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
       ok[kk] = m < p.M && n < p.N;
       src[kk] = true;
       int dst = m;
+      if (e.sub) {  // sub-pixel class row -> dx row
+        const uint32_t f = fdiv((uint32_t)m, e.fd_chw), r = (uint32_t)m - f * e.fd_chw.d;
+        const uint32_t i = fdiv(r, e.fd_cw), j = r - i * (uint32_t)e.cW;
+        dst = (int)((f * e.fH + 2 * i + e.ry) * e.fW + 2 * j + e.rx);
+      }
       if (shift != 0 && ok[kk]) {
         const int f = (int)fdiv((uint32_t)m, e.fd_hw);
         const int t = f - (int)fdiv((uint32_t)f, e.fd_T) * e.tsm_T;

@@ -119,7 +119,7 @@ def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_f
     _chk(dy, None, "dy")
     assert dy.numel() == N * OH * OW * Cout and wt.numel() == C * KH * KW * Cout
     g = out if out is not None else torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
-    nbytes = _lib.query("vcg_conv_dgrad_bwd_ws_bytes", C)
+    nbytes = _lib.query("vcg_conv_dgrad_bwd_ws_bytes", C, Cout, KH, KW)
     if workspace is None or workspace.numel() * 4 < nbytes:
         workspace = ws(nbytes, dy.device)
     for t in (res, y, y2):
