@@ -97,6 +97,9 @@ VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, in
    are HOST pointers to 3 floats. */
 VCG_API int vcg_window_frames_u8(int dtype, const uint8_t* frames, const long long* idx, void* dst, long long n_rows, int F, int H, int W, const float* mean3, const float* std3, hipStream_t s);
 VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int KH, int KW, int Cpad, int transposed, hipStream_t s);
+/* every conv of the trunk in one launch: desc = DEVICE array of n x 8 int64 (src OIHW f32 ptr, dst bf16 ptr, Cout,
+   Cin, KH, KW, Cpad, transposed), each as vcg_weight_prep; bf16 only, each tensor < 2^31 elements */
+VCG_API int vcg_weight_prep_multi(int dtype, const long long* desc, int n, hipStream_t s);
 /* out[c][r] = in[r][c] ([rows][cols], leading dims ld_in / ld_out): W^T for the BERT input-gradient GEMMs */
 VCG_API int vcg_transpose(int dtype, const void* in, void* out, int rows, int cols, long long ld_in, long long ld_out, hipStream_t s);
 VCG_API int vcg_cast_from_f32(int dtype, const float* in, void* out, long long n, hipStream_t s);

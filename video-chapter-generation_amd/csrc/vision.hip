@@ -115,6 +115,24 @@ __global__ void frames_to_nhwc_kernel(const float* __restrict__ src, T* __restri
   }
 }
 
+// The bf16 stem input (C = 3 -> Cpad = 8): one pixel per thread, its 3 plane loads coalesced across the wave
+// and ONE 16-B store of the padded pixel; 32-bit indices (the dispatcher checks N*H*W*C < 2^31).
+__global__ __launch_bounds__(256) void frames_to_nhwc8_kernel(const float* __restrict__ src, uint4* __restrict__ dst,
+                                                            int total, int HW) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int n = i / HW, hw = i - n * HW;
+    const float* s0 = src + (long long)n * 3 * HW + hw;
+    const float r = __builtin_nontemporal_load(s0), g = __builtin_nontemporal_load(s0 + HW),
+                b = __builtin_nontemporal_load(s0 + 2 * HW);
+    uint4 q;
+    q.x = (uint32_t)f2bf(r) | ((uint32_t)f2bf(g) << 16);
+    q.y = (uint32_t)f2bf(b);
+    q.z = 0u;
+    q.w = 0u;
+    dst[i] = q;
+  }
+}
+
 // Frame ingest: decoded u8 RGB frames of one video [F][H][W][3] -> the stem's
 // NHWC input [n_rows][H][W][8] (channels 3..7 zero) for the window frame table idx[n_rows]
 // (window-major, frame-minor: row = w*T + t), normalised as torchvision ToTensor + Normalize
@@ -288,7 +306,10 @@ VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, in
                                hipStream_t s) {
   VCG_REQUIRE(Cpad >= C, "Cpad < C");
   const long long tot = (long long)N * H * W;
-  if (dtype == VCG_BF16)
+  if (dtype == VCG_BF16 && C == 3 && Cpad == 8 && tot * 3 < (1LL << 31))
+    hipLaunchKernelGGL(frames_to_nhwc8_kernel, dim3(grid_for(tot)), dim3(256), 0, s, src, (uint4*)dst, (int)tot,
+                       H * W);
+  else if (dtype == VCG_BF16)
     hipLaunchKernelGGL(frames_to_nhwc_kernel<bf16_t>, dim3(grid_for(tot)), dim3(256), 0, s, src, (bf16_t*)dst, N, C,
                        H, W, Cpad);
   else
@@ -323,6 +344,46 @@ VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int 
   else
     hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(grid_for(tot)), dim3(256), 0, s, w, (float*)out, Cout, Cin, KH,
                        KW, Cpad, transposed);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+namespace {
+// vcg_weight_prep_multi: blockIdx.y = descriptor (8 int64: src, dst, Cout, Cin, KH, KW, Cpad, transposed)
+__global__ __launch_bounds__(256) void weight_prep_multi_kernel(const long long* __restrict__ desc) {
+  const long long* d = desc + 8 * blockIdx.y;
+  const float* w = reinterpret_cast<const float*>(d[0]);
+  bf16_t* out = reinterpret_cast<bf16_t*>(d[1]);
+  const int Cout = (int)d[2], Cin = (int)d[3], KH = (int)d[4], KW = (int)d[5], Cpad = (int)d[6];
+  const bool tr = d[7] != 0;
+  const int total = tr ? Cin * KH * KW * Cout : Cout * KH * KW * Cpad;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    float v;
+    if (!tr) {
+      const int ci = i % Cpad;
+      int r = i / Cpad;
+      const int kw = r % KW; r /= KW;
+      const int kh = r % KH;
+      const int co = r / KH;
+      v = ci < Cin ? w[((co * Cin + ci) * KH + kh) * KW + kw] : 0.f;
+    } else {
+      const int co = i % Cout;
+      int r = i / Cout;
+      const int kw = r % KW; r /= KW;
+      const int kh = r % KH;
+      const int ci = r / KH;
+      v = w[((co * Cin + ci) * KH + kh) * KW + kw];
+    }
+    out[i] = f2bf(v);
+  }
+}
+}  // namespace
+
+VCG_API int vcg_weight_prep_multi(int dtype, const long long* desc, int n, hipStream_t s) {
+  VCG_REQUIRE(dtype == VCG_BF16, "the batched weight prep writes bf16 GEMM layouts");
+  VCG_REQUIRE(n >= 0 && n <= 65535, "bad descriptor count");
+  if (n == 0) return VCG_OK;
+  hipLaunchKernelGGL(weight_prep_multi_kernel, dim3(64, n), dim3(256), 0, s, desc);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

@@ -399,27 +399,32 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
     float acc[VN];
 #pragma unroll
     for (int e = 0; e < VN; ++e) acc[e] = 0.f;
-    const int oh0 = ih / 2, oh1 = (ih + 1) / 2;  // windows with 2*oh-1 <= ih <= 2*oh+1
-    const int ow0 = iw / 2, ow1 = (iw + 1) / 2;
+    // the <= 2 x 2 windows with 2*oh-1 <= ih <= 2*oh+1: every candidate's loads are issued before any is used
+    const int oh0 = ih >> 1, oh1 = (ih + 1) >> 1;
+    const int ow0 = iw >> 1, ow1 = (iw + 1) >> 1;
     float yv[VN];
     if (RED) load16<T>(yb + v * VN, yv);
-    for (int oh = oh0; oh <= oh1; ++oh) {
-      if (oh >= OH) continue;
-      const int kh = ih - (oh * 2 - 1);
-      if (kh < 0 || kh > 2) continue;
-      for (int ow = ow0; ow <= ow1; ++ow) {
-        if (ow >= OW) continue;
-        const int kw = iw - (ow * 2 - 1);
-        if (kw < 0 || kw > 2) continue;
-        const long long o = (((long long)n * OH + oh) * OW + ow) * C + chunk * VN;
-        const uint8_t want = (uint8_t)(kh * 3 + kw);
-        float g[VN];
-        load16<T>(dy + o, g);
-        const IW w = *reinterpret_cast<const IW*>(idx + o);
+    float g[4][VN];
+    IW w[4];
+    bool use[4];
+    uint8_t want[4];
 #pragma unroll
-        for (int e = 0; e < VN; ++e)
-          if (idx_byte<VN>(w, e) == want) acc[e] += g[e];
+    for (int q = 0; q < 4; ++q) {
+      const int oh = (q & 2) ? oh1 : oh0, ow = (q & 1) ? ow1 : ow0;
+      use[q] = (!(q & 2) || oh1 != oh0) && (!(q & 1) || ow1 != ow0) && oh < OH && ow < OW;
+      want[q] = (uint8_t)((ih - (oh * 2 - 1)) * 3 + (iw - (ow * 2 - 1)));
+      if (use[q]) {
+        const long long o = (((long long)n * OH + oh) * OW + ow) * C + chunk * VN;
+        load16<T>(dy + o, g[q]);
+        w[q] = *reinterpret_cast<const IW*>(idx + o);
       }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!use[q]) continue;
+#pragma unroll
+      for (int e = 0; e < VN; ++e)
+        if (idx_byte<VN>(w[q], e) == want[q]) acc[e] += g[q][e];
     }
     if (RED) {
 #pragma unroll

@@ -117,6 +117,11 @@ class FlatParams:
     def _version(self):
         return sum(p._version for p in self.params)
 
+    # `generation` changes whenever the master weights may have changed (a fused optimizer step, an in-place
+    # write seen through the tensors' version counters): derived weight layouts (the trunk's bf16 conv GEMM
+    # operands) are rebuilt when it moves.
+    generation = 0
+
     def refresh_shadow(self, force=False):
         if self.shadow is None:
             return
@@ -124,7 +129,9 @@ class FlatParams:
         if force or v != self._shadow_version:
             ops.cast_from_f32(self.data, self.shadow.dtype, out=self.shadow)
             self._shadow_version = v
+            self.generation += 1
 
     def mark_shadow_current(self):
         """Called by the fused optimizer, which rewrote the shadow while updating."""
         self._shadow_version = self._version()
+        self.generation += 1

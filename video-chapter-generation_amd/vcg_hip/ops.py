@@ -316,6 +316,13 @@ def weight_prep(w, Cpad, dtype, transposed=False, out=None):
     return out
 
 
+def weight_prep_multi(desc, n):
+    """One launch of vcg_weight_prep_multi over a DEVICE int64 descriptor table [n, 8]."""
+    _chk(desc, torch.int64, "desc")
+    assert desc.numel() >= 8 * n
+    _lib.call("vcg_weight_prep_multi", BF16, P(desc), int(n), stream())
+
+
 def transpose(x, out=None):
     """[rows, cols] -> [cols, rows] (contiguous)."""
     _chk(x, None, "x")

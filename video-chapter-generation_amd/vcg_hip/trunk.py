@@ -44,14 +44,68 @@ def _tsm_info(conv1, Cin):
     return conv1, 0, 0
 
 
+class _ConvWeights:
+    """bf16 GEMM operands of every trunk conv -- [Cout][KH][KW][Cpad] (fwd) and [Cin][KH][KW][Cout] (dgrad) --
+    written by ONE vcg_weight_prep_multi launch per weight generation (flat.generation: once per optimizer
+    step) instead of one launch per conv and use."""
+
+    def __init__(self, net, flat, stem_cpad):
+        self.flat = flat
+        self.gen = None
+        convs = [m for m in net.modules() if isinstance(m, torch.nn.Conv2d)]
+        dev = convs[0].weight.device
+        self.fwd, self.bwd = {}, {}
+        desc = []
+        for conv in convs:
+            Cout, Cin, KH, KW = conv.weight.shape
+            stem = conv is net.conv1
+            cpad = stem_cpad if stem else Cin
+            wf = torch.empty((Cout, KH, KW, cpad), dtype=torch.bfloat16, device=dev)
+            self.fwd[id(conv)] = wf
+            desc.append([conv.weight.data_ptr(), wf.data_ptr(), Cout, Cin, KH, KW, cpad, 0])
+            if not stem:  # the frames need no gradient
+                wb = torch.empty((Cin, KH, KW, Cout), dtype=torch.bfloat16, device=dev)
+                self.bwd[id(conv)] = wb
+                desc.append([conv.weight.data_ptr(), wb.data_ptr(), Cout, Cin, KH, KW, Cin, 1])
+        self.desc = torch.tensor(desc, dtype=torch.int64).to(dev)
+        self.n = len(desc)
+        self.ptrs = [conv.weight.data_ptr() for conv in convs]
+        self.convs = convs
+
+    def valid_for(self, net, flat):
+        return flat is self.flat and [c.weight.data_ptr() for c in self.convs] == self.ptrs
+
+    def refresh(self):
+        if self.gen != self.flat.generation:
+            ops.weight_prep_multi(self.desc, self.n)
+            self.gen = self.flat.generation
+
+
 class ResNetTrunk:
     def __init__(self, net, dtype):
         self.net = net
         self.dtype = dtype
+        self.wc = None
+        flat = getattr(net, "_vcg_flat", None)
+        if dtype == torch.bfloat16 and flat is not None:
+            wc = getattr(net, "_vcg_convw", None)
+            if wc is None or not wc.valid_for(net, flat):
+                wc = _ConvWeights(net, flat, 8)
+                object.__setattr__(net, "_vcg_convw", wc)
+            wc.refresh()
+            self.wc = wc
 
     # ---------------------------------------------------------------- helpers
     def _wprep(self, conv, Cpad):
+        if self.wc is not None:
+            return self.wc.fwd[id(conv)]
         return ops.weight_prep(conv.weight.data, Cpad, self.dtype)
+
+    def _wprep_t(self, conv, Cin):
+        """[Cin][KH][KW][Cout]: the dgrad operand"""
+        if self.wc is not None:
+            return self.wc.bwd[id(conv)]
+        return ops.weight_prep(conv.weight.data, Cin, self.dtype, transposed=True)
 
     def _conv_bn(self, x, conv, bn, N, H, W, C, tsm_T=0, tsm_fold=0):
         Cout, _, KH, KW, s, p = _conv_shape(conv)
@@ -150,7 +204,7 @@ class ResNetTrunk:
 
     def _dgrad(self, conv, dy, N, H, W):
         Cout, Cin, KH, KW, s, p = _conv_shape(conv)
-        wt = ops.weight_prep(conv.weight.data, Cin, self.dtype, transposed=True)
+        wt = self._wprep_t(conv, Cin)
         return ops.conv_dgrad(dy, wt, N, H, W, Cin, Cout, KH, KW, s, p)
 
     def backward(self, d_emb, saved, hooks=None):
@@ -198,7 +252,7 @@ class ResNetTrunk:
         """Input gradient of `conv` followed by the backward of the BN (+ReLU) that produced its input:
         returns the gradient of that BN's conv output y."""
         Cout, Cin, KH, KW, s, p = _conv_shape(conv)
-        wt = ops.weight_prep(conv.weight.data, Cin, self.dtype, transposed=True)
+        wt = self._wprep_t(conv, Cin)
         sums = torch.empty((2, C), dtype=torch.float32, device=y.device)
         dg, db = self._bn_grads(st)
         g = ops.conv_dgrad_bwd(dy, wt, N, H, W, Cin, Cout, KH, KW, s, p, y=y, mean=st.mean, invstd=st.invstd,
@@ -239,7 +293,7 @@ class ResNetTrunk:
             if cds.stride[0] == 2 and self.dtype == torch.bfloat16:
                 # 1x1 / stride 2: only the even (h, w) inputs receive a gradient, so it is ONE dense GEMM over the
                 # output pixels (no 3/4-zero rows), added by the conv1 dgrad epilogue at those rows (res_stride 2)
-                wt_ds = ops.weight_prep(cds.weight.data, Cin, self.dtype, transposed=True)
+                wt_ds = self._wprep_t(cds, Cin)
                 Mo = dyd.numel() // C3
                 res = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3)
                 res_stride = 2
@@ -250,7 +304,7 @@ class ResNetTrunk:
         # conv1 input gradient + TSM adjoint + residual branch; fused: also the previous block's mask and sums
         conv1 = r["conv1"]
         Cout1, Cin1, KH, KW, s, p = _conv_shape(conv1)
-        wt = ops.weight_prep(conv1.weight.data, Cin1, self.dtype, transposed=True)
+        wt = self._wprep_t(conv1, Cin1)
         kw = dict(tsm_T=T if fold else 0, tsm_fold=fold, res=res, res_stride=res_stride)
         sums3 = sumsd = None
         if prev is not None:
