@@ -110,3 +110,21 @@ def test_clip_json_records(tmp_path):
     p = tmp_path / "clips.json"
     p.write_text(json.dumps(recs))
     assert json.loads(p.read_text()) == recs
+
+
+def test_long_video_host_side_and_metrics():
+    """long_video.py host logic: stride-1 windows, the reference frame-index rule, text encoding, and the
+    cut-point metrics at a window step of 1 s (eval_utils with max_offset = stride / 2)."""
+    import long_video as lv
+    from data import clip_windows as cw
+    from data.synthetic_dataset import HashTokenizer
+    subs = [{"start": 1.0, "text": "a b"}, {"start": 9.5, "text": "c"}]
+    win, idx, ids, mask = lv.window_inputs(30, 8, 1, subs, HashTokenizer(), 16)
+    assert win.shape == (22, 2) and np.array_equal(win[:, 0], np.arange(22))
+    assert np.array_equal(idx, cw.frame_index_table(win, 30))
+    assert ids[0, 0] == 101 and mask[0].sum() == 3  # "[CLS] a b"
+    # labels 1 for windows 3..5 (stride 1, T = 8): begin 3, end 5 + 8 -> round((3 + 13 - 1) / 2) = round(7.5) = 8
+    labels = [0, 0, 0, 1, 1, 1, 0] + [0] * 15
+    m = lv.boundary_metrics(labels, ["0:00 intro", "0:08 two", "0:29 late"], 30, 8, 1)
+    assert m["gt_cut_points"] == [8] and m["pred_cut_points"] == [8]
+    assert m["recall"] == 1.0 and m["precision"] == 1.0 and m["f"] == 1.0

@@ -90,6 +90,19 @@ class TwoStream(NativeRoot, nn.Module):
         object.__setattr__(self, "_vcg_hooks", hooks)
 
     def forward(self, img_clip, text_ids, attention_mask, return_emb=False):
+        # vision: rearrange 'b t c h w -> (b t) c h w' (two_stream.py:183) is a view of a contiguous clip
+        batch_size = img_clip.shape[0]
+        img = img_clip.float().contiguous()
+        img = img.view(batch_size * img.shape[1], *img.shape[2:])
+        return self._forward(img, batch_size, text_ids, attention_mask, return_emb, staged=False)
+
+    def forward_staged(self, frames, text_ids, attention_mask, return_emb=False):
+        """Frame-ingest entry: the window frames were gathered and normalised on the GPU
+        straight into the stem's NHWC layout, frames [B*T, H, W, 8] in the compute dtype
+        (ops.window_frames_u8 over a decoded u8 video); otherwise identical to forward()."""
+        return self._forward(frames, text_ids.shape[0], text_ids, attention_mask, return_emb, staged=True)
+
+    def _forward(self, img, batch_size, text_ids, attention_mask, return_emb, staged):
         from vcg_hip.bert import BertEncoderEngine
         from vcg_hip.functions import BertFn, HeadFn, TrunkFn
         from vcg_hip.head import HeadEngine
@@ -98,7 +111,7 @@ class TwoStream(NativeRoot, nn.Module):
         f = self.native_flat()
         dt = self.compute_dtype()
         need_grad = torch.is_grad_enabled()
-        dev = img_clip.device
+        dev = img.device
         anchor = self._anchor(dev)
         hooks = self._vcg_hooks
         if self.training:
@@ -122,11 +135,9 @@ class TwoStream(NativeRoot, nn.Module):
                 t.record_stream(side)
             with torch.cuda.stream(side):
                 lang_emb, _ = BertFn.apply(text_ids, attention_mask, anchor, bert, need_grad, new_seed(), hooks, main)
-        # vision: rearrange 'b t c h w -> (b t) c h w' (two_stream.py:183) is a view of a contiguous clip
-        batch_size = img_clip.shape[0]
-        img = img_clip.float().contiguous()
-        img = img.view(batch_size * img.shape[1], *img.shape[2:])
-        vision_emb = TrunkFn.apply(img, anchor, ResNetTrunk(self.vision_model, dt), need_grad, hooks)
+        trunk = ResNetTrunk(self.vision_model, dt)
+        trunk.staged = staged
+        vision_emb = TrunkFn.apply(img, anchor, trunk, need_grad, hooks)
         if side is not None:
             main.wait_stream(side)
             lang_emb.record_stream(main)

@@ -82,6 +82,8 @@ class _ConvWeights:
 
 
 class ResNetTrunk:
+    staged = False  # forward() input is already the stem's NHWC layout [N, H, W, Cpad] (ops.window_frames_u8)
+
     def __init__(self, net, dtype):
         self.net = net
         self.dtype = dtype
@@ -130,11 +132,19 @@ class ResNetTrunk:
 
     # ---------------------------------------------------------------- forward
     def forward(self, x, need_grad):
-        """x: [N, 3, H, W] fp32 frames ((b t) order). Returns (emb [N, 2048] fp32, saved)."""
+        """x: [N, 3, H, W] fp32 frames ((b t) order), or (staged) the stem's NHWC input [N, H, W, Cpad] in the
+        compute dtype. Returns (emb [N, 2048] fp32, saved)."""
         net, dt = self.net, self.dtype
-        N, C0, H, W = x.shape
-        cpad = 8 if dt == torch.bfloat16 else 4
-        xs = ops.frames_to_nhwc(x.contiguous(), N, C0, H, W, cpad, dt)
+        if self.staged:
+            N, H, W, cpad = x.shape
+            if x.dtype != dt or cpad < 3 or not x.is_contiguous():
+                raise RuntimeError(f"staged frames must be contiguous NHWC [N,H,W,>=3] {dt}, "
+                                   f"got {x.dtype} {tuple(x.shape)}")
+            xs = x
+        else:
+            N, C0, H, W = x.shape
+            cpad = 8 if dt == torch.bfloat16 else 4
+            xs = ops.frames_to_nhwc(x.contiguous(), N, C0, H, W, cpad, dt)
         y0, b0, H1, W1 = self._conv_bn(xs, net.conv1, net.bn1, N, H, W, cpad)
         a0 = ops.bn_apply(y0, b0.scale, b0.shift, 64, relu=True)
         mp, idx = ops.maxpool_fwd(a0, N, H1, W1, 64)
