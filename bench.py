@@ -172,9 +172,17 @@ def main():
         return long_video_bench(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # one process per GPU; VCG_DIST_BACKEND=gloo + more ranks than GPUs only for rehearsing the DDP path on a
+    # one-GPU box (ranks then share devices round-robin); the benchmark itself is RCCL ("nccl") over xGMI
+    backend = os.environ.get("VCG_DIST_BACKEND", "nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -9,8 +9,17 @@ exchange of layer i overlaps the backward of layer i-1. Reductions are SUM; the 
 is folded into the fused optimizer (FusedAdamW.grad_scale) so no extra pass over the grads runs.
 Skipping reductions on accumulation micro-steps (no_sync semantics) is `reducer.enabled = False`.
 """
+import os
+
 import torch
 import torch.distributed as dist
+
+
+_DEBUG = os.environ.get("VCG_DDP_DEBUG", "")
+
+
+def _sid(stream):
+    return None if stream is None else stream.cuda_stream
 
 
 class GradAllReducer:
@@ -36,7 +45,13 @@ class GradAllReducer:
         hi = max(f.offset_of(p) + p.numel() for p in params)
         hi = (hi + 255) // 256 * 256
         stream = torch.cuda.current_stream() if torch.cuda.is_available() and f.grad.is_cuda else None
-        if stream != self._stream:  # the encoders' backwards run on two streams: a bucket never spans both
+        if _DEBUG:
+            print(f"[ddp] hook stream={stream.cuda_stream if stream is not None else None} [{lo},{hi}) "
+                  f"open={self._lo},{self._hi} on {self._stream.cuda_stream if self._stream is not None else None}",
+                  flush=True)
+        # the encoders' backwards run on two streams: a bucket never spans both (compare the raw handles:
+        # torch.cuda.Stream's != against None is not reliable)
+        if _sid(stream) != _sid(self._stream):
             self._flush()
             self._stream = stream
         if self._lo is not None and (hi == self._lo or lo == self._hi):
@@ -51,7 +66,13 @@ class GradAllReducer:
         if self._lo is None:
             return
         buf = self.flat.grad[self._lo:min(self._hi, self.flat.total)]
-        if self._stream is not None and self._stream != torch.cuda.current_stream():
+        if _DEBUG:
+            print(f"[ddp] flush [{self._lo},{self._hi}) bucket stream "
+                  f"{self._stream.cuda_stream if self._stream is not None else None} current "
+                  f"{torch.cuda.current_stream().cuda_stream}", flush=True)
+            if _DEBUG == "sync":
+                (self._stream or torch.cuda.current_stream()).synchronize()
+        if self._stream is not None and _sid(self._stream) != _sid(torch.cuda.current_stream()):
             with torch.cuda.stream(self._stream):  # the collective waits on the stream that made the bucket
                 self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         else:
