@@ -5,7 +5,9 @@
 namespace vcg {
 
 enum { OP_DENSE_K = 0, OP_IM2COL = 1, OP_DGRAD = 2, OP_DENSE_MN = 3, OP_IM2COL_T = 4 };
-enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3 };
+// EPI_BWD_AFF: EPI_BWD without residual / mask bits / second BN / TSM (the conv2 / conv3 input gradients: mask
+// recomputed from y, BN sums): fewer live registers, so the 64-column kernel fits 3 workgroups per CU
+enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 4 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
 
 template <typename T> struct Cfg;
@@ -282,6 +284,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
 
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
 int fast_grid_rows(int M, int N, int z, int epi);
+int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an EPI_BWD launch of run_fast_gemm
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
                            float* dgamma, float* dbeta, int accumulate, hipStream_t s);  // grid rows (slots of EPI_BWD partials) of a fast-kernel launch
 int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s);

@@ -677,7 +677,7 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
         }
         int rc = run_fast_gemm(q, OP_DGRAD, EPI_BWD, 1, stream);
         if (rc) return rc;
-        slots += fast_grid_rows(q.M, q.N, 1, EPI_BWD);
+        slots += fast_bwd_slots(q);
       }
     if (e.nred > 0) {
       int rc = bn_bwd_finalize_launch(ws, slots, C, (long long)e.nred * C, C, sum_g, sum_gx, dgamma, dbeta, 1, stream);
@@ -697,7 +697,7 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   int rc = run_fast_gemm(p, dense ? OP_DENSE_K : OP_DGRAD, EPI_BWD, 1, stream);
   if (rc) return rc;
   if (e.nred > 0) {
-    const int slots = fast_grid_rows(p.M, p.N, 1, EPI_BWD);
+    const int slots = fast_bwd_slots(p);
     rc = bn_bwd_finalize_launch(ws, slots, C, (long long)e.nred * C, C, sum_g, sum_gx, dgamma, dbeta, 1, stream);
     if (rc) return rc;
     if (e.nred > 2) {

@@ -321,7 +321,7 @@ __device__ __forceinline__ void unpack8(const uint4& u, float (&v)[8]) {
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool LIGHT>
 __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t* stB, const GemmParams& p,
                                                 bf16_t* Cout, int m0, int n0, const float* cpar, float (&s1)[8],
                                                 float (&s2)[8], float (&s3)[8]) {
@@ -357,10 +357,11 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   int shift = 0;  // TSM adjoint: this column group's values move one frame later (+1) / earlier (-1)
-  if (e.tsm_T > 0) shift = n < e.tsm_fold ? 1 : (n < 2 * e.tsm_fold ? -1 : 0);
-  const bf16_t* res = reinterpret_cast<const bf16_t*>(e.res);
+  if (!LIGHT && e.tsm_T > 0) shift = n < e.tsm_fold ? 1 : (n < 2 * e.tsm_fold ? -1 : 0);
+  const bf16_t* res = LIGHT ? nullptr : reinterpret_cast<const bf16_t*>(e.res);
   const bf16_t* yp = reinterpret_cast<const bf16_t*>(e.y);
-  const bf16_t* y2p = reinterpret_cast<const bf16_t*>(e.y2);
+  const bf16_t* y2p = LIGHT ? nullptr : reinterpret_cast<const bf16_t*>(e.y2);
+  const uint8_t* bitsp = LIGHT ? nullptr : e.bits;
 #pragma unroll
   for (int k0 = 0; k0 < KC; k0 += KB) {
     long long off[KB];
@@ -391,7 +392,7 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
         if (res) {
           long long roff = off[kk];
           bool rok = true;
-          if (e.res_s > 1) {  // compact residual of a 1x1 / stride-2 conv: only even (h, w) rows carry one
+          if (!LIGHT && e.res_s > 1) {  // compact residual of a 1x1 / stride-2 conv: only even (h, w) rows carry one
             const uint32_t f = fdiv((uint32_t)dst, e.fd_hw), r = (uint32_t)dst - f * (uint32_t)e.hw;
             const uint32_t h = fdiv(r, e.fd_w), w = r - h * e.fd_w.d;
             rok = ((h | w) & 1u) == 0;
@@ -399,7 +400,7 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
           }
           rv[kk] = rok ? *reinterpret_cast<const uint4*>(res + roff) : make_uint4(0u, 0u, 0u, 0u);
         }
-        if (e.bits) bv[kk] = e.bits[off[kk] >> 3];
+        if (bitsp) bv[kk] = bitsp[off[kk] >> 3];
         if (yp) yv[kk] = *reinterpret_cast<const uint4*>(yp + off[kk]);
         if (y2p) y2v[kk] = *reinterpret_cast<const uint4*>(y2p + off[kk]);
       }
@@ -419,7 +420,7 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] += r[i];
       }
-      if (e.bits) {
+      if (bitsp) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = ((bv[kk] >> i) & 1u) ? v[i] : 0.f;
       }
@@ -578,7 +579,8 @@ __device__ __forceinline__ void stats_finish(const GemmParams& p, float* scratch
 }
 
 template <int BM, int BN, int AM, int EPI, bool RES>
-__global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) void igemm_fast_kernel(GemmParams p) {
+__global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(EPI == EPI_BWD_AFF && BN == 64 ? 3 : 2)))
+void igemm_fast_kernel(GemmParams p) {
   // Persistent-style grid: workgroup (bx, by) owns N-tile bx and M-tiles by, by + gy, by + 2gy, ...;
   // the (m-tile, k-tile) steps form one software pipeline, so the next tiles' loads are in flight while
   // a tile finishes its MFMAs and its epilogue. Workgroups are dealt round-robin to the 8 XCDs by
@@ -598,7 +600,8 @@ __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) voi
   constexpr int STAGES = BM == 256 ? 3 : 2;
   constexpr int AE = BM * FBK, BE = BN * FBK;  // elements per stage
   constexpr int NLD = BM / (8 * NW) + BN / (8 * NW);  // LDS-DMA instructions per thread per step
-  constexpr int CPAR = EPI == EPI_BWD ? 6 * BN : 0;  // EPI_BWD per-column parameters
+  constexpr bool BWD = EPI == EPI_BWD || EPI == EPI_BWD_AFF;
+  constexpr int CPAR = BWD ? 6 * BN : 0;  // EPI_BWD per-column parameters
   constexpr int RED = 2 * WM * BN + WM + 4;
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * (AE + BE) * 2 + (RED + CPAR) * 4];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
@@ -633,7 +636,7 @@ __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) voi
   const int my_tiles = by < mtiles ? (mtiles - 1 - by) / gy + 1 : 0;
   const int ntiles = (p.K + FBK - 1) / FBK;
   const int steps = my_tiles * ntiles;
-  if constexpr (EPI == EPI_BWD) {
+  if constexpr (BWD) {
     if (steps == 0) {  // no rows: an all-zero partial slot
       if (p.bwd.nred > 0 && tid < BN && n0 + tid < p.N)
         for (int r = 0; r < p.bwd.nred; ++r) p.bwd.part[((long long)by * p.bwd.nred + r) * p.N + n0 + tid] = 0.f;
@@ -728,7 +731,7 @@ __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) voi
       bf16_t* stB = BM == 256 ? stA + 64 * BN : Bs + cur * BE;
       // output tiles go through the LDS stage for full-row 16-B stores (VCG_STAGE_KT can limit it)
       const bool staged = ntiles <= p.stage_kt;
-      if constexpr (EPI == EPI_BWD) {
+      if constexpr (BWD) {
 #pragma unroll
         for (int h = 0; h < BM / 128; ++h) {
           if ((wm >> 1) == h) {
@@ -740,7 +743,7 @@ __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) voi
                 stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
               }
           }
-          stage_flush_bwd<BM, BN>(stA, stB, p, Cout, mt * BM + 128 * h, n0, cpar, b1, b2, b3);
+          stage_flush_bwd<BM, BN, EPI == EPI_BWD_AFF>(stA, stB, p, Cout, mt * BM + 128 * h, n0, cpar, b1, b2, b3);
         }
       } else if constexpr (EPI == EPI_STATS) {  // conv outputs: no bias / activation, alpha = 1
 #pragma unroll
@@ -773,14 +776,14 @@ __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(2))) voi
   }
   if constexpr (EPI == EPI_STATS)  // the stats buffer is laid out for 128-row tiles (vcg_conv_stats_tiles)
     stats_finish<BM, BN>(p, reinterpret_cast<float*>(smem), scnt, b1, b2, b3, n0, by, bx, gy, (p.M + 127) / 128);
-  if constexpr (EPI == EPI_BWD) {
+  if constexpr (BWD) {
     if (p.bwd.nred > 0) bwd_finish<BM, BN>(p, reinterpret_cast<float*>(smem), cpar + 4 * BN, b1, b2, b3, n0, by);
   }
 }
 
 // One resident round of workgroups (LDS allows 2 per CU at BM = 128 / BN = 128, 3 at BN = 64, 1 at BM = 256);
 // each walks ceil(mtiles / gy) M-tiles. gy is a multiple of 8 whenever possible (XCD-aware decode).
-// (EPI_BWD's BN = 64 kernel needs > 170 VGPRs: 2 workgroups per CU there too)
+// (EPI_BWD's BN = 64 kernel needs > 170 VGPRs: 2 workgroups per CU there too; EPI_BWD_AFF's fits 3)
 static int grid_rows(int M, int N, int z, int BM, int BN, int epi) {
   const int nx = (N + BN - 1) / BN, mtiles = (M + BM - 1) / BM;
   const int resident = (BM == 256 ? 1 : (BN == 128 || epi == EPI_BWD ? 2 : 3)) * 256;
@@ -814,6 +817,15 @@ int fast_grid_rows(int M, int N, int z, int epi) {
   return grid_rows(M, N, z, fast_bm(M, N, z, false), fast_bn_cols(N), epi);
 }
 
+static bool bwd_light(const GemmParams& p) {
+  const BwdEpi& e = p.bwd;
+  return !e.res && !e.bits && !e.y2 && e.tsm_T == 0;
+}
+
+int fast_bwd_slots(const GemmParams& p) {
+  return fast_grid_rows(p.M, p.N, 1, bwd_light(p) ? EPI_BWD_AFF : EPI_BWD);
+}
+
 template <int BM, int BN, int AM, int EPI, bool RES>
 static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   const int nx = (p.N + BN - 1) / BN;
@@ -845,6 +857,11 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   if (amode == OP_IM2COL && p.a.C < FBK) amode = OP_IM2COL_SMALLC;
   if (amode == OP_IM2COL_TSM && p.a.C < FBK) return -1;  // (dispatcher keeps these off the fast path)
   if (amode == OP_DGRAD && p.a.C < FBK) return -1;
+  if (epi == EPI_BWD && bwd_light(p)) {
+    if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_BWD_AFF>(p, z, s);
+    if (amode == OP_DENSE_K) return fast_bn<OP_DENSE_K, EPI_BWD_AFF>(p, z, s);
+    return -1;
+  }
   if (epi == EPI_BWD) {
     if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_BWD>(p, z, s);
     if (amode == OP_DENSE_K) return fast_bn<OP_DENSE_K, EPI_BWD>(p, z, s);
