@@ -573,7 +573,7 @@ __device__ __forceinline__ void stats_finish(const GemmParams& p, float* scratch
     float rows = 0.f;  // threads 0..CPR-1 cover every row of the workgroup once (one chunk column each)
     for (int t = 0; t < NTH; t += CPR) rows += scratch[2 * NTH * 8 + t];
     float2* cntrow = reinterpret_cast<float2*>(p.stats) + (long long)p.N * mslots;
-    cntrow[by] = make_float2(rows, 0.f);
+    cntrow[by] = make_float2(rows, by == 0 ? (float)gy : 0.f);  // slot 0 also tells bn_finalize: gy slots used
     for (int t = by + gy; t < mslots; t += gy) cntrow[t] = make_float2(0.f, 0.f);
   }
 }

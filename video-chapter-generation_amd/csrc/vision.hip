@@ -22,7 +22,9 @@ __global__ void bn_finalize_kernel(const float2* __restrict__ stats, int mtiles,
   __shared__ double sn[256], sm[256], s2[256];
   double n = 0, mean = 0, m2 = 0;
   const float2* cnt = stats + (long long)gridDim.x * mtiles;  // count row (slot row counts; 0 = empty)
-  for (int t = threadIdx.x; t < mtiles; t += blockDim.x) {
+  // the fast conv kernel fills only its gy leading slots and says so in the count row's slot 0 (.y = gy)
+  const int used = cnt[0].y > 0.f ? min(mtiles, (int)cnt[0].y) : mtiles;
+  for (int t = threadIdx.x; t < used; t += blockDim.x) {
     const float2 st = stats[(long long)c * mtiles + t];
     const double nb = (double)cnt[t].x;
     if (nb <= 0.0) continue;
