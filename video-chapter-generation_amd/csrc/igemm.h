@@ -287,7 +287,7 @@ int fast_grid_rows(int M, int N, int z, int epi);
 int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an EPI_BWD launch of run_fast_gemm
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
                            float* dgamma, float* dbeta, int accumulate, hipStream_t s);  // grid rows (slots of EPI_BWD partials) of a fast-kernel launch
-int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s);
+int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b = false);
 int wgrad_fast_tile_m(int M);
 int wgrad_fast_tile_n(int N);
 

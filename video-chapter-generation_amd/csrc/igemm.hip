@@ -845,6 +845,29 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
   p.ws = ws;
   p.alpha = 1.f;
   int rc;
+  // bf16 dW = A^T B with both operands row-major over K (the Linear weight gradients): the LDS-DMA wgrad kernel
+  // with a dense B operand; k per split in its 64-row steps (never more splits than the workspace query allows)
+  const long long a_ext = ((long long)(K - 1) * lda + M) * 2, b_ext = ((long long)(K - 1) * ldb + N) * 2;
+  if (dtype == VCG_BF16 && transA && transB && fast_gemm_enabled() && !getenv_flag("VCG_NO_FAST_DW") &&
+      M % 8 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && a_ext < 0xFFFFFF00LL && b_ext < 0xFFFFFF00LL) {
+    p.a.bytes = a_ext;  // [K][lda] operands: the LDS-DMA loaders' buffer range
+    p.b.bytes = b_ext;
+    int fk = (K + splits - 1) / splits;
+    fk = (fk + 63) / 64 * 64;
+    const int fsplits = (K + fk - 1) / fk;
+    p.k_per_split = fk;
+    if (FILE* f = gemm_log()) {
+      fprintf(f, "a=3 b=3 epi=2 M=%d N=%d K=%d z=%d fast=2 conv=0x0/0 C=0\n", M, N, K, fsplits);
+      fflush(f);
+    }
+    rc = run_fast_wgrad(p, fsplits, stream, true);
+    if (rc) return rc;
+    const long long MN = (long long)M * N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, fsplits,
+                       MN, N, out, accumulate, 0, 1, 1, 1, 1, 1.f);
+    VCG_LAUNCH_CHECK();
+    return VCG_OK;
+  }
 #define VCG_SK_CASE(TT)                                                                             \
   if (!transA && !transB) rc = run_gemm<TT, OP_DENSE_K, OP_DENSE_K>(p, EPI_SPLITK, splits, stream);       \
   else if (!transA && transB) rc = run_gemm<TT, OP_DENSE_K, OP_DENSE_MN>(p, EPI_SPLITK, splits, stream);  \

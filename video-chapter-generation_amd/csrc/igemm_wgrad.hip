@@ -153,11 +153,13 @@ __device__ __forceinline__ void lgkm0() {
 
 __device__ __forceinline__ constexpr int wvm(int n) { return (n & 0xF) | (0x7 << 4) | (0xF << 8) | (((n >> 4) & 3) << 14); }
 
-template <int BM, int BN>
+// BG: B is the im2col gather of x (conv wgrad); !BG: B is a dense [K][ld] operand (the Linear weight gradients
+// dW = dY^T X of BERT / the head: a 1x1 "conv" whose pixels are the token rows, any column count)
+template <int BM, int BN, bool BG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_fast_kernel(GemmParams p) {
   constexpr int MT = BM / 32, NT = BN / 32;
   constexpr int AE = WBK * BM, BE = WBK * BN;
-  constexpr int NLD = MNLoader<BM, false>::NI + MNLoader<BN, true>::NI;
+  constexpr int NLD = MNLoader<BM, false>::NI + MNLoader<BN, BG>::NI;
   __shared__ __attribute__((aligned(1024))) bf16_t smem[2 * (AE + BE)];
   bf16_t* As = smem;
   bf16_t* Bs = smem + 2 * AE;
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   const int ntiles = (ke - kb + WBK - 1) / WBK;
 
   MNLoader<BM, false> la;
-  MNLoader<BN, true> lb;
+  MNLoader<BN, BG> lb;
   la.init(p.a, m0, p.M, kb, wave, lane);
   lb.init(p.b, n0, p.N, kb, wave, lane);
 
@@ -246,14 +248,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   }
 }
 
-template <int BM, int BN> int launch_wgrad(const GemmParams& p0, int splits, hipStream_t s) {
+template <int BM, int BN, bool BG> int launch_wgrad(const GemmParams& p0, int splits, hipStream_t s) {
   GemmParams p = p0;
   p.batch_inner = splits;
   const long long per = (long long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   const long long wgs = (splits + 7) / 8 * 8 * per;
   VCG_REQUIRE(wgs < (1LL << 31), "wgrad grid too large");
   const int tk = timing_begin(s);
-  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN>), dim3((unsigned)wgs), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, BG>), dim3((unsigned)wgs), dim3(256), 0, s, p);
   timing_end(tk, s, TIMING_WGRAD, 2.0 * p.M * p.N * (double)p.K);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -264,13 +266,20 @@ template <int BM, int BN> int launch_wgrad(const GemmParams& p0, int splits, hip
 int wgrad_fast_tile_m(int M) { return M >= 128 ? 128 : 64; }
 int wgrad_fast_tile_n(int N) { return N > 64 ? 128 : 64; }
 
-// p.a: dy as a dense [K][M] operand (ld = M), p.b: x with IM2COL_T geometry; p.ws slabs.
-int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s) {
+// p.a: dy as a dense [K][M] operand (ld = M), p.b: x with IM2COL_T geometry (dense_b: a dense [K][ld] operand);
+// p.ws slabs.
+int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b) {
   const int bm = wgrad_fast_tile_m(p.M), bn = wgrad_fast_tile_n(p.N);
-  if (bm == 128 && bn == 128) return launch_wgrad<128, 128>(p, splits, s);
-  if (bm == 128) return launch_wgrad<128, 64>(p, splits, s);
-  if (bn == 128) return launch_wgrad<64, 128>(p, splits, s);
-  return launch_wgrad<64, 64>(p, splits, s);
+  if (dense_b) {
+    if (bm == 128 && bn == 128) return launch_wgrad<128, 128, false>(p, splits, s);
+    if (bm == 128) return launch_wgrad<128, 64, false>(p, splits, s);
+    if (bn == 128) return launch_wgrad<64, 128, false>(p, splits, s);
+    return launch_wgrad<64, 64, false>(p, splits, s);
+  }
+  if (bm == 128 && bn == 128) return launch_wgrad<128, 128, true>(p, splits, s);
+  if (bm == 128) return launch_wgrad<128, 64, true>(p, splits, s);
+  if (bn == 128) return launch_wgrad<64, 128, true>(p, splits, s);
+  return launch_wgrad<64, 64, true>(p, splits, s);
 }
 
 }  // namespace vcg
