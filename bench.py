@@ -4,10 +4,13 @@
 MI355X, one process per GPU (torchrun), RCCL all-reduce overlapped with the backward.
 
 Prints ONE JSON line (rank 0).
-- `roofline`: the dominant kernel (igemm_fast_kernel, the bf16 conv/linear GEMM engine): algorithmic
-  FLOPs (2*M*N*K per launch) over its launch durations, timed live with HIP events on the launch
-  stream during one extra instrumented step after the timed region (vcg_timing_*), against the bf16
-  dense MFMA peak; `traffic` = its HBM bytes per launch from the committed PMC pass, if any.
+- `roofline`: the dominant kernel (igemm_fast_kernel, the bf16 conv/linear GEMM engine), timed live with
+  HIP events on the launch stream during one extra instrumented step after the timed region
+  (vcg_timing_*). Each launch records its algorithmic FLOPs (2*M*N*K) and bytes (operands read once, a
+  gathered A as its source tensor, outputs and fused-epilogue operands once); the bound is the one that
+  dominates over the step (bytes / HBM peak vs FLOPs / MFMA peak), `achieved` the matching rate, and
+  `per_launch_roofline.frac` = sum of per-launch ideal times / measured. `traffic` = its HBM bytes per
+  launch from the committed PMC pass (profiles/traffic_*.json), if any.
 - `roofline_step`: the whole step priced against HBM with SURVEY Appendix A's fused-minimum bytes.
 - `cpu_baseline`: the CPU oracle (oracle/, test infrastructure) on a bounded sample on this host.
 """
@@ -77,6 +80,15 @@ def window_costs(T, HW, L, B, s_bytes, train):
         nbytes = act + frames + weights
         nflops = rf * T + bf
     return nbytes, nflops
+
+
+def _per_launch(r):
+    ms, ideal, nbytes, flops = r
+    if ms <= 0:
+        return None
+    return {"frac": round(ideal / ms, 4), "ideal_ms": round(ideal, 3), "measured_ms": round(ms, 3),
+            "algorithmic_gb": round(nbytes / 1e9, 3), "hbm_gbs": round(nbytes / (ms / 1e3) / 1e9, 1),
+            "tflops": round(flops / (ms / 1e3) / 1e12, 1)}
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -250,6 +262,8 @@ def main():
     step()
     torch.cuda.synchronize()
     k_ms, k_n, k_fl = ops.timing_query(ops.TIMING_FAST_GEMM)
+    peak_tf = MFMA_PEAK_TFLOPS[args.precision]
+    rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (ops.TIMING_FAST_GEMM, ops.TIMING_WGRAD)}
     ops.timing_enable(False)
     model.overlap_streams = overlap
     kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
@@ -274,13 +288,28 @@ def main():
             kern_traffic = tj.get("igemm_fast_kernel", {}).get("hbm_bytes_per_launch")
         dom = None
         if kern["launches"]:
+            # the dominant kernel's bound from its aggregate arithmetic intensity over the step: algorithmic
+            # bytes / HBM peak vs algorithmic FLOPs / MFMA peak (ridge ~312 flop/B in bf16)
+            r_ms, r_ideal, r_bytes, r_flops = rl[ops.TIMING_FAST_GEMM]
             k_tf = kern["flops"] / (kern["ms"] / 1e3) / 1e12
-            dom = {"kernel": "igemm_fast_kernel", "bound": "mfma", "achieved": round(k_tf, 2),
-                   "peak": MFMA_PEAK_TFLOPS[args.precision], "unit": "TFLOP/s",
-                   "frac": round(k_tf / MFMA_PEAK_TFLOPS[args.precision], 4), "traffic": kern_traffic,
+            k_gbs = r_bytes / (kern["ms"] / 1e3) / 1e9
+            hbm_bound = r_bytes / (HBM_PEAK_GBS * 1e9) >= r_flops / (peak_tf * 1e12)
+            dom = {"kernel": "igemm_fast_kernel", "bound": "hbm" if hbm_bound else "mfma",
+                   "achieved": round(k_gbs if hbm_bound else k_tf, 2),
+                   "peak": HBM_PEAK_GBS if hbm_bound else peak_tf, "unit": "GB/s" if hbm_bound else "TFLOP/s",
+                   "frac": round((k_gbs / HBM_PEAK_GBS) if hbm_bound else (k_tf / peak_tf), 4),
+                   "traffic": kern_traffic,
+                   "algorithmic_bytes_per_launch": round(r_bytes / kern["launches"]),
+                   "arithmetic_intensity_flop_per_byte": round(r_flops / max(r_bytes, 1.0), 1),
+                   "mfma_view": {"achieved": round(k_tf, 2), "peak": peak_tf, "unit": "TFLOP/s",
+                                 "frac": round(k_tf / peak_tf, 4)},
                    "launches_per_step": kern["launches"], "avg_launch_us": round(kern["ms"] * 1e3 / kern["launches"], 2),
                    "gflop_per_launch": round(kern["flops"] / kern["launches"] / 1e9, 3),
                    "share_of_step": round(kern["ms"] / ms, 4),
+                   # the same launches against their own roofline: ideal = sum of max(flops / MFMA peak,
+                   # algorithmic bytes / HBM peak) per launch
+                   "per_launch_roofline": _per_launch(rl[ops.TIMING_FAST_GEMM]),
+                   "wgrad_fast_kernel": _per_launch(rl[ops.TIMING_WGRAD]),
                    "timing": "HIP events around each launch on its stream, one instrumented step (no BERT side "
                              "stream in that step: unshared launch durations)"}
         out = {

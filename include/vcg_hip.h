@@ -38,6 +38,9 @@ VCG_API int vcg_sync(hipStream_t stream);
    id (0 igemm_fast_kernel, 1 wgrad_fast_kernel). Enabling (or disabling) clears the records. */
 VCG_API int vcg_timing_enable(int on);
 VCG_API int vcg_timing_query(int kernel_id, double* ms_total, long long* launches, double* flops);
+/* per-launch roofline of the recorded launches: ideal_ms = sum over launches of max(flops / peak_tflops,
+   algorithmic bytes / peak_gbs) (bytes: operands read once, outputs written once), with their total time */
+VCG_API int vcg_timing_roofline(int kernel_id, double peak_tflops, double peak_gbs, double* ms_total, double* ideal_ms, double* bytes, double* flops);
 
 /* ---- MFMA implicit-GEMM engine (igemm.hip) ---------------------------------------------- */
 /* torchvision conv2d inside Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15,68-77), with

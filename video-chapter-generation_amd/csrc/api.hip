@@ -12,7 +12,7 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 struct TimingRec {
   int id;
   hipEvent_t a, b;
-  double flops;
+  double flops, bytes;  // algorithmic work of the launch (bytes: every operand read once, outputs written once)
 };
 static std::vector<TimingRec> g_timing;
 static bool g_timing_on = false;
@@ -25,10 +25,11 @@ int timing_begin(hipStream_t s) {
   g_timing.push_back(r);
   return (int)g_timing.size() - 1;
 }
-void timing_end(int idx, hipStream_t s, int id, double flops) {
+void timing_end(int idx, hipStream_t s, int id, double flops, double bytes) {
   if (idx < 0) return;
   g_timing[idx].id = id;
   g_timing[idx].flops = flops;
+  g_timing[idx].bytes = bytes;
   hipEventRecord(g_timing[idx].b, s);
 }
 static void timing_clear() {
@@ -60,6 +61,29 @@ VCG_API int vcg_timing_query(int kernel_id, double* ms_total, long long* launche
   }
   *ms_total = ms;
   *launches = n;
+  *flops = fl;
+  return VCG_OK;
+}
+
+// Per-launch roofline: ideal = max(flops / peak_flops, bytes / peak_bytes_per_s) of each launch, summed.
+VCG_API int vcg_timing_roofline(int kernel_id, double peak_tflops, double peak_gbs, double* ms_total,
+                                double* ideal_ms, double* bytes, double* flops) {
+  VCG_REQUIRE(peak_tflops > 0.0 && peak_gbs > 0.0, "peaks must be positive");
+  double ms = 0.0, ideal = 0.0, by = 0.0, fl = 0.0;
+  for (auto& r : vcg::g_timing) {
+    if (r.id != kernel_id) continue;
+    VCG_CHECK_HIP(hipEventSynchronize(r.b));
+    float t = 0.f;
+    VCG_CHECK_HIP(hipEventElapsedTime(&t, r.a, r.b));
+    ms += t;
+    const double tf = r.flops / (peak_tflops * 1e12), tb = r.bytes / (peak_gbs * 1e9);
+    ideal += 1e3 * (tf > tb ? tf : tb);
+    by += r.bytes;
+    fl += r.flops;
+  }
+  *ms_total = ms;
+  *ideal_ms = ideal;
+  *bytes = by;
   *flops = fl;
   return VCG_OK;
 }

@@ -19,7 +19,7 @@ namespace vcg {
 // kernel ids of vcg_timing_query
 enum { TIMING_FAST_GEMM = 0, TIMING_WGRAD = 1, TIMING_GENERIC_GEMM = 2 };
 int timing_begin(hipStream_t s);
-void timing_end(int idx, hipStream_t s, int id, double flops);
+void timing_end(int idx, hipStream_t s, int id, double flops, double bytes);
 }  // namespace vcg
 
 enum vcg_dtype { VCG_F32 = 0, VCG_BF16 = 1 };

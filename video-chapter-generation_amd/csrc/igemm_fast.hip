@@ -826,6 +826,25 @@ int fast_bwd_slots(const GemmParams& p) {
   return fast_grid_rows(p.M, p.N, 1, bwd_light(p) ? EPI_BWD_AFF : EPI_BWD);
 }
 
+// Algorithmic HBM bytes of one launch (bench.py's per-launch roofline): every operand read once (a gathered A:
+// the source tensor once), the output written once, the epilogue's extra operands read once (bf16).
+template <int AM, int EPI, bool RES>
+static double algorithmic_bytes(const GemmParams& p, int z) {
+  const double mn = (double)p.M * p.N * z;
+  double b = (AM == OP_DENSE_K ? 2.0 * p.M * (double)p.K * z : (double)p.a.bytes) + 2.0 * p.N * (double)p.K * z;
+  b += 2.0 * mn;
+  if (RES) b += 2.0 * mn;
+  if (p.aux) b += 2.0 * mn;
+  if constexpr (EPI == EPI_BWD || EPI == EPI_BWD_AFF) {
+    const BwdEpi& e = p.bwd;
+    if (e.res) b += 2.0 * mn / (e.res_s > 1 ? 4.0 : 1.0);
+    if (e.y) b += 2.0 * mn;
+    if (e.y2) b += 2.0 * mn;
+    if (e.bits) b += mn / 8.0;
+  }
+  return b;
+}
+
 template <int BM, int BN, int AM, int EPI, bool RES>
 static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   const int nx = (p.N + BN - 1) / BN;
@@ -833,7 +852,7 @@ static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   dim3 grid(nx * gy, 1, z);
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((igemm_fast_kernel<BM, BN, AM, EPI, RES>), grid, dim3(BM * 2), 0, s, p);
-  timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K * z);
+  timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K * z, algorithmic_bytes<AM, EPI, RES>(p, z));
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

@@ -256,7 +256,9 @@ template <int BM, int BN, bool BG> int launch_wgrad(const GemmParams& p0, int sp
   VCG_REQUIRE(wgs < (1LL << 31), "wgrad grid too large");
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, BG>), dim3((unsigned)wgs), dim3(256), 0, s, p);
-  timing_end(tk, s, TIMING_WGRAD, 2.0 * p.M * p.N * (double)p.K);
+  // algorithmic bytes: dy and x read once, the fp32 weight gradient written once (the split slabs are not)
+  timing_end(tk, s, TIMING_WGRAD, 2.0 * p.M * p.N * (double)p.K,
+             (double)p.a.bytes + (double)p.b.bytes + 4.0 * p.M * (double)p.N);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

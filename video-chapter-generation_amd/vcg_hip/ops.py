@@ -72,6 +72,16 @@ def timing_query(kernel_id):
     return ms.value, n.value, fl.value
 
 
+def timing_roofline(kernel_id, peak_tflops, peak_gbs):
+    """(total ms, ideal ms, algorithmic bytes, flops) of the recorded launches of one kernel; ideal = sum of
+    max(flops / peak, bytes / HBM peak) per launch."""
+    import ctypes
+    ms, ideal, nb, fl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    _lib.call("vcg_timing_roofline", int(kernel_id), float(peak_tflops), float(peak_gbs), ctypes.addressof(ms),
+              ctypes.addressof(ideal), ctypes.addressof(nb), ctypes.addressof(fl))
+    return ms.value, ideal.value, nb.value, fl.value
+
+
 def stats_tiles(M):
     return _lib.query("vcg_conv_stats_tiles", M)
 
