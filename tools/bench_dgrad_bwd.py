@@ -15,8 +15,10 @@ DEV = "cuda"
 # (name, frames, H, C (dgrad output = conv input channels), Cout, k, stride, pad, mode)
 CASES = [
     ("l1.conv1 256<-64 tsm+bits", 1024, 56, 256, 64, 1, 1, 0, "tsm_bits"),
+    ("l1.conv1 256<-64 bits (no TSM)", 1024, 56, 256, 64, 1, 1, 0, "bits"),
     ("l1.b1 conv1 tsm+bits+y2", 1024, 56, 256, 64, 1, 1, 0, "tsm_bits_two"),
     ("l2.conv1 512<-128 tsm+bits", 1024, 28, 512, 128, 1, 1, 0, "tsm_bits"),
+    ("l2.conv1 512<-128 bits (no TSM)", 1024, 28, 512, 128, 1, 1, 0, "bits"),
     ("l1.conv2 3x3 64<-64 affine", 1024, 56, 64, 64, 3, 1, 1, "affine"),
     ("l1.conv3 64<-256 affine", 1024, 56, 64, 256, 1, 1, 0, "affine"),
     ("l3.conv1 1024<-256 tsm+bits", 1024, 14, 1024, 256, 1, 1, 0, "tsm_bits"),
@@ -60,8 +62,9 @@ def main():
         else:
             res = torch.randn((N, H, W, C), device=DEV).to(dt)
             _, bits = ops.bn_apply(y, torch.ones(C, device=DEV), torch.zeros(C, device=DEV), C, relu=True, bits=True)
-            kw = dict(tsm_T=16, tsm_fold=C // 8, res=res, bits=bits, y=y, mean=mean, invstd=inv, sums=sums,
-                      dgamma=dg, dbeta=db)
+            tsm = mode.startswith("tsm")
+            kw = dict(tsm_T=16 if tsm else 0, tsm_fold=C // 8 if tsm else 0, res=res, bits=bits, y=y, mean=mean,
+                      invstd=inv, sums=sums, dgamma=dg, dbeta=db)
             nbytes = dy.numel() * 2 + el * 2 * 3 + el // 8
             if mode == "tsm_bits_two":
                 y2 = torch.randn((N, H, W, C), device=DEV).to(dt)
