@@ -7,7 +7,9 @@ namespace vcg {
 enum { OP_DENSE_K = 0, OP_IM2COL = 1, OP_DGRAD = 2, OP_DENSE_MN = 3, OP_IM2COL_T = 4 };
 // EPI_BWD_AFF: EPI_BWD without residual / mask bits / second BN / TSM (the conv2 / conv3 input gradients: mask
 // recomputed from y, BN sums): fewer live registers, so the 64-column kernel fits 3 workgroups per CU
-enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 4 };
+// EPI_STORE_AUX (fast kernel): EPI_STORE whose pre-activation copy `aux` (the GELU input the backward needs) also
+// goes out through the LDS stage, in a round of its own
+enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 4, EPI_STORE_AUX = 5 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
 
 template <typename T> struct Cfg;

@@ -308,6 +308,32 @@ __device__ __forceinline__ void epilogue_staged(f32x4 (&acc)[4][BN / 32], const 
   }
 }
 
+// EPI_STORE_AUX: the pre-activation values (bias added) to p.aux, then the activated values to Cout, each a
+// staged round of its own
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue_staged_aux(f32x4 (&acc)[4][BN / 32], const GemmParams& p,
+                                                    const float (&bv)[BN / 32][4], bf16_t* Cout, bf16_t* stA,
+                                                    bf16_t* stB, int m0, int n0, int wm, int wn, int lane) {
+  constexpr int MT = 4, NT = BN / 32;
+  static_assert(BM == 128, "EPI_STORE_AUX runs on 128-row tiles");
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = acc[i][j][r] * p.alpha + bv[j][r];
+          v[r] = pass == 0 ? t : apply_act(t, p.act);
+        }
+        stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
+      }
+    stage_flush<BM, BN>(stA, stB, p, pass == 0 ? reinterpret_cast<bf16_t*>(p.aux) : Cout, m0, n0);
+  }
+}
+
 // ---- EPI_BWD (igemm.h BwdEpi): conv-dgrad epilogue of the trunk backward ------------------------------
 // Per-column parameters live in LDS (cpar[4][BN]: mean, msc, msh, mean2 of the workgroup's BN columns);
 // a thread of the flush always owns the same 8-column chunk c = tid % (BN / 8), so its per-column sums stay
@@ -759,6 +785,8 @@ void igemm_fast_kernel(GemmParams p) {
           }
           stage_flush_stats<BM, BN>(stA, stB, p, Cout, mt * BM + 128 * h, n0, scnt, b1, b2, b3);
         }
+      } else if constexpr (EPI == EPI_STORE_AUX) {
+        if constexpr (BM == 128) epilogue_staged_aux<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane);
       } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0)) {
         epilogue_staged<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane);
       } else {
@@ -894,6 +922,8 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
     return fast_bn<OP_DENSE_K, EPI_STATS>(p, z, s);
   }
   if (p.residual) return fast_bn<OP_DENSE_K, EPI_STORE, true>(p, z, s);  // dense layers only (BERT bwd)
+  if (p.aux && amode == OP_DENSE_K && (p.ldc & 7) == 0 && !getenv("VCG_NO_AUX_STAGE"))  // BERT FFN1 (GELU input)
+    return fast_bn<OP_DENSE_K, EPI_STORE_AUX>(p, z, s);
   if (amode == OP_IM2COL_SMALLC) return fast_bn<OP_IM2COL_SMALLC, EPI_STORE>(p, z, s);
   if (amode == OP_IM2COL_TSM) return fast_bn<OP_IM2COL_TSM, EPI_STORE>(p, z, s);
   if (amode == OP_IM2COL) return fast_bn<OP_IM2COL, EPI_STORE>(p, z, s);
