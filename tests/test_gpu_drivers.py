@@ -60,3 +60,21 @@ def test_ddp_driver_world1():
     os.environ.pop("WORLD_SIZE", None)
     r = drv.main(TINY + ["--epoch", "1", "--batch_size", "2", "--videos", "8"])
     assert r is None or r != r or 0.0 <= r <= 1.0
+
+
+def test_bench_script_small():
+    """bench.py end to end at a tiny size (the contract's JSON line: metric, value, roofline with the per-launch
+    accounting), so a broken bench is caught by the GPU suite, not at round end."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "1", "--batch",
+                          "2", "--frames", "4", "--res", "112", "--tokens", "32", "--no-cpu-baseline"],
+                         capture_output=True, text=True, timeout=300, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "ms_per_step", "roofline", "roofline_step", "config"):
+        assert k in d, k
+    assert d["value"] > 0 and d["roofline"]["bound"] in ("hbm", "mfma") and 0 < d["roofline"]["frac"] < 1
+    assert 0 < d["roofline"]["per_launch_roofline"]["frac"] <= 1
