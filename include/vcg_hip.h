@@ -47,7 +47,9 @@ VCG_API int vcg_timing_roofline(int kernel_id, double peak_tflops, double peak_g
  * TemporalShift.shift (ops/temporal_shift.py:33-51, inserted by make_temporal_shift :133-144)
  * fused into the input gather; optional BatchNorm partial statistics from the epilogue.
  * stats (optional): float2 [Cout + 1][vcg_conv_stats_tiles(M)] — per column and slot (mean, M2) of
- * the slot's rows, then the count row (rows per slot, 0 = unused slot); merged by vcg_bn_finalize. */
+ * the slot's rows, then the count row (rows per slot, 0 = unused slot); merged by vcg_bn_finalize.
+ * bf16 with C = 4 (RGB0, the stem): the pair-packed stem -- stride 2, even W; w in the layout of
+ * vcg_weight_prep(transposed = 2 + pad); two stride-2 taps per 16-B chunk (GEMM K 224 instead of 392). */
 VCG_API int vcg_conv_stats_tiles(int M);
 VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
 /* autograd of conv2d: input gradient (transposed-conv gather) */
@@ -61,7 +63,8 @@ VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
    bf16 fast engine only; VCG_ERR_UNSUPPORTED elsewhere. */
 VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C, int Cout, int KH, int KW);
 VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, const void* res, int res_stride, const unsigned char* bits, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, const void* y2, const float* mean2, const float* invstd2, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, float* sum_gx2, float* dgamma2, float* dbeta2, hipStream_t s);
-/* autograd of conv2d: weight gradient, split-K over pixels, written in OIHW (state-dict layout) */
+/* autograd of conv2d: weight gradient, split-K over pixels, written in OIHW (state-dict layout); bf16 C = 4:
+   the pair-packed stem gather (as vcg_conv_fwd) */
 VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad);
 VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
 /* nn.Linear / BertSelfAttention matmuls (HF BertModel via model/lang/bert_hugface.py:20; ChapterHead
@@ -99,6 +102,11 @@ VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, in
    normalised like ToTensor+Normalize (train_video_segment_point.py:383-386) into NHWC [n_rows][H][W][8]. mean3/std3
    are HOST pointers to 3 floats. */
 VCG_API int vcg_window_frames_u8(int dtype, const uint8_t* frames, const long long* idx, void* dst, long long n_rows, int F, int H, int W, const float* mean3, const float* std3, hipStream_t s);
+/* the same into NHWC [n_rows][H][W][Cpad], Cpad 4 (the pair-packed bf16 stem / fp32) or 8 */
+VCG_API int vcg_window_frames_u8_cpad(int dtype, const uint8_t* frames, const long long* idx, void* dst, long long n_rows, int F, int H, int W, int Cpad, const float* mean3, const float* std3, hipStream_t s);
+/* OIHW f32 -> GEMM operand: transposed 0 [Cout][KH][KW][Cpad], 1 [Cin][KH][KW][Cout], 2 + pad the pair-packed
+   stem [Cout][KH][KWp][8] (bf16, Cin <= 4; element 4j + c of super tap kwp = w[.][c][kh][2 (kwp - pwp) + j + pad],
+   pwp = -floor(-pad / 2), KWp = floor((KW - 1 - pad) / 2) + pwp + 1) */
 VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int KH, int KW, int Cpad, int transposed, hipStream_t s);
 /* every conv of the trunk in one launch: desc = DEVICE array of n x 8 int64 (src OIHW f32 ptr, dst bf16 ptr, Cout,
    Cin, KH, KW, Cpad, transposed), each as vcg_weight_prep; bf16 only, each tensor < 2^31 elements */

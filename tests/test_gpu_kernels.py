@@ -184,6 +184,59 @@ def test_conv_wgrad(K, dtype, case):
     _close(dw - 0.5, ref, dtype, "conv wgrad")
 
 
+@pytest.mark.parametrize("case", [(2, 16, 16, 7, 2, 3), (3, 17, 22, 7, 2, 3), (4, 64, 64, 7, 2, 3),
+                                  (2, 15, 12, 5, 2, 2), (2, 12, 14, 3, 2, 1)])
+def test_stem_pair(K, case):
+    """The pair-packed bf16 stem (C = 4 RGB0, two stride-2 taps per 16-B chunk): forward + BN statistics and the
+    weight gradient against float64 torch, and against the one-tap-per-chunk C = 8 path."""
+    N, H, W, k, s, p = case
+    dtype = torch.bfloat16
+    Cin, Cout = 3, 64
+    x = _rand((N, Cin, H, W), dtype, 11).double()
+    w = _rand((Cout, Cin, k, k), torch.float32, 12, 0.1)
+    ref = F.conv2d(x, w.to(dtype).double(), stride=s, padding=p)
+    OH, OW = ref.shape[2], ref.shape[3]
+    outs = {}
+    for cpad in (4, 8):
+        xs = torch.zeros((N, H, W, cpad), dtype=dtype)
+        xs[..., :Cin] = x.permute(0, 2, 3, 1).to(dtype)
+        xs = xs.to(DEV)
+        wd = K.weight_prep(w.to(DEV), cpad, dtype, pair_pad=p if cpad == 4 else None)
+        if cpad == 4:
+            assert wd.shape == (Cout, k, K.pair_taps(k, p)[0], 8)
+        M = N * OH * OW
+        stats = K.stats_buffer(Cout, M, DEV)
+        y = K.conv_fwd(xs, wd, N, H, W, cpad, Cout, k, k, s, p, 0, 0, stats=stats)
+        _close(y.permute(0, 3, 1, 2), ref, dtype, f"stem fwd cpad {cpad}")
+        mean, invstd, scale, shift = (torch.empty(Cout, device=DEV) for _ in range(4))
+        K.bn_finalize(stats, K.stats_tiles(M), M, Cout, torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV),
+                      mean, invstd, scale, shift, None, None, 0.1, 1e-5)
+        yd = y.double().cpu().reshape(M, Cout)
+        assert torch.allclose(mean.double().cpu(), yd.mean(0), atol=1e-5 * (1 + yd.mean(0).abs().max().item()))
+        dy = _rand((N, Cout, OH, OW), dtype, 13).double()
+        wr = w.double().requires_grad_()
+        (gref,) = torch.autograd.grad(F.conv2d(x, wr, stride=s, padding=p), wr, dy)
+        dw = torch.full((Cout, Cin, k, k), 0.5, dtype=torch.float32, device=DEV)
+        K.conv_wgrad(xs, dy.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV), dw, N, H, W, cpad, Cin, Cout, k, k,
+                     s, p, 0, 0, accumulate=True)
+        _close(dw - 0.5, gref, dtype, f"stem wgrad cpad {cpad}")
+        outs[cpad] = (y.float(), dw)
+    # same math, different K order: the two layouts agree to fp32 summation order (+ one bf16 rounding of y)
+    assert (outs[4][0] - outs[8][0]).abs().max().item() <= 1e-2 * (1 + outs[8][0].abs().max().item())
+    assert (outs[4][1] - outs[8][1]).abs().max().item() <= 1e-4 * (1 + outs[8][1].abs().max().item())
+
+
+def test_window_frames_u8_cpad4(K):
+    """The 4-channel staging of the pair-packed stem == the first 4 channels of the 8-channel one."""
+    g = torch.Generator().manual_seed(5)
+    frames = torch.randint(0, 256, (5, 6, 10, 3), dtype=torch.uint8, generator=g).to(DEV)
+    idx = torch.tensor([0, 4, 2, -1, 9, 3], dtype=torch.int64).to(DEV)
+    for dt in (torch.bfloat16, torch.float32):
+        a = K.window_frames_u8(frames, idx, dt, cpad=4)
+        b = K.window_frames_u8(frames, idx, dt, cpad=8)
+        assert a.shape[-1] == 4 and torch.equal(a, b[..., :4]) and not b[..., 4:].any()
+
+
 @pytest.mark.parametrize("case", [(16, 28, 28, 64, 64, 3, 1, 1, 4), (8, 30, 30, 64, 256, 1, 2, 0, 0),
                                   (4, 64, 64, 3, 64, 7, 2, 3, 0), (4, 14, 14, 256, 128, 3, 2, 1, 0),
                                   (8, 20, 20, 512, 192, 1, 1, 0, 8)])

@@ -55,6 +55,11 @@ struct OpArgs {
   // (2i + ry, 2j + rx) of the dx image, and the k tiles walk only the taps that reach them,
   // kh = tkh0 + 2a (a < tKH), kw = tkw0 + 2b (b < tKW) -- 1, 2 or 4 of the 9 taps of a 3x3 kernel
   int tKH, tKW, tkh0, tkw0, ry, rx;
+  // w-direction stride / pad of an im2col gather when they differ from (stride, pad) (sw = 0: the same).
+  // The pair-packed stem (vcg_conv_fwd / vcg_conv_wgrad, bf16, C = 4, stride 2): W / C / KW describe the
+  // image as W/2 "super pixels" of 8 channels (two adjacent RGB0 pixels, one 16-B chunk) that a stride-2
+  // tap pair reads together: sw = 1, pw = the super-pixel pad, KW = the super-pixel tap count.
+  int sw, pw;
 };
 
 // EPI_BWD (fast kernel, conv dgrad): the epilogue of a conv input gradient inside the trunk backward.

@@ -427,7 +427,7 @@ static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long MN,
                                                             int N, float* __restrict__ out, int accumulate,
                                                             int conv_perm, int KH, int KW, int Cpad, int Cin,
-                                                            float scale) {
+                                                            float scale, int KWp, int pwp, int pad) {
   const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (idx >= MN) return;
   float v = 0.f;
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   for (; s < splits; ++s) v += p[(long long)s * MN];
   v *= scale;
   long long dst = idx;
-  if (conv_perm) {
+  if (conv_perm == 1) {
     // idx = m * N + n, m = cout, n = (kh*KW + kw)*Cpad + ci  ->  OIHW [cout][ci][kh][kw]  (MN < 2^31)
     const int m = (int)idx / N;
     const int n = (int)idx - m * N;
@@ -451,6 +451,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     const int ci = n - tap * Cpad;
     if (ci >= Cin) return;
     const int kh = tap / KW, kw = tap - kh * KW;
+    dst = (((long long)m * Cin + ci) * KH + kh) * KW + kw;
+  } else if (conv_perm == 2) {
+    // pair-packed stem: n = (kh*KWp + kwp)*8 + 4j + ci, tap kw = 2 (kwp - pwp) + j + pad (outside the kernel:
+    // the GEMM's zero-weight half of an edge pair, dropped)
+    const int m = (int)idx / N;
+    const int n = (int)idx - m * N;
+    const int tap = n >> 3, j = (n >> 2) & 1, ci = n & 3;
+    const int kh = tap / KWp, kwp = tap - kh * KWp;
+    const int kw = 2 * (kwp - pwp) + j + pad;
+    if (ci >= Cin || kw < 0 || kw >= KW) return;
     dst = (((long long)m * Cin + ci) * KH + kh) * KW + kw;
   }
   if (accumulate) out[dst] += v;
@@ -464,6 +474,19 @@ static int choose_splits(int M, int N, int K, int BK) {
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   return splits;
+}
+
+// Pair-packed stem (bf16, C = 4 RGB0 channels, stride 2): stride-2 tap kw of output column ow reads pixel
+// 2 ow - pad + kw = 2 (ow + kwp - pwp) + j, i.e. half j of "super pixel" ow + kwp - pwp of the same image
+// seen as [N][H][W/2][8]. The 16-B chunk of one super pixel carries two taps, so the GEMM K of a 7x7/2
+// stem is 7 * 4 * 8 = 224 instead of 7 * 7 * 8 = 392 at C = 8 (the frames are also half as many bytes).
+// Weights: [Cout][KH][KWp][8], element 4j + c = w[cout][c][kh][2 (kwp - pwp) + j + pad] (zero outside).
+static bool stem_pair(int dtype, int C) { return dtype == VCG_BF16 && C == 4; }
+static int floor_half(int x) { return (x - (x & 1)) / 2; }
+static void pair_taps(int KW, int pad, int* KWp, int* pwp) {
+  const int lo = floor_half(-pad), hi = floor_half(KW - 1 - pad);
+  *KWp = hi - lo + 1;
+  *pwp = -lo;
 }
 
 }  // namespace vcg
@@ -482,16 +505,22 @@ VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float
                          int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold,
                          hipStream_t stream) {
   const int logC = ilog2_exact(C);
+  const bool pair = stem_pair(dtype, C);
   VCG_REQUIRE(logC >= 0, "C must be a power of two");
-  VCG_REQUIRE(dtype == VCG_F32 ? C >= 4 : C >= 8, "C too small for 16-B gathers");
+  VCG_REQUIRE(dtype == VCG_F32 ? C >= 4 : (C >= 8 || pair), "C too small for 16-B gathers");
   VCG_REQUIRE(Cout % 64 == 0, "Cout must be a multiple of 64");
   VCG_REQUIRE(tsm_fold == 0 || (tsm_T > 0 && N % tsm_T == 0 && tsm_fold % 8 == 0 && 2 * tsm_fold <= C),
               "bad TSM geometry");
+  VCG_REQUIRE(!pair || (stride == 2 && W % 2 == 0 && tsm_fold == 0 && fast_gemm_enabled() &&
+                        (long long)N * H * W * C * 2 < 0xFFFFFF00LL),
+              "bf16 C = 4 (pair-packed stem) needs stride 2, even W, no TSM, the fast engine and < 4 GB input");
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  int KWp = KW, pwp = 0;
+  if (pair) pair_taps(KW, pad, &KWp, &pwp);
   GemmParams p{};
   p.M = N * OH * OW;
   p.N = Cout;
-  p.K = KH * KW * C;
+  p.K = pair ? KH * KWp * 8 : KH * KW * C;
   p.k_per_split = p.K + 64;
   const bool dense = (KH == 1 && KW == 1 && stride == 1 && pad == 0 && tsm_fold == 0);
   if (dense) {
@@ -502,6 +531,9 @@ VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float
     a.GH = OH; a.GW = OW; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
     a.tsm_T = tsm_T; a.tsm_fold = tsm_fold;
     a.bytes = (long long)N * H * W * C * (dtype == VCG_BF16 ? 2 : 4);
+    if (pair) {  // the image as [N][H][W/2][8] super pixels, stride 1 / pad pwp along w
+      a.W = W / 2; a.C = 8; a.logC = 3; a.KW = KWp; a.sw = 1; a.pw = pwp;
+    }
     p.a = a;
   }
   p.b = dense_op(w, p.K, Cout, p.K, dtype == VCG_BF16 ? 2 : 4);
@@ -718,10 +750,13 @@ static bool wgrad_fast_ok(int dtype, int N, int H, int W, int C, int Cout, int K
 static void wgrad_geometry(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad,
                            int* M, int* Nn, int* K, int* splits, int* kps, bool* fast) {
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  const bool pair = stem_pair(dtype, C);  // gathered as [N][H][W/2][8] super pixels (see pair_taps)
+  int KWp = KW, pwp = 0;
+  if (pair) pair_taps(KW, pad, &KWp, &pwp);
   *M = Cout;
-  *Nn = KH * KW * C;
+  *Nn = pair ? KH * KWp * 8 : KH * KW * C;
   *K = N * OH * OW;
-  *fast = wgrad_fast_ok(dtype, N, H, W, C, Cout, *K);
+  *fast = wgrad_fast_ok(dtype, N, H, pair ? W / 2 : W, pair ? 8 : C, Cout, *K);
   int BK, sp;
   if (*fast) {
     BK = 64;
@@ -759,6 +794,11 @@ VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, 
   int M, Nn, K, splits, kps;
   bool fast;
   wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits, &kps, &fast);
+  const bool pair = stem_pair(dtype, C);
+  int KWp = KW, pwp = 0;
+  if (pair) pair_taps(KW, pad, &KWp, &pwp);
+  VCG_REQUIRE(!pair || (fast && stride == 2 && W % 2 == 0 && tsm_fold == 0),
+              "bf16 C = 4 (pair-packed stem) needs stride 2, even W, no TSM and the fast engine");
   VCG_REQUIRE(ws_bytes >= (long long)splits * M * Nn * 4, "workspace too small");
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   GemmParams p{};
@@ -774,6 +814,9 @@ VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, 
   b.GH = OH; b.GW = OW; b.KH = KH; b.KW = KW; b.stride = stride; b.pad = pad;
   b.tsm_T = tsm_T > 0 ? tsm_T : 1; b.tsm_fold = tsm_fold;
   b.fd_ghw = make_fastdiv(OH * OW); b.fd_gw = make_fastdiv(OW); b.fd_T = make_fastdiv(b.tsm_T);
+  if (pair) {
+    b.W = W / 2; b.C = 8; b.logC = 3; b.KW = KWp; b.sw = 1; b.pw = pwp;
+  }
   p.b = b;
   p.ws = ws;
   p.alpha = 1.f;
@@ -789,7 +832,7 @@ VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, 
   if (rc) return rc;
   const long long MN = (long long)M * Nn;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, splits,
-                     MN, Nn, dw, accumulate, 1, KH, KW, C, Cin, 1.f);
+                     MN, Nn, dw, accumulate, pair ? 2 : 1, KH, KW, C, Cin, 1.f, KWp, pwp, pad);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -864,7 +907,7 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
     if (rc) return rc;
     const long long MN = (long long)M * N;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, fsplits,
-                       MN, N, out, accumulate, 0, 1, 1, 1, 1, 1.f);
+                       MN, N, out, accumulate, 0, 1, 1, 1, 1, 1.f, 0, 0, 0);
     VCG_LAUNCH_CHECK();
     return VCG_OK;
   }
@@ -878,7 +921,7 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
   if (rc) return rc;
   const long long MN = (long long)M * N;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, splits,
-                     MN, N, out, accumulate, 0, 1, 1, 1, 1, 1.f);
+                     MN, N, out, accumulate, 0, 1, 1, 1, 1, 1.f, 0, 0, 0);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

@@ -69,7 +69,7 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
         int py, px;  // source pixel of tap (0, 0)
         if constexpr (IM2COL) {
           py = y * a.stride - a.pad;
-          px = x * a.stride - a.pad;
+          px = (SMALLC && a.sw) ? x * a.sw - a.pw : x * a.stride - a.pad;
         } else {
           py = y + a.pad;
           px = x + a.pad;

@@ -74,7 +74,7 @@ template <int COLS, bool GATHER> struct MNLoader {
         const int h = tap / a.KW;
         col[q] = (cc < ncols && tap < a.KH * a.KW) ? ci : -1;
         kh[q] = h - a.pad;
-        kw[q] = tap - h * a.KW - a.pad;
+        kw[q] = tap - h * a.KW - (a.sw ? a.pw : a.pad);
         dt[q] = a.tsm_fold > 0 ? (ci < a.tsm_fold ? 1 : (ci < 2 * a.tsm_fold ? -1 : 0)) : 0;
         const int k = kb + r;
         const int nn = (int)fdiv((uint32_t)k, a.fd_ghw);
@@ -97,7 +97,7 @@ template <int COLS, bool GATHER> struct MNLoader {
       if constexpr (!GATHER) {
         e = (k0 + row[q]) * (int)a.ld + col[q];
       } else {
-        const int ih = oh[q] * a.stride + kh[q], iw = ow[q] * a.stride + kw[q];
+        const int ih = oh[q] * a.stride + kh[q], iw = ow[q] * (a.sw ? a.sw : a.stride) + kw[q];
         ok = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         ok = ok && (unsigned)(t[q] + dt[q]) < (unsigned)a.tsm_T;
         e = (((n[q] + dt[q]) * a.H + ih) * a.W + iw) * a.C + col[q];

@@ -135,6 +135,21 @@ __global__ __launch_bounds__(256) void frames_to_nhwc8_kernel(const float* __res
   }
 }
 
+// The pair-packed bf16 stem input (C = 3 -> Cpad = 4, RGB0): one 8-B store per pixel.
+__global__ __launch_bounds__(256) void frames_to_nhwc4_kernel(const float* __restrict__ src, uint2* __restrict__ dst,
+                                                            int total, int HW) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int n = i / HW, hw = i - n * HW;
+    const float* s0 = src + (long long)n * 3 * HW + hw;
+    const float r = __builtin_nontemporal_load(s0), g = __builtin_nontemporal_load(s0 + HW),
+                b = __builtin_nontemporal_load(s0 + 2 * HW);
+    uint2 q;
+    q.x = (uint32_t)f2bf(r) | ((uint32_t)f2bf(g) << 16);
+    q.y = (uint32_t)f2bf(b);
+    dst[i] = q;
+  }
+}
+
 // Frame ingest: decoded u8 RGB frames of one video [F][H][W][3] -> the stem's
 // NHWC input [n_rows][H][W][8] (channels 3..7 zero) for the window frame table idx[n_rows]
 // (window-major, frame-minor: row = w*T + t), normalised as torchvision ToTensor + Normalize
@@ -142,7 +157,7 @@ __global__ __launch_bounds__(256) void frames_to_nhwc8_kernel(const float* __res
 template <typename T>
 __global__ void window_frames_u8_kernel(const uint8_t* __restrict__ frames, const long long* __restrict__ idx,
                                         T* __restrict__ dst, long long n_rows, int F, int HW, float m0, float m1,
-                                        float m2, float s0, float s1, float s2) {
+                                        float m2, float s0, float s1, float s2, int cpad) {
   const long long total = n_rows * HW;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -156,30 +171,55 @@ __global__ void window_frames_u8_kernel(const uint8_t* __restrict__ frames, cons
       v[1] = ((float)q[1] / 255.f - m1) / s1;
       v[2] = ((float)q[2] / 255.f - m2) / s2;
     }
-    T* d = dst + i * 8;
+    T* d = dst + i * cpad;
     if constexpr (sizeof(T) == 2) {
-      uint4 o;
-      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      o.y = (uint32_t)f2bf(v[2]);
-      o.z = 0u;
-      o.w = 0u;
-      *reinterpret_cast<uint4*>(d) = o;
+      const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), hi = (uint32_t)f2bf(v[2]);
+      if (cpad == 4) *reinterpret_cast<uint2*>(d) = make_uint2(lo, hi);
+      else *reinterpret_cast<uint4*>(d) = make_uint4(lo, hi, 0u, 0u);
     } else {
       *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], 0.f);
-      *reinterpret_cast<float4*>(d + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (cpad == 8) *reinterpret_cast<float4*>(d + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
 
-// OIHW fp32 -> [Cout][KH][KW][Cpad] (transposed = 0) or [Cin][KH][KW][Cout] (transposed = 1)
+// Pair-packed stem weights (igemm.hip pair_taps; mode = 2 + pad): [Cout][KH][KWp][8], element 4j + c of super
+// tap kwp = w[cout][c][kh][2 (kwp - pwp) + j + pad] (zero for c >= Cin or a tap outside the kernel).
+__host__ __device__ __forceinline__ int pair_floor_half(int x) { return (x - (x & 1)) / 2; }
+__host__ __device__ __forceinline__ void pair_geom(int KW, int pad, int& KWp, int& pwp) {
+  const int lo = pair_floor_half(-pad);
+  KWp = pair_floor_half(KW - 1 - pad) - lo + 1;
+  pwp = -lo;
+}
+__device__ __forceinline__ float pair_weight(const float* w, long long i, int Cin, int KH, int KW, int pad) {
+  int KWp, pwp;
+  pair_geom(KW, pad, KWp, pwp);
+  const int c8 = (int)(i & 7);
+  long long r = i >> 3;
+  const int kwp = (int)(r % KWp); r /= KWp;
+  const int kh = (int)(r % KH);
+  const int co = (int)(r / KH);
+  const int j = c8 >> 2, ci = c8 & 3;
+  const int kw = 2 * (kwp - pwp) + j + pad;
+  return (ci < Cin && kw >= 0 && kw < KW) ? w[(((long long)co * Cin + ci) * KH + kh) * KW + kw] : 0.f;
+}
+
+// OIHW fp32 -> [Cout][KH][KW][Cpad] (transposed = 0), [Cin][KH][KW][Cout] (transposed = 1) or the pair-packed
+// stem layout (transposed = 2 + pad)
 template <typename T>
 __global__ void weight_prep_kernel(const float* __restrict__ w, T* __restrict__ out, int Cout, int Cin, int KH, int KW,
                                    int Cpad, int transposed) {
-  const long long total = transposed ? (long long)Cin * KH * KW * Cout : (long long)Cout * KH * KW * Cpad;
+  int KWp = 0, pwp = 0;
+  if (transposed >= 2) pair_geom(KW, transposed - 2, KWp, pwp);
+  const long long total = transposed >= 2 ? (long long)Cout * KH * KWp * 8
+                          : transposed    ? (long long)Cin * KH * KW * Cout
+                                          : (long long)Cout * KH * KW * Cpad;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     float v;
-    if (!transposed) {
+    if (transposed >= 2) {
+      v = pair_weight(w, i, Cin, KH, KW, transposed - 2);
+    } else if (!transposed) {
       const int ci = (int)(i % Cpad);
       long long r = i / Cpad;
       const int kw = (int)(r % KW); r /= KW;
@@ -311,6 +351,9 @@ VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, in
   if (dtype == VCG_BF16 && C == 3 && Cpad == 8 && tot * 3 < (1LL << 31))
     hipLaunchKernelGGL(frames_to_nhwc8_kernel, dim3(grid_for(tot)), dim3(256), 0, s, src, (uint4*)dst, (int)tot,
                        H * W);
+  else if (dtype == VCG_BF16 && C == 3 && Cpad == 4 && tot * 3 < (1LL << 31))
+    hipLaunchKernelGGL(frames_to_nhwc4_kernel, dim3(grid_for(tot)), dim3(256), 0, s, src, (uint2*)dst, (int)tot,
+                       H * W);
   else if (dtype == VCG_BF16)
     hipLaunchKernelGGL(frames_to_nhwc_kernel<bf16_t>, dim3(grid_for(tot)), dim3(256), 0, s, src, (bf16_t*)dst, N, C,
                        H, W, Cpad);
@@ -321,24 +364,32 @@ VCG_API int vcg_frames_to_nhwc(int dtype, const float* src, void* dst, int N, in
   return VCG_OK;
 }
 
-VCG_API int vcg_window_frames_u8(int dtype, const uint8_t* frames, const long long* idx, void* dst, long long n_rows,
-                                 int F, int H, int W, const float* mean3, const float* std3, hipStream_t s) {
+VCG_API int vcg_window_frames_u8_cpad(int dtype, const uint8_t* frames, const long long* idx, void* dst,
+                                      long long n_rows, int F, int H, int W, int Cpad, const float* mean3,
+                                      const float* std3, hipStream_t s) {
   VCG_REQUIRE(mean3 && std3, "mean/std required");
+  VCG_REQUIRE(Cpad == 4 || Cpad == 8, "Cpad must be 4 or 8");
   VCG_REQUIRE(n_rows >= 0 && F > 0 && H > 0 && W > 0, "bad shape");
   const long long tot = n_rows * H * W;
   if (tot == 0) return VCG_OK;
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(window_frames_u8_kernel<bf16_t>, dim3(grid_for(tot)), dim3(256), 0, s, frames, idx,
-                       (bf16_t*)dst, n_rows, F, H * W, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2]);
+                       (bf16_t*)dst, n_rows, F, H * W, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2], Cpad);
   else
     hipLaunchKernelGGL(window_frames_u8_kernel<float>, dim3(grid_for(tot)), dim3(256), 0, s, frames, idx, (float*)dst,
-                       n_rows, F, H * W, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2]);
+                       n_rows, F, H * W, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2], Cpad);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
 
+VCG_API int vcg_window_frames_u8(int dtype, const uint8_t* frames, const long long* idx, void* dst, long long n_rows,
+                                 int F, int H, int W, const float* mean3, const float* std3, hipStream_t s) {
+  return vcg_window_frames_u8_cpad(dtype, frames, idx, dst, n_rows, F, H, W, 8, mean3, std3, s);
+}
+
 VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int KH, int KW, int Cpad,
                             int transposed, hipStream_t s) {
+  VCG_REQUIRE(transposed < 2 || (dtype == VCG_BF16 && Cin <= 4), "pair-packed layout: bf16, Cin <= 4");
   const long long tot = (long long)Cout * KH * KW * (transposed ? Cin : Cpad);
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(weight_prep_kernel<bf16_t>, dim3(grid_for(tot)), dim3(256), 0, s, w, (bf16_t*)out, Cout, Cin,
@@ -351,17 +402,23 @@ VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int 
 }
 
 namespace {
-// vcg_weight_prep_multi: blockIdx.y = descriptor (8 int64: src, dst, Cout, Cin, KH, KW, Cpad, transposed)
+// vcg_weight_prep_multi: blockIdx.y = descriptor (8 int64: src, dst, Cout, Cin, KH, KW, Cpad, mode = transposed
+// as in vcg_weight_prep: 0, 1 or 2 + pad for the pair-packed stem)
 __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const long long* __restrict__ desc) {
   const long long* d = desc + 8 * blockIdx.y;
   const float* w = reinterpret_cast<const float*>(d[0]);
   bf16_t* out = reinterpret_cast<bf16_t*>(d[1]);
   const int Cout = (int)d[2], Cin = (int)d[3], KH = (int)d[4], KW = (int)d[5], Cpad = (int)d[6];
-  const bool tr = d[7] != 0;
-  const int total = tr ? Cin * KH * KW * Cout : Cout * KH * KW * Cpad;
+  const int mode = (int)d[7];
+  const bool tr = mode == 1;
+  int KWp = 0, pwp = 0;
+  if (mode >= 2) pair_geom(KW, mode - 2, KWp, pwp);
+  const int total = mode >= 2 ? Cout * KH * KWp * 8 : tr ? Cin * KH * KW * Cout : Cout * KH * KW * Cpad;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     float v;
-    if (!tr) {
+    if (mode >= 2) {
+      v = pair_weight(w, i, Cin, KH, KW, mode - 2);
+    } else if (!tr) {
       const int ci = i % Cpad;
       int r = i / Cpad;
       const int kw = r % KW; r /= KW;

@@ -79,7 +79,7 @@ def score_windows(model, frames_u8, idx, ids, mask, batch_size, export=None):
     labels = torch.empty(n, dtype=torch.int64, device=frames_u8.device)
     for b0 in range(0, n, batch_size):
         b1 = min(n, b0 + batch_size)
-        fr = ops.window_frames_u8(frames_u8, idx[b0:b1].contiguous(), dt)
+        fr = ops.window_frames_u8(frames_u8, idx[b0:b1].contiguous(), dt, cpad=ops.stem_cpad(dt))
         out = model.forward_staged(fr, ids[b0:b1], mask[b0:b1], return_emb=export is not None)
         logits, prob = out[0], out[1]
         scores[b0:b1] = prob[:, 1]

@@ -4,6 +4,8 @@ Every wrapper checks device / dtype / contiguity, passes raw device pointers plu
 launches on torch's current HIP stream. There is no CPU or ATen fallback: a non-GPU tensor or
 a missing library raises.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -291,9 +293,17 @@ IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
-def window_frames_u8(frames, idx, dtype, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+def stem_cpad(dtype):
+    """Channels of the stem's NHWC input: bf16 -> 4 (RGB0, the pair-packed stem: two stride-2 taps per 16-B
+    chunk, vcg_conv_fwd) unless VCG_NO_STEM_PAIR=1 (8: one tap per chunk); fp32 -> 4."""
+    if dtype == torch.bfloat16 and os.environ.get("VCG_NO_STEM_PAIR", "0") == "1":
+        return 8
+    return 4
+
+
+def window_frames_u8(frames, idx, dtype, mean=IMAGENET_MEAN, std=IMAGENET_STD, cpad=8):
     """u8 RGB frames [F,H,W,3] gathered by an int64 frame table `idx` (any shape, 0-based) ->
-    normalised NHWC stem input [idx.numel(),H,W,8] (channels 3..7 zero)."""
+    normalised NHWC stem input [idx.numel(),H,W,cpad] (channels 3.. zero; cpad 4 or 8)."""
     import ctypes
 
     _chk(frames, torch.uint8, "frames")
@@ -302,10 +312,10 @@ def window_frames_u8(frames, idx, dtype, mean=IMAGENET_MEAN, std=IMAGENET_STD):
     if C != 3:
         raise ValueError("frames must be [F,H,W,3] RGB")
     n = idx.numel()
-    dst = torch.empty((n, H, W, 8), dtype=dtype, device=frames.device)
+    dst = torch.empty((n, H, W, cpad), dtype=dtype, device=frames.device)
     m = (ctypes.c_float * 3)(*mean)
     sd = (ctypes.c_float * 3)(*std)
-    _lib.call("vcg_window_frames_u8", dt_code(dtype), P(frames), P(idx), P(dst), n, F, H, W,
+    _lib.call("vcg_window_frames_u8_cpad", dt_code(dtype), P(frames), P(idx), P(dst), n, F, H, W, cpad,
               ctypes.addressof(m), ctypes.addressof(sd), stream())
     return dst
 
@@ -317,12 +327,23 @@ def frames_to_nhwc(src, N, C, H, W, Cpad, dtype):
     return dst
 
 
-def weight_prep(w, Cpad, dtype, transposed=False, out=None):
+def pair_taps(KW, pad):
+    """(KWp, pwp) of the pair-packed stem (igemm.hip pair_taps): super-pixel taps and pad."""
+    lo = (-pad) // 2
+    return (KW - 1 - pad) // 2 - lo + 1, -lo
+
+
+def weight_prep(w, Cpad, dtype, transposed=False, out=None, pair_pad=None):
+    """GEMM operand of a conv weight; pair_pad (bf16, Cpad = 4): the pair-packed stem layout for that pad."""
     _chk(w, torch.float32, "weight")
     Cout, Cin, KH, KW = w.shape
-    shape = (Cin, KH, KW, Cout) if transposed else (Cout, KH, KW, Cpad)
+    mode = int(transposed)
+    if pair_pad is not None:
+        shape, mode = (Cout, KH, pair_taps(KW, pair_pad)[0], 8), 2 + pair_pad
+    else:
+        shape = (Cin, KH, KW, Cout) if transposed else (Cout, KH, KW, Cpad)
     out = out if out is not None else torch.empty(shape, dtype=dtype, device=w.device)
-    _lib.call("vcg_weight_prep", dt_code(dtype), P(w), P(out), Cout, Cin, KH, KW, Cpad, int(transposed), stream())
+    _lib.call("vcg_weight_prep", dt_code(dtype), P(w), P(out), Cout, Cin, KH, KW, Cpad, mode, stream())
     return out
 
 

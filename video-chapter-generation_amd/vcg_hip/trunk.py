@@ -56,13 +56,20 @@ class _ConvWeights:
         dev = convs[0].weight.device
         self.fwd, self.bwd = {}, {}
         desc = []
+        self.stem_cpad = stem_cpad
         for conv in convs:
             Cout, Cin, KH, KW = conv.weight.shape
             stem = conv is net.conv1
             cpad = stem_cpad if stem else Cin
-            wf = torch.empty((Cout, KH, KW, cpad), dtype=torch.bfloat16, device=dev)
+            if stem and cpad == 4:  # the pair-packed stem layout (ops.weight_prep pair_pad)
+                pad = conv.padding[1]
+                wf = torch.empty((Cout, KH, ops.pair_taps(KW, pad)[0], 8), dtype=torch.bfloat16, device=dev)
+                mode = 2 + pad
+            else:
+                wf = torch.empty((Cout, KH, KW, cpad), dtype=torch.bfloat16, device=dev)
+                mode = 0
             self.fwd[id(conv)] = wf
-            desc.append([conv.weight.data_ptr(), wf.data_ptr(), Cout, Cin, KH, KW, cpad, 0])
+            desc.append([conv.weight.data_ptr(), wf.data_ptr(), Cout, Cin, KH, KW, cpad, mode])
             if not stem:  # the frames need no gradient
                 wb = torch.empty((Cin, KH, KW, Cout), dtype=torch.bfloat16, device=dev)
                 self.bwd[id(conv)] = wb
@@ -72,8 +79,9 @@ class _ConvWeights:
         self.ptrs = [conv.weight.data_ptr() for conv in convs]
         self.convs = convs
 
-    def valid_for(self, net, flat):
-        return flat is self.flat and [c.weight.data_ptr() for c in self.convs] == self.ptrs
+    def valid_for(self, net, flat, stem_cpad):
+        return (flat is self.flat and stem_cpad == self.stem_cpad
+                and [c.weight.data_ptr() for c in self.convs] == self.ptrs)
 
     def refresh(self):
         if self.gen != self.flat.generation:
@@ -91,8 +99,8 @@ class ResNetTrunk:
         flat = getattr(net, "_vcg_flat", None)
         if dtype == torch.bfloat16 and flat is not None:
             wc = getattr(net, "_vcg_convw", None)
-            if wc is None or not wc.valid_for(net, flat):
-                wc = _ConvWeights(net, flat, 8)
+            if wc is None or not wc.valid_for(net, flat, ops.stem_cpad(dtype)):
+                wc = _ConvWeights(net, flat, ops.stem_cpad(dtype))
                 object.__setattr__(net, "_vcg_convw", wc)
             wc.refresh()
             self.wc = wc
@@ -101,7 +109,8 @@ class ResNetTrunk:
     def _wprep(self, conv, Cpad):
         if self.wc is not None:
             return self.wc.fwd[id(conv)]
-        return ops.weight_prep(conv.weight.data, Cpad, self.dtype)
+        pair = self.dtype == torch.bfloat16 and Cpad == 4  # the stem (ops.stem_cpad)
+        return ops.weight_prep(conv.weight.data, Cpad, self.dtype, pair_pad=conv.padding[1] if pair else None)
 
     def _wprep_t(self, conv, Cin):
         """[Cin][KH][KW][Cout]: the dgrad operand"""
@@ -137,13 +146,13 @@ class ResNetTrunk:
         net, dt = self.net, self.dtype
         if self.staged:
             N, H, W, cpad = x.shape
-            if x.dtype != dt or cpad < 3 or not x.is_contiguous():
-                raise RuntimeError(f"staged frames must be contiguous NHWC [N,H,W,>=3] {dt}, "
+            if x.dtype != dt or cpad != ops.stem_cpad(dt) or not x.is_contiguous():
+                raise RuntimeError(f"staged frames must be contiguous NHWC [N,H,W,{ops.stem_cpad(dt)}] {dt}, "
                                    f"got {x.dtype} {tuple(x.shape)}")
             xs = x
         else:
             N, C0, H, W = x.shape
-            cpad = 8 if dt == torch.bfloat16 else 4
+            cpad = ops.stem_cpad(dt)
             xs = ops.frames_to_nhwc(x.contiguous(), N, C0, H, W, cpad, dt)
         y0, b0, H1, W1 = self._conv_bn(xs, net.conv1, net.bn1, N, H, W, cpad)
         a0 = ops.bn_apply(y0, b0.scale, b0.shift, 64, relu=True)
