@@ -145,6 +145,13 @@ VCG_API int vcg_head_attn_fwd(int dtype, const void* Vout, const void* Lout, con
    are accumulated (+=). ws: f32 workspace of vcg_head_attn_bwd_ws_floats. */
 VCG_API long long vcg_head_attn_bwd_ws_floats(int B, int T, int hid);
 VCG_API int vcg_head_attn_bwd(int dtype, const float* saved, const float* Wq, const float* Wk, const float* Wv, const float* Wp, const float* dlogits, void* dVout, void* dLout, float* dWq, float* dbq, float* dWk, float* dbk, float* dWv, float* dbv, float* dWp, float* dbp, float* ws, long long ws_floats, int B, int T, int hid, int nh, int O, float dropout_p, unsigned long long seed, int relu_mask, hipStream_t s);
+/* Window transformer StackedVideoChapterAttention, inference (window_attn.hip; replaces the module at
+ * model/fusion/stacked_window_self_attention.py:150-223 as called by two_stream_window.py:444): emb [B][S][H] f32
+ * per-clip fusion embeddings (S = 2w+1 <= 16, S*H <= 2048), 16 heads in the reference (nh), P = 2w+1 entries of
+ * window_pos_bias. `weights` = the f32 parameters packed by vcg_hip/window.py pack_window_weights (Linear weights
+ * transposed to [in][out]); logits / prob [B][2]. */
+VCG_API long long vcg_window_attn_weight_floats(int H, int nh, int P);
+VCG_API int vcg_window_attn_fwd(const float* emb, const float* weights, long long weight_floats, float* logits, float* prob, int B, int S, int H, int nh, int P, hipStream_t s);
 VCG_API int vcg_cross_entropy_fwd(const float* logits, const long long* labels, float* loss, int B, int C, hipStream_t s);
 VCG_API int vcg_cross_entropy_bwd(const float* logits, const long long* labels, const float* dloss, float* dlogits, int B, int C, hipStream_t s);
 

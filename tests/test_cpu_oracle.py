@@ -178,3 +178,43 @@ def test_oracle_c1_attn_forward_matches_reference():
         lg, pr, _, _ = om.two_stream(dict(m.state_dict()), frames, ids, mask, bn_mode="running", head_type="attn")
     assert np.abs(lg.numpy() - g["c1attn_logits_running"]).max() < 1e-5
     assert np.abs(pr.numpy() - g["c1attn_prob_running"]).max() < 1e-5
+
+
+def _window_module(w):
+    """The native StackedVideoChapterAttention (parameters only on CPU), initialised like the golden's
+    reference module (vcg_hip/synth.py by state-dict name, prefix "window_attn.")."""
+    from model.fusion.stacked_window_self_attention import StackedVideoChapterAttention
+    from vcg_hip import synth
+    cfg = type("Config", (), {"hidden_size": 128, "num_attention_heads": 16, "attention_probs_dropout_prob": 0.1,
+                              "window_size": w})
+    m = StackedVideoChapterAttention(cfg)
+    synth.init_params(m, 123, prefix="window_attn.")
+    return m.eval()
+
+
+@pytest.mark.parametrize("case,w", [("w1", 1), ("w2", 2), ("short", 2)])
+def test_oracle_window_attention_matches_reference(case, w):
+    """oracle.window.stacked_window_attention against the reference StackedVideoChapterAttention
+    (stacked_window_self_attention.py:148-223) on window_attn.npz; the native module's parameter names are
+    the reference's (the golden's weights are regenerated by those names)."""
+    from oracle import window as ow
+    g = _gold("window_attn.npz")
+    p = {n: t.detach() for n, t in _window_module(w).named_parameters()}
+    lg, pr = ow.stacked_window_attention(p, torch.from_numpy(g[f"{case}_emb"]))
+    assert np.abs(lg.numpy() - g[f"{case}_logits"]).max() < 1e-5
+    assert np.abs(pr.numpy() - g[f"{case}_probs"]).max() < 1e-6
+
+
+def test_window_weight_packing_layout():
+    """pack_window_weights covers every parameter once, in the size the C-ABI expects
+    (vcg_window_attn_weight_floats; a size query, no GPU compute)."""
+    from vcg_hip import _lib
+    from vcg_hip.window import pack_window_weights
+    m = _window_module(2)
+    flat = pack_window_weights(m)
+    assert flat.numel() == sum(p.numel() for p in m.parameters())
+    assert flat.numel() == _lib.query("vcg_window_attn_weight_floats", 128, 16, 5)
+    # first layer: attention_norm gamma, beta, then [H][3H] = (query | key | value)^T
+    at = m.layers[0].attention
+    qkvT = flat[256:256 + 3 * 128 * 128].view(128, 384)
+    assert torch.equal(qkvT[:, 128:256], at.key.weight.detach().t())

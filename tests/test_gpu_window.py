@@ -1,0 +1,73 @@
+"""Window transformer StackedVideoChapterAttention (reference model/fusion/stacked_window_self_attention.py:148-223)
+on libvcg_hip (window_attn.hip, inference): parity with the reference's own outputs (tests/golden/window_attn.npz,
+tools/oracle/make_golden_window.py) and with the CPU oracle (oracle/window.py) at other shapes.
+
+Tolerances (fp32 throughout, per north_star's 1e-3 on logits): golden cases 1e-4 absolute on logits and probs;
+oracle cases (other hidden sizes / windows / batch 64) 1e-3 absolute.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DEV = "cuda"
+
+
+def _module(H, w, nh=16, seed=123):
+    from model.fusion.stacked_window_self_attention import StackedVideoChapterAttention
+    from vcg_hip import synth
+    cfg = type("Config", (), {"hidden_size": H, "num_attention_heads": nh, "attention_probs_dropout_prob": 0.1,
+                              "window_size": w})
+    m = StackedVideoChapterAttention(cfg)
+    synth.init_params(m, seed, prefix="window_attn.")
+    return m.eval()
+
+
+@pytest.mark.parametrize("case,w", [("w1", 1), ("w2", 2), ("short", 2)])
+def test_window_attn_matches_reference_golden(case, w):
+    g = np.load(os.path.join(GOLD, "window_attn.npz"), allow_pickle=False)
+    m = _module(128, w).to(DEV)
+    with torch.no_grad():
+        lg, pr = m(torch.from_numpy(g[f"{case}_emb"]).to(DEV), None)
+    torch.cuda.synchronize()
+    assert np.abs(lg.cpu().numpy() - g[f"{case}_logits"]).max() < 1e-4
+    assert np.abs(pr.cpu().numpy() - g[f"{case}_probs"]).max() < 1e-4
+
+
+@pytest.mark.parametrize("H,w,nh,B", [(128, 2, 16, 64), (256, 3, 16, 8), (64, 7, 8, 5), (32, 0, 4, 3)])
+def test_window_attn_matches_oracle(H, w, nh, B):
+    from oracle import window as ow
+    m = _module(H, w, nh, seed=7)
+    gen = torch.Generator().manual_seed(H * 31 + w)
+    emb = torch.randn(B, 2 * w + 1, H, generator=gen)
+    p = {n: t.detach() for n, t in m.named_parameters()}
+    ref_lg, ref_pr = ow.stacked_window_attention(p, emb, nh=nh)
+    m = m.to(DEV)
+    with torch.no_grad():
+        lg, pr = m(emb.to(DEV))
+    torch.cuda.synchronize()
+    assert np.abs(lg.cpu().numpy() - ref_lg.numpy()).max() < 1e-3
+    assert np.abs(pr.cpu().numpy() - ref_pr.numpy()).max() < 1e-3
+
+
+def test_window_attn_repacks_after_weight_update():
+    m = _module(128, 1).to(DEV)
+    emb = torch.randn(4, 3, 128, device=DEV)
+    with torch.no_grad():
+        a, _ = m(emb)
+        m.classifier[16].bias.add_(1.0)  # in-place update bumps the parameter version
+        b, _ = m(emb)
+    torch.cuda.synchronize()
+    assert torch.allclose(b - a, torch.ones_like(a), atol=1e-5)
+
+
+def test_window_attn_rejects_bad_input():
+    m = _module(128, 1).to(DEV)
+    with pytest.raises(RuntimeError):
+        m(torch.randn(2, 5, 128, device=DEV))  # more clips than 2w+1
+    m.train()
+    with pytest.raises(RuntimeError):
+        m(torch.randn(2, 3, 128, device=DEV))  # training: no native backward, no silent fallback

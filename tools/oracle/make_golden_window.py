@@ -1,0 +1,54 @@
+"""Goldens for the window transformer StackedVideoChapterAttention (reference
+model/fusion/stacked_window_self_attention.py:148-223, configured as two_stream_window.TwoStream.build_chapter_head
+does at :342-348: 16 heads, attention dropout 0.1), produced by running the REFERENCE module in this container
+(only the .npz output is committed; the reference never travels).
+
+tests/golden/window_attn.npz
+  w{w}_emb / w{w}_logits / w{w}_probs : hidden 128, window_size w in (1, 2) -> S = 2w+1 clips, batch 4, eval
+      (dropout inactive); weights from vcg_hip/synth.py by state-dict name with prefix "window_attn."; inputs
+      from numpy's default_rng(11 + w).
+  short_*: window_size 2 module fed S = 3 clips (the reference slices window_pos_bias[..., :S]).
+usage: python tools/oracle/make_golden_window.py
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import make_golden as mg  # noqa: E402  (puts the reference on sys.path; loads vcg_hip/synth.py by path)
+from model.fusion.stacked_window_self_attention import StackedVideoChapterAttention  # noqa: E402  (reference)
+
+H, NH, B = 128, 16, 4
+
+
+def build(w):
+    cfg = type("Config", (), {"hidden_size": H, "num_attention_heads": NH, "attention_probs_dropout_prob": 0.1,
+                              "window_size": w})
+    m = StackedVideoChapterAttention(cfg)
+    mg.synth.init_params(m, mg.SEED, prefix="window_attn.")
+    return m.eval()
+
+
+def main():
+    out = {}
+    for w in (1, 2):
+        m = build(w)
+        rng = np.random.default_rng(11 + w)
+        emb = rng.standard_normal((B, 2 * w + 1, H)).astype(np.float32)
+        with torch.no_grad():
+            lg, pr = m(torch.from_numpy(emb), None)
+        out.update({f"w{w}_emb": emb, f"w{w}_logits": lg.numpy(), f"w{w}_probs": pr.numpy()})
+        if w == 2:
+            short = emb[:, :3].copy()
+            with torch.no_grad():
+                lg, pr = m(torch.from_numpy(short), None)
+            out.update({"short_emb": short, "short_logits": lg.numpy(), "short_probs": pr.numpy()})
+    np.savez_compressed(os.path.join(mg.GOLD, "window_attn.npz"), **out)
+    print({k: v.shape for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()

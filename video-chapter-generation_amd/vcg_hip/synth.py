@@ -88,6 +88,15 @@ def init_rule(name, shape):
     BERT Linear/Embedding N(0, 0.02), biases N(0, 0.02), LayerNorm gamma U(0.8,1.2), beta U(-0.1,0.1);
     head Linear U(+-1/sqrt(fan_in)) (nn.Linear default bound)."""
     leaf = name.rsplit(".", 1)[-1]
+    if name.startswith("window_attn."):  # StackedVideoChapterAttention (stacked_window_self_attention.py)
+        if leaf == "window_pos_bias":
+            return KIND_NORMAL, 0.0, 0.02
+        if len(shape) == 2:  # Linear weight [out][in]: U(+-1/sqrt(fan_in)); Linear(1, H): U(+-1)
+            bound = 1.0 / np.sqrt(shape[1])
+            return KIND_UNIFORM, -bound, bound
+        if leaf == "weight":  # every 1-D weight is a LayerNorm gamma
+            return KIND_UNIFORM, 0.8, 1.2
+        return KIND_UNIFORM, -0.1, 0.1  # Linear biases and LayerNorm betas
     if len(shape) == 4:
         fan_out = shape[0] * shape[2] * shape[3]
         return KIND_NORMAL, 0.0, float(np.sqrt(2.0 / fan_out))

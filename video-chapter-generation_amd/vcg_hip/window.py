@@ -1,0 +1,57 @@
+"""Window transformer (StackedVideoChapterAttention, reference model/fusion/stacked_window_self_attention.py:150-223)
+on libvcg_hip: one launch of window_attn.hip per batch of windows (inference).
+
+pack_window_weights() lays the module's f32 parameters out as window_attn.hip reads them (Linear weights
+transposed to [in][out] so a workgroup reads one weight row per k-step as consecutive words):
+  per layer l (6):  attention_norm g, b | query|key|value W^T [H][3H], bias [3H] | out_proj W^T [H][H], b |
+                    position_encoding w [H] (Linear(1, H) weight column), b | window_pos_bias [nh][P] |
+                    ffn_norm g, b | ffn.0 W^T [H][2H], b | ffn.3 W^T [2H][4H], b | ffn.6 W^T [4H][2H], b |
+                    ffn.9 W^T [2H][H], b
+  final_layer_norm g, b
+  classifier c in (0, 4, 8, 12): W^T, b, then its LayerNorm (c + 1) g, b ; classifier.16 W^T [H/4][2], b
+"""
+import torch
+
+from . import _lib
+from .ops import P, _chk, stream
+
+
+def _t(lin):
+    return lin.weight.detach().t().contiguous().reshape(-1)
+
+
+def pack_window_weights(m):
+    """Flat f32 device buffer of a StackedVideoChapterAttention's parameters (layout above)."""
+    parts = []
+    for layer in m.layers:
+        at = layer.attention
+        parts += [layer.attention_norm.weight, layer.attention_norm.bias]
+        parts.append(torch.cat([at.query.weight, at.key.weight, at.value.weight], 0).detach().t().contiguous()
+                     .reshape(-1))
+        parts += [torch.cat([at.query.bias, at.key.bias, at.value.bias]), _t(at.out_proj), at.out_proj.bias,
+                  at.position_encoding.weight.reshape(-1), at.position_encoding.bias,
+                  at.window_pos_bias.reshape(-1), layer.ffn_norm.weight, layer.ffn_norm.bias]
+        for i in (0, 3, 6, 9):
+            parts += [_t(layer.ffn[i]), layer.ffn[i].bias]
+    parts += [m.final_layer_norm.weight, m.final_layer_norm.bias]
+    for c in (0, 4, 8, 12):
+        parts += [_t(m.classifier[c]), m.classifier[c].bias, m.classifier[c + 1].weight, m.classifier[c + 1].bias]
+    parts += [_t(m.classifier[16]), m.classifier[16].bias]
+    return torch.cat([p.detach().reshape(-1).float() for p in parts]).contiguous()
+
+
+def window_attn_fwd(emb, weights, H, nh, P_len):
+    """emb [B, S, H] f32 (GPU) -> logits, prob [B, 2] f32."""
+    _chk(emb, torch.float32, "fusion_emb")
+    _chk(weights, torch.float32, "packed window weights")
+    B, S, Hd = emb.shape
+    if Hd != H:
+        raise RuntimeError(f"fusion_emb hidden size {Hd} != {H}")
+    need = _lib.query("vcg_window_attn_weight_floats", H, nh, P_len)
+    if weights.numel() != need:
+        raise RuntimeError(f"packed window weights have {weights.numel()} floats, expected {need}")
+    logits = torch.empty((B, 2), dtype=torch.float32, device=emb.device)
+    prob = torch.empty((B, 2), dtype=torch.float32, device=emb.device)
+    _lib.call("vcg_window_attn_fwd", P(emb), P(weights), weights.numel(), P(logits), P(prob), B, S, H, nh, P_len,
+              stream())
+    return logits, prob
