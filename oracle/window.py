@@ -52,3 +52,35 @@ def stacked_window_attention(p, emb, nh=16, n_layers=6):
         x = F.gelu(_ln(p, f"classifier.{c + 1}", _lin(p, f"classifier.{c}", x)))
     logits = _lin(p, "classifier.16", x)
     return logits, F.softmax(logits, dim=-1)
+
+
+def _chain(p, pre, x, n_lin, final_relu=False):
+    """Linear(pre.0) LN(pre.1) ReLU Dropout Linear(pre.4) ... Linear(pre.{4(n_lin-1)}) (eval)."""
+    for j in range(n_lin):
+        x = _lin(p, f"{pre}.{4 * j}", x)
+        if j < n_lin - 1:
+            x = F.relu(_ln(p, f"{pre}.{4 * j + 1}", x))
+    return F.relu(x) if final_relu else x
+
+
+def chapter_head_mlp_window(p, lang_emb, vision_emb, i, prefix="fusion_head."):
+    """Window ChapterHead.forward, head_type "mlp" (two_stream_window.py:251-272) for clip index i."""
+    B, T, _ = vision_emb.shape
+    lang_out = _chain(p, f"{prefix}lang_proj_heads.{i}", lang_emb, 2, final_relu=True)
+    vis_out = _chain(p, f"{prefix}vision_proj_heads.{i}", vision_emb.reshape(B * T, -1), 3, final_relu=True)
+    fusion = torch.cat([vis_out.view(B, T, -1), lang_out.unsqueeze(1)], 1).reshape(B, -1)
+    return _chain(p, f"{prefix}head.{i}", fusion, 3)
+
+
+def two_stream_window(p, img_clips, ids, mask, bn_mode="running", nh=16):
+    """Window TwoStream.forward (two_stream_window.py:391-444): per clip BERT pooler + TSM-ResNet-50 + window
+    ChapterHead, then StackedVideoChapterAttention. img_clips [B, n, T, 3, H, W], ids / mask [B, n, L]."""
+    from .model import bert, resnet50_tsm
+    B, n, T = img_clips.shape[:3]
+    embs = []
+    for i in range(n):
+        lang_emb, _ = bert(p, ids[:, i], mask[:, i])
+        vis = resnet50_tsm(p, img_clips[:, i].reshape(B * T, *img_clips.shape[3:]), T, bn_mode).view(B, T, -1)
+        embs.append(chapter_head_mlp_window(p, lang_emb, vis, i))
+    wp = {k[len("window_attn."):]: v for k, v in p.items() if k.startswith("window_attn.")}
+    return stacked_window_attention(wp, torch.stack(embs, 1), nh=nh)

@@ -218,3 +218,46 @@ def test_window_weight_packing_layout():
     at = m.layers[0].attention
     qkvT = flat[256:256 + 3 * 128 * 128].view(128, 384)
     assert torch.equal(qkvT[:, 128:256], at.key.weight.detach().t())
+
+
+def _window_two_stream(w=1, T=4, device=None):
+    """The native window TwoStream (two_stream_window.py drop-in) built and initialised like the c1win golden."""
+    import contextlib
+    import io
+    from model.fusion.two_stream_window import TwoStream
+    from model.lang.bert_hugface import BertHugface
+    from model.vision.resnet50_tsm import Resnet50TSM
+    from vcg_hip import synth
+    from vcg_hip.nn import BertConfig
+    with contextlib.redirect_stdout(io.StringIO()):
+        lang = BertHugface(pretrain_stage=False, config=BertConfig(output_attentions=True))
+    vis = Resnet50TSM(segments_size=T, shift_div=8, pretrain_stage=False)
+    m = TwoStream(lang.base_model, vis.base_model, lang.embed_size, vis.feature_dim, T, 128, w)
+    m.build_chapter_head(output_size=2, head_type="mlp")
+    if device is not None:
+        m = m.to(device)
+    synth.init_params(m, 123)
+    synth.load_bn_stats(m, dict(_gold("bn_running_stats.npz")))
+    return m.eval()
+
+
+def _c1win_inputs(B=2, n=3, T=4):
+    from vcg_hip import synth
+    frames, ids, mask, _ = synth.clip_batch(B * n, T, 112, 112, 32, seed=123)
+    return frames.view(B, n, T, 3, 112, 112), ids.view(B, n, 32), mask.view(B, n, 32)
+
+
+def test_oracle_two_stream_window_matches_reference():
+    """oracle.window.two_stream_window against the reference window TwoStream (two_stream_window.py:291-444,
+    head "mlp") at C1 shapes, running-stats eval; parameters by the native module's (= reference) names."""
+    from oracle import window as ow
+    torch.set_num_threads(min(8, os.cpu_count() or 8))
+    g = _gold("window_attn.npz")
+    m = _window_two_stream()
+    p = {n: t.detach() for n, t in m.named_parameters()}
+    p.update({n: b for n, b in m.named_buffers()})
+    frames, ids, mask = _c1win_inputs()
+    with torch.no_grad():
+        lg, pr = ow.two_stream_window(p, frames, ids, mask)
+    assert np.abs(lg.numpy() - g["c1win_logits"]).max() < 1e-4
+    assert np.abs(pr.numpy() - g["c1win_prob"]).max() < 1e-4

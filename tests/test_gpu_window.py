@@ -71,3 +71,35 @@ def test_window_attn_rejects_bad_input():
     m.train()
     with pytest.raises(RuntimeError):
         m(torch.randn(2, 3, 128, device=DEV))  # training: no native backward, no silent fallback
+
+
+def test_ln_act_matches_torch():
+    """vcg_ln_act_fwd (LayerNorm + ReLU / GELU row kernel) against torch fp32, rows of 96 / 1024 / 8 features."""
+    import torch.nn.functional as F
+    from vcg_hip.window import ln_act
+    for rows, D, act in [(7, 96, 1), (300, 1024, 2), (5, 8, 0)]:
+        ln = torch.nn.LayerNorm(D).to(DEV)
+        with torch.no_grad():
+            ln.weight.uniform_(0.5, 1.5)
+            ln.bias.uniform_(-0.5, 0.5)
+        x = torch.randn(rows, D, device=DEV) * 3 + 1
+        ref = F.layer_norm(x, (D,), ln.weight, ln.bias, ln.eps)
+        ref = F.relu(ref) if act == 1 else F.gelu(ref) if act == 2 else ref
+        out = ln_act(x, ln, act)
+        torch.cuda.synchronize()
+        assert (out - ref).abs().max().item() < 1e-4
+
+
+def test_two_stream_window_matches_reference_golden():
+    """The native window TwoStream (BERT + TSM-ResNet-50 engines per clip, window ChapterHead "mlp" on the fp32
+    GEMM / LN kernels, window transformer kernel) against the reference's own output at C1 shapes (c1win, 3 clips
+    of 4 x 112^2 + 32 tokens, batch 2, running-stats eval): logits / prob within 1e-3."""
+    from test_cpu_oracle import _c1win_inputs, _window_two_stream
+    g = np.load(os.path.join(GOLD, "window_attn.npz"), allow_pickle=False)
+    m = _window_two_stream(device=DEV)
+    frames, ids, mask = _c1win_inputs()
+    with torch.no_grad():
+        lg, pr = m(frames.to(DEV), ids.to(DEV), mask.to(DEV), None)
+    torch.cuda.synchronize()
+    assert np.abs(lg.cpu().numpy() - g["c1win_logits"]).max() < 1e-3
+    assert np.abs(pr.cpu().numpy() - g["c1win_prob"]).max() < 1e-3

@@ -15,6 +15,7 @@
 // packed once per weight version by the host as W^T ([in][out], f32), so the threads of a workgroup read
 // one weight row per k-step as consecutive 4-byte words (coalesced, L2-resident across windows).
 #include "common.h"
+#include "igemm.h"
 
 using namespace vcg;
 
@@ -192,6 +193,33 @@ __global__ void __launch_bounds__(kThreads) window_attn_fwd_kernel(const float* 
   }
 }
 
+// LayerNorm + activation over rows of a f32 matrix (the Linear -> LayerNorm -> ReLU chains of the window
+// ChapterHead, two_stream_window.py:145-176): one wave per row, two-pass statistics, act 0 / ACT_RELU / ACT_GELU.
+__global__ void __launch_bounds__(kThreads) ln_act_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                          const float* __restrict__ b, float* __restrict__ out, int rows,
+                                                          int D, float eps, int act) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * D;
+  float* o = out + (long long)row * D;
+  float sum = 0.f;
+  for (int d = lane; d < D; d += 64) sum += xr[d];
+  const float mean = warp_sum(sum) / (float)D;
+  float var = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float t = xr[d] - mean;
+    var = fmaf(t, t, var);
+  }
+  const float rstd = rsqrtf(warp_sum(var) / (float)D + eps);
+  for (int d = lane; d < D; d += 64) {
+    float v = (xr[d] - mean) * rstd * g[d] + b[d];
+    if (act == ACT_RELU) v = fmaxf(v, 0.f);
+    else if (act == ACT_GELU) v = gelu_erf(v);
+    o[d] = v;
+  }
+}
+
 }  // namespace
 
 // Packed f32 weight floats (layout documented in include/vcg_hip.h and vcg_hip/window.py pack_window_weights).
@@ -218,6 +246,19 @@ VCG_API int vcg_window_attn_fwd(const float* emb, const float* weights, long lon
   const size_t lds = (size_t)8 * S * H * sizeof(float);
   hipLaunchKernelGGL(window_attn_fwd_kernel, dim3(B), dim3(kThreads), lds, s, emb, weights, logits, prob, S, H, nh,
                      P);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_ln_act_fwd(const float* x, const float* gamma, const float* beta, float* out, int rows, int D,
+                           float eps, int act, hipStream_t s) {
+  VCG_REQUIRE(rows >= 0 && D >= 1, "bad shape");
+  VCG_REQUIRE(act == 0 || act == ACT_RELU || act == ACT_GELU, "act must be none, relu or gelu");
+  VCG_REQUIRE(x && gamma && beta && out, "null operand");
+  if (rows == 0) return VCG_OK;
+  constexpr int rpb = kThreads / 64;
+  hipLaunchKernelGGL(ln_act_kernel, dim3((rows + rpb - 1) / rpb), dim3(kThreads), 0, s, x, gamma, beta, out, rows, D,
+                     eps, act);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

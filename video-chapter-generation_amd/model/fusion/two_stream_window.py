@@ -1,0 +1,160 @@
+"""Drop-in for reference model/fusion/two_stream_window.py (CrossAttention 11-91, SelfAttention 93-131,
+ChapterHead 134-288, TwoStream 291-444): the window model that scores the middle clip of 2w+1 consecutive
+clips. Same constructors, submodule / parameter names and head types; inference runs on libvcg_hip:
+
+  per clip i:  BERT pooler (native BertModel), TSM-ResNet-50 trunk (native ResNet50 engine),
+               ChapterHead(window_idx=i): the Linear -> LayerNorm -> ReLU chains as fp32 GEMMs with fused
+               bias/activation epilogues + one LayerNorm/activation row kernel (vcg_hip/window.py mlp_chain)
+  window:      StackedVideoChapterAttention over the stacked [B, 2w+1, hidden] fusion embeddings
+               (one window_attn.hip launch).
+
+Native scope: eval-mode forward with head_type "mlp" (the drivers' default, train_video_segment_update_accumulate.py
+:443). The other head types ("bilinear", "multiplication", "self_attn", "cross_attn") are constructed with the
+reference's parameters (state dicts load) but their forward raises, as does training: no CPU / eager fallback.
+"""
+import torch
+from torch import nn
+from einops import rearrange
+
+from vcg_hip.optim import param_groups
+from vcg_hip.window import linear, mlp_chain
+
+from .stacked_window_self_attention import StackedVideoChapterAttention
+
+
+class CrossAttention(nn.Module):
+    """two_stream_window.py:11-91 (parameters only)."""
+
+    def __init__(self, hidden_size, num_heads, dropout=0.1):
+        super().__init__()
+        if hidden_size % num_heads != 0:
+            raise ValueError(f"The hidden size {hidden_size} is not a multiple of the number of attention "
+                             f"heads {num_heads}.")
+        self.hidden_size, self.num_heads, self.head_dim = hidden_size, num_heads, hidden_size // num_heads
+        self.query_proj = nn.Linear(hidden_size, hidden_size)
+        self.key_proj = nn.Linear(hidden_size, hidden_size)
+        self.value_proj = nn.Linear(hidden_size, hidden_size)
+        self.out_proj = nn.Linear(hidden_size, hidden_size)
+        self.lang_norm = nn.LayerNorm(hidden_size)
+        self.vision_norm = nn.LayerNorm(hidden_size)
+        self.attention_dropout = nn.Dropout(dropout)
+        self.output_dropout = nn.Dropout(dropout)
+        self.frame_pos_encoding = nn.Linear(1, hidden_size)
+
+
+class SelfAttention(nn.Module):
+    """two_stream_window.py:93-131 (parameters only)."""
+
+    def __init__(self, n_embd, n_head, output_size, attn_pdrop=0.1, resid_pdrop=0.1):
+        super().__init__()
+        assert n_embd % n_head == 0
+        self.n_head, self.n_embd = n_head, n_embd
+        self.key = nn.Linear(n_embd, n_embd)
+        self.query = nn.Linear(n_embd, n_embd)
+        self.value = nn.Linear(n_embd, n_embd)
+        self.attn_drop = nn.Dropout(attn_pdrop)
+        self.resid_drop = nn.Dropout(resid_pdrop)
+        self.proj = nn.Linear(n_embd, output_size)
+
+
+def _proj(i, h1, h2, o):
+    """Linear(i, h1) LN ReLU Dropout Linear(h1, h2) LN ReLU Dropout Linear(h2, o) (the per-clip projections)."""
+    return nn.Sequential(nn.Linear(i, h1), nn.LayerNorm(h1), nn.ReLU(), nn.Dropout(0.1),
+                         nn.Linear(h1, h2), nn.LayerNorm(h2), nn.ReLU(), nn.Dropout(0.1), nn.Linear(h2, o))
+
+
+class ChapterHead(nn.Module):
+    """two_stream_window.py:134-288: per-clip (window_idx) projection heads and fusion head."""
+
+    def __init__(self, lang_emb_size, vision_emb_size, segment_size, hidden_size, window_size, output_size,
+                 head_type="mlp"):
+        super().__init__()
+        self.lang_emb_size, self.vision_emb_size = lang_emb_size, vision_emb_size
+        self.segment_size, self.hidden_size, self.head_type = segment_size, hidden_size, head_type
+        self.window_size = window_size
+        self.num_clips = n = 2 * window_size + 1
+        h = hidden_size
+        self.lang_proj_heads = nn.ModuleList([
+            nn.Sequential(nn.Linear(lang_emb_size, lang_emb_size // 2), nn.LayerNorm(lang_emb_size // 2), nn.ReLU(),
+                          nn.Dropout(0.1), nn.Linear(lang_emb_size // 2, h)) for _ in range(n)])
+        self.vision_proj_heads = nn.ModuleList([_proj(vision_emb_size, 8 * h, 4 * h, h) for _ in range(n)])
+        if head_type == "mlp":
+            self.head = nn.ModuleList([_proj((segment_size + 1) * h, 8 * h, 4 * h, h) for _ in range(n)])
+        elif head_type == "bilinear":
+            self.bilinear_layers = nn.ModuleList([nn.Bilinear(h, h * segment_size, h * 2) for _ in range(n)])
+            self.head = nn.ModuleList([
+                nn.Sequential(nn.LayerNorm(h * 2), nn.ReLU(), nn.Dropout(0.1), nn.Linear(h * 2, h), nn.LayerNorm(h),
+                              nn.ReLU(), nn.Dropout(0.1), nn.Linear(h, h)) for _ in range(n)])
+        elif head_type == "multiplication":
+            self.lang_expand_layers = nn.ModuleList([
+                nn.Sequential(nn.Linear(h, h * 8), nn.LayerNorm(h * 8), nn.ReLU(), nn.Dropout(0.1),
+                              nn.Linear(h * 8, h * segment_size), nn.LayerNorm(h * segment_size), nn.ReLU(),
+                              nn.Dropout(0.1)) for _ in range(n)])
+            self.head = nn.ModuleList([_proj(h * segment_size, 8 * h, 4 * h, h) for _ in range(n)])
+        elif head_type == "self_attn":
+            self.head = SelfAttention(h, 4, h)
+        elif head_type == "cross_attn":
+            self.head = CrossAttention(h, num_heads=16)
+            self.output_proj = nn.Linear(h, output_size)
+        else:
+            raise RuntimeError(f"Unknown head_type {head_type}")
+
+    def forward(self, lang_emb, vision_emb, window_idx):
+        """lang_emb [B, lang_emb_size], vision_emb [B, segment_size, vision_emb_size] (f32) -> [B, hidden]."""
+        from vcg_hip.ops import ACT_RELU
+        if self.head_type != "mlp":
+            raise RuntimeError(f"window ChapterHead head_type {self.head_type!r} has no native forward yet "
+                               "(native: 'mlp')")
+        B = lang_emb.shape[0]
+        lp, vp = self.lang_proj_heads[window_idx], self.vision_proj_heads[window_idx]
+        lang_out = linear(mlp_chain(lang_emb.float().contiguous(), lp[:-1]), lp[-1], ACT_RELU)  # :262-263
+        vis = vision_emb.reshape(-1, self.vision_emb_size).float().contiguous()
+        vision_out = linear(mlp_chain(vis, vp[:-1]), vp[-1], ACT_RELU)                           # :265-267
+        fusion = torch.cat([vision_out.view(B, self.segment_size, self.hidden_size), lang_out.unsqueeze(1)], 1)
+        return mlp_chain(fusion.view(B, -1), self.head[window_idx])                                 # :269-272
+
+
+class TwoStream(nn.Module):
+    """two_stream_window.py:291-444. forward(img_clips [B, 2w+1, T, 3, H, W], text_ids [B, 2w+1, L],
+    attention_masks [B, 2w+1, L], clip_info) -> (logits [B, 2], prob [B, 2]) of each window's middle clip."""
+
+    def __init__(self, lang_model, vision_model, lang_embed_size, vision_embed_size, segment_size, hidden_size,
+                 window_size):
+        super().__init__()
+        self.lang_model = lang_model
+        self.vision_model = vision_model
+        self.segment_size = segment_size
+        self.lang_embed_size = lang_embed_size
+        self.vision_embed_size = vision_embed_size
+        self.hidden_size = hidden_size
+        self.window_size = window_size
+        h, layers, d = hidden_size, [], hidden_size * (2 * window_size + 1)
+        for o in (h, h // 2, h // 4, h // 8, h // 16):  # window_mlp (:303-331; unused by the forward, kept for
+            layers += [nn.Linear(d, o), nn.LayerNorm(o), nn.ReLU(), nn.Dropout(0.1)]  # state-dict parity)
+            d = o
+        self.window_mlp = nn.Sequential(*layers, nn.Linear(h // 16, 2))
+
+    def build_chapter_head(self, output_size, head_type="mlp"):
+        self.fusion_head = ChapterHead(self.lang_embed_size, self.vision_embed_size, self.segment_size,
+                                       self.hidden_size, self.window_size, output_size, head_type)
+        cfg = type("Config", (), {"hidden_size": self.hidden_size, "num_attention_heads": 16,
+                                  "attention_probs_dropout_prob": 0.1, "window_size": self.window_size})
+        self.window_attn = StackedVideoChapterAttention(cfg)
+
+    def configure_optimizers(self, train_config):
+        """AdamW with the reference's decay grouping (:355-388)."""
+        return torch.optim.AdamW(param_groups(self, train_config.weight_decay), lr=train_config.learning_rate,
+                                 betas=train_config.betas)
+
+    def forward(self, img_clips, text_ids, attention_masks, clip_info=None):
+        if self.training and torch.is_grad_enabled():
+            raise RuntimeError("window TwoStream: only inference (eval mode) runs natively on MI355X")
+        B, n_clips, _ = text_ids.shape
+        embs = []
+        for i in range(n_clips):  # :395-433
+            lang_emb = self.lang_model(input_ids=text_ids[:, i, :].contiguous(),
+                                       attention_mask=attention_masks[:, i, :].contiguous()).pooler_output
+            img = rearrange(img_clips[:, i], "b t c h w -> (b t) c h w").contiguous()
+            vision_emb = self.vision_model(img).view(B, self.segment_size, -1)
+            embs.append(self.fusion_head(lang_emb, vision_emb, i))
+        return self.window_attn(torch.stack(embs, 1).contiguous(), clip_info)  # :435-444

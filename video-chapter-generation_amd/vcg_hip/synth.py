@@ -110,6 +110,8 @@ def init_rule(name, shape):
     if "LayerNorm" in name:
         return (KIND_UNIFORM, 0.8, 1.2) if leaf == "weight" else (KIND_UNIFORM, -0.1, 0.1)
     if "fusion_head" in name or name.startswith(("head.", "lang_proj_head", "vision_proj_head")):
+        if len(shape) == 1 and leaf == "weight":  # LayerNorm gamma of the window ChapterHead's projection chains
+            return KIND_UNIFORM, 0.8, 1.2
         fan_in = shape[-1] if len(shape) == 2 else None
         if fan_in is None:  # bias: bound from the matching weight's fan_in is not known here; use 1/sqrt(D)
             fan_in = max(1, shape[0])

@@ -55,3 +55,42 @@ def window_attn_fwd(emb, weights, H, nh, P_len):
     _lib.call("vcg_window_attn_fwd", P(emb), P(weights), weights.numel(), P(logits), P(prob), B, S, H, nh, P_len,
               stream())
     return logits, prob
+
+
+def ln_act(x, ln, act):
+    """act(LayerNorm(x)) for x [rows, D] f32 with an nn.LayerNorm's parameters (act: ops.ACT_*)."""
+    _chk(x, torch.float32, "LayerNorm input")
+    D = x.shape[-1]
+    out = torch.empty_like(x)
+    _lib.call("vcg_ln_act_fwd", P(x), P(ln.weight), P(ln.bias), P(out), x.numel() // D, D, float(ln.eps), int(act),
+              stream())
+    return out
+
+
+def linear(x, lin, act=0):
+    """act(x W^T + b) on the fp32 GEMM path (x [rows, in] f32)."""
+    from .ops import gemm
+    _chk(x, torch.float32, "Linear input")
+    M, K = x.shape
+    N = lin.weight.shape[0]
+    return gemm(x, lin.weight, M, N, K, K, K, bias=lin.bias, act=act)
+
+
+def mlp_chain(x, seq):
+    """Run an nn.Sequential of Linear / LayerNorm / ReLU / GELU / Dropout (eval) natively: Linear + activation
+    fuse into the GEMM epilogue, LayerNorm + activation into one row kernel."""
+    from .ops import ACT_GELU, ACT_RELU
+    mods = [m for m in seq if not isinstance(m, torch.nn.Dropout)]
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        nxt = mods[i + 1] if i + 1 < len(mods) else None
+        act = ACT_RELU if isinstance(nxt, torch.nn.ReLU) else ACT_GELU if isinstance(nxt, torch.nn.GELU) else 0
+        if isinstance(m, torch.nn.Linear):
+            x = linear(x, m, act)
+        elif isinstance(m, torch.nn.LayerNorm):
+            x = ln_act(x, m, act)
+        else:
+            raise RuntimeError(f"mlp_chain: unsupported module {type(m).__name__}")
+        i += 2 if act else 1
+    return x
