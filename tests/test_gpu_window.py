@@ -53,6 +53,23 @@ def test_window_attn_matches_oracle(H, w, nh, B):
     assert np.abs(pr.cpu().numpy() - ref_pr.numpy()).max() < 1e-3
 
 
+@pytest.mark.parametrize("G", ["1", "2", "3", "5"])
+def test_window_attn_windows_per_workgroup(G, monkeypatch):
+    """Several windows per workgroup (VCG_WINDOW_G; the default picks G from the batch size): identical math per
+    window, including a ragged last workgroup (B = 61)."""
+    from oracle import window as ow
+    monkeypatch.setenv("VCG_WINDOW_G", G)
+    w = 1 if G == "5" else 2
+    m = _module(128, w, seed=5)
+    emb = torch.randn(61, 2 * w + 1, 128, generator=torch.Generator().manual_seed(3))
+    ref_lg, _ = ow.stacked_window_attention({n: t.detach() for n, t in m.named_parameters()}, emb)
+    m = m.to(DEV)
+    with torch.no_grad():
+        lg, _ = m(emb.to(DEV))
+    torch.cuda.synchronize()
+    assert np.abs(lg.cpu().numpy() - ref_lg.numpy()).max() < 1e-3
+
+
 def test_window_attn_repacks_after_weight_update():
     m = _module(128, 1).to(DEV)
     emb = torch.randn(4, 3, 128, device=DEV)

@@ -23,10 +23,12 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxS = 16;
-constexpr int kMaxSH = 2048;  // LDS: 8 * S * H floats <= 64 KB
+constexpr int kMaxSH = 2048;  // LDS: 8 * rows * H floats <= 64 KB
 constexpr int kLayers = 6;
 
-// out[s][n] = act(sum_k in[s][k] * WT[k][n] + b[n]) (+ out[s][n] when ACC); in / out in LDS.
+// out[s][n] = act(sum_k in[s][k] * WT[k][n] + b[n]) (+ out[s][n] when ACC); in / out in LDS. A thread owns
+// whole columns and keeps up to 8 weight loads in flight (L2 / MALL latency bound). (Splitting K over idle
+// threads for the narrow layers, with an LDS reduction, measured 1.7x slower.)
 template <bool ACC>
 __device__ void lin(const float* in, int S, int K, const float* __restrict__ WT, const float* __restrict__ b, int N,
                     float* out, bool gelu) {
@@ -34,6 +36,7 @@ __device__ void lin(const float* in, int S, int K, const float* __restrict__ WT,
     float acc[kMaxS];
 #pragma unroll
     for (int s = 0; s < kMaxS; ++s) acc[s] = 0.f;
+#pragma unroll 8
     for (int k = 0; k < K; ++k) {
       const float w = WT[(long long)k * N + n];
 #pragma unroll
@@ -81,14 +84,18 @@ __device__ void layer_norm(const float* in, int S, int D, const float* __restric
 
 __global__ void __launch_bounds__(kThreads) window_attn_fwd_kernel(const float* __restrict__ emb,
                                                                    const float* __restrict__ W, float* __restrict__ logits,
-                                                                   float* __restrict__ prob, int S, int H, int nh, int P) {
+                                                                   float* __restrict__ prob, int B, int S, int G, int H,
+                                                                   int nh, int P) {
+  // G windows per workgroup (R = G * S rows): every weight row read from L2 feeds all R rows; attention,
+  // position encoding and the target-clip pick stay per window.
   extern __shared__ float sm[];
-  const int SH = S * H, hd = H / nh, mid = S / 2, tid = threadIdx.x;
-  float* X = sm;            // residual stream [S][H]
-  float* Nn = X + SH;       // normed input / attention context / FFN output [S][H]
-  float* T1 = Nn + SH;      // Q K V [S][3H] / FFN hidden [S][4H]
-  float* T2 = T1 + 4 * SH;  // FFN hidden [S][2H]
-  const float* src = emb + (long long)blockIdx.x * SH;
+  const int w0 = blockIdx.x * G, g_n = min(G, B - w0);
+  const int R = g_n * S, SH = R * H, hd = H / nh, mid = S / 2, tid = threadIdx.x;
+  float* X = sm;            // residual stream [R][H]
+  float* Nn = X + SH;       // normed input / attention context / FFN output [R][H]
+  float* T1 = Nn + SH;      // Q K V [R][3H] / FFN hidden [R][4H]
+  float* T2 = T1 + 4 * SH;  // FFN hidden [R][2H]
+  const float* src = emb + (long long)w0 * S * H;
   for (int i = tid; i < SH; i += kThreads) X[i] = src[i];
   __syncthreads();
   const float pden = (float)((double)mid + 1e-6);
@@ -115,22 +122,22 @@ __global__ void __launch_bounds__(kThreads) window_attn_fwd_kernel(const float* 
     const float* f3b = f3T + 2 * H * H;
     w = f3b + H;
 
-    layer_norm(X, S, H, ln_g, ln_b, Nn, false);
+    layer_norm(X, R, H, ln_g, ln_b, Nn, false);
     for (int i = tid; i < SH; i += kThreads) {
-      const int s = i / H, d = i - s * H;
+      const int r = i / H, d = i - r * H, s = r % S;
       Nn[i] += fmaf(pe_w[d], (float)(s - mid) / pden, pe_b[d]);
     }
     __syncthreads();
-    lin<false>(Nn, S, H, qkvT, qkvb, 3 * H, T1, false);  // T1[s] = [q | k | v]
-    // one thread per (head, query row): scores over the S keys in registers, softmax, context -> Nn
-    for (int t = tid; t < nh * S; t += kThreads) {
-      const int h = t / S, i = t - h * S;
+    lin<false>(Nn, R, H, qkvT, qkvb, 3 * H, T1, false);  // T1[r] = [q | k | v]
+    // one thread per (head, query row): scores over its window's S keys in registers, softmax, context -> Nn
+    for (int t = tid; t < nh * R; t += kThreads) {
+      const int h = t / R, i = t - h * R, kb = (i / S) * S;  // kb: first row of this query's window
       const float* q = T1 + i * 3 * H + h * hd;
       float sc[kMaxS], mx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < kMaxS; ++j) {
         if (j < S) {
-          const float* k = T1 + j * 3 * H + H + h * hd;
+          const float* k = T1 + (kb + j) * 3 * H + H + h * hd;
           float a = 0.f;
           for (int d = 0; d < hd; ++d) a = fmaf(q[d], k[d], a);
           sc[j] = a * qscale + wpb[h * P + j];
@@ -149,22 +156,28 @@ __global__ void __launch_bounds__(kThreads) window_attn_fwd_kernel(const float* 
         float a = 0.f;
 #pragma unroll
         for (int j = 0; j < kMaxS; ++j)
-          if (j < S) a = fmaf(sc[j], T1[j * 3 * H + 2 * H + h * hd + d], a);
+          if (j < S) a = fmaf(sc[j], T1[(kb + j) * 3 * H + 2 * H + h * hd + d], a);
         Nn[i * H + h * hd + d] = a * inv;
       }
     }
     __syncthreads();
-    lin<true>(Nn, S, H, oT, ob, H, X, false);  // X += out_proj(ctx)
-    layer_norm(X, S, H, f_g, f_b, Nn, false);
-    lin<false>(Nn, S, H, f0T, f0b, 2 * H, T2, true);
-    lin<false>(T2, S, 2 * H, f1T, f1b, 4 * H, T1, true);
-    lin<false>(T1, S, 4 * H, f2T, f2b, 2 * H, T2, true);
-    lin<true>(T2, S, 2 * H, f3T, f3b, H, X, false);  // X += FFN
+    lin<true>(Nn, R, H, oT, ob, H, X, false);  // X += out_proj(ctx)
+    layer_norm(X, R, H, f_g, f_b, Nn, false);
+    lin<false>(Nn, R, H, f0T, f0b, 2 * H, T2, true);
+    lin<false>(T2, R, 2 * H, f1T, f1b, 4 * H, T1, true);
+    lin<false>(T1, R, 4 * H, f2T, f2b, 2 * H, T2, true);
+    lin<true>(T2, R, 2 * H, f3T, f3b, H, X, false);  // X += FFN
   }
-  // final LayerNorm of the middle (target) clip only, then the classifier on that one row
+  // final LayerNorm of each window's middle (target) clip only (gathered to rows 0..g_n-1 of T2), then the
+  // classifier on those g_n rows
+  for (int i = tid; i < g_n * H; i += kThreads) {
+    const int g = i / H, d = i - g * H;
+    T2[i] = X[(g * S + mid) * H + d];
+  }
+  __syncthreads();
   const float *fin_g = w, *fin_b = w + H;
   w = fin_b + H;
-  layer_norm(X + mid * H, 1, H, fin_g, fin_b, Nn, false);
+  layer_norm(T2, g_n, H, fin_g, fin_b, Nn, false);
   float* a = Nn;
   float* t = T1;
   const int dims[5] = {H, H, H, H / 2, H / 4};
@@ -175,20 +188,21 @@ __global__ void __launch_bounds__(kThreads) window_attn_fwd_kernel(const float* 
     const float* lg = cb + N;
     const float* lb = lg + N;
     w = lb + N;
-    lin<false>(a, 1, K, cT, cb, N, t, false);
-    layer_norm(t, 1, N, lg, lb, a, true);  // LN then GELU
+    lin<false>(a, g_n, K, cT, cb, N, t, false);
+    layer_norm(t, g_n, N, lg, lb, a, true);  // LN then GELU
   }
   const float* cT = w;
   const float* cb = cT + (H / 4) * 2;
-  lin<false>(a, 1, H / 4, cT, cb, 2, t, false);
-  if (tid == 0) {
-    const float l0 = t[0], l1 = t[1], m = fmaxf(l0, l1);
+  lin<false>(a, g_n, H / 4, cT, cb, 2, t, false);
+  if (tid < g_n) {
+    const float l0 = t[2 * tid], l1 = t[2 * tid + 1], m = fmaxf(l0, l1);
     const float e0 = expf(l0 - m), e1 = expf(l1 - m), inv = 1.f / (e0 + e1);
-    logits[2 * blockIdx.x] = l0;
-    logits[2 * blockIdx.x + 1] = l1;
+    const long long o = 2LL * (w0 + tid);
+    logits[o] = l0;
+    logits[o + 1] = l1;
     if (prob) {
-      prob[2 * blockIdx.x] = e0 * inv;
-      prob[2 * blockIdx.x + 1] = e1 * inv;
+      prob[o] = e0 * inv;
+      prob[o + 1] = e1 * inv;
     }
   }
 }
@@ -243,9 +257,16 @@ VCG_API int vcg_window_attn_fwd(const float* emb, const float* weights, long lon
   VCG_REQUIRE(weight_floats >= vcg_window_attn_weight_floats(H, nh, P), "packed weight buffer too small");
   VCG_REQUIRE(emb && weights && logits, "null operand");
   if (B == 0) return VCG_OK;
-  const size_t lds = (size_t)8 * S * H * sizeof(float);
-  hipLaunchKernelGGL(window_attn_fwd_kernel, dim3(B), dim3(kThreads), lds, s, emb, weights, logits, prob, S, H, nh,
-                     P);
+  // as many windows per workgroup as fit the row budget (R = G * S <= 16 rows, R * H <= 2048 floats), but keep
+  // at least one workgroup per CU when the batch is small
+  int G = min(kMaxS / S, kMaxSH / (S * H));
+  if (const char* e = getenv("VCG_WINDOW_G")) G = min(G, atoi(e));  // fixed G (tests, A/B in tools/bench_window.py)
+  else
+    while (G > 1 && (B + G - 1) / G < 1024) --G;  // measured (S = 5): G = 1 best at 512 windows, G = 3 at 4096
+  if (G < 1) G = 1;
+  const size_t lds = (size_t)8 * G * S * H * sizeof(float);
+  hipLaunchKernelGGL(window_attn_fwd_kernel, dim3((B + G - 1) / G), dim3(kThreads), lds, s, emb, weights, logits,
+                     prob, B, S, G, H, nh, P);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
