@@ -152,6 +152,11 @@ VCG_API int vcg_head_attn_bwd(int dtype, const float* saved, const float* Wq, co
  * transposed to [in][out]); logits / prob [B][2]. */
 VCG_API long long vcg_window_attn_weight_floats(int H, int nh, int P);
 VCG_API int vcg_window_attn_fwd(const float* emb, const float* weights, long long weight_floats, float* logits, float* prob, int B, int S, int H, int nh, int P, hipStream_t s);
+/* CrossAttention of the window ChapterHead, head_type "cross_attn" (two_stream_window.py:11-91): lang [B][H] and vis
+ * [B][T][H] (the ReLU'd projections) -> out [B][H]; 2 <= T <= 16, T*H <= 2048. `weights` packed by
+ * vcg_hip/window.py pack_cross_attn_weights (LN / pos-encoding vectors, then q, k|v, out Linear weights as W^T). */
+VCG_API long long vcg_cross_attn_weight_floats(int H);
+VCG_API int vcg_cross_attn_fwd(const float* lang, const float* vis, const float* weights, long long weight_floats, float* out, int B, int T, int H, int nh, hipStream_t s);
 /* out = act(LayerNorm(x) * gamma + beta) over `rows` rows of D f32 features (window ChapterHead's Linear -> LN -> ReLU
  * chains, two_stream_window.py:145-176); act 0 = none, 1 = ReLU, 2 = GELU (erf). */
 VCG_API int vcg_ln_act_fwd(const float* x, const float* gamma, const float* beta, float* out, int rows, int D, float eps, int act, hipStream_t s);

@@ -63,16 +63,35 @@ def _chain(p, pre, x, n_lin, final_relu=False):
     return F.relu(x) if final_relu else x
 
 
-def chapter_head_mlp_window(p, lang_emb, vision_emb, i, prefix="fusion_head."):
-    """Window ChapterHead.forward, head_type "mlp" (two_stream_window.py:251-272) for clip index i."""
+def cross_attention(p, pre, lang, vis, nh=16):
+    """CrossAttention.forward (two_stream_window.py:60-91), dropout inactive. lang [B, H], vis [B, T, H]."""
+    B, T, H = vis.shape
+    hd = H // nh
+    lang = _ln(p, pre + "lang_norm", lang)
+    vis = _ln(p, pre + "vision_norm", vis)
+    pos = (torch.arange(T).float() / (T - 1)).unsqueeze(-1)  # :55-58
+    vis = vis + _lin(p, pre + "frame_pos_encoding", pos)
+    q = _lin(p, pre + "query_proj", lang).view(B, 1, nh, hd).transpose(1, 2)
+    k = _lin(p, pre + "key_proj", vis).view(B, T, nh, hd).transpose(1, 2)
+    v = _lin(p, pre + "value_proj", vis).view(B, T, nh, hd).transpose(1, 2)
+    a = F.softmax(q @ k.transpose(-2, -1) / math.sqrt(hd), dim=-1)
+    ctx = (a @ v).transpose(1, 2).reshape(B, H)
+    return _lin(p, pre + "out_proj", ctx)
+
+
+def chapter_head_mlp_window(p, lang_emb, vision_emb, i, prefix="fusion_head.", head_type="mlp"):
+    """Window ChapterHead.forward (two_stream_window.py:251-288) for clip index i, head_type "mlp" or
+    "cross_attn"."""
     B, T, _ = vision_emb.shape
     lang_out = _chain(p, f"{prefix}lang_proj_heads.{i}", lang_emb, 2, final_relu=True)
     vis_out = _chain(p, f"{prefix}vision_proj_heads.{i}", vision_emb.reshape(B * T, -1), 3, final_relu=True)
+    if head_type == "cross_attn":
+        return cross_attention(p, f"{prefix}head.", lang_out, vis_out.view(B, T, -1))
     fusion = torch.cat([vis_out.view(B, T, -1), lang_out.unsqueeze(1)], 1).reshape(B, -1)
     return _chain(p, f"{prefix}head.{i}", fusion, 3)
 
 
-def two_stream_window(p, img_clips, ids, mask, bn_mode="running", nh=16):
+def two_stream_window(p, img_clips, ids, mask, bn_mode="running", nh=16, head_type="mlp"):
     """Window TwoStream.forward (two_stream_window.py:391-444): per clip BERT pooler + TSM-ResNet-50 + window
     ChapterHead, then StackedVideoChapterAttention. img_clips [B, n, T, 3, H, W], ids / mask [B, n, L]."""
     from .model import bert, resnet50_tsm
@@ -81,6 +100,6 @@ def two_stream_window(p, img_clips, ids, mask, bn_mode="running", nh=16):
     for i in range(n):
         lang_emb, _ = bert(p, ids[:, i], mask[:, i])
         vis = resnet50_tsm(p, img_clips[:, i].reshape(B * T, *img_clips.shape[3:]), T, bn_mode).view(B, T, -1)
-        embs.append(chapter_head_mlp_window(p, lang_emb, vis, i))
+        embs.append(chapter_head_mlp_window(p, lang_emb, vis, i, head_type=head_type))
     wp = {k[len("window_attn."):]: v for k, v in p.items() if k.startswith("window_attn.")}
     return stacked_window_attention(wp, torch.stack(embs, 1), nh=nh)

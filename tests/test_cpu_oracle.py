@@ -220,7 +220,7 @@ def test_window_weight_packing_layout():
     assert torch.equal(qkvT[:, 128:256], at.key.weight.detach().t())
 
 
-def _window_two_stream(w=1, T=4, device=None):
+def _window_two_stream(w=1, T=4, device=None, head_type="mlp"):
     """The native window TwoStream (two_stream_window.py drop-in) built and initialised like the c1win golden."""
     import contextlib
     import io
@@ -233,7 +233,7 @@ def _window_two_stream(w=1, T=4, device=None):
         lang = BertHugface(pretrain_stage=False, config=BertConfig(output_attentions=True))
     vis = Resnet50TSM(segments_size=T, shift_div=8, pretrain_stage=False)
     m = TwoStream(lang.base_model, vis.base_model, lang.embed_size, vis.feature_dim, T, 128, w)
-    m.build_chapter_head(output_size=2, head_type="mlp")
+    m.build_chapter_head(output_size=2, head_type=head_type)
     if device is not None:
         m = m.to(device)
     synth.init_params(m, 123)
@@ -247,17 +247,18 @@ def _c1win_inputs(B=2, n=3, T=4):
     return frames.view(B, n, T, 3, 112, 112), ids.view(B, n, 32), mask.view(B, n, 32)
 
 
-def test_oracle_two_stream_window_matches_reference():
+@pytest.mark.parametrize("head_type,tag", [("mlp", "c1win"), ("cross_attn", "c1xattn")])
+def test_oracle_two_stream_window_matches_reference(head_type, tag):
     """oracle.window.two_stream_window against the reference window TwoStream (two_stream_window.py:291-444,
     head "mlp") at C1 shapes, running-stats eval; parameters by the native module's (= reference) names."""
     from oracle import window as ow
     torch.set_num_threads(min(8, os.cpu_count() or 8))
     g = _gold("window_attn.npz")
-    m = _window_two_stream()
+    m = _window_two_stream(head_type=head_type)
     p = {n: t.detach() for n, t in m.named_parameters()}
     p.update({n: b for n, b in m.named_buffers()})
     frames, ids, mask = _c1win_inputs()
     with torch.no_grad():
-        lg, pr = ow.two_stream_window(p, frames, ids, mask)
-    assert np.abs(lg.numpy() - g["c1win_logits"]).max() < 1e-4
-    assert np.abs(pr.numpy() - g["c1win_prob"]).max() < 1e-4
+        lg, pr = ow.two_stream_window(p, frames, ids, mask, head_type=head_type)
+    assert np.abs(lg.numpy() - g[f"{tag}_logits"]).max() < 1e-4
+    assert np.abs(pr.numpy() - g[f"{tag}_prob"]).max() < 1e-4

@@ -107,16 +107,36 @@ def test_ln_act_matches_torch():
         assert (out - ref).abs().max().item() < 1e-4
 
 
-def test_two_stream_window_matches_reference_golden():
+@pytest.mark.parametrize("T,H,nh,B", [(16, 128, 16, 64), (4, 128, 16, 3), (2, 64, 8, 5)])
+def test_cross_attn_matches_oracle(T, H, nh, B):
+    """vcg_cross_attn_fwd (window ChapterHead "cross_attn", two_stream_window.py:11-91) against the oracle."""
+    from model.fusion.two_stream_window import CrossAttention
+    from oracle import window as ow
+    from vcg_hip import synth
+    from vcg_hip.window import cross_attn_fwd, pack_cross_attn_weights
+    ca = CrossAttention(H, nh)
+    synth.init_params(ca, 9, prefix="fusion_head.head.")
+    gen = torch.Generator().manual_seed(T * 7 + H)
+    lang, vis = torch.rand(B, H, generator=gen), torch.rand(B, T, H, generator=gen)  # post-ReLU-like inputs
+    ref = ow.cross_attention({n: t.detach() for n, t in ca.named_parameters()}, "", lang, vis, nh=nh)
+    ca = ca.to(DEV)
+    out = cross_attn_fwd(lang.to(DEV), vis.to(DEV), pack_cross_attn_weights(ca), H, nh)
+    torch.cuda.synchronize()
+    assert (out.cpu() - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("head_type,tag", [("mlp", "c1win"), ("cross_attn", "c1xattn")])
+def test_two_stream_window_matches_reference_golden(head_type, tag):
     """The native window TwoStream (BERT + TSM-ResNet-50 engines per clip, window ChapterHead "mlp" on the fp32
-    GEMM / LN kernels, window transformer kernel) against the reference's own output at C1 shapes (c1win, 3 clips
+    GEMM / LN kernels or the cross-attention kernel, window transformer kernel) against the reference's own output
+    at C1 shapes (c1win / c1xattn, 3 clips
     of 4 x 112^2 + 32 tokens, batch 2, running-stats eval): logits / prob within 1e-3."""
     from test_cpu_oracle import _c1win_inputs, _window_two_stream
     g = np.load(os.path.join(GOLD, "window_attn.npz"), allow_pickle=False)
-    m = _window_two_stream(device=DEV)
+    m = _window_two_stream(device=DEV, head_type=head_type)
     frames, ids, mask = _c1win_inputs()
     with torch.no_grad():
         lg, pr = m(frames.to(DEV), ids.to(DEV), mask.to(DEV), None)
     torch.cuda.synchronize()
-    assert np.abs(lg.cpu().numpy() - g["c1win_logits"]).max() < 1e-3
-    assert np.abs(pr.cpu().numpy() - g["c1win_prob"]).max() < 1e-3
+    assert np.abs(lg.cpu().numpy() - g[f"{tag}_logits"]).max() < 1e-3
+    assert np.abs(pr.cpu().numpy() - g[f"{tag}_prob"]).max() < 1e-3

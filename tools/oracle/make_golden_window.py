@@ -8,7 +8,7 @@ tests/golden/window_attn.npz
       (dropout inactive); weights from vcg_hip/synth.py by state-dict name with prefix "window_attn."; inputs
       from numpy's default_rng(11 + w).
   short_*: window_size 2 module fed S = 3 clips (the reference slices window_pos_bias[..., :S]).
-  c1win_*: the full window TwoStream at C1 shapes (see c1_window).
+  c1win_* / c1xattn_*: the full window TwoStream at C1 shapes with head_type "mlp" / "cross_attn" (c1_window).
 usage: python tools/oracle/make_golden_window.py
 """
 import os
@@ -33,14 +33,14 @@ def build(w):
     return m.eval()
 
 
-def c1_window(out, w=1, T=4, B=2):
+def c1_window(out, w=1, T=4, B=2, head_type="mlp", tag="c1win"):
     """The reference window TwoStream (two_stream_window.py:291-444, head_type "mlp") at C1 shapes: 2w+1 clips of
     T=4 frames 112^2 + 32 tokens, batch 2, eval with the calibrated running BN statistics of bn_running_stats.npz.
     Inputs: synth.clip_batch over B*(2w+1) clips (clip-major within each window)."""
     from model.fusion import two_stream_window as ref_win
     ref = mg.build_reference(T=T)  # lang / TSM vision models, initialised by name
     m = ref_win.TwoStream(ref.lang_model, ref.vision_model, 768, 2048, T, 128, w)
-    m.build_chapter_head(output_size=2, head_type="mlp")
+    m.build_chapter_head(output_size=2, head_type=head_type)
     mg.synth.init_params(m, mg.SEED)
     mg.synth.load_bn_stats(m, dict(np.load(os.path.join(mg.GOLD, "bn_running_stats.npz"))))
     m.eval()
@@ -52,7 +52,7 @@ def c1_window(out, w=1, T=4, B=2):
             "target_clip_idx": torch.full((B,), w), "total_num_clips": torch.full((B,), n)}
     with torch.no_grad():
         lg, pr = m(frames, ids, mask, info)
-    out.update({"c1win_logits": lg.numpy(), "c1win_prob": pr.numpy()})
+    out.update({f"{tag}_logits": lg.numpy(), f"{tag}_prob": pr.numpy()})
 
 
 def main():
@@ -70,6 +70,7 @@ def main():
                 lg, pr = m(torch.from_numpy(short), None)
             out.update({"short_emb": short, "short_logits": lg.numpy(), "short_probs": pr.numpy()})
     c1_window(out)
+    c1_window(out, head_type="cross_attn", tag="c1xattn")
     np.savez_compressed(os.path.join(mg.GOLD, "window_attn.npz"), **out)
     print({k: v.shape for k, v in out.items()})
 

@@ -234,6 +234,70 @@ __global__ void __launch_bounds__(kThreads) ln_act_kernel(const float* __restric
   }
 }
 
+// CrossAttention of the window ChapterHead, head_type "cross_attn" (two_stream_window.py:11-91, used at :284-286):
+//   l = LN_lang(lang_out) ; V = LN_vis(vision_out) + pe(t), pe(t) = W_pe * t / (T - 1) + b_pe
+//   q = l Wq^T + bq ; K, V' = V Wk^T + bk, V Wv^T + bv ; 16 heads: a = softmax(q K^T / sqrt(hd)) ; y = (a V') Wo^T + bo
+// One workgroup per clip window (T <= 16 frames, T*H <= 2048), all intermediates in LDS; weights packed as W^T.
+__global__ void __launch_bounds__(kThreads) cross_attn_fwd_kernel(const float* __restrict__ lang,
+                                                                  const float* __restrict__ vis,
+                                                                  const float* __restrict__ W, float* __restrict__ out,
+                                                                  int T, int H, int nh) {
+  extern __shared__ float sm[];
+  const int TH = T * H, hd = H / nh, tid = threadIdx.x, b = blockIdx.x;
+  float* Xv = sm;          // vision rows [T][H]
+  float* Nv = Xv + TH;     // normalised + position-encoded [T][H]
+  float* KV = Nv + TH;     // [T][2H] = k | v
+  float* sl = KV + 2 * TH; // lang [H] | normed lang [H] | q [H] | out [H]
+  const float *ln_g = W, *ln_b = ln_g + H, *vn_g = ln_b + H, *vn_b = vn_g + H, *pe_w = vn_b + H, *pe_b = pe_w + H;
+  const float *qT = pe_b + H, *qb = qT + H * H, *kvT = qb + H, *kvb = kvT + 2 * H * H, *oT = kvb + 2 * H;
+  const float* ob = oT + H * H;
+  for (int i = tid; i < TH; i += kThreads) Xv[i] = vis[(long long)b * TH + i];
+  for (int i = tid; i < H; i += kThreads) sl[i] = lang[(long long)b * H + i];
+  __syncthreads();
+  layer_norm(Xv, T, H, vn_g, vn_b, Nv, false);
+  layer_norm(sl, 1, H, ln_g, ln_b, sl + H, false);
+  const float tden = (float)(T - 1);
+  for (int i = tid; i < TH; i += kThreads) {
+    const int t = i / H, d = i - t * H;
+    Nv[i] += fmaf(pe_w[d], (float)t / tden, pe_b[d]);
+  }
+  __syncthreads();
+  lin<false>(sl + H, 1, H, qT, qb, H, sl + 2 * H, false);
+  lin<false>(Nv, T, H, kvT, kvb, 2 * H, KV, false);
+  const float qscale = 1.f / sqrtf((float)hd);
+  for (int h = tid; h < nh; h += kThreads) {  // one thread per head: T scores in registers
+    const float* q = sl + 2 * H + h * hd;
+    float sc[kMaxS], mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kMaxS; ++j) {
+      if (j < T) {
+        float a = 0.f;
+        for (int d = 0; d < hd; ++d) a = fmaf(q[d], KV[j * 2 * H + h * hd + d], a);
+        sc[j] = a * qscale;
+        mx = fmaxf(mx, sc[j]);
+      }
+    }
+    float den = 0.f;
+#pragma unroll
+    for (int j = 0; j < kMaxS; ++j)
+      if (j < T) {
+        sc[j] = expf(sc[j] - mx);
+        den += sc[j];
+      }
+    const float inv = 1.f / den;
+    for (int d = 0; d < hd; ++d) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < kMaxS; ++j)
+        if (j < T) a = fmaf(sc[j], KV[j * 2 * H + H + h * hd + d], a);
+      sl[h * hd + d] = a * inv;  // context over the raw-lang slot (no longer needed)
+    }
+  }
+  __syncthreads();
+  lin<false>(sl, 1, H, oT, ob, H, sl + 3 * H, false);
+  for (int i = tid; i < H; i += kThreads) out[(long long)b * H + i] = sl[3 * H + i];
+}
+
 }  // namespace
 
 // Packed f32 weight floats (layout documented in include/vcg_hip.h and vcg_hip/window.py pack_window_weights).
@@ -280,6 +344,21 @@ VCG_API int vcg_ln_act_fwd(const float* x, const float* gamma, const float* beta
   constexpr int rpb = kThreads / 64;
   hipLaunchKernelGGL(ln_act_kernel, dim3((rows + rpb - 1) / rpb), dim3(kThreads), 0, s, x, gamma, beta, out, rows, D,
                      eps, act);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API long long vcg_cross_attn_weight_floats(int H) { return 6LL * H + 4LL * H * H + 4LL * H; }
+
+VCG_API int vcg_cross_attn_fwd(const float* lang, const float* vis, const float* weights, long long weight_floats,
+                               float* out, int B, int T, int H, int nh, hipStream_t s) {
+  VCG_REQUIRE(B >= 0 && T >= 2 && T <= kMaxS, "frames per clip T must be in [2, 16]");
+  VCG_REQUIRE(H >= 1 && nh >= 1 && H % nh == 0 && (long long)T * H <= kMaxSH, "bad hidden size / heads");
+  VCG_REQUIRE(weight_floats >= vcg_cross_attn_weight_floats(H), "packed weight buffer too small");
+  VCG_REQUIRE(lang && vis && weights && out, "null operand");
+  if (B == 0) return VCG_OK;
+  const size_t lds = (size_t)(4 * T * H + 4 * H) * sizeof(float);
+  hipLaunchKernelGGL(cross_attn_fwd_kernel, dim3(B), dim3(kThreads), lds, s, lang, vis, weights, out, T, H, nh);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

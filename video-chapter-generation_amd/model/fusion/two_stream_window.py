@@ -8,16 +8,17 @@ clips. Same constructors, submodule / parameter names and head types; inference 
   window:      StackedVideoChapterAttention over the stacked [B, 2w+1, hidden] fusion embeddings
                (one window_attn.hip launch).
 
-Native scope: eval-mode forward with head_type "mlp" (the drivers' default, train_video_segment_update_accumulate.py
-:443). The other head types ("bilinear", "multiplication", "self_attn", "cross_attn") are constructed with the
-reference's parameters (state dicts load) but their forward raises, as does training: no CPU / eager fallback.
+Native scope: eval-mode forward with head_type "mlp" (train_video_segment_update_accumulate.py:360's default) and
+"cross_attn" (test_video_segment_update.py:43's default; one cross_attn_fwd_kernel launch per clip). The other head
+types ("bilinear", "multiplication", "self_attn") are constructed with the reference's parameters (state dicts
+load) but their forward raises, as does training: no CPU / eager fallback.
 """
 import torch
 from torch import nn
 from einops import rearrange
 
 from vcg_hip.optim import param_groups
-from vcg_hip.window import linear, mlp_chain
+from vcg_hip.window import cross_attn_fwd, linear, mlp_chain, pack_cross_attn_weights
 
 from .stacked_window_self_attention import StackedVideoChapterAttention
 
@@ -102,16 +103,27 @@ class ChapterHead(nn.Module):
     def forward(self, lang_emb, vision_emb, window_idx):
         """lang_emb [B, lang_emb_size], vision_emb [B, segment_size, vision_emb_size] (f32) -> [B, hidden]."""
         from vcg_hip.ops import ACT_RELU
-        if self.head_type != "mlp":
+        if self.head_type not in ("mlp", "cross_attn"):
             raise RuntimeError(f"window ChapterHead head_type {self.head_type!r} has no native forward yet "
-                               "(native: 'mlp')")
+                               "(native: 'mlp', 'cross_attn')")
         B = lang_emb.shape[0]
         lp, vp = self.lang_proj_heads[window_idx], self.vision_proj_heads[window_idx]
         lang_out = linear(mlp_chain(lang_emb.float().contiguous(), lp[:-1]), lp[-1], ACT_RELU)  # :262-263
         vis = vision_emb.reshape(-1, self.vision_emb_size).float().contiguous()
         vision_out = linear(mlp_chain(vis, vp[:-1]), vp[-1], ACT_RELU)                           # :265-267
+        if self.head_type == "cross_attn":  # :284-286 (output_proj's result is unused by the reference)
+            return cross_attn_fwd(lang_out, vision_out.view(B, self.segment_size, self.hidden_size),
+                                  self._cross_weights(), self.hidden_size, self.head.num_heads)
         fusion = torch.cat([vision_out.view(B, self.segment_size, self.hidden_size), lang_out.unsqueeze(1)], 1)
         return mlp_chain(fusion.view(B, -1), self.head[window_idx])                                 # :269-272
+
+    def _cross_weights(self):
+        key = tuple((p.data_ptr(), p._version) for p in self.head.parameters())
+        if getattr(self, "_xkey", None) != key:
+            with torch.no_grad():
+                self._xpacked = pack_cross_attn_weights(self.head)
+            self._xkey = key
+        return self._xpacked
 
 
 class TwoStream(nn.Module):

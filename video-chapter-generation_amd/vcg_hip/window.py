@@ -94,3 +94,30 @@ def mlp_chain(x, seq):
             raise RuntimeError(f"mlp_chain: unsupported module {type(m).__name__}")
         i += 2 if act else 1
     return x
+
+
+def pack_cross_attn_weights(ca):
+    """Flat f32 buffer of a CrossAttention's parameters as cross_attn_fwd_kernel reads them: lang_norm g, b |
+    vision_norm g, b | frame_pos_encoding w [H], b | query W^T [H][H], b | key|value W^T [H][2H], b [2H] |
+    out_proj W^T [H][H], b."""
+    parts = [ca.lang_norm.weight, ca.lang_norm.bias, ca.vision_norm.weight, ca.vision_norm.bias,
+             ca.frame_pos_encoding.weight.reshape(-1), ca.frame_pos_encoding.bias, _t(ca.query_proj),
+             ca.query_proj.bias,
+             torch.cat([ca.key_proj.weight, ca.value_proj.weight], 0).detach().t().contiguous().reshape(-1),
+             torch.cat([ca.key_proj.bias, ca.value_proj.bias]), _t(ca.out_proj), ca.out_proj.bias]
+    return torch.cat([p.detach().reshape(-1).float() for p in parts]).contiguous()
+
+
+def cross_attn_fwd(lang, vis, weights, H, nh):
+    """lang [B, H], vis [B, T, H] f32 (GPU) -> [B, H] (two_stream_window.py CrossAttention.forward, eval)."""
+    _chk(lang, torch.float32, "lang_out")
+    _chk(vis, torch.float32, "vision_out")
+    _chk(weights, torch.float32, "packed cross-attention weights")
+    B, T, Hd = vis.shape
+    if Hd != H or lang.shape != (B, H):
+        raise RuntimeError(f"cross attention shapes: lang {tuple(lang.shape)}, vision {tuple(vis.shape)}, hidden {H}")
+    if weights.numel() != _lib.query("vcg_cross_attn_weight_floats", H):
+        raise RuntimeError("packed cross-attention weights have the wrong size")
+    out = torch.empty((B, H), dtype=torch.float32, device=vis.device)
+    _lib.call("vcg_cross_attn_fwd", P(lang), P(vis), P(weights), weights.numel(), P(out), B, T, H, nh, stream())
+    return out
