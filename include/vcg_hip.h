@@ -135,7 +135,7 @@ VCG_API int vcg_tanh_bwd(int dtype, const void* dy, const void* t, void* dx, lon
  *      F.cross_entropy (train_video_segment_point.py:165) ----------------------------------- */
 VCG_API int vcg_head_mlp_fwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* bias, float* logits, float* prob, int B, int T, int hid, int O, hipStream_t s);
 VCG_API int vcg_head_mlp_bwd(int dtype, const void* Vout, const void* Lout, const float* W, const float* dlogits, void* dV, void* dL, float* dW, float* dbias, int B, int T, int hid, int O, int relu_mask, hipStream_t s);
-/* ChapterHead head_type "attn" (head_attn.hip): SelfAttention(hid, n_head, O) (two_stream.py:8-48) over the T+1
+/* ChapterHead head_type "attn" (head_attn.hip; also the window ChapterHead "self_attn", O = hid <= 256): SelfAttention(hid, n_head, O) (two_stream.py:8-48) over the T+1
  * fused tokens cat([Vout [B*T][hid], Lout [B][hid]]) of each window, output proj of token 0, softmax. Weights are
  * the fp32 nn.Linear parameters ([out][in]). `saved` (f32, vcg_head_attn_saved_floats) keeps the state of the
  * backward; dropout_p = attn_drop.p in training (counter-hash mask, regenerated by the backward with `seed`). */
@@ -157,6 +157,10 @@ VCG_API int vcg_window_attn_fwd(const float* emb, const float* weights, long lon
  * vcg_hip/window.py pack_cross_attn_weights (LN / pos-encoding vectors, then q, k|v, out Linear weights as W^T). */
 VCG_API long long vcg_cross_attn_weight_floats(int H);
 VCG_API int vcg_cross_attn_fwd(const float* lang, const float* vis, const float* weights, long long weight_floats, float* out, int B, int T, int H, int nh, hipStream_t s);
+/* Window ChapterHead "multiplication" / "bilinear" pieces (two_stream_window.py:269-281): out = a * b over n f32
+ * (n % 4 == 0); out[b][r] = sum_i U[b][r][i] x[b][i] + bias[r] (nn.Bilinear's second contraction after U = x2 A^T). */
+VCG_API int vcg_mul_fwd(const float* a, const float* b, float* out, long long n, hipStream_t s);
+VCG_API int vcg_rowdot_fwd(const float* U, const float* x, const float* bias, float* out, int B, int R, int K, hipStream_t s);
 /* out = act(LayerNorm(x) * gamma + beta) over `rows` rows of D f32 features (window ChapterHead's Linear -> LN -> ReLU
  * chains, two_stream_window.py:145-176); act 0 = none, 1 = ReLU, 2 = GELU (erf). */
 VCG_API int vcg_ln_act_fwd(const float* x, const float* gamma, const float* beta, float* out, int rows, int D, float eps, int act, hipStream_t s);

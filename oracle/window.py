@@ -87,6 +87,27 @@ def chapter_head_mlp_window(p, lang_emb, vision_emb, i, prefix="fusion_head.", h
     vis_out = _chain(p, f"{prefix}vision_proj_heads.{i}", vision_emb.reshape(B * T, -1), 3, final_relu=True)
     if head_type == "cross_attn":
         return cross_attention(p, f"{prefix}head.", lang_out, vis_out.view(B, T, -1))
+    if head_type == "self_attn":  # :280-282 (SelfAttention of two_stream_window.py:93-131, token 0 -> proj)
+        x = torch.cat([vis_out.view(B, T, -1), lang_out.unsqueeze(1)], 1)
+        C, nh = x.shape[-1], 4
+        hs = C // nh
+
+        def heads(name):
+            return _lin(p, f"{prefix}head.{name}", x).view(B, T + 1, nh, hs).transpose(1, 2)
+        k, q, v = heads("key"), heads("query"), heads("value")
+        att = F.softmax((q @ k.transpose(-2, -1)) * (1.0 / math.sqrt(hs)), dim=-1)
+        y = (att @ v).transpose(1, 2).reshape(B, T + 1, C)
+        return _lin(p, f"{prefix}head.proj", y[:, 0])
+    if head_type == "bilinear":  # :271-273
+        w, b = p[f"{prefix}bilinear_layers.{i}.weight"], p[f"{prefix}bilinear_layers.{i}.bias"]
+        fusion = F.bilinear(lang_out, vis_out.reshape(B, -1), w, b)
+        x = F.relu(_ln(p, f"{prefix}head.{i}.0", fusion))
+        x = F.relu(_ln(p, f"{prefix}head.{i}.4", _lin(p, f"{prefix}head.{i}.3", x)))
+        return _lin(p, f"{prefix}head.{i}.7", x)
+    if head_type == "multiplication":  # :275-279
+        e = F.relu(_ln(p, f"{prefix}lang_expand_layers.{i}.1", _lin(p, f"{prefix}lang_expand_layers.{i}.0", lang_out)))
+        e = F.relu(_ln(p, f"{prefix}lang_expand_layers.{i}.5", _lin(p, f"{prefix}lang_expand_layers.{i}.4", e)))
+        return _chain(p, f"{prefix}head.{i}", vis_out.reshape(B, -1) * e, 3)
     fusion = torch.cat([vis_out.view(B, T, -1), lang_out.unsqueeze(1)], 1).reshape(B, -1)
     return _chain(p, f"{prefix}head.{i}", fusion, 3)
 

@@ -247,7 +247,11 @@ def _c1win_inputs(B=2, n=3, T=4):
     return frames.view(B, n, T, 3, 112, 112), ids.view(B, n, 32), mask.view(B, n, 32)
 
 
-@pytest.mark.parametrize("head_type,tag", [("mlp", "c1win"), ("cross_attn", "c1xattn")])
+WINDOW_HEADS = [("mlp", "c1win"), ("cross_attn", "c1xattn"), ("self_attn", "c1self_attn"),
+                ("bilinear", "c1bilinear"), ("multiplication", "c1multiplication")]
+
+
+@pytest.mark.parametrize("head_type,tag", WINDOW_HEADS)
 def test_oracle_two_stream_window_matches_reference(head_type, tag):
     """oracle.window.two_stream_window against the reference window TwoStream (two_stream_window.py:291-444,
     head "mlp") at C1 shapes, running-stats eval; parameters by the native module's (= reference) names."""

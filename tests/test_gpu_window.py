@@ -125,7 +125,8 @@ def test_cross_attn_matches_oracle(T, H, nh, B):
     assert (out.cpu() - ref).abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("head_type,tag", [("mlp", "c1win"), ("cross_attn", "c1xattn")])
+@pytest.mark.parametrize("head_type,tag", [("mlp", "c1win"), ("cross_attn", "c1xattn"), ("self_attn", "c1self_attn"),
+                                          ("bilinear", "c1bilinear"), ("multiplication", "c1multiplication")])
 def test_two_stream_window_matches_reference_golden(head_type, tag):
     """The native window TwoStream (BERT + TSM-ResNet-50 engines per clip, window ChapterHead "mlp" on the fp32
     GEMM / LN kernels or the cross-attention kernel, window transformer kernel) against the reference's own output

@@ -8,7 +8,8 @@ tests/golden/window_attn.npz
       (dropout inactive); weights from vcg_hip/synth.py by state-dict name with prefix "window_attn."; inputs
       from numpy's default_rng(11 + w).
   short_*: window_size 2 module fed S = 3 clips (the reference slices window_pos_bias[..., :S]).
-  c1win_* / c1xattn_*: the full window TwoStream at C1 shapes with head_type "mlp" / "cross_attn" (c1_window).
+  c1win_* / c1xattn_* / c1{self_attn,bilinear,multiplication}_*: the full window TwoStream at C1 shapes with
+      head_type "mlp" / "cross_attn" / the other three (c1_window).
 usage: python tools/oracle/make_golden_window.py
 """
 import os
@@ -71,6 +72,8 @@ def main():
             out.update({"short_emb": short, "short_logits": lg.numpy(), "short_probs": pr.numpy()})
     c1_window(out)
     c1_window(out, head_type="cross_attn", tag="c1xattn")
+    for ht in ("self_attn", "bilinear", "multiplication"):
+        c1_window(out, head_type=ht, tag=f"c1{ht}")
     np.savez_compressed(os.path.join(mg.GOLD, "window_attn.npz"), **out)
     print({k: v.shape for k, v in out.items()})
 

@@ -22,7 +22,7 @@ namespace {
 constexpr int kMaxTok = 64;   // T + 1
 constexpr int kMaxHid = 256;
 constexpr int kMaxHeads = 16;
-constexpr int kMaxOut = 16;
+constexpr int kMaxOut = 256;  // output_size (2 for the fusion head, hidden for the window self_attn head)
 
 // token j of window b: vision rows first, then the language row
 template <typename T>
@@ -277,7 +277,7 @@ int check_shapes(int B, int T, int hid, int nh, int O) {
   VCG_REQUIRE(B > 0 && T > 0 && T + 1 <= kMaxTok, "need 1 <= T and T + 1 <= 64 tokens");
   VCG_REQUIRE(hid > 0 && hid <= kMaxHid && nh > 0 && nh <= kMaxHeads && hid % nh == 0,
               "need hid <= 256 divisible by n_head <= 16");
-  VCG_REQUIRE(O > 0 && O <= kMaxOut, "need 1 <= output_size <= 16");
+  VCG_REQUIRE(O > 0 && O <= kMaxOut, "need 1 <= output_size <= 256");
   return VCG_OK;
 }
 

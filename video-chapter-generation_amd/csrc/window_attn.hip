@@ -362,3 +362,57 @@ VCG_API int vcg_cross_attn_fwd(const float* lang, const float* vis, const float*
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
+
+namespace {
+
+// out = a * b elementwise (window ChapterHead "multiplication": vision_out * expanded_lang, :275-277)
+__global__ void __launch_bounds__(kThreads) mul_kernel(const float4* __restrict__ a, const float4* __restrict__ b,
+                                                       float4* __restrict__ out, long long n4) {
+  for (long long i = blockIdx.x * (long long)kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
+    const float4 x = a[i], y = b[i];
+    out[i] = make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
+  }
+}
+
+// out[b][r] = sum_i U[b][r][i] * x[b][i] + bias[r]: the second contraction of nn.Bilinear (window ChapterHead
+// "bilinear", :271-273) after U = x2 A^T on the GEMM path; one wave per output.
+__global__ void __launch_bounds__(kThreads) rowdot_kernel(const float* __restrict__ U, const float* __restrict__ x,
+                                                          const float* __restrict__ bias, float* __restrict__ out,
+                                                          int B, int R, int K) {
+  const int lane = threadIdx.x & 63;
+  const long long o = blockIdx.x * (long long)(kThreads / 64) + (threadIdx.x >> 6);
+  if (o >= (long long)B * R) return;
+  const int b = (int)(o / R), r = (int)(o - (long long)b * R);
+  const float* u = U + o * K;
+  const float* xb = x + (long long)b * K;
+  float s = 0.f;
+  for (int i = lane; i < K; i += 64) s = fmaf(u[i], xb[i], s);
+  s = warp_sum(s);
+  if (lane == 0) out[o] = s + (bias ? bias[r] : 0.f);
+}
+
+}  // namespace
+
+VCG_API int vcg_mul_fwd(const float* a, const float* b, float* out, long long n, hipStream_t s) {
+  VCG_REQUIRE(n >= 0 && n % 4 == 0, "n must be a multiple of 4");
+  VCG_REQUIRE(a && b && out, "null operand");
+  if (n == 0) return VCG_OK;
+  const long long n4 = n / 4;
+  const int grid = (int)std::min<long long>((n4 + kThreads - 1) / kThreads, 4096);
+  hipLaunchKernelGGL(mul_kernel, dim3(grid), dim3(kThreads), 0, s, (const float4*)a, (const float4*)b, (float4*)out,
+                     n4);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_rowdot_fwd(const float* U, const float* x, const float* bias, float* out, int B, int R, int K,
+                           hipStream_t s) {
+  VCG_REQUIRE(B >= 0 && R >= 1 && K >= 1, "bad shape");
+  VCG_REQUIRE(U && x && out, "null operand");
+  if (B == 0) return VCG_OK;
+  const long long rows = (long long)B * R, rpb = kThreads / 64;
+  hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)((rows + rpb - 1) / rpb)), dim3(kThreads), 0, s, U, x, bias, out, B,
+                     R, K);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}

@@ -8,17 +8,17 @@ clips. Same constructors, submodule / parameter names and head types; inference 
   window:      StackedVideoChapterAttention over the stacked [B, 2w+1, hidden] fusion embeddings
                (one window_attn.hip launch).
 
-Native scope: eval-mode forward with head_type "mlp" (train_video_segment_update_accumulate.py:360's default) and
-"cross_attn" (test_video_segment_update.py:43's default; one cross_attn_fwd_kernel launch per clip). The other head
-types ("bilinear", "multiplication", "self_attn") are constructed with the reference's parameters (state dicts
-load) but their forward raises, as does training: no CPU / eager fallback.
+Native scope: eval-mode forward of every head type: "mlp" (train_video_segment_update_accumulate.py:360's default),
+"cross_attn" (test_video_segment_update.py:43's default; one cross_attn_fwd_kernel launch per clip), "self_attn"
+(head_attn.hip's SelfAttention kernel, output_size = hidden), "bilinear" (x2 A^T on the GEMM path + a row-dot
+kernel), "multiplication" (elementwise kernel). Training raises: no CPU / eager fallback.
 """
 import torch
 from torch import nn
 from einops import rearrange
 
 from vcg_hip.optim import param_groups
-from vcg_hip.window import cross_attn_fwd, linear, mlp_chain, pack_cross_attn_weights
+from vcg_hip.window import bilinear, cross_attn_fwd, linear, mlp_chain, mul, pack_cross_attn_weights
 
 from .stacked_window_self_attention import StackedVideoChapterAttention
 
@@ -102,10 +102,7 @@ class ChapterHead(nn.Module):
 
     def forward(self, lang_emb, vision_emb, window_idx):
         """lang_emb [B, lang_emb_size], vision_emb [B, segment_size, vision_emb_size] (f32) -> [B, hidden]."""
-        from vcg_hip.ops import ACT_RELU
-        if self.head_type not in ("mlp", "cross_attn"):
-            raise RuntimeError(f"window ChapterHead head_type {self.head_type!r} has no native forward yet "
-                               "(native: 'mlp', 'cross_attn')")
+        from vcg_hip.ops import ACT_RELU, head_attn_fwd
         B = lang_emb.shape[0]
         lp, vp = self.lang_proj_heads[window_idx], self.vision_proj_heads[window_idx]
         lang_out = linear(mlp_chain(lang_emb.float().contiguous(), lp[:-1]), lp[-1], ACT_RELU)  # :262-263
@@ -114,7 +111,17 @@ class ChapterHead(nn.Module):
         if self.head_type == "cross_attn":  # :284-286 (output_proj's result is unused by the reference)
             return cross_attn_fwd(lang_out, vision_out.view(B, self.segment_size, self.hidden_size),
                                   self._cross_weights(), self.hidden_size, self.head.num_heads)
-        fusion = torch.cat([vision_out.view(B, self.segment_size, self.hidden_size), lang_out.unsqueeze(1)], 1)
+        T, h = self.segment_size, self.hidden_size
+        if self.head_type == "self_attn":  # :280-282: SelfAttention over cat([vision, lang]), token 0 -> proj
+            at = self.head
+            return head_attn_fwd(vision_out, lang_out, at.query, at.key, at.value, at.proj, B, T, h, at.n_head)[0]
+        if self.head_type == "bilinear":  # :271-273
+            fusion = bilinear(lang_out, vision_out.view(B, T * h), self.bilinear_layers[window_idx])
+            return mlp_chain(fusion, self.head[window_idx])
+        if self.head_type == "multiplication":  # :275-279
+            expanded = mlp_chain(lang_out, self.lang_expand_layers[window_idx])
+            return mlp_chain(mul(vision_out.view(B, T * h), expanded), self.head[window_idx])
+        fusion = torch.cat([vision_out.view(B, T, h), lang_out.unsqueeze(1)], 1)
         return mlp_chain(fusion.view(B, -1), self.head[window_idx])                                 # :269-272
 
     def _cross_weights(self):

@@ -121,3 +121,28 @@ def cross_attn_fwd(lang, vis, weights, H, nh):
     out = torch.empty((B, H), dtype=torch.float32, device=vis.device)
     _lib.call("vcg_cross_attn_fwd", P(lang), P(vis), P(weights), weights.numel(), P(out), B, T, H, nh, stream())
     return out
+
+
+def mul(a, b):
+    """a * b elementwise (f32, same shape)."""
+    _chk(a, torch.float32, "mul operand")
+    _chk(b, torch.float32, "mul operand")
+    if a.shape != b.shape:
+        raise RuntimeError(f"mul shapes differ: {tuple(a.shape)} vs {tuple(b.shape)}")
+    out = torch.empty_like(a)
+    _lib.call("vcg_mul_fwd", P(a), P(b), P(out), a.numel(), stream())
+    return out
+
+
+def bilinear(x1, x2, bl):
+    """nn.Bilinear(x1 [B, I], x2 [B, J]) natively: U = x2 A^T (A = weight viewed [O*I][J], fp32 GEMM), then
+    out[b][o] = sum_i U[b][o*I + i] x1[b][i] + bias[o] (vcg_rowdot_fwd)."""
+    from .ops import gemm
+    _chk(x1, torch.float32, "bilinear input1")
+    _chk(x2, torch.float32, "bilinear input2")
+    O, I, J = bl.weight.shape
+    B = x1.shape[0]
+    U = gemm(x2, bl.weight.detach().reshape(O * I, J), B, O * I, J, J, J)
+    out = torch.empty((B, O), dtype=torch.float32, device=x1.device)
+    _lib.call("vcg_rowdot_fwd", P(U), P(x1), P(bl.bias), P(out), B, O, I, stream())
+    return out
