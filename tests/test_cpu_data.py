@@ -128,3 +128,18 @@ def test_long_video_host_side_and_metrics():
     m = lv.boundary_metrics(labels, ["0:00 intro", "0:08 two", "0:29 late"], 30, 8, 1)
     assert m["gt_cut_points"] == [8] and m["pred_cut_points"] == [8]
     assert m["recall"] == 1.0 and m["precision"] == 1.0 and m["f"] == 1.0
+
+
+def test_window_clip_indices_known_answers():
+    """WindowClipDataset's window around a target clip (youtube_dataset.py:438-446): with T = 16 and max_offset = 2
+    clips start every 4 s and window clips are skip = 4 clip indices (16 s) apart; off-video clips are -1."""
+    from data.clip_windows import clip_windows, window_clip_indices, window_clip_info
+    assert window_clip_indices(10, 30, 16, 2) == [2, 6, 10, 14, 18]
+    assert window_clip_indices(1, 30, 16, 2) == [-1, -1, 1, 5, 9]
+    assert window_clip_indices(28, 30, 16, 1) == [24, 28, -1]
+    assert window_clip_indices(0, 1, 16, 0) == [0]
+    assert window_clip_indices(5, 30, 8, 1) == [3, 5, 7]  # T = 8: skip 2
+    w = clip_windows(120, 16)  # 26 clips
+    info = window_clip_info(w, 3, 16, 1, 120)
+    assert info["clip_start_frame"].tolist() == [-1, 12, 28]
+    assert int(info["total_num_clips"]) == len(w) == 26 and int(info["target_clip_idx"]) == 3

@@ -241,10 +241,15 @@ def _window_two_stream(w=1, T=4, device=None, head_type="mlp"):
     return m.eval()
 
 
-def _c1win_inputs(B=2, n=3, T=4):
+def _c1win_inputs(B=2, n=3, T=4, pad_first=False):
     from vcg_hip import synth
     frames, ids, mask, _ = synth.clip_batch(B * n, T, 112, 112, 32, seed=123)
-    return frames.view(B, n, T, 3, 112, 112), ids.view(B, n, 32), mask.view(B, n, 32)
+    frames, ids, mask = frames.view(B, n, T, 3, 112, 112), ids.view(B, n, 32), mask.view(B, n, 32)
+    if pad_first:  # zero padding clip (youtube_dataset.py:460-470)
+        frames[:, 0] = 0
+        ids[:, 0] = 0
+        mask[:, 0] = 0
+    return frames, ids, mask
 
 
 WINDOW_HEADS = [("mlp", "c1win"), ("cross_attn", "c1xattn"), ("self_attn", "c1self_attn"),
@@ -266,3 +271,17 @@ def test_oracle_two_stream_window_matches_reference(head_type, tag):
         lg, pr = ow.two_stream_window(p, frames, ids, mask, head_type=head_type)
     assert np.abs(lg.numpy() - g[f"{tag}_logits"]).max() < 1e-4
     assert np.abs(pr.numpy() - g[f"{tag}_prob"]).max() < 1e-4
+
+
+def test_oracle_two_stream_window_padding_clip():
+    """oracle.window.two_stream_window on the c1pad golden: clip 0 of each window is the zero padding clip
+    (fully masked BERT input -> HF's uniform attention over all keys)."""
+    from oracle import window as ow
+    torch.set_num_threads(min(8, os.cpu_count() or 8))
+    g = _gold("window_attn.npz")
+    m = _window_two_stream()
+    p = {n: t.detach() for n, t in m.named_parameters()}
+    p.update({n: b for n, b in m.named_buffers()})
+    with torch.no_grad():
+        lg, _ = ow.two_stream_window(p, *_c1win_inputs(pad_first=True))
+    assert np.abs(lg.numpy() - g["c1pad_logits"]).max() < 1e-4

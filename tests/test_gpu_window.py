@@ -141,3 +141,17 @@ def test_two_stream_window_matches_reference_golden(head_type, tag):
     torch.cuda.synchronize()
     assert np.abs(lg.cpu().numpy() - g[f"{tag}_logits"]).max() < 1e-3
     assert np.abs(pr.cpu().numpy() - g[f"{tag}_prob"]).max() < 1e-3
+
+
+def test_two_stream_window_padding_clip_matches_reference_golden():
+    """A window that runs off the start of the video: clip 0 is the reference's zero padding (frames, text ids and
+    attention mask all 0, youtube_dataset.py:460-470) -- BERT sees a fully masked sequence there (c1pad golden)."""
+    from test_cpu_oracle import _c1win_inputs, _window_two_stream
+    g = np.load(os.path.join(GOLD, "window_attn.npz"), allow_pickle=False)
+    m = _window_two_stream(device=DEV)
+    frames, ids, mask = _c1win_inputs(pad_first=True)
+    with torch.no_grad():
+        lg, pr = m(frames.to(DEV), ids.to(DEV), mask.to(DEV), None)
+    torch.cuda.synchronize()
+    assert np.isfinite(lg.cpu().numpy()).all()
+    assert np.abs(lg.cpu().numpy() - g["c1pad_logits"]).max() < 1e-3

@@ -9,7 +9,8 @@ tests/golden/window_attn.npz
       from numpy's default_rng(11 + w).
   short_*: window_size 2 module fed S = 3 clips (the reference slices window_pos_bias[..., :S]).
   c1win_* / c1xattn_* / c1{self_attn,bilinear,multiplication}_*: the full window TwoStream at C1 shapes with
-      head_type "mlp" / "cross_attn" / the other three (c1_window).
+      head_type "mlp" / "cross_attn" / the other three (c1_window); c1pad_*: "mlp" with clip 0 of every window
+      the zero padding clip (frames, ids and mask all 0).
 usage: python tools/oracle/make_golden_window.py
 """
 import os
@@ -34,7 +35,7 @@ def build(w):
     return m.eval()
 
 
-def c1_window(out, w=1, T=4, B=2, head_type="mlp", tag="c1win"):
+def c1_window(out, w=1, T=4, B=2, head_type="mlp", tag="c1win", pad_first=False):
     """The reference window TwoStream (two_stream_window.py:291-444, head_type "mlp") at C1 shapes: 2w+1 clips of
     T=4 frames 112^2 + 32 tokens, batch 2, eval with the calibrated running BN statistics of bn_running_stats.npz.
     Inputs: synth.clip_batch over B*(2w+1) clips (clip-major within each window)."""
@@ -49,6 +50,10 @@ def c1_window(out, w=1, T=4, B=2, head_type="mlp", tag="c1win"):
     frames, ids, mask, _ = mg.synth.clip_batch(B * n, T, 112, 112, 32, seed=mg.SEED)
     frames = frames.view(B, n, T, 3, 112, 112)
     ids, mask = ids.view(B, n, 32), mask.view(B, n, 32)
+    if pad_first:  # a window running off the video start: clip 0 is the zero padding of youtube_dataset.py:460-470
+        frames[:, 0] = 0
+        ids[:, 0] = 0
+        mask[:, 0] = 0
     info = {"clip_start_frame": torch.zeros(B, n, dtype=torch.long), "total_frames": torch.full((B,), 100),
             "target_clip_idx": torch.full((B,), w), "total_num_clips": torch.full((B,), n)}
     with torch.no_grad():
@@ -74,6 +79,7 @@ def main():
     c1_window(out, head_type="cross_attn", tag="c1xattn")
     for ht in ("self_attn", "bilinear", "multiplication"):
         c1_window(out, head_type=ht, tag=f"c1{ht}")
+    c1_window(out, tag="c1pad", pad_first=True)
     np.savez_compressed(os.path.join(mg.GOLD, "window_attn.npz"), **out)
     print({k: v.shape for k, v in out.items()})
 

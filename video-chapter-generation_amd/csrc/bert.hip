@@ -290,7 +290,7 @@ __global__ void colsum_part_kernel(const T* __restrict__ x, long long ld, int ro
 // S [Z][L][Lp] raw scores (Z = B*nh). P = softmax(scale*S + mask_add) over valid keys.
 // Writes P (pre-dropout, needed by the backward) and Pd = dropout(P) (input of the PV GEMM).
 // HF eager attention adds finfo(f32).min to padded keys; exp() of that underflows to exactly 0,
-// which is what excluding the key gives.
+// which is what excluding the key gives (a row with no valid key is uniform over all L keys, as in HF).
 template <typename T> __device__ __forceinline__ void ld2(const T* p, float& a, float& b) {
   if constexpr (sizeof(T) == 4) {
     const float2 q = *reinterpret_cast<const float2*>(p);
@@ -339,12 +339,16 @@ __global__ __launch_bounds__(256) void attn_softmax_fwd_kernel(const T* __restri
     }
   }
   mx = warp_max(mx);
+  // every key masked (a zero-padding clip of the window dataset): HF's finfo.min bias absorbs the scores, so the
+  // reference's softmax is uniform over all L keys
+  const bool none = mx == -INFINITY;
   float sum = 0.f;
 #pragma unroll
   for (int e = 0; e < MAXE; ++e)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      v[e][k] = (v[e][k] == -INFINITY) ? 0.f : __expf(v[e][k] - mx);
+      const bool in = 2 * lane + 128 * e + k < L;
+      v[e][k] = none ? (in ? 1.f : 0.f) : (v[e][k] == -INFINITY) ? 0.f : __expf(v[e][k] - mx);
       sum += v[e][k];
     }
   sum = warp_sum(sum);

@@ -144,3 +144,22 @@ def video_clip_infos(vid, image_dir, image_num, timestamps, subtitles, clip_fram
             "vid": vid,
         })
     return out
+
+
+def window_clip_indices(target_idx, n_clips, clip_frame_num, window_size, max_offset=MAX_OFFSET):
+    """Clip indices of the window around `target_idx` (youtube_dataset.py:438-446, WindowClipDataset): 2w+1 clips
+    `skip = T // (2 * max_offset)` apart (so consecutive window clips do not overlap), -1 where the window runs off
+    either end of the video (the reference pads those clips with zero frames / text / mask)."""
+    skip = clip_frame_num // (2 * max_offset)
+    return [i if 0 <= i < n_clips else -1
+            for i in range(target_idx - skip * window_size, target_idx + skip * window_size + 1, skip)]
+
+
+def window_clip_info(windows, target_idx, clip_frame_num, window_size, image_num, max_offset=MAX_OFFSET):
+    """The reference's `clips_info` dict (youtube_dataset.py:507-527) as int64 arrays: clip_start_frame [2w+1]
+    (-1 for padding clips), total_frames, target_clip_idx, total_num_clips."""
+    windows = np.asarray(windows, dtype=np.int64).reshape(-1, 2)
+    idx = window_clip_indices(target_idx, len(windows), clip_frame_num, window_size, max_offset)
+    starts = np.array([windows[i, 0] if i >= 0 else -1 for i in idx], dtype=np.int64)
+    return {"clip_start_frame": starts, "total_frames": np.int64(image_num), "target_clip_idx": np.int64(target_idx),
+            "total_num_clips": np.int64(len(windows))}
