@@ -155,3 +155,26 @@ def test_two_stream_window_padding_clip_matches_reference_golden():
     torch.cuda.synchronize()
     assert np.isfinite(lg.cpu().numpy()).all()
     assert np.abs(lg.cpu().numpy() - g["c1pad_logits"]).max() < 1e-3
+
+
+def test_window_scoring_from_clip_embeddings_matches_forward():
+    """TwoStream.forward_embeddings (each clip's BERT / trunk pass once, windows gathered from the per-clip
+    embeddings, -1 = the zero padding clip) equals forward() on the materialised windows (C1 shapes, w = 1)."""
+    from test_cpu_oracle import _window_two_stream
+    from vcg_hip import synth
+    m = _window_two_stream(device=DEV)
+    N, T, L = 5, 4, 32
+    frames, ids, mask, _ = synth.clip_batch(N, T, 112, 112, L, seed=77, device=DEV)
+    win = torch.tensor([[-1, 0, 1], [0, 1, 2], [2, 3, 4], [3, 4, -1], [1, 3, 0]], device=DEV)
+    zf = torch.zeros((1, T, 3, 112, 112), device=DEV)
+    zi = torch.zeros((1, L), dtype=torch.long, device=DEV)
+    with torch.no_grad():
+        lang, vis = m.clip_embeddings(frames, ids, mask, chunk=2)
+        pl, pv = m.clip_embeddings(zf, zi, zi)
+        lg, pr = m.forward_embeddings(lang, vis, win, pl[0], pv[0])
+        allf, alli, allm = torch.cat([frames, zf]), torch.cat([ids, zi]), torch.cat([mask, zi])
+        sel = torch.where(win < 0, torch.full_like(win, N), win)
+        lg_ref, _ = m(allf[sel], alli[sel], allm[sel], None)
+    torch.cuda.synchronize()
+    assert torch.isfinite(lg).all()
+    assert (lg - lg_ref).abs().max().item() < 1e-4

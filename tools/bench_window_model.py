@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--res", type=int, default=224)
     ap.add_argument("--tokens", type=int, default=128)
+    ap.add_argument("--cached", action="store_true", help="score all `batch` clips of a video as targets from "
+                    "per-clip embeddings (each clip's BERT / trunk pass once, TwoStream.forward_embeddings)")
     a = ap.parse_args()
     from model.fusion.two_stream_window import TwoStream
     from model.lang.bert_hugface import BertHugface
@@ -42,6 +44,8 @@ def main():
     m = m.cuda().eval()
     synth.init_params(m, 123)
     m.lang_model.precision = m.vision_model.precision = a.precision
+    if a.cached:
+        return cached(m, a, B, n, T, R, L)
     frames, ids, mask, _ = synth.clip_batch(B * n, T, R, R, L, seed=123, device="cuda")
     frames = frames.view(B, n, T, 3, R, R)
     ids, mask = ids.view(B, n, L), mask.view(B, n, L)
@@ -58,6 +62,36 @@ def main():
     print(json.dumps({"model": "window TwoStream (eval)", "head_type": a.head, "windows": B, "clips_per_window": n,
                       "frames": T, "res": R, "tokens": L, "precision": a.precision, "ms_per_batch": round(ms, 2),
                       "windows_per_s": round(B / ms * 1e3, 1), "clips_per_s": round(B * n / ms * 1e3, 1),
+                      "finite": bool(torch.isfinite(lg).all().item())}))
+
+
+def cached(m, a, V, n, T, R, L):
+    """A video of V clips, every clip a window target (window_clip_indices, -1 = zero padding clip): embeddings of
+    the V clips + the zero clip once, then V windows from them."""
+    from data.clip_windows import window_clip_indices
+    from vcg_hip import synth
+    frames, ids, mask, _ = synth.clip_batch(V + 1, T, R, R, L, seed=123, device="cuda")
+    frames[V].zero_()
+    ids[V].zero_()
+    mask[V].zero_()
+    win = torch.tensor([window_clip_indices(t, V, T, a.window) for t in range(V)], device="cuda")
+
+    def run():
+        lang, vis = m.clip_embeddings(frames, ids, mask)
+        return m.forward_embeddings(lang[:V], vis[:V], win, lang[V], vis[V])
+    with torch.no_grad():
+        run()
+        torch.cuda.synchronize()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(a.iters):
+            lg, _ = run()
+        t1.record()
+        torch.cuda.synchronize()
+    ms = t0.elapsed_time(t1) / a.iters
+    print(json.dumps({"model": "window TwoStream (eval, per-clip embeddings cached)", "head_type": a.head,
+                      "windows": V, "clips_per_window": n, "clip_passes": V + 1, "frames": T, "res": R, "tokens": L,
+                      "precision": a.precision, "ms_per_video": round(ms, 2), "windows_per_s": round(V / ms * 1e3, 1),
                       "finite": bool(torch.isfinite(lg).all().item())}))
 
 

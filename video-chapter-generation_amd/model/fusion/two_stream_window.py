@@ -177,3 +177,37 @@ class TwoStream(nn.Module):
             vision_emb = self.vision_model(img).view(B, self.segment_size, -1)
             embs.append(self.fusion_head(lang_emb, vision_emb, i))
         return self.window_attn(torch.stack(embs, 1).contiguous(), clip_info)  # :435-444
+
+    # ---- long-video scoring from per-clip embeddings (not in the reference: a clip belongs to 2w+1 windows, so
+    # ---- scoring every window with forward() runs its BERT / trunk pass 2w+1 times)
+    def clip_embeddings(self, frames, text_ids, attention_mask, chunk=64):
+        """Per-clip (lang_emb [N, 768], vision_emb [N, T, 2048]) f32 for N clips (frames [N, T, 3, H, W], ids / mask
+        [N, L]), computed once per clip in chunks of `chunk` clips."""
+        if self.training and torch.is_grad_enabled():
+            raise RuntimeError("window TwoStream: only inference (eval mode) runs natively on MI355X")
+        langs, viss = [], []
+        for c0 in range(0, frames.shape[0], chunk):
+            f = frames[c0:c0 + chunk]
+            n = f.shape[0]
+            langs.append(self.lang_model(input_ids=text_ids[c0:c0 + chunk].contiguous(),
+                                         attention_mask=attention_mask[c0:c0 + chunk].contiguous()).pooler_output.float())
+            img = rearrange(f, "b t c h w -> (b t) c h w").contiguous()
+            viss.append(self.vision_model(img).float().view(n, self.segment_size, -1))
+        return torch.cat(langs), torch.cat(viss)
+
+    def forward_embeddings(self, lang_embs, vision_embs, window_indices, pad_lang=None, pad_vision=None):
+        """Score windows from per-clip embeddings: window_indices [B, 2w+1] int64 clip rows (-1 = the zero padding
+        clip, whose embeddings pad_lang [768] / pad_vision [T, 2048] are clip_embeddings() of an all-zero clip).
+        Same result as forward() on the materialised windows; each clip's BERT / trunk pass runs once."""
+        if self.training and torch.is_grad_enabled():
+            raise RuntimeError("window TwoStream: only inference (eval mode) runs natively on MI355X")
+        idx = window_indices.to(lang_embs.device).long()
+        if bool((idx < 0).any()):
+            if pad_lang is None or pad_vision is None:
+                raise RuntimeError("window_indices hold padding (-1) clips: pass pad_lang / pad_vision")
+            lang_embs = torch.cat([lang_embs, pad_lang.reshape(1, -1).float()])
+            vision_embs = torch.cat([vision_embs, pad_vision.reshape(1, *vision_embs.shape[1:]).float()])
+            idx = torch.where(idx < 0, torch.full_like(idx, lang_embs.shape[0] - 1), idx)
+        embs = [self.fusion_head(lang_embs.index_select(0, idx[:, i]).contiguous(),
+                                 vision_embs.index_select(0, idx[:, i]).contiguous(), i) for i in range(idx.shape[1])]
+        return self.window_attn(torch.stack(embs, 1).contiguous(), None)
