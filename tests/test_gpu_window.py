@@ -178,3 +178,17 @@ def test_window_scoring_from_clip_embeddings_matches_forward():
     torch.cuda.synchronize()
     assert torch.isfinite(lg).all()
     assert (lg - lg_ref).abs().max().item() < 1e-4
+
+
+def test_window_kernels_empty_batch():
+    """B = 0 windows: the C-ABI returns at once and the wrappers give empty [0, 2] / [0, H] results."""
+    from model.fusion.two_stream_window import CrossAttention
+    from vcg_hip.window import cross_attn_fwd, pack_cross_attn_weights
+    m = _module(128, 1).to(DEV)
+    with torch.no_grad():
+        lg, pr = m(torch.empty((0, 3, 128), device=DEV))
+        ca = CrossAttention(128, 16).to(DEV)
+        out = cross_attn_fwd(torch.empty((0, 128), device=DEV), torch.empty((0, 4, 128), device=DEV),
+                             pack_cross_attn_weights(ca), 128, 16)
+    torch.cuda.synchronize()
+    assert lg.shape == (0, 2) and pr.shape == (0, 2) and out.shape == (0, 128)

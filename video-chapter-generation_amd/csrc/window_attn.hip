@@ -319,8 +319,8 @@ VCG_API int vcg_window_attn_fwd(const float* emb, const float* weights, long lon
   VCG_REQUIRE((long long)S * H <= kMaxSH, "S * hidden must be <= 2048 (LDS-resident window)");
   VCG_REQUIRE(P >= S, "window_pos_bias length must cover the window");
   VCG_REQUIRE(weight_floats >= vcg_window_attn_weight_floats(H, nh, P), "packed weight buffer too small");
+  if (B == 0) return VCG_OK;  // (empty tensors may carry null pointers)
   VCG_REQUIRE(emb && weights && logits, "null operand");
-  if (B == 0) return VCG_OK;
   // as many windows per workgroup as fit the row budget (R = G * S <= 16 rows, R * H <= 2048 floats), but keep
   // at least one workgroup per CU when the batch is small
   int G = min(kMaxS / S, kMaxSH / (S * H));
@@ -355,8 +355,8 @@ VCG_API int vcg_cross_attn_fwd(const float* lang, const float* vis, const float*
   VCG_REQUIRE(B >= 0 && T >= 2 && T <= kMaxS, "frames per clip T must be in [2, 16]");
   VCG_REQUIRE(H >= 1 && nh >= 1 && H % nh == 0 && (long long)T * H <= kMaxSH, "bad hidden size / heads");
   VCG_REQUIRE(weight_floats >= vcg_cross_attn_weight_floats(H), "packed weight buffer too small");
-  VCG_REQUIRE(lang && vis && weights && out, "null operand");
   if (B == 0) return VCG_OK;
+  VCG_REQUIRE(lang && vis && weights && out, "null operand");
   const size_t lds = (size_t)(4 * T * H + 4 * H) * sizeof(float);
   hipLaunchKernelGGL(cross_attn_fwd_kernel, dim3(B), dim3(kThreads), lds, s, lang, vis, weights, out, T, H, nh);
   VCG_LAUNCH_CHECK();
