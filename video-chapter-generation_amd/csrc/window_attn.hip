@@ -339,8 +339,8 @@ VCG_API int vcg_ln_act_fwd(const float* x, const float* gamma, const float* beta
                            float eps, int act, hipStream_t s) {
   VCG_REQUIRE(rows >= 0 && D >= 1, "bad shape");
   VCG_REQUIRE(act == 0 || act == ACT_RELU || act == ACT_GELU, "act must be none, relu or gelu");
-  VCG_REQUIRE(x && gamma && beta && out, "null operand");
   if (rows == 0) return VCG_OK;
+  VCG_REQUIRE(x && gamma && beta && out, "null operand");
   constexpr int rpb = kThreads / 64;
   hipLaunchKernelGGL(ln_act_kernel, dim3((rows + rpb - 1) / rpb), dim3(kThreads), 0, s, x, gamma, beta, out, rows, D,
                      eps, act);
@@ -395,8 +395,8 @@ __global__ void __launch_bounds__(kThreads) rowdot_kernel(const float* __restric
 
 VCG_API int vcg_mul_fwd(const float* a, const float* b, float* out, long long n, hipStream_t s) {
   VCG_REQUIRE(n >= 0 && n % 4 == 0, "n must be a multiple of 4");
-  VCG_REQUIRE(a && b && out, "null operand");
   if (n == 0) return VCG_OK;
+  VCG_REQUIRE(a && b && out, "null operand");
   const long long n4 = n / 4;
   const int grid = (int)std::min<long long>((n4 + kThreads - 1) / kThreads, 4096);
   hipLaunchKernelGGL(mul_kernel, dim3(grid), dim3(kThreads), 0, s, (const float4*)a, (const float4*)b, (float4*)out,
@@ -408,8 +408,8 @@ VCG_API int vcg_mul_fwd(const float* a, const float* b, float* out, long long n,
 VCG_API int vcg_rowdot_fwd(const float* U, const float* x, const float* bias, float* out, int B, int R, int K,
                            hipStream_t s) {
   VCG_REQUIRE(B >= 0 && R >= 1 && K >= 1, "bad shape");
-  VCG_REQUIRE(U && x && out, "null operand");
   if (B == 0) return VCG_OK;
+  VCG_REQUIRE(U && x && out, "null operand");
   const long long rows = (long long)B * R, rpb = kThreads / 64;
   hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)((rows + rpb - 1) / rpb)), dim3(kThreads), 0, s, U, x, bias, out, B,
                      R, K);
