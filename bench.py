@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(REPO, "video-chapter-generation_amd"))
 sys.path.insert(0, REPO)
 
 METRIC = "clip-windows/sec (16f×224²+128tok) train-step at 1/2/4/8 MI355X; % HBM roofline"
+METRIC_FWD = "clip-windows/sec (16f×224²+128tok) fwd-only scoring (config 2) on 1 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
 N_PARAMS = 133355074
@@ -92,11 +93,38 @@ def _per_launch(r):
 
 
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(T, HW, L, threads, B=2, reps=2):
+def cpu_threads():
+    """Threads for the CPU baseline: the cores this process may run on, capped at 16 (a one-GPU box's CPU share;
+    os.cpu_count() reports the whole host there, many times more than the share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 8
+    return max(1, min(16, n))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=3):
+    """The oracle (oracle/model.py: fp32 CPU restatement of the reference path, test infrastructure) timed on this
+    host: train = one reference train step (fwd BN-train + CE + bwd + clip_grad_norm_ + AdamW), fwd = the eval
+    forward (running-stat BN). Median of `reps` timed runs after 1 warm-up. B is a bounded sample (2 windows train,
+    4 fwd: 10-30 s of CPU work in all) so the default bench finishes in minutes; clip-windows/sec does not depend
+    on B on a CPU (the CPU path has no batch-level parallelism beyond the threads)."""
     import torch
     from oracle import model as om
     from vcg_hip.build import build_two_stream
     from vcg_hip import synth
+    B = B or (2 if mode == "train" else 4)
     torch.set_num_threads(threads)
     m = build_two_stream(clip_frame_num=T, dropout=0.1)
     sd = m.state_dict()
@@ -104,17 +132,26 @@ def cpu_baseline(T, HW, L, threads, B=2, reps=2):
     frames, ids, mask, labels = synth.clip_batch(B, T, HW, HW, L, seed=7)
     times = []
     for r in range(reps + 1):
-        params = {n: sd[n].detach().clone().requires_grad_() for n in names}
+        params = {n: sd[n].detach().clone().requires_grad_(mode == "train") for n in names}
         buffers = {n: sd[n].detach().clone() for n in sd if n not in params}
         t0 = time.perf_counter()
-        om.train_step(params, buffers, frames, ids, mask, labels, lr=1e-5)
+        if mode == "train":
+            om.train_step(params, buffers, frames, ids, mask, labels, lr=1e-5)
+        else:
+            p = dict(buffers)
+            p.update(params)
+            with torch.no_grad():
+                om.two_stream(p, frames, ids, mask, bn_mode="running")
         dt = time.perf_counter() - t0
         if r > 0:
             times.append(dt)
     med = sorted(times)[len(times) // 2]
-    return {"value": B / med, "unit": "clip-windows/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle/ CPU fp32 train step (fwd+bwd+clip+AdamW, BN train, dropout 0.1) on B={B} windows of "
-                      f"{T}x{HW}^2 + {L} tokens; median of {reps} after 1 warm-up; {threads} threads"}
+    what = ("fp32 train step (fwd + bwd + clip + AdamW, BN train, dropout 0.1)" if mode == "train"
+            else "fp32 eval forward (running-stat BN)")
+    return {"value": round(B / med, 4), "unit": "clip-windows/sec", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "sample": f"oracle/ CPU {what} on B={B} windows of {T}x{HW}^2 + {L} tokens; median of {reps} timed runs "
+                      f"({', '.join(f'{t:.2f}' for t in times)} s) after 1 warm-up; torch.set_num_threads({threads})"}
 
 
 # ----------------------------------------------------------------------------- config 5
@@ -200,7 +237,7 @@ def main():
 
     from vcg_hip import _lib, ops, synth
     from vcg_hip.build import build_two_stream
-    from vcg_hip.ddp import GradAllReducer, broadcast_parameters
+    from vcg_hip.ddp import BufferBroadcaster, GradAllReducer, broadcast_parameters
     from vcg_hip.functions import cross_entropy
 
     _lib.call("vcg_init", local)
@@ -215,11 +252,20 @@ def main():
         betas = (0.9, 0.95)
     opt = model.configure_optimizers(Cfg)
     flat = model.native_flat()
-    reducer = GradAllReducer(flat)
+    # DDP transport: torch.distributed RCCL (default) or libvcg_hip's RCCL C ABI on a side stream (VCG_COMM=native);
+    # fp32 wire as the reference's DDP, or bf16 (VCG_DDP_WIRE=bf16)
+    comm = None
+    if world > 1 and os.environ.get("VCG_COMM", "") == "native":
+        from vcg_hip.comm import NativeComm
+        comm = NativeComm()
+    wire = torch.bfloat16 if os.environ.get("VCG_DDP_WIRE", "") == "bf16" else None
+    reducer = GradAllReducer(flat, comm=comm, wire_dtype=wire)
+    bufsync = None
     if world > 1:
         broadcast_parameters(model)
         model.set_grad_hooks(reducer)
         opt.grad_scale = 1.0 / world
+        bufsync = BufferBroadcaster(model, comm=comm)  # DDP broadcast_buffers: rank 0's BN stats each forward
     frames, ids, mask, labels = synth.clip_batch(B, T, HW, HW, L, seed=123 + rank, device=dev)
 
     def step():
@@ -228,6 +274,8 @@ def main():
                 model(frames, ids, mask)
             return
         opt.zero_grad()
+        if bufsync is not None:
+            bufsync()
         logits, prob = model(frames, ids, mask)
         loss = cross_entropy(logits, labels)
         loss.backward()
@@ -279,13 +327,17 @@ def main():
         nbytes, nflops = window_costs(T, HW, L, B, s_bytes, args.mode == "train")
         achieved = nbytes * B / (ms / 1000.0) / 1e9  # per GPU
         tflops = nflops * B / (ms / 1000.0) / 1e12
-        traffic = kern_traffic = None
+        traffic = kern_traffic = mfma_busy = None
         tf = os.path.join(REPO, "profiles", f"traffic_{args.mode}_{args.precision}_b{B}.json")
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
             traffic = tj.get("hbm_bytes_per_step")
             kern_traffic = tj.get("igemm_fast_kernel", {}).get("hbm_bytes_per_launch")
+        mf = os.path.join(REPO, "profiles", f"mfma_{args.mode}_{args.precision}_b{B}.json")
+        if os.path.exists(mf):  # PMC SQ_VALU_MFMA_BUSY_CYCLES pass (tools/mfma.sh)
+            with open(mf) as f:
+                mfma_busy = json.load(f).get("igemm_fast_kernel")
         dom = None
         if kern["launches"]:
             # the dominant kernel's bound from its aggregate arithmetic intensity over the step: algorithmic
@@ -303,6 +355,7 @@ def main():
                    "arithmetic_intensity_flop_per_byte": round(r_flops / max(r_bytes, 1.0), 1),
                    "mfma_view": {"achieved": round(k_tf, 2), "peak": peak_tf, "unit": "TFLOP/s",
                                  "frac": round(k_tf / peak_tf, 4)},
+                   "mfma_busy_pmc": mfma_busy,
                    "launches_per_step": kern["launches"], "avg_launch_us": round(kern["ms"] * 1e3 / kern["launches"], 2),
                    "gflop_per_launch": round(kern["flops"] / kern["launches"] / 1e9, 3),
                    "share_of_step": round(kern["ms"] / ms, 4),
@@ -313,7 +366,7 @@ def main():
                    "timing": "HIP events around each launch on its stream, one instrumented step (no BERT side "
                              "stream in that step: unshared launch durations)"}
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "clip-windows/sec", "n_gpus": world,
+            "metric": METRIC if args.mode == "train" else METRIC_FWD, "value": round(value, 3), "unit": "clip-windows/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded clip windows generated in HBM; random-init weights)",
@@ -330,9 +383,9 @@ def main():
                          "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / MFMA_PEAK_TFLOPS[args.precision], 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 8)
+            threads = args.cpu_threads or cpu_threads()
             try:
-                out["cpu_baseline"] = cpu_baseline(T, HW, L, threads)
+                out["cpu_baseline"] = cpu_baseline(T, HW, L, threads, args.mode)
             except Exception as e:  # the GPU number stands on its own; report why the baseline is missing
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), flush=True)

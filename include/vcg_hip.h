@@ -173,6 +173,19 @@ VCG_API long long vcg_sumsq_ws_bytes(void);
 VCG_API int vcg_sumsq(const float* x, long long n, float* ws, float* out, hipStream_t s);
 VCG_API int vcg_adamw(float* p, const float* g, float* m, float* v, const unsigned char* wd_flags, int flag_shift, long long n, float lr, float beta1, float beta2, float eps, float wd, float step_size, float bc2_sqrt, const float* sumsq, float max_norm, float grad_scale, void* bf16_shadow, hipStream_t s);
 
+/* ---- gradient exchange over RCCL / xGMI (comm.hip) --------------------------------------------
+ * Replaces the NCCL communicator of DDP(model) in train_video_segment_ddp.py:64-86 (init_process_group) and :148
+ * (bucketed gradient all-reduce on every backward) and the parameter broadcast of :261-263. One communicator per
+ * process (one process per GPU); RCCL is the one already mapped into the process (PyTorch-ROCm's) or
+ * /opt/rocm/lib/librccl.so.1. Calls are asynchronous on `s`: issue them on a side stream that waits for the
+ * bucket's producer to overlap the exchange with the backward (vcg_hip/comm.py). */
+VCG_API int vcg_comm_unique_id(void* uid_out, int uid_bytes);                 /* rank 0: 128-byte id */
+VCG_API int vcg_comm_init(int rank, int world, const void* uid, int uid_bytes); /* collective */
+VCG_API int vcg_comm_world(int* rank, int* world);
+VCG_API int vcg_allreduce_bucket(void* ptr, long long count, int dtype, hipStream_t s);  /* in-place SUM */
+VCG_API int vcg_broadcast_bucket(void* ptr, long long count, int dtype, int root, hipStream_t s);
+VCG_API int vcg_comm_finalize(void);
+
 /* ---- synthetic inputs (synth.hip): seeded clip windows / weights, bit-identical to numpy ---- */
 VCG_API int vcg_synth(int kind, void* out, long long n, unsigned long long key, double a, double b, hipStream_t s);
 

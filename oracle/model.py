@@ -36,9 +36,10 @@ def _bn(p, name, y, mode, momentum=0.1, eps=1e-5):
     return F.batch_norm(y, None, None, w, b, True, momentum, eps)  # "batch": test driver semantics
 
 
-def resnet50_tsm(p, x, n_segment, bn_mode, prefix="vision_model.", shift_div=8):
+def resnet50_tsm(p, x, n_segment, bn_mode, prefix="vision_model.", shift_div=8, tsm=True):
     """torchvision resnet50 (fc = Identity) with TemporalShift on each bottleneck conv1
-    (make_temporal_shift blockres, temporal_shift.py:128-144). x [N,3,H,W] -> [N,2048]."""
+    (make_temporal_shift blockres, temporal_shift.py:128-144). x [N,3,H,W] -> [N,2048].
+    tsm=False: the plain torchvision resnet50 of model/vision/resnet50.py:9-73 (conv1 names without `.net`)."""
     y = F.conv2d(x, p[prefix + "conv1.weight"], stride=2, padding=3)
     y = F.relu(_bn(p, prefix + "bn1", y, bn_mode))
     y = F.max_pool2d(y, 3, 2, 1)
@@ -47,7 +48,10 @@ def resnet50_tsm(p, x, n_segment, bn_mode, prefix="vision_model.", shift_div=8):
             pre = f"{prefix}layer{li + 1}.{bi}."
             s = stride if bi == 0 else 1
             identity = y
-            out = F.conv2d(tsm_shift(y, n_segment, shift_div), p[pre + "conv1.net.weight"])
+            if tsm:
+                out = F.conv2d(tsm_shift(y, n_segment, shift_div), p[pre + "conv1.net.weight"])
+            else:
+                out = F.conv2d(y, p[pre + "conv1.weight"])
             out = F.relu(_bn(p, pre + "bn1", out, bn_mode))
             out = F.conv2d(out, p[pre + "conv2.weight"], stride=s, padding=1)
             out = F.relu(_bn(p, pre + "bn2", out, bn_mode))
@@ -127,6 +131,13 @@ def two_stream(p, img_clip, ids, mask, bn_mode="running", p_drop=0.0, training=F
     vis = resnet50_tsm(p, x, T, bn_mode).view(B, T, -1)
     logits = (chapter_head_attn if head_type == "attn" else chapter_head_mlp)(p, lang_emb, vis)
     return logits, torch.softmax(logits, 1), vis, lang_emb
+
+
+def linear_head(p, x, prefix="head."):
+    """Single-model head: Linear + softmax (bert_hugface.py:124-126 on pooler_output, resnet50_tsm.py:68-77 on the
+    [B, T*2048] concatenated frame embeddings)."""
+    logits = F.linear(x, p[prefix + "weight"], p[prefix + "bias"])
+    return logits, torch.softmax(logits, 1)
 
 
 def param_groups(named, weight_decay):

@@ -1,6 +1,7 @@
 """world_size-2 gloo tests (CPU) of the data-parallel exchange in vcg_hip/ddp.py: bucketed
-all-reduce of a flat gradient buffer as parameters are reported final in backward order,
-no_sync-style micro-steps, rank-0 parameter broadcast and the metric gather."""
+all-reduce of a flat gradient buffer as parameters are reported final in backward order (buckets
+flushed while hooks are still arriving), the bf16 wire format, no_sync-style micro-steps, rank-0
+parameter broadcast, the per-forward BN-buffer broadcast and the metric gather."""
 import os
 import socket
 
@@ -47,11 +48,11 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from vcg_hip.ddp import GradAllReducer, all_gather_object, broadcast_parameters
+        from vcg_hip.ddp import BufferBroadcaster, GradAllReducer, all_gather_object, broadcast_parameters
         sizes = [1000, 300, 70000, 5, 2048, 77777, 256, 1]
         flat = _FakeFlat(sizes, seed=100 + rank)
         local = flat.grad.clone()
-        red = GradAllReducer(flat, bucket_bytes=64 * 1024)      # small buckets: many flushes
+        red = GradAllReducer(flat, bucket_bytes=64 * 1024, record=True)  # small buckets: many flushes
         # backward order: last parameters first, in groups (as the engines report them)
         groups = [[flat.params[7], flat.params[6]], [flat.params[5]], [flat.params[4], flat.params[3]],
                   [flat.params[2]], [flat.params[1], flat.params[0]]]
@@ -62,6 +63,36 @@ def _worker(rank, world, port, q):
         for r in range(world):
             total += _FakeFlat(sizes, seed=100 + r).grad
         ok_sum = torch.allclose(flat.grad, total, rtol=0, atol=1e-5)
+        # overlap: buckets went out while the backward was still reporting parameters (a flush precedes the last
+        # hook), every flush before finish() except the final one, and the flushed ranges tile the buffer once
+        kinds = [e[0] for e in red.log]
+        last_hook = max(i for i, k in enumerate(kinds) if k == "hook")
+        flushes = [e for e in red.log if e[0] == "flush"]
+        ok_overlap = kinds.index("flush") < last_hook and sum(1 for i, k in enumerate(kinds)
+                                                               if k == "flush" and i > last_hook) <= 1
+        covered = sorted((lo, hi) for _, lo, hi in flushes)
+        ok_overlap = ok_overlap and all(a[1] <= b[0] for a, b in zip(covered, covered[1:])) and len(flushes) >= 3
+        # bf16 wire format: the sum of the bf16-rounded local gradients, back in the fp32 buffer
+        flat2 = _FakeFlat(sizes, seed=100 + rank)
+        red2 = GradAllReducer(flat2, bucket_bytes=64 * 1024, wire_dtype=torch.bfloat16)
+        for g in [[flat2.params[i] for i in grp] for grp in ([7, 6], [5], [4, 3], [2], [1, 0])]:
+            red2(g)
+        red2.finish()
+        tot16 = torch.zeros_like(local)
+        for r in range(world):
+            tot16 += _FakeFlat(sizes, seed=100 + r).grad.bfloat16().float()
+        ok_wire = torch.allclose(flat2.grad, tot16.bfloat16().float(), rtol=1e-2, atol=1e-2) and \
+            flat2.grad.dtype == torch.float32
+        # BN-buffer sync before each forward (DDP broadcast_buffers): rank 1's drifted stats become rank 0's
+        mb = torch.nn.Module()
+        mb.register_buffer("running_mean", torch.full((3,), 10.0 + rank))
+        mb.register_buffer("running_var", torch.full((5,), 20.0 + rank))
+        mb.register_buffer("num_batches_tracked", torch.tensor(rank))
+        bb = BufferBroadcaster(mb)
+        mb.running_mean.add_(rank)  # updates through the module's (re-bound) buffer
+        bb()
+        ok_bufs = bool((mb.running_mean == 10.0).all()) and bool((mb.running_var == 20.0).all()) and \
+            int(mb.num_batches_tracked) == rank
         # disabled reducer (accumulation micro-step) leaves the local gradient alone
         before = flat.grad.clone()
         red.enabled = False
@@ -74,7 +105,7 @@ def _worker(rank, world, port, q):
         ok_bcast = torch.equal(flat.data, _FakeFlat(sizes, seed=100).data) and bool((m.running_mean == 0).all())
         gathered = all_gather_object({"rank": rank, "m_ap": 0.5 + rank})
         ok_gather = [g["rank"] for g in gathered] == list(range(world))
-        q.put((rank, ok_sum, ok_nosync, ok_bcast and flat.refreshed, ok_gather))
+        q.put((rank, ok_sum, ok_nosync, ok_bcast and flat.refreshed, ok_gather, ok_overlap, ok_wire, ok_bufs))
     finally:
         dist.destroy_process_group()
 
@@ -98,7 +129,10 @@ def test_grad_allreduce_buckets_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, ok_sum, ok_nosync, ok_bcast, ok_gather in res:
+    for rank, ok_sum, ok_nosync, ok_bcast, ok_gather, ok_overlap, ok_wire, ok_bufs in res:
+        assert ok_overlap, f"rank {rank}: buckets were not issued during the backward"
+        assert ok_wire, f"rank {rank}: bf16 wire all-reduce"
+        assert ok_bufs, f"rank {rank}: BufferBroadcaster"
         assert ok_sum, f"rank {rank}: bucketed all-reduce != sum of local grads"
         assert ok_nosync, f"rank {rank}: disabled reducer touched the gradient"
         assert ok_bcast, f"rank {rank}: broadcast_parameters"

@@ -4,7 +4,7 @@ FETCH_SIZE / WRITE_SIZE are reported in KiB (x1024). gfx950 correction (MI355X_M
 FETCH_SIZE counts half the bytes of 16-B/lane streaming reads -> x2; WRITE_SIZE is exact for 16-B/lane
 stores. Both are L2 memory-side request
 bytes (Infinity-Cache hits included), i.e. an upper bound on HBM bytes.
-usage: traffic.py FETCH_DIR WRITE_DIR STEPS_IN_RUN"""
+usage: traffic.py FETCH_DIR WRITE_DIR STEPS_IN_RUN [MODE]"""
 import collections
 import csv
 import glob
@@ -33,11 +33,12 @@ def load(d):
 
 def main():
     fetch, write, steps = load(sys.argv[1]), load(sys.argv[2]), float(sys.argv[3])
+    mode = sys.argv[4] if len(sys.argv) > 4 else "train"
     tot = sum(2 * v[0] for v in fetch.values()) + sum(v[0] for v in write.values())
     g_f, g_w = fetch.get("igemm_fast_kernel", [0, 0]), write.get("igemm_fast_kernel", [0, 0])
     launches = max(g_f[1], 1)
     out = {
-        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --steps 1 --warmup 1 "
+        "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, bench.py --mode {mode} --steps 1 --warmup 1 "
                   "(3 steps incl. the instrumented one); FETCH x2 (gfx950 correction)",
         "hbm_bytes_per_step": tot / steps,
         "igemm_fast_kernel": {"hbm_bytes_per_launch": (2 * g_f[0] + g_w[0]) / launches,
@@ -46,7 +47,7 @@ def main():
         "top_kernels_bytes_per_step": dict(sorted(
             ((k, (2 * fetch[k][0] + write.get(k, [0, 0])[0]) / steps) for k in fetch), key=lambda kv: -kv[1])[:15]),
     }
-    path = os.path.join(REPO, "profiles", "traffic_train_bf16_b64.json")
+    path = os.path.join(REPO, "profiles", f"traffic_{mode}_bf16_b64.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in ("hbm_bytes_per_step", "igemm_fast_kernel")}))

@@ -123,13 +123,65 @@ __global__ void embed_ln_bwd_kernel(const T* __restrict__ dout, const long long*
   }
 }
 
-// word grad scatter-add (atomics), position grad (sum over batch), token-type grad (sum over all)
-__global__ void embed_scatter_kernel(const float* __restrict__ de, const long long* __restrict__ ids,
-                                     float* __restrict__ word_grad, int H, long long rows, long long pad_idx) {
+// word grad, deterministic (no atomics): the workgroup of the FIRST token row carrying an id sums the de rows of
+// every token with that id in ascending row order and adds the total to word_grad[id] (the only writer of that row);
+// workgroups of later occurrences return. Rows are scanned in 256-id chunks: one ballot mask per wave in LDS, the
+// matches of a chunk are then walked in row order. Same result on every run, whatever the schedule.
+// Then: position grad (sum over batch), token-type grad (sum over all).
+constexpr int SCAT_MAXE = 4;  // H <= 4 * 256
+__global__ __launch_bounds__(256) void embed_scatter_kernel(const float* __restrict__ de,
+                                                            const long long* __restrict__ ids,
+                                                            float* __restrict__ word_grad, int H, long long rows,
+                                                            long long pad_idx) {
   const long long row = blockIdx.x;
   const long long id = ids[row];
   if (id == pad_idx) return;  // nn.Embedding(padding_idx): the padding row never receives gradient
-  for (int c = threadIdx.x; c < H; c += blockDim.x) atomicAdd(&word_grad[id * H + c], de[row * H + c]);
+  __shared__ unsigned long long masks[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float acc[SCAT_MAXE];
+#pragma unroll
+  for (int e = 0; e < SCAT_MAXE; ++e) acc[e] = 0.f;
+  for (long long base = 0; base < rows; base += 256) {
+    const long long j = base + tid;
+    const bool hit = j < rows && ids[j] == id;
+    const unsigned long long m = __ballot(hit);
+    if (lane == 0) masks[wave] = m;
+    __syncthreads();
+    // an earlier row with this id exists: that row's workgroup owns the sum (block-uniform decision)
+    bool earlier = false;
+    if (base < row) {
+      const long long lim = row - base;  // rows base .. row-1 of this chunk
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const long long lo = 64 * w;
+        if (lo >= lim) break;
+        unsigned long long mw = masks[w];
+        if (lim - lo < 64) mw &= (1ull << (lim - lo)) - 1ull;
+        earlier |= mw != 0ull;
+      }
+    }
+    if (earlier) return;  // (every thread read the same masks)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      unsigned long long mw = masks[w];
+      while (mw) {
+        const int b = __builtin_ctzll(mw);
+        mw &= mw - 1ull;
+        const long long r = base + 64 * w + b;
+#pragma unroll
+        for (int e = 0; e < SCAT_MAXE; ++e) {
+          const int c = tid + 256 * e;
+          if (c < H) acc[e] += de[r * H + c];
+        }
+      }
+    }
+    __syncthreads();  // masks are rewritten by the next chunk
+  }
+#pragma unroll
+  for (int e = 0; e < SCAT_MAXE; ++e) {
+    const int c = tid + 256 * e;
+    if (c < H) word_grad[id * H + c] += acc[e];
+  }
 }
 
 // position grad: thread (l, c) sums the batch; the per-position sums also go to tmp [L][H]
@@ -686,6 +738,7 @@ VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, 
                              unsigned long long seed, long long pad_idx, hipStream_t s) {
   const int rows = B * L;
   VCG_REQUIRE(ws_bytes >= vcg_ln_bwd_ws_bytes(rows, H), "workspace too small");
+  VCG_REQUIRE(H <= SCAT_MAXE * 256, "hidden size > 1024 not supported by the word-grad reduction");
   int rpb;
   const int nb = row_blocks(rows, &rpb);
   float* part = ws;

@@ -4,13 +4,15 @@ This replaces the reference's `train_video_segment_ddp.py`. The reference wraps 
 `DDP(model)` with NCCL and 25 MB buckets, all-reducing on every backward (`:131-148`); it draws
 data with a DistributedSampler (`:210-243`), broadcasts the rank-0 parameters (`:261-263`) and
 averages the validation metric with `all_gather_object` (`:276-281`). Here:
-- `vcg_hip.ddp.GradAllReducer` reduces the flat fp32 gradient buffer in 64 MB contiguous
-  buckets. Each bucket is sent as an async RCCL all_reduce(SUM) as soon as the native backward
+- `vcg_hip.ddp.GradAllReducer` reduces the flat fp32 gradient buffer in 25 MB contiguous
+  buckets (DDP's default). Each bucket is sent as an async RCCL all_reduce(SUM) as soon as the native backward
   reports its parameters final, so the exchange overlaps the rest of the backward.
 - The 1/world average is folded into the fused AdamW (`grad_scale`).
 - Gradient accumulation reduces only on the last micro-step (`reducer.enabled`). The sum of the
   micro-step gradients is linear, so the result equals DDP's reduce-every-backward.
-- Parameters start identical through one broadcast of the flat parameter buffer.
+- Parameters start identical through one broadcast of the flat parameter buffer; the BatchNorm running
+  statistics are re-broadcast from rank 0 before every training forward (DDP's broadcast_buffers=True),
+  as one collective over a flat buffer (`vcg_hip.ddp.BufferBroadcaster`).
 
 Launch: `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 train_video_segment_ddp.py`.
 """
@@ -30,7 +32,7 @@ from train_video_segment_point import TrainerConfig, lr_multiplier  # noqa: E402
 
 class DDPTrainer:
     def __init__(self, model, train_dataset, test_dataset, config, rank, world_size, device):
-        from vcg_hip.ddp import GradAllReducer, broadcast_parameters
+        from vcg_hip.ddp import BufferBroadcaster, GradAllReducer, broadcast_parameters
         self.model, self.train_dataset, self.test_dataset = model, train_dataset, test_dataset
         self.config, self.rank, self.world, self.device = config, rank, world_size, device
         self.optimizer = model.configure_optimizers(config)
@@ -38,6 +40,8 @@ class DDPTrainer:
         broadcast_parameters(model)
         self.reducer = GradAllReducer(model.native_flat())
         model.set_grad_hooks(self.reducer)
+        # DDP(model)'s broadcast_buffers=True: rank 0's BatchNorm running stats before every training forward
+        self.buffers = BufferBroadcaster(model)
         self.history = []
 
     def run_epoch(self, split, epoch):
@@ -60,6 +64,8 @@ class DDPTrainer:
                                      label.to(self.device))
             last_micro = (it + 1) % accum == 0
             self.reducer.enabled = is_train and self.world > 1 and last_micro
+            if is_train and self.world > 1:
+                self.buffers()
             with torch.set_grad_enabled(is_train):
                 logits, prob = self.model(img, ids, mask)
                 loss = cross_entropy(logits, label)

@@ -2,12 +2,18 @@
 
 Replaces the NCCL DDP of reference train_video_segment_ddp.py:131-148 (DDP(model) with 25 MB
 buckets firing on every backward). One process per GPU; the flat fp32 gradient buffer is reduced
-in contiguous buckets as soon as the native backward reports a group of parameters final (per
-BERT layer, per ResNet block, head, embeddings). torch.distributed's "nccl" backend is RCCL on
-ROCm; each collective runs on RCCL's own stream after an event wait on the compute stream, so the
-exchange of layer i overlaps the backward of layer i-1. Reductions are SUM; the 1/world average
-is folded into the fused optimizer (FusedAdamW.grad_scale) so no extra pass over the grads runs.
+in contiguous buckets (25 MB by default, as DDP) as soon as the native backward reports a group of
+parameters final (per BERT layer, per ResNet block, head, embeddings). Two transports:
+  * torch.distributed (default): the "nccl" backend is RCCL on ROCm; each collective runs on RCCL's
+    own stream after an event wait on the producing stream;
+  * `comm=NativeComm(...)` (vcg_hip/comm.py): libvcg_hip's own RCCL C ABI (vcg_allreduce_bucket),
+    issued on a side HIP stream that waits for the bucket's producer; finish() joins it.
+Either way the exchange of layer i overlaps the backward of layer i-1. Reductions are SUM; the 1/world
+average is folded into the fused optimizer (FusedAdamW.grad_scale) so no extra pass over the grads runs.
+`wire_dtype=torch.bfloat16` halves the bytes on xGMI (267 MB instead of 533 MB per step): each bucket
+is cast to bf16 on its producing stream, reduced, and cast back into the fp32 gradient at finish().
 Skipping reductions on accumulation micro-steps (no_sync semantics) is `reducer.enabled = False`.
+`record=True` keeps a log of hook calls and bucket flushes (the overlap evidence of tests/test_*_ddp.py).
 """
 import os
 
@@ -18,21 +24,37 @@ import torch.distributed as dist
 _DEBUG = os.environ.get("VCG_DDP_DEBUG", "")
 
 
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
 def _sid(stream):
     return None if stream is None else stream.cuda_stream
 
 
 class GradAllReducer:
-    def __init__(self, flat, bucket_bytes=64 << 20, group=None):
+    def __init__(self, flat, bucket_bytes=25 << 20, group=None, wire_dtype=None, comm=None, record=False):
         self.flat = flat
         self.bucket_elems = max(1, bucket_bytes // 4)
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.world = comm.world if comm is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
         self.enabled = self.world > 1
+        self.comm = comm
+        if wire_dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError("wire_dtype must be None / torch.float32 / torch.bfloat16")
+        self.wire = None if wire_dtype in (None, torch.float32) else wire_dtype
+        self._wire_buf = None
+        self._pending_casts = []  # (fp32 view, wire view) to cast back at finish()
         self._lo = self._hi = None
         self._works = []
-        self._done_lo = None
         self._stream = None  # stream the open bucket's gradients were produced on
+        self._side = None    # NativeComm: the side stream the collectives run on
+        self.record = record
+        self.log = []        # ("hook", lo, hi) / ("flush", lo, hi) in call order (record=True)
 
     # called by the engines (autograd backward thread) with parameters whose grads are final
     def __call__(self, params):
@@ -44,6 +66,8 @@ class GradAllReducer:
         lo = min(f.offset_of(p) for p in params)
         hi = max(f.offset_of(p) + p.numel() for p in params)
         hi = (hi + 255) // 256 * 256
+        if self.record:
+            self.log.append(("hook", lo, hi))
         stream = torch.cuda.current_stream() if torch.cuda.is_available() and f.grad.is_cuda else None
         if _DEBUG:
             print(f"[ddp] hook stream={stream.cuda_stream if stream is not None else None} [{lo},{hi}) "
@@ -62,21 +86,43 @@ class GradAllReducer:
         if self._hi - self._lo >= self.bucket_elems:
             self._flush()
 
+    def _wire_view(self, lo, hi):
+        if self._wire_buf is None:
+            self._wire_buf = torch.empty(self.flat.total, dtype=self.wire, device=self.flat.grad.device)
+        return self._wire_buf[lo:hi]
+
     def _flush(self):
         if self._lo is None:
             return
-        buf = self.flat.grad[self._lo:min(self._hi, self.flat.total)]
+        lo, hi = self._lo, min(self._hi, self.flat.total)
+        buf = self.flat.grad[lo:hi]
+        if self.record:
+            self.log.append(("flush", lo, hi))
         if _DEBUG:
-            print(f"[ddp] flush [{self._lo},{self._hi}) bucket stream "
+            print(f"[ddp] flush [{lo},{hi}) bucket stream "
                   f"{self._stream.cuda_stream if self._stream is not None else None} current "
                   f"{torch.cuda.current_stream().cuda_stream}", flush=True)
             if _DEBUG == "sync":
                 (self._stream or torch.cuda.current_stream()).synchronize()
-        if self._stream is not None and _sid(self._stream) != _sid(torch.cuda.current_stream()):
-            with torch.cuda.stream(self._stream):  # the collective waits on the stream that made the bucket
+        prod = self._stream
+        cur = torch.cuda.current_stream() if buf.is_cuda else None
+        with torch.cuda.stream(prod) if (prod is not None and _sid(prod) != _sid(cur)) else _nullctx():
+            if self.wire is not None:  # cast on the producing stream (ordered after the bucket's kernels)
+                wbuf = self._wire_view(lo, hi)
+                if buf.is_cuda:
+                    from . import ops
+                    ops.cast_from_f32(buf, self.wire, out=wbuf)
+                else:
+                    wbuf.copy_(buf)
+                self._pending_casts.append((buf, wbuf))
+                buf = wbuf
+            if self.comm is not None:
+                if self._side is None:
+                    self._side = torch.cuda.Stream(device=buf.device)
+                self._side.wait_stream(torch.cuda.current_stream())  # the side stream waits for the producer
+                self.comm.all_reduce(buf, stream=self._side)
+            else:
                 self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
-        else:
-            self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         self._lo = self._hi = None
 
     def finish(self):
@@ -87,6 +133,15 @@ class GradAllReducer:
         for w in self._works:
             w.wait()
         self._works = []
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
+        for dst, src in self._pending_casts:  # bf16 wire -> the fp32 gradient (current stream, after the waits)
+            if dst.is_cuda:
+                from . import ops
+                ops.cast_to_f32(src, out=dst)
+            else:
+                dst.copy_(src)
+        self._pending_casts = []
 
     def reduce_all(self):
         """Synchronous fallback: one all-reduce of the whole flat gradient buffer."""
@@ -105,6 +160,40 @@ def broadcast_parameters(model, src=0, group=None):
         if b is not None and b.is_floating_point():
             dist.broadcast(b, src=src, group=group)
     f.refresh_shadow(force=True)
+
+
+class BufferBroadcaster:
+    """DDP's broadcast_buffers=True (the default of the reference's DDP(model), train_video_segment_ddp.py:148):
+    before every training forward, rank 0's floating-point buffers (BatchNorm running_mean / running_var) are
+    copied to every rank, so the running statistics do not drift apart across ranks (each rank's BN sees only its
+    own shard). The module buffers are re-bound to views of ONE flat buffer, so a sync is one collective."""
+
+    def __init__(self, model, src=0, group=None, comm=None):
+        self.src, self.group, self.comm = src, group, comm
+        bufs = [(m, n, b) for m in model.modules() for n, b in m._buffers.items()
+                if b is not None and b.is_floating_point()]
+        self.flat = None
+        if not bufs:
+            return
+        dt = bufs[0][2].dtype
+        if any(b.dtype != dt for _, _, b in bufs):
+            raise TypeError("BufferBroadcaster: floating buffers of mixed dtypes")
+        total = sum(b.numel() for _, _, b in bufs)
+        self.flat = torch.empty(total, dtype=dt, device=bufs[0][2].device)
+        o = 0
+        for m, n, b in bufs:
+            v = self.flat[o:o + b.numel()].view_as(b)
+            v.copy_(b)
+            m._buffers[n] = v
+            o += b.numel()
+
+    def __call__(self):
+        if self.flat is None:
+            return
+        if self.comm is not None:
+            self.comm.broadcast(self.flat, root=self.src)
+        elif dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.broadcast(self.flat, src=self.src, group=self.group)
 
 
 def all_gather_object(obj, group=None):

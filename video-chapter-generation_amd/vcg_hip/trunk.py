@@ -91,6 +91,11 @@ class _ConvWeights:
 
 class ResNetTrunk:
     staged = False  # forward() input is already the stem's NHWC layout [N, H, W, Cpad] (ops.window_frames_u8)
+    # backward-path census (tests: the bf16 step must run the fused conv_dgrad_bwd engine everywhere)
+    path_counts = {"fused": 0, "unfused": 0}
+    # False: run the bf16 backward through the unfused ops (conv_dgrad + bn_bwd_reduce / apply + tsm_unshift_add),
+    # the reference path the fused conv_dgrad_bwd engine is checked against (tests/test_gpu_bf16_train.py)
+    fused_bwd = True
 
     def __init__(self, net, dtype):
         self.net = net
@@ -274,8 +279,11 @@ class ResNetTrunk:
         wt = self._wprep_t(conv, Cin)
         sums = torch.empty((2, C), dtype=torch.float32, device=y.device)
         dg, db = self._bn_grads(st)
-        g = ops.conv_dgrad_bwd(dy, wt, N, H, W, Cin, Cout, KH, KW, s, p, y=y, mean=st.mean, invstd=st.invstd,
-                               mscale=st.scale, mshift=st.shift, sums=sums, dgamma=dg, dbeta=db)
+        g = None
+        if ResNetTrunk.fused_bwd:
+            g = ops.conv_dgrad_bwd(dy, wt, N, H, W, Cin, Cout, KH, KW, s, p, y=y, mean=st.mean, invstd=st.invstd,
+                                   mscale=st.scale, mshift=st.shift, sums=sums, dgamma=dg, dbeta=db)
+        ResNetTrunk.path_counts["unfused" if g is None else "fused"] += 1
         if g is None:
             da = ops.conv_dgrad(dy, wt, N, H, W, Cin, Cout, KH, KW, s, p)
             return self._bn_bwd(da, y, st, C, affine=True)
@@ -309,7 +317,7 @@ class ResNetTrunk:
         if ds:
             cds = blk.downsample[0]
             self._wgrad(cds, r["x"], dyd, N, H, W, Cin)
-            if cds.stride[0] == 2 and self.dtype == torch.bfloat16:
+            if cds.stride[0] == 2 and self.dtype == torch.bfloat16 and ResNetTrunk.fused_bwd:
                 # 1x1 / stride 2: only the even (h, w) inputs receive a gradient, so it is ONE dense GEMM over the
                 # output pixels (no 3/4-zero rows), added by the conv1 dgrad epilogue at those rows (res_stride 2)
                 wt_ds = self._wprep_t(cds, Cin)
@@ -336,7 +344,8 @@ class ResNetTrunk:
                 dg2, db2 = self._bn_grads(prev["bd"])
                 kw.update(y2=prev["yd"], mean2=prev["bd"].mean, invstd2=prev["bd"].invstd, sum_gx2=sumsd[1],
                           dgamma2=dg2, dbeta2=db2)
-        out = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, **kw)
+        out = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, **kw) if ResNetTrunk.fused_bwd else None
+        ResNetTrunk.path_counts["unfused" if out is None else "fused"] += 1
         if ds:
             if out is None and res_stride == 2:  # unfused fallback: the full-grid downsample input gradient
                 res = self._dgrad(blk.downsample[0], dyd, N, H, W)
