@@ -71,3 +71,51 @@ def cut_points(first_timestamps_sec, image_num, mode):
             continue
         out.append(sec)
     return out
+
+
+def youtube_clip_item(img_dir, vid, timestamps_sec, subtitles, tokenizer, clip_frame_num, max_text_len, rng):
+    """YoutubeClipDataset.__getitem__ (youtube_dataset.py:64-194) for one video, statement by statement, with
+    `rng` in place of the module-level `random` and ToTensor + Normalize written out (PIL decode, /255, (x -
+    mean) / std in fp32). Returns (img_clip f32 [T,3,H,W] as nested lists -> numpy by the caller, ids, mask,
+    label, (clip_start_sec, clip_end_sec))."""
+    import glob
+    import os
+
+    import numpy as np
+    from PIL import Image
+
+    image_path = os.path.join(img_dir, vid)
+    image_num = len(glob.glob(image_path + "/*.jpg"))
+    cps = []
+    for sec in timestamps_sec:  # :73-87
+        if sec < 4:
+            continue
+        if sec > image_num:
+            continue
+        cps.append(sec)
+    max_offset = 2
+    clips = [[s, s + clip_frame_num] for s in range(0, image_num - clip_frame_num, 2 * max_offset)]
+    pos, neg = [], []
+    for idx, (s, e) in enumerate(clips):  # :96-117
+        if clip_label(s, e, cps, clip_frame_num, max_offset):
+            pos.append(idx)
+        else:
+            neg.append(idx)
+    is_positive = 0 if not pos else rng.sample([0, 1], k=1)[0]  # :121-125
+    clip = clips[rng.sample(pos, k=1)[0]] if is_positive else clips[rng.sample(neg, k=1)[0]]
+    s, e = clip
+    text_clip = "[CLS] " + window_text(subtitles, s, e)  # :141-154
+    tokens = tokenizer.tokenize(text_clip)[:max_text_len]  # :155-166
+    attention_mask = [1] * len(tokens)
+    if len(tokens) < max_text_len:
+        attention_mask += [0] * (max_text_len - len(tokens))
+        tokens += ["[PAD]"] * (max_text_len - len(tokens))
+    ids = tokenizer.convert_tokens_to_ids(tokens)
+    mean = np.array([0.485, 0.456, 0.406], dtype=np.float32)
+    std = np.array([0.229, 0.224, 0.225], dtype=np.float32)
+    imgs = []
+    for n in frame_numbers(s, e, image_num, clip_frame_num):  # :176-192
+        with Image.open(os.path.join(image_path, "%05d.jpg" % n)) as im:
+            a = np.asarray(im.convert("RGB"), dtype=np.float32) / np.float32(255.0)
+        imgs.append(((a - mean) / std).transpose(2, 0, 1))
+    return np.stack(imgs), ids, attention_mask, 1 if is_positive else 0, (s, e)

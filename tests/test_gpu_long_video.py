@@ -75,3 +75,75 @@ def test_long_video_bf16_runs_and_exports(tmp_path):
     assert np.array_equal(load_vision_emb(str(tmp_path), "v", int(s), int(e)), saved[3])
     m = lv.boundary_metrics(labels.cpu().tolist(), timestamps, F, T, 1)
     assert m["gt_cut_points"] and 0.0 <= m["recall"] <= 1.0
+
+
+def test_c5_full_size_bf16_vs_fp32_and_oracle():
+    """BASELINE config 5 at its configured size: a 3600-frame (1 h @ 1 fps) 224² video, T=16, L=128, stride-1 s
+    windows (3584 of them), running-stat BN (eval). Every window is scored by the benchmarked bf16 path and by the
+    fp32 parity mode; 16 windows spread over the video are checked against the CPU oracle (fp32, 1e-3).
+
+    The random-init head is re-biased (fusion_head.head.bias, from a 256-window fp32 sample) so that about half the
+    windows are positive -- otherwise every window lands on one side of 0.5 and the label / F1 comparison is empty.
+    bf16 vs fp32: prob[:, 1] within 5e-2 everywhere; labels may differ only on windows whose fp32 probability is
+    within 5 x the median |p_bf16 - p_fp32| of the 0.5 boundary; the boundary metrics of both are reported and the
+    F scores must agree within the share of flipped windows."""
+    import long_video as lv
+    from data.synthetic_dataset import HashTokenizer, normalize_frames
+    from oracle import model as om
+    from vcg_hip import ops
+    from vcg_hip.build import build_two_stream
+    stats = dict(np.load(os.path.join(GOLD, "bn_running_stats.npz"), allow_pickle=False))
+    F, T, HW, L, S = 3600, 16, 224, 128, 1
+    frames, timestamps, subtitles = lv.synthetic_long_video(F, HW, HW, seed=123, device=DEV)
+    win, idx, ids, mask = lv.window_inputs(F, T, S, subtitles, HashTokenizer(), L)
+    assert len(win) == 3584
+    idx_d, ids_d, mask_d = (torch.from_numpy(a).to(DEV) for a in (idx, ids, mask))
+    models = {p: build_two_stream(clip_frame_num=T, seed=123, device=DEV, precision=p, bn_stats=stats,
+                                  dropout=0.0).eval() for p in ("fp32", "bf16")}
+    # re-bias the 2-way head so the decisions split: shift logit 1 by the median margin of a sample
+    samp = np.linspace(0, len(win) - 1, 256).astype(np.int64)
+    with torch.no_grad():
+        fr = ops.window_frames_u8(frames, idx_d[samp].contiguous(), torch.float32, cpad=ops.stem_cpad(torch.float32))
+        lg, _ = models["fp32"].forward_staged(fr, ids_d[samp], mask_d[samp])
+        shift = (lg[:, 0] - lg[:, 1]).median().item()
+        for m in models.values():
+            m.fusion_head.head.bias.data[1] += shift
+            m.native_flat().refresh_shadow(force=True)
+    res = {}
+    for p, m in models.items():
+        sc, lab = lv.score_windows(m, frames, idx_d, ids_d, mask_d, batch_size=64)
+        torch.cuda.synchronize()
+        res[p] = (sc.cpu().numpy().astype(np.float64), lab.cpu().numpy())
+    p32, l32 = res["fp32"]
+    p16, l16 = res["bf16"]
+    d = np.abs(p16 - p32)
+    flips = np.nonzero(l16 != l32)[0]
+    pos = l32.mean()
+    m32 = lv.boundary_metrics(l32.tolist(), timestamps, F, T, S)
+    m16 = lv.boundary_metrics(l16.tolist(), timestamps, F, T, S)
+    print(f"C5: {len(win)} windows, positive share {pos:.3f}; |p16 - p32| median {np.median(d):.2e} max {d.max():.2e}; "
+          f"{len(flips)} label flips, max |p32 - 0.5| among them "
+          f"{(np.abs(p32[flips] - 0.5).max() if len(flips) else 0):.2e}")
+    print("C5 fp32 metrics", {k: m32[k] for k in ("recall", "precision", "f", "f_3", "f_5")})
+    print("C5 bf16 metrics", {k: m16[k] for k in ("recall", "precision", "f", "f_3", "f_5")})
+    assert 0.2 < pos < 0.8
+    assert d.max() <= 5e-2
+    if len(flips):
+        assert np.abs(p32[flips] - 0.5).max() <= 5 * np.median(d), "labels flipped far from the decision boundary"
+    share = len(flips) / len(win)
+    for k in ("f", "f_3", "f_5"):
+        assert abs(m16[k] - m32[k]) <= max(2 * share, 1e-9) + (0.0 if share == 0 else 0.05), k
+    if len(flips) == 0:
+        assert m16 == m32
+    # the fp32 parity mode against the CPU oracle on 16 windows spread over the video
+    pick = np.linspace(0, len(win) - 1, 16).astype(np.int64)
+    p = {k: v.detach().cpu() for k, v in models["fp32"].state_dict().items()}
+    img = normalize_frames(frames[torch.from_numpy(idx[pick].reshape(-1)).to(DEV)].cpu().numpy().reshape(
+        16, T, HW, HW, 3))
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    with torch.no_grad():
+        _, pr, _, _ = om.two_stream(p, img, torch.from_numpy(ids[pick]), torch.from_numpy(mask[pick]),
+                                    bn_mode="running")
+    e = np.abs(pr[:, 1].numpy() - p32[pick]).max()
+    print(f"C5 fp32 native vs oracle on 16 windows: max |dprob| {e:.2e}")
+    assert e < 1e-3
