@@ -173,6 +173,38 @@ VCG_API long long vcg_sumsq_ws_bytes(void);
 VCG_API int vcg_sumsq(const float* x, long long n, float* ws, float* out, hipStream_t s);
 VCG_API int vcg_adamw(float* p, const float* g, float* m, float* v, const unsigned char* wd_flags, int flag_shift, long long n, float lr, float beta1, float beta2, float eps, float wd, float step_size, float bc2_sqrt, const float* sumsq, float max_norm, float grad_scale, void* bf16_shadow, hipStream_t s);
 
+/* ---- window-model training (wtrain.hip): model/fusion/two_stream_window.py ChapterHead chains / CrossAttention and
+ *      stacked_window_self_attention.py (trained by train_video_segment_ddp.py:294-342). fp32 [rows][D]; dropout masks
+ *      regenerated in the backward from (seed, element index); act 0 none / 1 ReLU / 2 erf-GELU ------------------- */
+/* out = Dropout(act(LayerNorm(x))) (nn.LayerNorm, eps given); mean / rstd [rows] saved for the backward */
+VCG_API int vcg_ln_act_drop_fwd(const float* x, const float* gamma, const float* beta, float* out, float* mean, float* rstd, int rows, int D, float eps, int act, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API long long vcg_ln_act_drop_bwd_ws_bytes(int rows, int D);
+/* dx (written) and gamma_grad / beta_grad (accumulated, fixed-order reduction) */
+VCG_API int vcg_ln_act_drop_bwd(const float* dout, const float* x, const float* gamma, const float* beta, const float* mean, const float* rstd, float* dx, float* gamma_grad, float* beta_grad, float* ws, long long ws_bytes, int rows, int D, int act, float dropout_p, unsigned long long seed, hipStream_t s);
+/* out = Dropout(act(x)) (+ res) ; dx = d/dx of Dropout(act(x)) */
+VCG_API int vcg_act_drop_fwd(const float* x, const float* res, float* out, long long n, int act, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_act_drop_bwd(const float* dout, const float* x, float* dx, long long n, int act, float dropout_p, unsigned long long seed, hipStream_t s);
+/* da = dout * b, db = dout * a (either may be NULL) */
+VCG_API int vcg_mul_bwd(const float* dout, const float* a, const float* b, float* da, float* db, long long n, hipStream_t s);
+/* multi-head attention of short windows (VideoChapterWindowAttention.forward stacked_window_self_attention.py:55-95,
+   CrossAttention.forward two_stream_window.py:55-91): per window b, Sq queries over Sk keys (<= 32), nh heads of dh
+   (<= 16) columns of row-major q / k / v (leading dims given), scores * scale + bias[h][j] (bias [nh][Pb] or NULL),
+   softmax -> probs [B][nh][Sq][Sk] (saved), dropout, ctx = P V. Backward: dq / dk / dv written, dbias accumulated. */
+VCG_API int vcg_mha_small_fwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv, const float* bias, int Pb, float* ctx, long long ldc, float* probs, int B, int Sq, int Sk, int nh, int dh, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API long long vcg_mha_small_bwd_ws_bytes(int B, int nh, int Pb);
+VCG_API int vcg_mha_small_bwd(const float* q, long long ldq, const float* k, long long ldk, const float* v, long long ldv, const float* probs, const float* dctx, long long lddc, float* dq, long long lddq, float* dk, long long lddk, float* dv, long long lddv, float* dbias, int Pb, float* ws, long long ws_bytes, int B, int Sq, int Sk, int nh, int dh, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
+
+/* Linear(1, H) position encoding of token r % S added to row r: out = x + pos[r % S] * w + b; backward accumulates
+   dw / db (fixed row order); the input gradient is dout itself */
+VCG_API int vcg_posenc_fwd(const float* x, const float* pos, const float* w, const float* b, float* out, long long rows, int S, int H, hipStream_t s);
+VCG_API int vcg_posenc_bwd(const float* d, const float* pos, float* dw, float* db, long long rows, int S, int H, hipStream_t s);
+/* Linear layers narrower than the GEMM's 16-byte tiles (K or N % 4 != 0: the 2-way classifiers):
+   y = act(x W^T + b + res); backward: dx written, dw / db accumulated (fixed order) */
+VCG_API int vcg_linear_small_fwd(const float* x, const float* W, const float* b, const float* res, float* y, int M, int N, int K, int act, hipStream_t s);
+VCG_API int vcg_linear_small_bwd(const float* g, const float* x, const float* W, float* dx, float* dw, float* db, int M, int N, int K, hipStream_t s);
+/* softmax over the C entries of each row (the window model's prob output) */
+VCG_API int vcg_softmax_rows(const float* x, float* out, int rows, int C, hipStream_t s);
+
 /* ---- gradient exchange over RCCL / xGMI (comm.hip) --------------------------------------------
  * Replaces the NCCL communicator of DDP(model) in train_video_segment_ddp.py:64-86 (init_process_group) and :148
  * (bucketed gradient all-reduce on every backward) and the parameter broadcast of :261-263. One communicator per

@@ -4,9 +4,8 @@ names (state dicts interchange) and initialisation rules; the forward runs as ON
 of windows (window_attn.hip: each workgroup keeps its window's residual stream and activations in LDS through
 all 6 layers and the classifier).
 
-Native scope: inference (eval mode, dropout inactive) -- the reference's test/infer drivers. The window
-transformer's backward is not native yet: forward() in training mode raises instead of falling back to a
-CPU / eager path.
+Training mode runs vcg_hip/wtrain.py instead: the same blocks as native autograd Functions (GEMMs, LayerNorm,
+dropout, the short-window attention core with window_pos_bias), forward and backward on libvcg_hip.
 """
 
 import torch
@@ -35,10 +34,14 @@ class VideoChapterWindowAttention(nn.Module):
         self.attention_dropout = nn.Dropout(dropout)
         self.position_encoding = nn.Linear(1, hidden_size)
         self.window_pos_bias = nn.Parameter(torch.zeros(1, num_attention_heads, 1, 2 * window_size + 1))
-        for lin in (self.query, self.key, self.value, self.out_proj, self.position_encoding):
+        # _init_weights order of :33-46 (RNG consumption order matters for seeded runs)
+        for lin in (self.query, self.key, self.value, self.out_proj):
             nn.init.xavier_uniform_(lin.weight)
+        for lin in (self.query, self.key, self.value, self.out_proj):
             nn.init.zeros_(lin.bias)
         nn.init.normal_(self.window_pos_bias, mean=0.0, std=0.02)
+        nn.init.xavier_uniform_(self.position_encoding.weight)
+        nn.init.zeros_(self.position_encoding.bias)
 
 
 class VideoChapterBlock(nn.Module):
@@ -98,9 +101,10 @@ class StackedVideoChapterAttention(nn.Module):
         return self._packed
 
     def forward(self, fusion_emb, clip_info=None):
-        if self.training and torch.is_grad_enabled():
-            raise RuntimeError("StackedVideoChapterAttention: only inference (eval mode) runs natively on MI355X; "
-                               "the window-transformer backward is not implemented")
+        if self.training:  # native forward + backward, vcg_hip/wtrain.py
+            from vcg_hip import wtrain
+            logits = wtrain.window_attention(self, fusion_emb.float().contiguous())
+            return logits, wtrain.softmax_rows(logits)
         S, P = fusion_emb.shape[1], 2 * self.window_size + 1
         if S > P:  # the reference's window_pos_bias[..., :S] broadcast fails the same way
             raise RuntimeError(f"window of {S} clips exceeds 2 * window_size + 1 = {P} (window_pos_bias length)")

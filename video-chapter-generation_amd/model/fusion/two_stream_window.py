@@ -11,20 +11,30 @@ clips. Same constructors, submodule / parameter names and head types; inference 
 Native scope: eval-mode forward of every head type: "mlp" (train_video_segment_update_accumulate.py:360's default),
 "cross_attn" (test_video_segment_update.py:43's default; one cross_attn_fwd_kernel launch per clip), "self_attn"
 (head_attn.hip's SelfAttention kernel, output_size = hidden), "bilinear" (x2 A^T on the GEMM path + a row-dot
-kernel), "multiplication" (elementwise kernel). Training raises: no CPU / eager fallback.
+kernel), "multiplication" (elementwise kernel).
+Training (model.train()): forward and backward of "mlp", "cross_attn" (train_video_segment_ddp.py:579's default),
+"self_attn" and "multiplication" through vcg_hip/wtrain.py (every op a libvcg_hip kernel pair: GEMMs, LayerNorm +
+activation + dropout, the short-window attention core, position encodings), the per-clip BERT / trunk passes
+through the native engines with the model's flat parameter / gradient buffers (TwoStream is the NativeRoot), and
+the reference's AdamW grouping on the fused optimizer. "bilinear" trains nowhere yet (raises). No CPU / eager path.
 """
+import math
+
 import torch
 from torch import nn
 from einops import rearrange
 
-from vcg_hip.optim import param_groups
+from vcg_hip import wtrain
+from vcg_hip.nn import NativeRoot, new_seed
+from vcg_hip.optim import configure_adamw
 from vcg_hip.window import bilinear, cross_attn_fwd, linear, mlp_chain, mul, pack_cross_attn_weights
 
 from .stacked_window_self_attention import StackedVideoChapterAttention
 
 
 class CrossAttention(nn.Module):
-    """two_stream_window.py:11-91 (parameters only)."""
+    """two_stream_window.py:11-91 (parameters and their _init_weights :38-48; the forward is a kernel:
+    cross_attn_fwd in eval, vcg_hip/wtrain.cross_attention in training)."""
 
     def __init__(self, hidden_size, num_heads, dropout=0.1):
         super().__init__()
@@ -41,6 +51,12 @@ class CrossAttention(nn.Module):
         self.attention_dropout = nn.Dropout(dropout)
         self.output_dropout = nn.Dropout(dropout)
         self.frame_pos_encoding = nn.Linear(1, hidden_size)
+        scale = 1.0 / math.sqrt(self.head_dim)  # _init_weights (:38-48), in the reference's RNG order
+        for proj in (self.query_proj, self.key_proj, self.value_proj, self.out_proj):
+            nn.init.xavier_uniform_(proj.weight, gain=scale)
+            nn.init.zeros_(proj.bias)
+        nn.init.xavier_uniform_(self.frame_pos_encoding.weight)
+        nn.init.zeros_(self.frame_pos_encoding.bias)
 
 
 class SelfAttention(nn.Module):
@@ -103,6 +119,8 @@ class ChapterHead(nn.Module):
     def forward(self, lang_emb, vision_emb, window_idx):
         """lang_emb [B, lang_emb_size], vision_emb [B, segment_size, vision_emb_size] (f32) -> [B, hidden]."""
         from vcg_hip.ops import ACT_RELU, head_attn_fwd
+        if self.training:
+            return wtrain.chapter_head(self, lang_emb, vision_emb, window_idx)
         B = lang_emb.shape[0]
         lp, vp = self.lang_proj_heads[window_idx], self.vision_proj_heads[window_idx]
         lang_out = linear(mlp_chain(lang_emb.float().contiguous(), lp[:-1]), lp[-1], ACT_RELU)  # :262-263
@@ -133,7 +151,7 @@ class ChapterHead(nn.Module):
         return self._xpacked
 
 
-class TwoStream(nn.Module):
+class TwoStream(NativeRoot, nn.Module):
     """two_stream_window.py:291-444. forward(img_clips [B, 2w+1, T, 3, H, W], text_ids [B, 2w+1, L],
     attention_masks [B, 2w+1, L], clip_info) -> (logits [B, 2], prob [B, 2]) of each window's middle clip."""
 
@@ -161,13 +179,12 @@ class TwoStream(nn.Module):
         self.window_attn = StackedVideoChapterAttention(cfg)
 
     def configure_optimizers(self, train_config):
-        """AdamW with the reference's decay grouping (:355-388)."""
-        return torch.optim.AdamW(param_groups(self, train_config.weight_decay), lr=train_config.learning_rate,
-                                 betas=train_config.betas)
+        """AdamW with the reference's decay grouping (:355-388), as one fused kernel over the flat buffers."""
+        return configure_adamw(self, train_config)
 
     def forward(self, img_clips, text_ids, attention_masks, clip_info=None):
-        if self.training and torch.is_grad_enabled():
-            raise RuntimeError("window TwoStream: only inference (eval mode) runs natively on MI355X")
+        if self.training:
+            return self._train_forward(img_clips, text_ids, attention_masks)
         B, n_clips, _ = text_ids.shape
         embs = []
         for i in range(n_clips):  # :395-433
@@ -178,13 +195,38 @@ class TwoStream(nn.Module):
             embs.append(self.fusion_head(lang_emb, vision_emb, i))
         return self.window_attn(torch.stack(embs, 1).contiguous(), clip_info)  # :435-444
 
+    def _train_forward(self, img_clips, text_ids, attention_masks):
+        """Training (and train-mode) forward, :390-444: per clip i BERT (pooler) and the TSM trunk run as native
+        autograd Functions over the root's flat buffers (BatchNorm statistics of clip i's B*T frames, as the
+        reference's per-clip vision_model call), then ChapterHead(window_idx=i) and the window transformer through
+        vcg_hip/wtrain.py."""
+        from vcg_hip.bert import BertEncoderEngine
+        from vcg_hip.functions import BertFn, TrunkFn
+        from vcg_hip.trunk import ResNetTrunk
+        B, n_clips, _ = text_ids.shape
+        f = self.native_flat()
+        dt = self.compute_dtype()
+        need_grad = torch.is_grad_enabled()
+        dev = img_clips.device
+        anchor = self._anchor(dev)
+        embs = []
+        for i in range(n_clips):
+            if self.vision_model.training:
+                self._bump_bn_counters()  # every BatchNorm forward of the reference counts once per clip
+            lang_emb, _ = BertFn.apply(text_ids[:, i, :].contiguous(), attention_masks[:, i, :].contiguous(), anchor,
+                                       BertEncoderEngine(self.lang_model, f, dt), need_grad, new_seed(), None)
+            img = rearrange(img_clips[:, i], "b t c h w -> (b t) c h w").float().contiguous()
+            vision_emb = TrunkFn.apply(img, anchor, ResNetTrunk(self.vision_model, dt), need_grad, None)
+            embs.append(self.fusion_head(lang_emb, vision_emb.view(B, self.segment_size, -1), i))
+        return self.window_attn(torch.stack(embs, 1).contiguous(), None)
+
     # ---- long-video scoring from per-clip embeddings (not in the reference: a clip belongs to 2w+1 windows, so
     # ---- scoring every window with forward() runs its BERT / trunk pass 2w+1 times)
     def clip_embeddings(self, frames, text_ids, attention_mask, chunk=64):
         """Per-clip (lang_emb [N, 768], vision_emb [N, T, 2048]) f32 for N clips (frames [N, T, 3, H, W], ids / mask
         [N, L]), computed once per clip in chunks of `chunk` clips."""
-        if self.training and torch.is_grad_enabled():
-            raise RuntimeError("window TwoStream: only inference (eval mode) runs natively on MI355X")
+        if self.training:
+            raise RuntimeError("clip_embeddings is an inference helper: call model.eval() first")
         langs, viss = [], []
         for c0 in range(0, frames.shape[0], chunk):
             f = frames[c0:c0 + chunk]
@@ -199,8 +241,8 @@ class TwoStream(nn.Module):
         """Score windows from per-clip embeddings: window_indices [B, 2w+1] int64 clip rows (-1 = the zero padding
         clip, whose embeddings pad_lang [768] / pad_vision [T, 2048] are clip_embeddings() of an all-zero clip).
         Same result as forward() on the materialised windows; each clip's BERT / trunk pass runs once."""
-        if self.training and torch.is_grad_enabled():
-            raise RuntimeError("window TwoStream: only inference (eval mode) runs natively on MI355X")
+        if self.training:
+            raise RuntimeError("forward_embeddings is an inference helper: call model.eval() first")
         idx = window_indices.to(lang_embs.device).long()
         if bool((idx < 0).any()):
             if pad_lang is None or pad_vision is None:

@@ -18,6 +18,14 @@ def _seed(base, layer, site):
     return (base * 0x9E3779B1 + layer * 7919 + site * 104729) & ((1 << 63) - 1)
 
 
+def _uniform_p(mods, what):
+    """The common dropout rate of training-mode nn.Dropout modules (0 for modules in eval mode)."""
+    ps = {float(d.p) if d.training else 0.0 for d in mods}
+    if len(ps) != 1:
+        raise NotImplementedError(f"native BERT: {what} dropout modules with different rates {sorted(ps)}")
+    return ps.pop()
+
+
 class BertEncoderEngine:
     def __init__(self, model, flat, dtype):
         self.m = model
@@ -45,9 +53,13 @@ class BertEncoderEngine:
         dh = H // nh
         Lp = (L + 7) // 8 * 8
         rows = B * L
-        train = m.training
-        p_h = cfg.hidden_dropout_prob if train else 0.0
-        p_a = cfg.attention_probs_dropout_prob if train else 0.0
+        # dropout rates from the nn.Dropout modules, as HF's BertModel applies them (a caller may change .p after
+        # construction); hidden dropout sites share one rate, attention-probability sites another
+        hid = [emb_d for emb_d in [m.embeddings.dropout] + [d for lyr in m.encoder.layer
+                                                            for d in (lyr.attention.output.dropout, lyr.output.dropout)]]
+        att = [lyr.attention.self.dropout for lyr in m.encoder.layer]
+        p_h = _uniform_p(hid, "hidden")
+        p_a = _uniform_p(att, "attention-probability")
         eps = cfg.layer_norm_eps
         scale = 1.0 / math.sqrt(dh)
         dev = ids.device
