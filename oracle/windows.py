@@ -119,3 +119,63 @@ def youtube_clip_item(img_dir, vid, timestamps_sec, subtitles, tokenizer, clip_f
             a = np.asarray(im.convert("RGB"), dtype=np.float32) / np.float32(255.0)
         imgs.append(((a - mean) / std).transpose(2, 0, 1))
     return np.stack(imgs), ids, attention_mask, 1 if is_positive else 0, (s, e)
+
+
+def window_clip_item(img_dir, vid, timestamps_sec, subtitles, tokenizer, clip_frame_num, max_text_len, window_size,
+                     rng):
+    """WindowClipDataset.__getitem__ (youtube_dataset.py:389-536) statement by statement, `rng` for the module-level
+    `random`, ToTensor + Normalize written out. Returns (img_clips [2w+1, T, 3, H, W] numpy (zeros for padding
+    clips), ids [2w+1][L], masks [2w+1][L], label, clip_start_frames, image_num, target_idx, n_clips)."""
+    import glob
+    import os
+
+    import numpy as np
+    from PIL import Image
+
+    fps = 1
+    image_path = os.path.join(img_dir, vid)
+    image_num = len(glob.glob(image_path + "/*.jpg"))
+    cps = [sec for sec in timestamps_sec if not (sec < 4 * fps or sec > image_num - 4 * fps)]  # :398-403
+    max_offset = 2 * fps
+    clips = [[s, s + clip_frame_num] for s in range(0, image_num - clip_frame_num, 2 * max_offset)]
+    pos, neg = [], []
+    for idx, (s, e) in enumerate(clips):
+        (pos if clip_label(s, e, cps, clip_frame_num, max_offset) else neg).append(idx)
+    is_positive = rng.choice([0, 1]) if pos else 0  # :428
+    target_idx = rng.choice(pos if is_positive else neg)
+    window_indices = []
+    skip = clip_frame_num // (2 * max_offset)  # :432-438
+    for idx in range(target_idx - skip * window_size, target_idx + skip * window_size + 1, skip):
+        window_indices.append(idx if 0 <= idx < len(clips) else -1)
+    mean = np.array([0.485, 0.456, 0.406], dtype=np.float32)
+    std = np.array([0.229, 0.224, 0.225], dtype=np.float32)
+    imgs, ids, masks, shape = [], [], [], None
+    for idx in window_indices:
+        if idx == -1:
+            imgs.append(None)
+            ids.append([0] * max_text_len)
+            masks.append([0] * max_text_len)
+            continue
+        s, e = clips[idx]
+        frames = []
+        for n in frame_numbers(s, e, image_num, clip_frame_num):
+            with Image.open(os.path.join(image_path, "%05d.jpg" % n)) as im:
+                a = np.asarray(im.convert("RGB"), dtype=np.float32) / np.float32(255.0)
+            frames.append(((a - mean) / std).transpose(2, 0, 1))
+        imgs.append(np.stack(frames))
+        shape = imgs[-1].shape
+        text_clip = "[CLS] "  # :479-483
+        for sub in subtitles:
+            if s - fps < sub["start"] < e + fps:
+                text_clip += sub["text"] + " "
+        tokens = tokenizer.tokenize(text_clip)[:max_text_len]
+        mask = [1] * len(tokens)
+        pad = max_text_len - len(tokens)
+        if pad > 0:
+            tokens.extend(["[PAD]"] * pad)
+            mask.extend([0] * pad)
+        ids.append(tokenizer.convert_tokens_to_ids(tokens))
+        masks.append(mask)
+    img_clips = np.stack([x if x is not None else np.zeros(shape, np.float32) for x in imgs])
+    starts = [-1 if idx == -1 else clips[idx][0] for idx in window_indices]
+    return img_clips, ids, masks, 1 if is_positive else 0, starts, image_num, target_idx, len(clips)

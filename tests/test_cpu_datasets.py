@@ -124,3 +124,41 @@ def test_infer_dataset_reads_clip_json(tmp_path):
         assert label == info["clip_label"]
     text_ds = InferYoutubeClipDataset(img_dir, paths[0], tok, 16, 24, mode="text")
     assert text_ds[0][0] == 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_window_clip_dataset_matches_reference_restatement(tmp_path, seed):
+    from data.clip_windows import extract_first_timestamp
+    from data.transforms import train_vision_preprocess
+    from data.youtube_dataset import WindowClipDataset
+    from oracle.windows import window_clip_item
+    img_dir, data_file, vid_file, subs, ts, vocab = _write_corpus(str(tmp_path))
+    tok = _tokenizer(vocab)
+    ds = WindowClipDataset(img_dir, data_file, vid_file, tok, 8, 24, window_size=2, transform=train_vision_preprocess())
+    for i, vid in enumerate(ds.vids):
+        random.seed(seed + i)
+        torch.manual_seed(seed)
+        img, ids, mask, label, info = ds[i]
+        rng = random.Random(seed + i)
+        exp = window_clip_item(img_dir, vid, [extract_first_timestamp(t)[0] for t in ts[i]], subs[vid], tok, 8, 24, 2, rng)
+        e_img, e_ids, e_mask, e_label, starts, image_num, target, n_clips = exp
+        assert int(label) == e_label
+        assert ids.tolist() == [list(x) for x in e_ids] and mask.tolist() == e_mask
+        assert img.shape == (5, 8, 3, 32, 32) and np.array_equal(img.numpy(), e_img)
+        assert info["clip_start_frame"].tolist() == starts
+        assert int(info["total_frames"]) == image_num and int(info["target_clip_idx"]) == target
+        assert int(info["total_num_clips"]) == n_clips
+
+
+def test_synthetic_corpus_round_trips_through_disk(tmp_path):
+    """SyntheticVideoCorpus.write -> the reference-format tree; YoutubeClipDataset over it returns the corpus's own
+    frames (JPEG-decoded) for the sampled window."""
+    from data.synthetic_dataset import HashTokenizer, SyntheticVideoCorpus
+    from data.youtube_dataset import YoutubeClipDataset
+    c = SyntheticVideoCorpus(2, 30, 40, H=32, W=32, seed=4)
+    img_dir, data_file, vid_file = c.write(str(tmp_path))
+    ds = YoutubeClipDataset(img_dir, data_file, vid_file, HashTokenizer(), 8, 16, u8=True)
+    random.seed(0)
+    img, ids, mask, label = ds[1]
+    assert img.shape == (8, 32, 32, 3) and img.dtype == torch.uint8
+    assert len(os.listdir(os.path.join(img_dir, c.vids[1]))) == c.image_num[c.vids[1]]

@@ -93,6 +93,35 @@ class SyntheticVideoCorpus:
     def all_frames(self, vid):
         return self.frames(vid, range(self.image_num[vid]))
 
+    def write(self, root, split_name="train.txt", quality=95):
+        """Write the corpus in the reference's on-disk layout (the inputs of data/youtube_dataset.py's datasets):
+        <root>/frames/<vid>/%05d.jpg (1-based, PIL JPEG), <root>/subtitles/<vid>/subtitle_<vid>.json, the dataset
+        CSV <root>/subtitles/data.csv ("%^&*"-joined timestamps) and the vid list <root>/<split_name>.
+        Returns (img_dir, data_file, vid_file)."""
+        import os
+
+        from PIL import Image
+
+        from .common_utils import write_csv
+        img_dir = os.path.join(root, "frames")
+        sub_dir = os.path.join(root, "subtitles")
+        for vid in self.vids:
+            d = os.path.join(img_dir, vid)
+            os.makedirs(d, exist_ok=True)
+            for f, fr in enumerate(self.all_frames(vid)):
+                Image.fromarray(fr).save(os.path.join(d, "%05d.jpg" % (f + 1)), quality=quality)
+            sd = os.path.join(sub_dir, vid)
+            os.makedirs(sd, exist_ok=True)
+            with open(os.path.join(sd, f"subtitle_{vid}.json"), "w") as fh:
+                json.dump(self.subtitles[vid], fh)
+        data_file = os.path.join(sub_dir, "data.csv")
+        write_csv(data_file, self.vids, [f"synthetic {v}" for v in self.vids],
+                  [float(self.image_num[v]) for v in self.vids], [self.timestamps[v] for v in self.vids])
+        vid_file = os.path.join(root, split_name)
+        with open(vid_file, "w") as fh:
+            fh.write("\n".join(self.vids) + "\n")
+        return img_dir, data_file, vid_file
+
 
 def _encode(tokenizer, text, max_text_len):
     ids, mask = cw.encode_text(tokenizer, text, max_text_len)

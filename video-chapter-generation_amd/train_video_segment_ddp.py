@@ -39,7 +39,11 @@ class DDPTrainer:
         self.optimizer.grad_scale = 1.0 / world_size
         broadcast_parameters(model)
         self.reducer = GradAllReducer(model.native_flat())
-        model.set_grad_hooks(self.reducer)
+        # the point model reports its gradients final block by block (buckets overlap the backward); the window model
+        # (its heads are autograd Functions) is reduced in one collective after the backward
+        self.overlap = hasattr(model, "set_grad_hooks")
+        if self.overlap:
+            model.set_grad_hooks(self.reducer)
         # DDP(model)'s broadcast_buffers=True: rank 0's BatchNorm running stats before every training forward
         self.buffers = BufferBroadcaster(model)
         self.history = []
@@ -59,16 +63,22 @@ class DDPTrainer:
         accum = self.config.gradient_accumulation_steps
         scored = []
         order = list(sampler)
-        for it, (img, ids, mask, label) in enumerate(loader):
-            img, ids, mask, label = (img.float().to(self.device), ids.to(self.device), mask.to(self.device),
-                                     label.to(self.device))
+        window = []
+        for it, batch in enumerate(loader):
+            img, ids, mask, label = (batch[0].float().to(self.device), batch[1].to(self.device),
+                                     batch[2].to(self.device), batch[3].to(self.device))
+            clip_info = batch[4] if len(batch) > 4 else None  # the window model's window metadata
             last_micro = (it + 1) % accum == 0
             self.reducer.enabled = is_train and self.world > 1 and last_micro
             if is_train and self.world > 1:
                 self.buffers()
             with torch.set_grad_enabled(is_train):
-                logits, prob = self.model(img, ids, mask)
+                logits, prob = (self.model(img, ids, mask, clip_info) if clip_info is not None
+                                else self.model(img, ids, mask))
                 loss = cross_entropy(logits, label)
+            if not is_train and clip_info is not None:
+                window += list(zip(label.cpu().tolist(), prob[:, 1].float().cpu().tolist()))
+                continue
             if not is_train:
                 idx = order[it * bs:it * bs + len(label)]
                 for k, s in zip(idx, prob[:, 1].float().cpu().tolist()):
@@ -76,7 +86,10 @@ class DDPTrainer:
                 continue
             (loss / accum).backward()
             if last_micro:
-                self.reducer.finish()
+                if self.overlap:
+                    self.reducer.finish()
+                else:
+                    self.reducer.reduce_all()
                 self.optimizer.clip_and_step(self.config.grad_norm_clip)
                 self.model.zero_grad()
                 if self.config.lr_decay:
@@ -86,6 +99,12 @@ class DDPTrainer:
         self.reducer.enabled = self.world > 1
         if is_train:
             return None
+        if window:  # window model: average precision of the target clips over every rank's windows
+            from sklearn.metrics import average_precision_score
+            allw = [x for part in all_gather_object(window) for x in part]
+            labels = [a for a, _ in allw]
+            return float(average_precision_score(labels, [b for _, b in allw])) if 0 < sum(labels) < len(labels) \
+                else float("nan")
         for part in all_gather_object(scored):  # every rank gets every clip's score (clip order restored)
             for k, s in part:
                 ds.all_clip_infos[k]["pred_score"] = s
@@ -102,6 +121,11 @@ def main(argv=None):
     p.add_argument("--videos", default=16, type=int)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--seed", default=123, type=int)
+    p.add_argument("--window_size", default=0, type=int,
+                   help="0: the point clip scorer; w > 0: the window model of the reference's DDP driver "
+                        "(two_stream_window.TwoStream over 2w+1 clips, WindowClipDataset)")
+    p.add_argument("--head_type", default="cross_attn", help="window model head (reference default cross_attn)")
+    p.add_argument("--data_dir", default=None, help="window model: directory for the reference-format corpus")
     args = p.parse_args(argv)
 
     from common_utils import set_random_seed
@@ -117,6 +141,8 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=device)
     set_random_seed.use_fix_random_seed(args.seed + rank)
     tok = HashTokenizer()
+    if args.window_size > 0:
+        return _window_main(args, rank, world, device, tok)
     train_ds = YoutubeClipDataset(SyntheticVideoCorpus(args.videos, H=args.resolution, W=args.resolution, seed=args.seed),
                                   tok, args.clip_frame_num, args.max_text_len)
     test_ds = InferYoutubeClipDataset(SyntheticVideoCorpus(2, H=args.resolution, W=args.resolution, seed=args.seed + 1),
@@ -132,6 +158,45 @@ def main(argv=None):
         result = tr.run_epoch("infer_test", epoch)
         if rank == 0:
             print(f"epoch {epoch}: val m_ap {result}")
+    if world > 1:
+        dist.destroy_process_group()
+    return result
+
+
+def _window_main(args, rank, world, device, tok):
+    """The reference driver's own configuration (train_video_segment_ddp.py:445-564): the window TwoStream with
+    WindowClipDataset batches over a corpus in the reference's on-disk format (written from the synthetic corpus)."""
+    import tempfile
+
+    from data.synthetic_dataset import SyntheticVideoCorpus
+    from data.transforms import test_vision_preprocess, train_vision_preprocess
+    from data.youtube_dataset import WindowClipDataset
+    from vcg_hip.build import build_window_two_stream
+    root = args.data_dir or tempfile.mkdtemp(prefix="vcg_win_")
+    paths = {}
+    for split, n, seed in (("train", args.videos, args.seed), ("test", 2, args.seed + 1)):
+        d = os.path.join(root, split)
+        if rank == 0 and not os.path.exists(os.path.join(d, f"{split}.txt")):
+            SyntheticVideoCorpus(n, H=args.resolution, W=args.resolution, seed=seed).write(d, f"{split}.txt")
+        paths[split] = (os.path.join(d, "frames"), os.path.join(d, "subtitles", "data.csv"), os.path.join(d, f"{split}.txt"))
+    if world > 1:
+        dist.barrier()
+    train_ds = WindowClipDataset(*paths["train"], tok, args.clip_frame_num, args.max_text_len, args.window_size,
+                                 transform=train_vision_preprocess())
+    test_ds = WindowClipDataset(*paths["test"], tok, args.clip_frame_num, args.max_text_len, args.window_size,
+                                transform=test_vision_preprocess())
+    model = build_window_two_stream(clip_frame_num=args.clip_frame_num, window_size=args.window_size,
+                                    head_type=args.head_type, seed=args.seed, device=device, precision=args.precision)
+    conf = TrainerConfig(max_epochs=args.epoch, batch_size=args.batch_size, val_batch_size=args.batch_size,
+                         gradient_accumulation_steps=4, num_workers=0, lr_decay=True,
+                         warmup_epochs=args.epoch // 100, final_epochs=args.epoch // 100 * 90)
+    tr = DDPTrainer(model, train_ds, test_ds, conf, rank, world, device)
+    result = None
+    for epoch in range(1, args.epoch + 1):
+        tr.run_epoch("train", epoch)
+        result = tr.run_epoch("infer_test", epoch)
+        if rank == 0:
+            print(f"epoch {epoch}: val window AP {result}")
     if world > 1:
         dist.destroy_process_group()
     return result

@@ -74,3 +74,30 @@ def build_model(data_mode="all", clip_frame_num=16, hidden_size=128, head_type="
         synth.init_params(model, seed)
     model.precision = precision
     return model
+
+
+def build_window_two_stream(clip_frame_num=16, window_size=1, hidden_size=128, head_type="cross_attn", seed=None,
+                            device=None, precision="fp32", bn_stats=None):
+    """The window model as the reference DDP driver builds it (train_video_segment_ddp.py:463-486):
+    two_stream_window.TwoStream(lang.base_model, vision.base_model, 768, 2048, T, 128, window_size) +
+    build_chapter_head(2, head_type)."""
+    from model.fusion.two_stream_window import TwoStream
+    from model.lang.bert_hugface import BertHugface
+    from model.vision.resnet50_tsm import Resnet50TSM
+    from vcg_hip.nn import BertConfig
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        lang_model = BertHugface(pretrain_stage=False, config=BertConfig(output_attentions=True))
+    vision_model = Resnet50TSM(segments_size=clip_frame_num, shift_div=8, pretrain_stage=False)
+    model = TwoStream(lang_model.base_model, vision_model.base_model, lang_model.embed_size, vision_model.feature_dim,
+                      clip_frame_num, hidden_size, window_size)
+    with contextlib.redirect_stdout(io.StringIO()):
+        model.build_chapter_head(output_size=2, head_type=head_type)
+    if device is not None:
+        model = model.to(device)
+    if seed is not None:
+        synth.init_params(model, seed)
+    if bn_stats is not None:
+        synth.load_bn_stats(model, bn_stats)
+    model.precision = precision
+    return model
