@@ -35,12 +35,18 @@ VCG_API int vcg_finalize(void);
 VCG_API int vcg_sync(hipStream_t stream);
 /* Live launch timing (bench.py's dominant-kernel roofline): while enabled, every fast-GEMM / wgrad launch is
    bracketed with HIP events on its stream; query sums durations (ms), launches and algorithmic FLOPs per kernel
-   id (0 igemm_fast_kernel, 1 wgrad_fast_kernel). Enabling (or disabling) clears the records. */
+   id (0 igemm_fast_kernel, 1 wgrad_fast_kernel, 3 conv3x3_patch_kernel). Enabling (or disabling) clears the
+   records. */
 VCG_API int vcg_timing_enable(int on);
 VCG_API int vcg_timing_query(int kernel_id, double* ms_total, long long* launches, double* flops);
 /* per-launch roofline of the recorded launches: ideal_ms = sum over launches of max(flops / peak_tflops,
    algorithmic bytes / peak_gbs) (bytes: operands read once, outputs written once), with their total time */
 VCG_API int vcg_timing_roofline(int kernel_id, double peak_tflops, double peak_gbs, double* ms_total, double* ideal_ms, double* bytes, double* flops);
+/* Profiling aid (no reference counterpart): phase stamps (s_memtime) of workgroup 0 / wave 0 of the last
+   conv3x3_patch_kernel launch made with VCG_PATCH_STAMPS=1 in the environment, 6 per tile for the first 64 tiles:
+   tile top, after the DMA wait + barrier, after the next DMA issue, after the MFMAs, after the barrier, after the
+   epilogue. Returns 1 when no stamped launch happened. */
+VCG_API int vcg_patch_stamps(unsigned long long* out, int n);
 
 /* ---- MFMA implicit-GEMM engine (igemm.hip) ---------------------------------------------- */
 /* torchvision conv2d inside Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15,68-77), with

@@ -17,7 +17,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 namespace vcg {
 // kernel ids of vcg_timing_query
-enum { TIMING_FAST_GEMM = 0, TIMING_WGRAD = 1, TIMING_GENERIC_GEMM = 2 };
+enum { TIMING_FAST_GEMM = 0, TIMING_WGRAD = 1, TIMING_GENERIC_GEMM = 2, TIMING_PATCH_CONV = 3 };
 int timing_begin(hipStream_t s);
 void timing_end(int idx, hipStream_t s, int id, double flops, double bytes);
 }  // namespace vcg
