@@ -96,9 +96,17 @@ VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, int mask_mode, const v
 VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* idx, int N, int H, int W, int C, hipStream_t s);
 VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C, hipStream_t s);
 /* maxpool backward fused with the stem BatchNorm backward reduction (BN + ReLU before the pool): g = mask(dx),
-   mask = fma(y, mscale, mshift) > 0; sum_g / sum_gx finalized, dgamma / dbeta accumulated */
+   mask = fma(y, mscale, mshift) > 0; sum_g / sum_gx finalized, dgamma / dbeta accumulated; g = NULL: the sums
+   only (for vcg_maxpool_bwd_bn_apply) */
 VCG_API long long vcg_maxpool_bwd_bn_ws_bytes(int C);
 VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* idx, void* g, int N, int H, int W, int C, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t s);
+/* the stem backward in two streaming passes (reference resnet50_tsm.py:19 torchvision stem: conv1 -> bn1 -> relu ->
+   maxpool): dx = BN-backward-apply(g) with g = mask(maxpool_bwd(dy)) recomputed (rounded to dtype), sums from
+   vcg_maxpool_bwd_bn(g = NULL) -- vcg_maxpool_bwd_bn + vcg_bn_bwd_apply without the g tensor */
+VCG_API int vcg_maxpool_bwd_bn_apply(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, const float* gamma, const float* sum_g, const float* sum_gx, long long count, int train_stats, hipStream_t s);
+/* the stem forward's BN + ReLU + maxpool 3x3/2 in one pass: out / idx = maxpool(relu(fma(y, scale, shift))) with the
+   activation rounded to dtype (bit-identical to vcg_bn_apply then vcg_maxpool_fwd; no activation tensor) */
+VCG_API int vcg_bn_relu_maxpool(int dtype, const void* y, const float* scale, const float* shift, void* out, unsigned char* idx, int N, int H, int W, int C, hipStream_t s);
 VCG_API int vcg_avgpool_fwd(int dtype, const void* x, float* y, int N, int HW, int C, hipStream_t s);
 VCG_API int vcg_avgpool_bwd(int dtype, const float* dy, void* dx, int N, int HW, int C, hipStream_t s);
 /* rearrange 'b t c h w -> (b t) c h w' (two_stream.py:183) + NCHW->NHWC staging */

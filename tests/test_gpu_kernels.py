@@ -579,6 +579,38 @@ def test_maxpool_bwd_bn(K):
     assert (dg.double() - 0.5 - sx).abs().max().item() <= 1e-4 * (sx.abs().max().item() + 1)
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("train", [True, False])
+@pytest.mark.parametrize("hw", [(13, 12), (14, 12), (16, 10)])
+def test_fused_stem_bn_relu_maxpool(K, dtype, train, hw):
+    """The fused stem passes == the unfused ops, bit for bit: bn_relu_maxpool == bn_apply(relu) + maxpool_fwd
+    (values and argmax); maxpool_bwd_bn(store_g=False) + maxpool_bwd_bn_apply == maxpool_bwd_bn + bn_bwd_apply.
+    Even H and W take the 2x2-block backward kernel, odd ones the per-pixel kernel: both == maxpool_bwd masked."""
+    N, C = 3, 64
+    H, W = hw
+    y = _rand((N, H, W, C), dtype, 85).to(DEV)
+    g0 = torch.Generator().manual_seed(86)
+    sc = (torch.rand(C, generator=g0) * 2 - 0.5).to(DEV)   # some negative scales: no monotonicity shortcut
+    sh = (torch.randn(C, generator=g0) * 0.3).to(DEV)
+    a = K.bn_apply(y, sc, sh, C, relu=True)
+    mp_ref, idx_ref = K.maxpool_fwd(a, N, H, W, C)
+    mp, idx = K.bn_relu_maxpool(y, sc, sh, N, H, W, C)
+    assert torch.equal(mp, mp_ref) and torch.equal(idx, idx_ref)
+    dys = _rand(mp.shape, dtype, 87).to(DEV)
+    mean = (torch.randn(C, generator=g0) * 0.1).to(DEV)
+    inv = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    gamma = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    s_ref, s_new = torch.zeros((2, C), device=DEV), torch.zeros((2, C), device=DEV)
+    g = K.maxpool_bwd_bn(dys, idx, N, H, W, C, y, mean, inv, sc, sh, s_ref)
+    plain = K.maxpool_bwd(dys, idx, N, H, W, C)
+    assert torch.equal(g, torch.where(y.float() * sc + sh > 0, plain, torch.zeros_like(plain)))
+    dx_ref = K.bn_bwd_apply(g, None, y, mean, inv, gamma, s_ref[0], s_ref[1], C, train_stats=train)
+    assert K.maxpool_bwd_bn(dys, idx, N, H, W, C, y, mean, inv, sc, sh, s_new, store_g=False) is None
+    assert torch.equal(s_new, s_ref)
+    dx = K.maxpool_bwd_bn_apply(dys, idx, N, H, W, C, y, mean, inv, sc, sh, gamma, s_new, N * H * W, train)
+    assert torch.equal(dx, dx_ref)
+
+
 def test_attention_softmax_dropout(K):
     """Masked softmax + dropout: P matches torch softmax over the valid keys; Pd = P / (1 - p) on kept
     entries and 0 on dropped ones (drop rate ~ p); the backward regenerates the same mask."""

@@ -35,6 +35,23 @@ namespace vcg {
 void set_error(const std::string& msg);
 
 __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+struct FastDiv {  // q = n / d for 0 <= n < 2^31
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  uint32_t hi = __umulhi(n, f.m);
+  return (uint32_t)(((uint64_t)hi + n) >> f.s);
+}
+
 __device__ __forceinline__ bf16_t f2bf(float f) {
   // plain cast lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
   __bf16 b = (__bf16)f;

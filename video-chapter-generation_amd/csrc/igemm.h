@@ -23,23 +23,6 @@ template <typename T, int COLS> struct LdMN {
 
 constexpr bool is_kcontig(int mode) { return mode == OP_DENSE_K || mode == OP_IM2COL || mode == OP_DGRAD; }
 
-struct FastDiv {  // q = n / d for 0 <= n < 2^31
-  uint32_t d, m, s;
-};
-static inline FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  f.d = d;
-  uint32_t s = 0;
-  while ((1ull << s) < d) ++s;
-  f.s = s;
-  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-  return f;
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  uint32_t hi = __umulhi(n, f.m);
-  return (uint32_t)(((uint64_t)hi + n) >> f.s);
-}
-
 struct OpArgs {
   const void* ptr;
   long long bytes;  // extent of the tensor behind ptr (buffer-descriptor range for LDS-DMA loads)

@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
       if (gout) store16<T>(gout + v * VN, d[u]);
       float o[VN];
 #pragma unroll
-      for (int e = 0; e < VN; ++e) o[e] = TRAIN ? A[e] * d[u][e] + Bc[e] * yv[u][e] + Cc[e] : A[e] * d[u][e];
+      for (int e = 0; e < VN; ++e) o[e] = TRAIN ? fmaf(A[e], d[u][e], fmaf(Bc[e], yv[u][e], Cc[e])) : A[e] * d[u][e];
       store16<T>(dy + v * VN, o);
     }
   }
@@ -330,19 +330,28 @@ template <int VN> __device__ __forceinline__ uint8_t idx_byte(const typename Idx
   else return (uint8_t)((w >> (8 * e)) & 0xFF);
 }
 
-template <typename T>
+// BN: the input is the stem conv output y and the pooled values are a = relu(fma(y, scale, shift)) rounded to T
+// exactly as vcg_bn_apply stores them (the fused stem: no a tensor in HBM, same pooled values and argmax)
+template <typename T, bool BN>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int H, int W, int C, int OH,
-                                                          int OW, int lcpr, long long TV) {
+                                                          int OW, int lcpr, long long TV, FastDiv fd_ow, FastDiv fd_oh,
+                                                          const float* __restrict__ scale = nullptr,
+                                                          const float* __restrict__ shift = nullptr) {
   constexpr int VN = V<T>::N;
   const long long v = (long long)blockIdx.x * 256 + threadIdx.x;
   if (v >= TV) return;
   const int chunk = (int)(v & ((1 << lcpr) - 1));
+  float sc[VN], sh[VN];
+  if (BN) {
+    load_params<VN>(scale, chunk * VN, sc);
+    load_params<VN>(shift, chunk * VN, sh);
+  }
   const int pix = (int)(v >> lcpr);
-  const int ow = pix % OW;
-  const int t = pix / OW;
-  const int oh = t % OH;
-  const int n = t / OH;
+  const int t = (int)fdiv((uint32_t)pix, fd_ow);
+  const int ow = pix - t * OW;
+  const int n = (int)fdiv((uint32_t)t, fd_oh);
+  const int oh = t - n * OH;
   float best[VN];
   uint8_t bi[VN];
 #pragma unroll
@@ -355,6 +364,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
       if (iw < 0 || iw >= W) continue;
       float a[VN];
       load16<T>(x + (((long long)n * H + ih) * W + iw) * C + chunk * VN, a);
+      if (BN) {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) a[e] = to_f<T>(from_f<T>(fmaxf(fmaf(a[e], sc[e], sh[e]), 0.f)));
+      }
 #pragma unroll
       for (int e = 0; e < VN; ++e)
         if (a[e] > best[e] || isnan(a[e])) { best[e] = a[e]; bi[e] = (uint8_t)(kh * 3 + kw); }
@@ -365,37 +378,60 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
 }
 
 // thread = (input pixel, chunk): sums dy over the <= 4 windows whose argmax is this pixel. Grid-stride with
-// a fixed chunk per thread (cpr <= 256). RED: the result is the upstream gradient of the stem BN + ReLU:
-// masked by fma(y, msc, msh) > 0, stored as g, and reduced into per-block partials part[block][2C] of
-// sum g and sum g * (y - mean) * invstd (the BatchNorm backward sums; bn_bwd_finalize_kernel).
-template <typename T, bool RED>
+// a fixed chunk per thread (cpr <= 256). MODE (the stem's BN + ReLU backward around the pool):
+//   MP_PLAIN: dx = that sum;
+//   MP_RED / MP_RED_ONLY: g = the sum masked by the forward ReLU (fma(y, msc, msh) > 0), stored (MP_RED) or not,
+//     and reduced into per-block partials part[block][2C] of sum g and sum g * (y - mean) * invstd (the
+//     BatchNorm backward sums; bn_bwd_finalize_kernel) -- of g as stored (rounded to T);
+//   MP_APPLY: the same g (rounded to T) through the BatchNorm backward apply of bn_bwd_apply_kernel,
+//     dx = A g + B y + Cc (train statistics) or A g (running), so the stem needs no g tensor in HBM.
+enum { MP_PLAIN = 0, MP_RED = 1, MP_RED_ONLY = 2, MP_APPLY = 3 };
+struct MpBn {
+  const float *mean, *invstd, *msc, *msh;
+  float* part;
+  const float *gamma, *sum_g, *sum_gx;  // MP_APPLY
+  float inv_count;
+  int train;
+};
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                           T* __restrict__ dx, int H, int W, int C, int OH, int OW,
-                                                          int lcpr, long long TV, const T* __restrict__ yb,
-                                                          const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd,
-                                                          const float* __restrict__ msc,
-                                                          const float* __restrict__ msh, float* __restrict__ part) {
+                                                          int lcpr, long long TV, const T* __restrict__ yb, MpBn bn,
+                                                          FastDiv fd_w, FastDiv fd_h) {
   constexpr int VN = V<T>::N;
+  constexpr bool RED = MODE == MP_RED || MODE == MP_RED_ONLY;
+  constexpr bool MASK = MODE != MP_PLAIN;
   typedef typename IdxWord<VN>::t IW;
   __shared__ float red[RED ? 2 : 1][RED ? 256 : 1][VN];
   const int cpr = 1 << lcpr;
   const int chunk = threadIdx.x & (cpr - 1);
   const int c0 = chunk * VN;
-  float mu[VN], sc[VN], sh[VN], s1[VN], s2[VN];
-  if (RED) {
-    load_params<VN>(mean, c0, mu);
-    load_params<VN>(msc, c0, sc);
-    load_params<VN>(msh, c0, sh);
+  float mu[VN], sc[VN], sh[VN], s1[VN], s2[VN], A[VN], Bc[VN], Cc[VN];
+  if (MASK) {
+    load_params<VN>(bn.mean, c0, mu);
+    load_params<VN>(bn.msc, c0, sc);
+    load_params<VN>(bn.msh, c0, sh);
 #pragma unroll
     for (int e = 0; e < VN; ++e) s1[e] = s2[e] = 0.f;
   }
+  if (MODE == MP_APPLY) {  // bn_bwd_apply_kernel's affine map, same arithmetic
+    float is[VN], sgx[VN], sgg[VN];
+    load_params<VN>(bn.invstd, c0, is);
+    load_params<VN>(bn.sum_gx, c0, sgx);
+    load_params<VN>(bn.sum_g, c0, sgg);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      A[e] = (bn.gamma ? bn.gamma[c0 + e] : 1.f) * is[e];
+      Bc[e] = -A[e] * is[e] * sgx[e] * bn.inv_count;
+      Cc[e] = -A[e] * sgg[e] * bn.inv_count - Bc[e] * mu[e];
+    }
+  }
   for (long long v = (long long)blockIdx.x * 256 + threadIdx.x; v < TV; v += (long long)gridDim.x * 256) {
     const int pix = (int)(v >> lcpr);
-    const int iw = pix % W;
-    const int t = pix / W;
-    const int ih = t % H;
-    const int n = t / H;
+    const int t = (int)fdiv((uint32_t)pix, fd_w);
+    const int iw = pix - t * W;
+    const int n = (int)fdiv((uint32_t)t, fd_h);
+    const int ih = t - n * H;
     float acc[VN];
 #pragma unroll
     for (int e = 0; e < VN; ++e) acc[e] = 0.f;
@@ -403,7 +439,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
     const int oh0 = ih >> 1, oh1 = (ih + 1) >> 1;
     const int ow0 = iw >> 1, ow1 = (iw + 1) >> 1;
     float yv[VN];
-    if (RED) load16<T>(yb + v * VN, yv);
+    if (MASK) load16<T>(yb + v * VN, yv);
     float g[4][VN];
     IW w[4];
     bool use[4];
@@ -426,16 +462,20 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
       for (int e = 0; e < VN; ++e)
         if (idx_byte<VN>(w[q], e) == want[q]) acc[e] += g[q][e];
     }
-    if (RED) {
+    if (MASK) {
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
         acc[e] = fmaf(yv[e], sc[e], sh[e]) > 0.f ? acc[e] : 0.f;
-        const float gr = to_f<T>(from_f<T>(acc[e]));  // statistics of the stored gradient
-        s1[e] += gr;
-        s2[e] = fmaf(gr, yv[e] - mu[e], s2[e]);
+        const float gr = to_f<T>(from_f<T>(acc[e]));  // the gradient as stored
+        if (RED) {
+          s1[e] += gr;
+          s2[e] = fmaf(gr, yv[e] - mu[e], s2[e]);
+        } else {
+          acc[e] = bn.train ? fmaf(A[e], gr, fmaf(Bc[e], yv[e], Cc[e])) : A[e] * gr;  // bn_bwd_apply_kernel's order
+        }
       }
     }
-    store16<T>(dx + v * VN, acc);
+    if (MODE != MP_RED_ONLY) store16<T>(dx + v * VN, acc);
   }
   if (RED) {
 #pragma unroll
@@ -449,8 +489,124 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
       const int ch = c / VN, e = c - ch * VN;
       float a = 0.f;
       for (int k = ch; k < 256; k += cpr) a += red[which][k][e];
-      if (which) a *= invstd[c];
-      part[(long long)blockIdx.x * 2 * C + i] = a;
+      if (which) a *= bn.invstd[c];
+      bn.part[(long long)blockIdx.x * 2 * C + i] = a;
+    }
+  }
+}
+
+// The same backward with one thread per (2x2 input block, chunk) for even H and W: the block's 4 pixels are
+// reached by the 4 windows (k + {0,1}, j + {0,1}) only, so the 4 windows' dy / argmax loads and the index math are
+// shared by 4 pixels (9 pixel-window pairs: (0,0) <- 1 window, (0,1) / (1,0) <- 2, (1,1) <- 4); the per-pixel
+// work (ReLU mask, rounding, sums or BN apply) is the per-pixel kernel's, in the same order.
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                           T* __restrict__ dx, int H, int W, int C, int OH, int OW,
+                                                           int lcpr, long long TB, const T* __restrict__ yb, MpBn bn,
+                                                           FastDiv fd_bw, FastDiv fd_bh) {
+  constexpr int VN = V<T>::N;
+  constexpr bool RED = MODE == MP_RED || MODE == MP_RED_ONLY;
+  constexpr bool MASK = MODE != MP_PLAIN;
+  typedef typename IdxWord<VN>::t IW;
+  __shared__ float red[RED ? 2 : 1][RED ? 256 : 1][VN];
+  const int cpr = 1 << lcpr;
+  const int chunk = threadIdx.x & (cpr - 1);
+  const int c0 = chunk * VN;
+  const int BW = W >> 1, BH = H >> 1;
+  float mu[VN], sc[VN], sh[VN], s1[VN], s2[VN], A[VN], Bc[VN], Cc[VN];
+  if (MASK) {
+    load_params<VN>(bn.mean, c0, mu);
+    load_params<VN>(bn.msc, c0, sc);
+    load_params<VN>(bn.msh, c0, sh);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) s1[e] = s2[e] = 0.f;
+  }
+  if (MODE == MP_APPLY) {
+    float is[VN], sgx[VN], sgg[VN];
+    load_params<VN>(bn.invstd, c0, is);
+    load_params<VN>(bn.sum_gx, c0, sgx);
+    load_params<VN>(bn.sum_g, c0, sgg);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      A[e] = (bn.gamma ? bn.gamma[c0 + e] : 1.f) * is[e];
+      Bc[e] = -A[e] * is[e] * sgx[e] * bn.inv_count;
+      Cc[e] = -A[e] * sgg[e] * bn.inv_count - Bc[e] * mu[e];
+    }
+  }
+  for (long long b = (long long)blockIdx.x * 256 + threadIdx.x; b < TB; b += (long long)gridDim.x * 256) {
+    const int blk = (int)(b >> lcpr);
+    const int t = (int)fdiv((uint32_t)blk, fd_bw);
+    const int j = blk - t * BW;
+    const int n = (int)fdiv((uint32_t)t, fd_bh);
+    const int k = t - n * BH;
+    // windows q = 2 dr + dc at (k + dr, j + dc)
+    float g[4][VN];
+    IW w[4];
+    bool use[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oh = k + (q >> 1), ow = j + (q & 1);
+      use[q] = oh < OH && ow < OW;
+      if (use[q]) {
+        const long long o = (((long long)n * OH + oh) * OW + ow) * C + c0;
+        load16<T>(dy + o, g[q]);
+        w[q] = *reinterpret_cast<const IW*>(idx + o);
+      }
+    }
+    float yv[4][VN];
+    long long pv[4];
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) {  // pixel (2k + a, 2j + c), pp = 2a + c
+      pv[pp] = ((((long long)n * H + 2 * k + (pp >> 1)) * W + 2 * j + (pp & 1)) << lcpr) + chunk;
+      if (MASK) load16<T>(yb + pv[pp] * VN, yv[pp]);
+    }
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) {
+      const int a = pp >> 1, c = pp & 1;
+      float acc[VN];
+#pragma unroll
+      for (int e = 0; e < VN; ++e) acc[e] = 0.f;
+      // windows in the per-pixel kernel's order (oh0, ow0), (oh0, ow1), (oh1, ow0), (oh1, ow1): kh = a + 1 - 2 dr
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dr = q >> 1, dc = q & 1;
+        if ((dr && !a) || (dc && !c)) continue;  // window row / column does not contain this pixel
+        if (!use[q]) continue;
+        const uint8_t want = (uint8_t)((a + 1 - 2 * dr) * 3 + (c + 1 - 2 * dc));
+#pragma unroll
+        for (int e = 0; e < VN; ++e)
+          if (idx_byte<VN>(w[q], e) == want) acc[e] += g[q][e];
+      }
+      if (MASK) {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) {
+          acc[e] = fmaf(yv[pp][e], sc[e], sh[e]) > 0.f ? acc[e] : 0.f;
+          const float gr = to_f<T>(from_f<T>(acc[e]));
+          if (RED) {
+            s1[e] += gr;
+            s2[e] = fmaf(gr, yv[pp][e] - mu[e], s2[e]);
+          } else {
+            acc[e] = bn.train ? fmaf(A[e], gr, fmaf(Bc[e], yv[pp][e], Cc[e])) : A[e] * gr;
+          }
+        }
+      }
+      if (MODE != MP_RED_ONLY) store16<T>(dx + pv[pp] * VN, acc);
+    }
+  }
+  if (RED) {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      red[0][threadIdx.x][e] = s1[e];
+      red[1][threadIdx.x][e] = s2[e];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * C; i += 256) {
+      const int which = i >= C, c = i - which * C;
+      const int ch = c / VN, e = c - ch * VN;
+      float a = 0.f;
+      for (int kk = ch; kk < 256; kk += cpr) a += red[which][kk][e];
+      if (which) a *= bn.invstd[c];
+      bn.part[(long long)blockIdx.x * 2 * C + i] = a;
     }
   }
 }
@@ -672,11 +828,11 @@ VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* id
   const long long TV = (long long)N * OH * OW * (C / VN);
   VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
   if (dtype == VCG_BF16)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const bf16_t*)x,
-                       (bf16_t*)y, idx, H, W, C, OH, OW, lcpr, TV);
+    hipLaunchKernelGGL((maxpool_fwd_kernel<bf16_t, false>), dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const bf16_t*)x,
+                       (bf16_t*)y, idx, H, W, C, OH, OW, lcpr, TV, make_fastdiv(OW), make_fastdiv(OH));
   else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const float*)x,
-                       (float*)y, idx, H, W, C, OH, OW, lcpr, TV);
+    hipLaunchKernelGGL((maxpool_fwd_kernel<float, false>), dim3(blocks_for(TV, 256)), dim3(256), 0, s, (const float*)x,
+                       (float*)y, idx, H, W, C, OH, OW, lcpr, TV, make_fastdiv(OW), make_fastdiv(OH));
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -691,11 +847,11 @@ VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx,
   VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
   const unsigned g = stream_grid(TV);
   if (dtype == VCG_BF16)
-    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16_t, false>), dim3(g), dim3(256), 0, s, (const bf16_t*)dy, idx,
-                       (bf16_t*)dx, H, W, C, OH, OW, lcpr, TV, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16_t, MP_PLAIN>), dim3(g), dim3(256), 0, s, (const bf16_t*)dy, idx,
+                       (bf16_t*)dx, H, W, C, OH, OW, lcpr, TV, nullptr, MpBn{}, make_fastdiv(W), make_fastdiv(H));
   else
-    hipLaunchKernelGGL((maxpool_bwd_kernel<float, false>), dim3(g), dim3(256), 0, s, (const float*)dy, idx,
-                       (float*)dx, H, W, C, OH, OW, lcpr, TV, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<float, MP_PLAIN>), dim3(g), dim3(256), 0, s, (const float*)dy, idx,
+                       (float*)dx, H, W, C, OH, OW, lcpr, TV, nullptr, MpBn{}, make_fastdiv(W), make_fastdiv(H));
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -703,7 +859,8 @@ VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx,
 VCG_API long long vcg_maxpool_bwd_bn_ws_bytes(int C) { return GRID_MAX * 2 * C * 4 + 64; }
 
 // max-pool backward fused with the stem BatchNorm-backward reduction: g = maxpool_bwd(dy) masked by the
-// forward ReLU (fma(y, mscale, mshift) > 0); sum_g / sum_gx finalized, dgamma / dbeta accumulated.
+// forward ReLU (fma(y, mscale, mshift) > 0); sum_g / sum_gx finalized, dgamma / dbeta accumulated. g == NULL:
+// the sums only (vcg_maxpool_bwd_bn_apply then recomputes g).
 VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* idx, void* g, int N, int H, int W,
                                int C, const void* y, const float* mean, const float* invstd, const float* mscale,
                                const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx,
@@ -717,15 +874,77 @@ VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* i
   const long long TV = (long long)N * H * W * (C / VN);
   VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
   const unsigned nb = stream_grid(TV);
-  if (dtype == VCG_BF16)
-    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16_t, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dy, idx,
-                       (bf16_t*)g, H, W, C, OH, OW, lcpr, TV, (const bf16_t*)y, mean, invstd, mscale, mshift, ws);
-  else
-    hipLaunchKernelGGL((maxpool_bwd_kernel<float, true>), dim3(nb), dim3(256), 0, s, (const float*)dy, idx,
-                       (float*)g, H, W, C, OH, OW, lcpr, TV, (const float*)y, mean, invstd, mscale, mshift, ws);
+  MpBn bn{};
+  bn.mean = mean; bn.invstd = invstd; bn.msc = mscale; bn.msh = mshift; bn.part = ws;
+#define VCG_MPB(T, M, OUT)                                                                                          \
+  do {                                                                                                              \
+    if ((H & 1) == 0 && (W & 1) == 0)                                                                               \
+      hipLaunchKernelGGL((maxpool_bwd2_kernel<T, M>), dim3(nb), dim3(256), 0, s, (const T*)dy, idx, (T*)OUT, H, W, C, \
+                         OH, OW, lcpr, TV / 4, (const T*)y, bn, make_fastdiv(W / 2), make_fastdiv(H / 2));           \
+    else                                                                                                            \
+      hipLaunchKernelGGL((maxpool_bwd_kernel<T, M>), dim3(nb), dim3(256), 0, s, (const T*)dy, idx, (T*)OUT, H, W, C, \
+                         OH, OW, lcpr, TV, (const T*)y, bn, make_fastdiv(W), make_fastdiv(H));                       \
+  } while (0)
+  if (dtype == VCG_BF16) {
+    if (g) VCG_MPB(bf16_t, MP_RED, g); else VCG_MPB(bf16_t, MP_RED_ONLY, g);
+  } else {
+    if (g) VCG_MPB(float, MP_RED, g); else VCG_MPB(float, MP_RED_ONLY, g);
+  }
   VCG_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
                      sum_g, sum_gx, dgamma, dbeta, 1);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+// The stem's BatchNorm backward apply fused with the max-pool backward: dx = bn_bwd_apply(g) with g =
+// maxpool_bwd(dy) masked by the forward ReLU and rounded to the storage type (the value vcg_maxpool_bwd_bn
+// would store), sums from vcg_maxpool_bwd_bn(g = NULL). Equals vcg_maxpool_bwd_bn + vcg_bn_bwd_apply (mask
+// mode 0) on that g, without the g round trip through HBM.
+VCG_API int vcg_maxpool_bwd_bn_apply(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H,
+                                     int W, int C, const void* y, const float* mean, const float* invstd,
+                                     const float* mscale, const float* mshift, const float* gamma, const float* sum_g,
+                                     const float* sum_gx, long long count, int train_stats, hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && C / VN <= 256, "C must be a power of two multiple of the vector width");
+  VCG_REQUIRE(y && mean && invstd && mscale && mshift && sum_g && sum_gx && count > 0, "BN arguments required");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int lcpr = ilog2i(C / VN);
+  const long long TV = (long long)N * H * W * (C / VN);
+  VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
+  MpBn bn{};
+  bn.mean = mean; bn.invstd = invstd; bn.msc = mscale; bn.msh = mshift;
+  bn.gamma = gamma; bn.sum_g = sum_g; bn.sum_gx = sum_gx; bn.inv_count = 1.f / (float)count; bn.train = train_stats;
+  const unsigned nb = stream_grid(TV);
+  if (dtype == VCG_BF16) {
+    VCG_MPB(bf16_t, MP_APPLY, dx);
+  } else {
+    VCG_MPB(float, MP_APPLY, dx);
+  }
+#undef VCG_MPB
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+// The stem's BatchNorm + ReLU fused into the max-pool: out / idx = maxpool(relu(fma(y, scale, shift))) with the
+// activation rounded to the storage type first (the values and argmax of vcg_bn_apply then vcg_maxpool_fwd).
+VCG_API int vcg_bn_relu_maxpool(int dtype, const void* y, const float* scale, const float* shift, void* out,
+                                unsigned char* idx, int N, int H, int W, int C, hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && C / VN <= 256, "C must be a power of two multiple of the vector width");
+  VCG_REQUIRE(scale && shift, "scale / shift required");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const int lcpr = ilog2i(C / VN);
+  const long long TV = (long long)N * OH * OW * (C / VN);
+  VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<bf16_t, true>), dim3(blocks_for(TV, 256)), dim3(256), 0, s,
+                       (const bf16_t*)y, (bf16_t*)out, idx, H, W, C, OH, OW, lcpr, TV, make_fastdiv(OW),
+                       make_fastdiv(OH), scale, shift);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<float, true>), dim3(blocks_for(TV, 256)), dim3(256), 0, s,
+                       (const float*)y, (float*)out, idx, H, W, C, OH, OW, lcpr, TV, make_fastdiv(OW),
+                       make_fastdiv(OH), scale, shift);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

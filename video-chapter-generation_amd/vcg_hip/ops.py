@@ -268,13 +268,35 @@ def maxpool_bwd(dy, idx, N, H, W, C):
     return dx
 
 
-def maxpool_bwd_bn(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, sums, dgamma=None, dbeta=None):
-    """maxpool backward + the stem BN + ReLU mask + BN-backward sums (sums [2, C] = sum_g, sum_gx)."""
-    g = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+def maxpool_bwd_bn(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, sums, dgamma=None, dbeta=None,
+                   store_g=True):
+    """maxpool backward + the stem BN + ReLU mask + BN-backward sums (sums [2, C] = sum_g, sum_gx). Returns the
+    masked gradient g, or None with store_g=False (sums only: maxpool_bwd_bn_apply recomputes g)."""
+    g = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device) if store_g else None
     w = ws(_lib.query("vcg_maxpool_bwd_bn_ws_bytes", C), dy.device)
     _lib.call("vcg_maxpool_bwd_bn", dt_code(dy.dtype), P(dy), P(idx), P(g), N, H, W, C, P(y), P(mean), P(invstd),
               P(mscale), P(mshift), P(w), w.numel() * 4, P(sums[0]), P(sums[1]), P(dgamma), P(dbeta), stream())
     return g
+
+
+def maxpool_bwd_bn_apply(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, gamma, sums, count, train_stats):
+    """The stem's BN-backward apply on g = mask(maxpool_bwd(dy)) recomputed in the same pass (sums from
+    maxpool_bwd_bn(store_g=False)): returns the gradient of the stem conv output y."""
+    dx = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    _lib.call("vcg_maxpool_bwd_bn_apply", dt_code(dy.dtype), P(dy), P(idx), P(dx), N, H, W, C, P(y), P(mean),
+              P(invstd), P(mscale), P(mshift), P(gamma), P(sums[0]), P(sums[1]), int(count), int(bool(train_stats)),
+              stream())
+    return dx
+
+
+def bn_relu_maxpool(y, scale, shift, N, H, W, C):
+    """maxpool3x3/2(relu(y * scale + shift)) with the activation rounded to y's dtype (the values and argmax of
+    bn_apply + maxpool_fwd, without the activation tensor). Returns (pooled, idx)."""
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = torch.empty((N, OH, OW, C), dtype=y.dtype, device=y.device)
+    idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=y.device)
+    _lib.call("vcg_bn_relu_maxpool", dt_code(y.dtype), P(y), P(scale), P(shift), P(out), P(idx), N, H, W, C, stream())
+    return out, idx
 
 
 def avgpool_fwd(x, N, HW, C):
