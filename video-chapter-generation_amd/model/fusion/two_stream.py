@@ -13,13 +13,13 @@ import torch
 from torch import nn
 from torch.nn import functional as F
 
-from vcg_hip.nn import BertModel, NativeRoot, ResNet50, new_seed
+from vcg_hip.nn import BertConfig, BertModel, NativeRoot, ResNet50, new_seed
 from vcg_hip.optim import configure_adamw
 
 
 class SelfAttention(nn.Module):
-    """Reference SelfAttention (two_stream.py:8-48): parameters and names only; the 'attn' head is
-    not on the native path yet (the benchmarked configuration is head_type='mlp')."""
+    """Reference SelfAttention (two_stream.py:8-48): parameters and state-dict names; the 'attn' head's forward
+    and backward run natively (vcg_head_attn_fwd / _bwd, head_attn.hip)."""
 
     def __init__(self, n_embd, n_head, output_size, attn_pdrop=0.1, resid_pdrop=0.1):
         super().__init__()
@@ -52,14 +52,60 @@ class ChapterHead(nn.Module):
             raise RuntimeError(f"Unknown head_type {head_type}")
 
 
+_BERT_CFG_KEYS = ("vocab_size", "hidden_size", "num_hidden_layers", "num_attention_heads", "intermediate_size",
+                  "hidden_dropout_prob", "attention_probs_dropout_prob", "max_position_embeddings", "type_vocab_size",
+                  "layer_norm_eps", "pad_token_id", "initializer_range")
+
+
+def adopt_lang_model(m):
+    """The lang encoder as the native BertModel. A foreign BERT encoder (the transformers.BertModel that the
+    reference's BertHugface holds as base_model, bert_hugface.py:20) is converted: same config, same state-dict
+    names, weights copied; dropout rates come from its config as in the reference."""
+    if isinstance(m, BertModel):
+        return m
+    cfg = getattr(m, "config", None)
+    if cfg is None or not hasattr(m, "embeddings") or not hasattr(m, "encoder"):
+        raise TypeError(f"TwoStream: cannot adopt lang model {type(m).__name__} (expected a BERT encoder)")
+    if getattr(cfg, "hidden_act", "gelu") != "gelu" or getattr(cfg, "position_embedding_type", "absolute") != "absolute":
+        raise TypeError("TwoStream: the native BERT implements hidden_act='gelu' with absolute position embeddings")
+    native = BertModel(BertConfig(**{k: getattr(cfg, k) for k in _BERT_CFG_KEYS if hasattr(cfg, k)}),
+                       add_pooling_layer=getattr(m, "pooler", None) is not None)
+    sd = {k: v for k, v in m.state_dict().items() if not k.endswith(("position_ids", "token_type_ids"))}
+    missing, unexpected = native.load_state_dict(sd, strict=False)
+    if missing or unexpected:
+        raise TypeError(f"TwoStream: BERT state dict mismatch (missing {missing[:4]}, unexpected {unexpected[:4]})")
+    return native.train(m.training)
+
+
+def adopt_vision_model(m):
+    """The vision trunk as the native ResNet50. A foreign torchvision-topology resnet50 (the reference's
+    Resnet50TSM.base_model: TemporalShift(n_segment, fold_div) around every bottleneck conv1, fc = Identity,
+    resnet50_tsm.py:10-20) is rebuilt natively with the same shift geometry and its weights / BN buffers copied."""
+    if isinstance(m, ResNet50):
+        return m
+    from ops.basic_ops import Identity
+    from ops.temporal_shift import make_temporal_shift
+    shifts = [x for x in m.modules() if hasattr(x, "n_segment") and hasattr(x, "fold_div") and hasattr(x, "net")]
+    native = ResNet50()
+    if shifts:
+        make_temporal_shift(native, n_segment=shifts[0].n_segment, n_div=shifts[0].fold_div)
+    fc = getattr(m, "fc", None)
+    if fc is not None and not any(True for _ in fc.parameters()):
+        native.fc = Identity()
+    missing, unexpected = native.load_state_dict(m.state_dict(), strict=False)
+    if missing or unexpected:
+        raise TypeError(f"TwoStream: cannot adopt vision model {type(m).__name__} (missing {missing[:4]}, "
+                        f"unexpected {unexpected[:4]})")
+    return native.train(m.training)
+
+
 class TwoStream(NativeRoot, nn.Module):
     def __init__(self, lang_model, vision_model, lang_embed_size, vision_embed_size, segment_size, hidden_size):
         super().__init__()
-        if not isinstance(lang_model, BertModel) or not isinstance(vision_model, ResNet50):
-            raise TypeError("TwoStream expects the native BertModel (BertHugface.base_model) and ResNet50 "
-                            "(Resnet50TSM.base_model)")
-        self.lang_model = lang_model
-        self.vision_model = vision_model
+        # the native encoders (BertHugface / Resnet50TSM .base_model) are used as given; a reference-built
+        # transformers BertModel / torchvision-topology TSM resnet50 is converted (weights copied)
+        self.lang_model = adopt_lang_model(lang_model)
+        self.vision_model = adopt_vision_model(vision_model)
         self.segment_size = segment_size
         self.lang_embed_size = lang_embed_size
         self.vision_embed_size = vision_embed_size

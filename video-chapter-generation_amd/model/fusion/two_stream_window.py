@@ -158,8 +158,9 @@ class TwoStream(NativeRoot, nn.Module):
     def __init__(self, lang_model, vision_model, lang_embed_size, vision_embed_size, segment_size, hidden_size,
                  window_size):
         super().__init__()
-        self.lang_model = lang_model
-        self.vision_model = vision_model
+        from model.fusion.two_stream import adopt_lang_model, adopt_vision_model
+        self.lang_model = adopt_lang_model(lang_model)      # foreign (reference-built) encoders are converted
+        self.vision_model = adopt_vision_model(vision_model)
         self.segment_size = segment_size
         self.lang_embed_size = lang_embed_size
         self.vision_embed_size = vision_embed_size

@@ -12,30 +12,28 @@ from . import flat as flatmod
 from . import ops
 
 
+def _no_decay(full_name, leaf_name):
+    """The reference grouping rule (two_stream.py:135-164, resnet50_tsm.py:35-65): biases, LayerNorm, BatchNorm
+    ("bn") and embedding ("emb") parameters take no weight decay."""
+    return leaf_name.endswith("bias") or any(tag in full_name for tag in ("LayerNorm", "bn", "emb"))
+
+
 def param_groups(model, weight_decay):
-    decay, no_decay = set(), set()
-    for mn, m in model.named_modules():
-        for pn, p in m.named_parameters():
-            fpn = "%s.%s" % (mn, pn) if mn else pn
-            if pn.endswith("bias"):
-                no_decay.add(fpn)
-            elif "LayerNorm" in fpn:
-                no_decay.add(fpn)
-            elif "bn" in fpn:
-                no_decay.add(fpn)
-            elif "emb" in fpn:
-                no_decay.add(fpn)
-            else:
-                decay.add(fpn)
-    param_dict = {pn: p for pn, p in model.named_parameters()}
-    inter = decay & no_decay
-    union = decay | no_decay
-    assert len(inter) == 0, "parameters %s made it into both decay/no_decay sets!" % (str(inter),)
-    assert len(param_dict.keys() - union) == 0, "parameters %s were not separated into either decay/no_decay set!" % (
-        str(param_dict.keys() - union),)
+    """[decay group, no-decay group] over every parameter, each sorted by name (the reference's order)."""
+    named = dict(model.named_parameters())
+    owner = {}  # full name -> decided by the module that owns it directly
+    for mod_name, mod in model.named_modules():
+        for leaf, _ in mod.named_parameters(recurse=False):
+            full = f"{mod_name}.{leaf}" if mod_name else leaf
+            owner[full] = _no_decay(full, leaf)
+    unassigned = set(named) - set(owner)
+    if unassigned:
+        raise ValueError(f"param_groups: no owning module found for {sorted(unassigned)}")
+    decay = sorted(n for n, nd in owner.items() if not nd and n in named)
+    no_decay = sorted(n for n, nd in owner.items() if nd and n in named)
     return [
-        {"params": [param_dict[pn] for pn in sorted(list(decay))], "weight_decay": weight_decay},
-        {"params": [param_dict[pn] for pn in sorted(list(no_decay))], "weight_decay": 0.0},
+        {"params": [named[n] for n in decay], "weight_decay": weight_decay},
+        {"params": [named[n] for n in no_decay], "weight_decay": 0.0},
     ]
 
 
