@@ -47,6 +47,10 @@ VCG_API int vcg_timing_roofline(int kernel_id, double peak_tflops, double peak_g
    tile top, after the DMA wait + barrier, after the next DMA issue, after the MFMAs, after the barrier, after the
    epilogue. Returns 1 when no stamped launch happened. */
 VCG_API int vcg_patch_stamps(unsigned long long* out, int n);
+/* Profiling aid: per-tile phase stamps of workgroup 0 / wave 0 of the last igemm_fast launch, 4 per tile (first
+   k-step, after the last MFMAs, after the output staging, after the epilogue) -- only in a library built with
+   -DVCG_FAST_STAMPS (make EXTRA=-DVCG_FAST_STAMPS); returns 1 otherwise. */
+VCG_API int vcg_fast_stamps(unsigned long long* out, int n);
 
 /* ---- MFMA implicit-GEMM engine (igemm.hip) ---------------------------------------------- */
 /* torchvision conv2d inside Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15,68-77), with

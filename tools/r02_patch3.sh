@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/p3_tests.log
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/p3_bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/p3_bench.log; exit 1; }
 tail -1 gpurun_out/p3_bench.log | cut -c1-400
-bash tools/r02_prof.sh r02stem
+bash tools/r02_prof.sh r02flush

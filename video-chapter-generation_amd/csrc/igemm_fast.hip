@@ -388,17 +388,24 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
   const bf16_t* yp = reinterpret_cast<const bf16_t*>(e.y);
   const bf16_t* y2p = LIGHT ? nullptr : reinterpret_cast<const bf16_t*>(e.y2);
   const uint8_t* bitsp = LIGHT ? nullptr : e.bits;
+  // (rows beyond mlim / columns beyond N are clamped to a valid address and discarded after the load: a load
+  // under a per-element condition makes hipcc branch around it and wait vmcnt(0) per element, i.e. one HBM round
+  // trip per chunk; each operand's loads sit under ONE uniform branch per batch instead: l1 / l2 / l3 conv1 fused
+  // dgrads 1453 / 760 / 421 -> 1354 / 615 / 355 us, tools/bench_dgrad.py. Rejected: pulling the next tile's
+  // residual / y rows into L2 by LDS-DMA pieces into a scratch slot after each flush, +15-20 %.)
+  const int nc = min(n, p.N - 8);
 #pragma unroll
   for (int k0 = 0; k0 < KC; k0 += KB) {
-    long long off[KB];
-    bool ok[KB], src[KB];
+    long long off[KB], roff[KB];
+    bool ok[KB], src[KB], rok[KB];
     uint4 rv[KB], yv[KB], y2v[KB];
     uint32_t bv[KB];
 #pragma unroll
-    for (int kk = 0; kk < KB; ++kk) {  // all loads of the batch first
+    for (int kk = 0; kk < KB; ++kk) {  // addresses of the batch
       const int id = threadIdx.x + NTH * (k0 + kk);
-      const int m = m0 + id / CPR;
-      ok[kk] = m < mlim && n < p.N;
+      const int mr = m0 + id / CPR;
+      ok[kk] = mr < mlim && n < p.N;
+      const int m = min(mr, mlim - 1);
       src[kk] = true;
       int dst = m;
       if (e.sub) {  // sub-pixel class row -> dx row
@@ -406,7 +413,7 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
         const uint32_t i = fdiv(r, e.fd_cw), j = r - i * (uint32_t)e.cW;
         dst = (int)((f * e.fH + 2 * i + e.ry) * e.fW + 2 * j + e.rx);
       }
-      if (shift != 0 && ok[kk]) {
+      if (shift != 0) {
         const int f = (int)fdiv((uint32_t)m, e.fd_hw);
         const int t = f - (int)fdiv((uint32_t)f, e.fd_T) * e.tsm_T;
         const bool edge = shift > 0 ? t == e.tsm_T - 1 : t == 0;
@@ -414,22 +421,35 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
         dst = edge ? m - shift * (e.tsm_T - 1) * e.hw : m + shift * e.hw;
       }
       off[kk] = (long long)dst * p.ldc + n;
-      if (ok[kk]) {
-        if (res) {
-          long long roff = off[kk];
-          bool rok = true;
-          if (!LIGHT && e.res_s > 1) {  // compact residual of a 1x1 / stride-2 conv: only even (h, w) rows carry one
-            const uint32_t f = fdiv((uint32_t)dst, e.fd_hw), r = (uint32_t)dst - f * (uint32_t)e.hw;
-            const uint32_t h = fdiv(r, e.fd_w), w = r - h * e.fd_w.d;
-            rok = ((h | w) & 1u) == 0;
-            roff = ((long long)(f * e.rH + (h >> 1)) * e.rW + (w >> 1)) * p.ldc + n;
-          }
-          rv[kk] = rok ? *reinterpret_cast<const uint4*>(res + roff) : make_uint4(0u, 0u, 0u, 0u);
-        }
-        if (bitsp) bv[kk] = bitsp[off[kk] >> 3];
-        if (yp) yv[kk] = *reinterpret_cast<const uint4*>(yp + off[kk]);
-        if (y2p) y2v[kk] = *reinterpret_cast<const uint4*>(y2p + off[kk]);
+      roff[kk] = (long long)dst * p.ldc + nc;
+      rok[kk] = true;
+      if (!LIGHT && e.res_s > 1) {  // compact residual of a 1x1 / stride-2 conv: only even (h, w) rows carry one
+        const uint32_t f = fdiv((uint32_t)dst, e.fd_hw), r = (uint32_t)dst - f * (uint32_t)e.hw;
+        const uint32_t h = fdiv(r, e.fd_w), w = r - h * e.fd_w.d;
+        rok[kk] = ((h | w) & 1u) == 0;
+        roff[kk] = ((long long)(f * e.rH + (h >> 1)) * e.rW + (w >> 1)) * p.ldc + nc;
       }
+    }
+    const long long* loff = off;  // y / y2 / bits rows (column clamped below)
+    if (res) {
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) rv[kk] = *reinterpret_cast<const uint4*>(res + roff[kk]);
+    }
+    if (bitsp) {
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) bv[kk] = bitsp[(loff[kk] - n + nc) >> 3];
+    }
+    if (yp) {
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) yv[kk] = *reinterpret_cast<const uint4*>(yp + loff[kk] - n + nc);
+    }
+    if (y2p) {
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) y2v[kk] = *reinterpret_cast<const uint4*>(y2p + loff[kk] - n + nc);
+    }
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      if (!rok[kk]) rv[kk] = make_uint4(0u, 0u, 0u, 0u);
     }
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk) {
@@ -604,6 +624,19 @@ __device__ __forceinline__ void stats_finish(const GemmParams& p, float* scratch
   }
 }
 
+// Profiling build (make EXTRA=-DVCG_FAST_STAMPS OUT=... OBJDIR=...): s_memtime per tile phase of workgroup 0,
+// wave 0 of every igemm_fast launch (the last launch's survive): tile's first k-step, after its last MFMAs,
+// after the output staging, after the epilogue flush. vcg_fast_stamps() copies them out.
+#ifdef VCG_FAST_STAMPS
+__device__ unsigned long long g_fast_stamps[64 * 4];
+#define FAST_STAMP(t, k)                                                                       \
+  do {                                                                                         \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (t) < 64) g_fast_stamps[(t) * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define FAST_STAMP(t, k) do {} while (0)
+#endif
+
 template <int BM, int BN, int AM, int EPI, bool RES>
 __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(EPI == EPI_BWD_AFF && BN == 64 ? 3 : 2)))
 void igemm_fast_kernel(GemmParams p) {
@@ -733,6 +766,7 @@ void igemm_fast_kernel(GemmParams p) {
     else if (ahead >= 1) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NLD));
     else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
     __builtin_amdgcn_s_barrier();
+    if (kt == 0) FAST_STAMP(tile, 0);
     const bf16_t* Ac = As + cur * AE;
     const bf16_t* Bc = Bs + cur * BE;
 #pragma unroll
@@ -752,6 +786,7 @@ void igemm_fast_kernel(GemmParams p) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
     __builtin_amdgcn_s_barrier();
     if (++kt == ntiles) {
+      FAST_STAMP(tile, 1);
       const int mt = by + tile * gy;
       bf16_t* stA = As + cur * AE;  // the finished stage holds the output rounds (see stage_put)
       bf16_t* stB = BM == 256 ? stA + 64 * BN : Bs + cur * BE;
@@ -769,6 +804,7 @@ void igemm_fast_kernel(GemmParams p) {
                 stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
               }
           }
+          FAST_STAMP(tile, 2);
           stage_flush_bwd<BM, BN, EPI == EPI_BWD_AFF>(stA, stB, p, Cout, mt * BM + 128 * h, n0, cpar, b1, b2, b3, p.M);
         }
       } else if constexpr (EPI == EPI_STATS) {  // conv outputs: no bias / activation, alpha = 1
@@ -793,6 +829,7 @@ void igemm_fast_kernel(GemmParams p) {
         if constexpr (BM == 128)
           gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);
       }
+      FAST_STAMP(tile, 3);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -1296,6 +1333,18 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
 
 // Profiling aid: the phase stamps (s_memtime) of the last patch-conv launch with VCG_PATCH_STAMPS=1, workgroup 0
 // wave 0, 6 per tile (top, after wait+barrier, after DMA issue, after MFMAs, after barrier, after epilogue).
+VCG_API int vcg_fast_stamps(unsigned long long* out, int n) {
+#ifdef VCG_FAST_STAMPS
+  n = n < 64 * 4 ? n : 64 * 4;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vcg::g_fast_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0 : 2;
+#else
+  (void)out;
+  (void)n;
+  return 1;
+#endif
+}
+
 VCG_API int vcg_patch_stamps(unsigned long long* out, int n) {
   if (!vcg::g_patch_stamps) return 1;
   n = n < 64 * 6 ? n : 64 * 6;

@@ -92,12 +92,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, 
   for (; base < TV; base += stride) {
     float a[SU][VN], r[SU][VN];
 #pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const long long v = base + u * 256;
-      if (v < TV) {
-        load16<T>(y + v * VN, a[u]);
-        if (RES) load16<T>(res + v * VN, r[u]);
-      }
+    for (int u = 0; u < SU; ++u) {  // unconditional loads (clamped index): no per-vector branch + wait
+      const long long v = min(base + u * 256, TV - 1);
+      load16<T>(y + v * VN, a[u]);
+      if (RES) load16<T>(res + v * VN, r[u]);
     }
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
@@ -152,13 +150,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   for (long long r = r0 + (narrow ? tid / cpr : 0); r < r1; r += (long long)rstep * SU) {
     float d[SU][VN], yv[SU][VN];
 #pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const long long rr = r + (long long)u * rstep;
-      if (rr < r1) {
-        const long long v = rr * cpr + chunk;
-        load16<T>(dout + v * VN, d[u]);
-        load16<T>(y + v * VN, yv[u]);
-      }
+    for (int u = 0; u < SU; ++u) {  // unconditional loads (clamped row): no per-vector branch + wait
+      const long long rr = min(r + (long long)u * rstep, r1 - 1);
+      const long long v = rr * cpr + chunk;
+      load16<T>(dout + v * VN, d[u]);
+      load16<T>(y + v * VN, yv[u]);
     }
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
@@ -283,12 +279,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   for (; base < TV; base += stride) {
     float d[SU][VN], yv[SU][VN];
 #pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const long long v = base + u * 256;
-      if (v < TV) {
-        load16<T>(dout + v * VN, d[u]);
-        if (NEED_Y) load16<T>(y + v * VN, yv[u]);
-      }
+    for (int u = 0; u < SU; ++u) {  // unconditional loads (clamped index): no per-vector branch + wait
+      const long long v = min(base + u * 256, TV - 1);
+      load16<T>(dout + v * VN, d[u]);
+      if (NEED_Y) load16<T>(y + v * VN, yv[u]);
     }
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
@@ -356,22 +350,25 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
   uint8_t bi[VN];
 #pragma unroll
   for (int e = 0; e < VN; ++e) { best[e] = -INFINITY; bi[e] = 0; }
-  for (int kh = 0; kh < 3; ++kh) {
-    const int ih = oh * 2 - 1 + kh;
-    if (ih < 0 || ih >= H) continue;
-    for (int kw = 0; kw < 3; ++kw) {
-      const int iw = ow * 2 - 1 + kw;
-      if (iw < 0 || iw >= W) continue;
-      float a[VN];
-      load16<T>(x + (((long long)n * H + ih) * W + iw) * C + chunk * VN, a);
-      if (BN) {
+  // all 9 window loads first, from clamped (always valid) pixels; padding taps are dropped after the load (a
+  // load under a per-tap condition makes hipcc wait for each one separately)
+  float a[9][VN];
 #pragma unroll
-        for (int e = 0; e < VN; ++e) a[e] = to_f<T>(from_f<T>(fmaxf(fmaf(a[e], sc[e], sh[e]), 0.f)));
-      }
+  for (int k = 0; k < 9; ++k) {
+    const int ih = min(max(oh * 2 - 1 + k / 3, 0), H - 1), iw = min(max(ow * 2 - 1 + k % 3, 0), W - 1);
+    load16<T>(x + (((long long)n * H + ih) * W + iw) * C + chunk * VN, a[k]);
+  }
 #pragma unroll
-      for (int e = 0; e < VN; ++e)
-        if (a[e] > best[e] || isnan(a[e])) { best[e] = a[e]; bi[e] = (uint8_t)(kh * 3 + kw); }
+  for (int k = 0; k < 9; ++k) {
+    const int ih = oh * 2 - 1 + k / 3, iw = ow * 2 - 1 + k % 3;
+    if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+    if (BN) {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) a[k][e] = to_f<T>(from_f<T>(fmaxf(fmaf(a[k][e], sc[e], sh[e]), 0.f)));
     }
+#pragma unroll
+    for (int e = 0; e < VN; ++e)
+      if (a[k][e] > best[e] || isnan(a[k][e])) { best[e] = a[k][e]; bi[e] = (uint8_t)k; }
   }
   store16<T>(y + v * VN, best);
   idx_store<VN>(idx + v * VN, bi);
@@ -449,11 +446,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
       const int oh = (q & 2) ? oh1 : oh0, ow = (q & 1) ? ow1 : ow0;
       use[q] = (!(q & 2) || oh1 != oh0) && (!(q & 1) || ow1 != ow0) && oh < OH && ow < OW;
       want[q] = (uint8_t)((ih - (oh * 2 - 1)) * 3 + (iw - (ow * 2 - 1)));
-      if (use[q]) {
-        const long long o = (((long long)n * OH + oh) * OW + ow) * C + chunk * VN;
-        load16<T>(dy + o, g[q]);
-        w[q] = *reinterpret_cast<const IW*>(idx + o);
-      }
+      const long long o = (((long long)n * OH + min(oh, OH - 1)) * OW + min(ow, OW - 1)) * C + chunk * VN;
+      load16<T>(dy + o, g[q]);  // unconditional (clamped) loads: see maxpool_fwd_kernel
+      w[q] = *reinterpret_cast<const IW*>(idx + o);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -547,11 +542,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const T* __restrict__
     for (int q = 0; q < 4; ++q) {
       const int oh = k + (q >> 1), ow = j + (q & 1);
       use[q] = oh < OH && ow < OW;
-      if (use[q]) {
-        const long long o = (((long long)n * OH + oh) * OW + ow) * C + c0;
-        load16<T>(dy + o, g[q]);
-        w[q] = *reinterpret_cast<const IW*>(idx + o);
-      }
+      const long long o = (((long long)n * OH + min(oh, OH - 1)) * OW + min(ow, OW - 1)) * C + c0;
+      load16<T>(dy + o, g[q]);  // unconditional (clamped) loads: see maxpool_fwd_kernel
+      w[q] = *reinterpret_cast<const IW*>(idx + o);
     }
     float yv[4][VN];
     long long pv[4];

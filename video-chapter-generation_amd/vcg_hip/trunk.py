@@ -255,10 +255,12 @@ class ResNetTrunk:
         xs, y0, a0, idx, b0, N, H, W, cpad, H1, W1 = saved["stem"]
         sums0 = torch.empty((2, 64), dtype=torch.float32, device=y0.device)
         dg0, db0 = self._bn_grads(b0)
-        # (ops.maxpool_bwd_bn_apply recomputes g inside the BN apply instead of storing it: measured no faster at
-        # the bench shape, 1.81 vs 1.89 ms, since the pool's dy / argmax / y are then read twice)
-        g0 = ops.maxpool_bwd_bn(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift, sums0, dg0, db0)
-        dy0 = self._bn_apply_bwd(g0, y0, b0, 64, sums0)
+        # two passes over (dout, idx, y0): the BN sums, then the BN-backward apply with g recomputed -- no g tensor
+        # (1.34 ms vs 0.77 + 0.88 ms for storing g and applying it, tools/bench_stem.py)
+        ops.maxpool_bwd_bn(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift, sums0, dg0, db0,
+                           store_g=False)
+        dy0 = ops.maxpool_bwd_bn_apply(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift,
+                                       b0.bn.weight, sums0, N * H1 * W1, b0.mode != "running")
         self._wgrad(self.net.conv1, xs, dy0, N, H, W, cpad)
         if hooks is not None:
             hooks(list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
