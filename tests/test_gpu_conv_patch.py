@@ -132,3 +132,33 @@ def test_patch_dgrad_bwd_affine(K, case):
     assert (dg.double() - sx).abs().max().item() <= tol(sx)
     # same partial sums, different slot partition: equal to f32 rounding
     assert torch.allclose(sums, sums0, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 16), (3, 17, 22), (4, 64, 64), (2, 224, 224), (3, 30, 46)])
+def test_stem_patch(K, shape):
+    """The pair-packed 7x7 / 2 stem on the LDS-patch kernel (stem_patch_kernel) == the im2col engine bit for bit
+    (values), BN statistics to f32 rounding, and == float64 torch within bf16 tolerance."""
+    N, H, W = shape
+    Cin, Cout, k, s, p = 3, 64, 7, 2, 3
+    x = _rand((N, Cin, H, W), 21).double()
+    w = _rand((Cout, Cin, k, k), 22, 0.1)
+    xs = torch.zeros((N, H, W, 4), dtype=BF)
+    xs[..., :Cin] = x.permute(0, 2, 3, 1).to(BF)
+    xs = xs.to(DEV)
+    wd = K.weight_prep(w.float().to(DEV), 4, BF, pair_pad=p)
+    OH, OW = K.conv_out_hw(H, W, k, k, s, p)
+    M = N * OH * OW
+
+    def run():
+        st = K.stats_buffer(Cout, M, DEV)
+        y = K.conv_fwd(xs, wd, N, H, W, 4, Cout, k, k, s, p, 0, 0, stats=st)
+        mean, invstd, scale, shift = (torch.empty(Cout, device=DEV) for _ in range(4))
+        K.bn_finalize(st, K.stats_tiles(M), M, Cout, None, None, mean, invstd, scale, shift, None, None, 0.1, 1e-5)
+        return y, st, mean, invstd
+
+    (y, st, mean, inv), (y0, _, mean0, inv0) = _both(run)
+    assert torch.equal(y, y0), "stem patch != stem im2col"
+    assert float(st[Cout, :, 0].sum()) == M
+    assert torch.allclose(mean, mean0, rtol=1e-5, atol=1e-6) and torch.allclose(inv, inv0, rtol=1e-4)
+    ref = F.conv2d(x, w.to(BF).double(), stride=s, padding=p).permute(0, 2, 3, 1)
+    _close(y, ref, "stem patch fwd")

@@ -1179,6 +1179,214 @@ void conv3x3_patch_kernel(GemmParams p, PatchGeom g) {
   }
 }
 
+// ---- the pair-packed stem (7x7 / stride 2 / pad 3 over RGB0 bf16 frames, vcg_conv_fwd's C = 4 layout) --------
+// Same scheme as the layer-1 patch kernel: an M-tile is R whole output rows of one image; its input rows
+// (2R + KH - 2 rows of OW + KWp - 1 super pixels, 16 B = two RGB0 pixels each) are one LDS-DMA patch, and the
+// KH k-units (4 taps each: the super-pixel pairs kwp = 0..3 of filter row kh) read fragments straight from it:
+// lane group g = kwp, so a fragment read is 16 consecutive super pixels (contiguous 256 B, conflict-free). The
+// im2col engine gathers every input super pixel ~14 times through L2. The filter (64 x 224) stays in registers
+// (14 fragments per lane), 2 workgroups per CU, a 3-deep patch ring, the deferred epilogue of the patch kernel.
+constexpr int SPATCH_MAXPIX = 1024;  // super pixels per patch buffer (16 KiB)
+
+struct StemGeom {
+  int R, TM, TPI, PW, NP, NS, NR;  // rows / GEMM rows per tile, tiles per image, patch width, pixels, slices, rows
+  unsigned long long* stamps;
+};
+
+template <int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void stem_patch_kernel(GemmParams p, StemGeom g) {
+  constexpr int BM = 128, BN = 64, NW = 4, MT = 4, NT = 2, KHMAX = 8, RING = 3, NIP = 4;
+  constexpr int PE = SPATCH_MAXPIX * 8;  // elements per patch buffer
+  __shared__ __attribute__((aligned(1024))) char smem[RING * PE * 2];
+  bf16_t* Ps = reinterpret_cast<bf16_t*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nx = p.N / BN, gy = gridDim.x / nx;
+  int bx, by;
+  if ((gy & 7) == 0) {
+    const int sidx = blockIdx.x >> 3;
+    bx = sidx % nx;
+    by = (sidx / nx) * 8 + (blockIdx.x & 7);
+  } else {
+    bx = blockIdx.x % nx;
+    by = blockIdx.x / nx;
+  }
+  const int n0 = bx * BN;
+  bf16_t* Cout = reinterpret_cast<bf16_t*>(p.C);
+  const int mtiles = p.M / g.TM;
+  const int my_tiles = by < mtiles ? (mtiles - 1 - by) / gy + 1 : 0;
+  if (my_tiles == 0) return;
+
+  const OpArgs& a = p.a;  // a.W: super pixels per image row, a.C = 8, a.KW = 4 super-pixel taps, a.pw their pad
+  const int KH = a.KH;
+  const uint32_t nbytes = (uint32_t)min(a.bytes, (long long)0xFFFFFF00LL);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr), 0, nbytes, 0x00020000);
+  // piece q < NIP of tile lt: 64 super pixels (slice wave + 4 q, repeated past NS - 1: fixed count per wave)
+  auto issue_piece = [&](int lt, int img, int h0, int q) {
+    bf16_t* dst = Ps + (lt % RING) * PE;
+    const int slice = min(wave + NW * q, g.NS - 1);
+    const int pix = 64 * slice + lane;
+    const int pr = pix / g.PW, pc = pix - pr * g.PW;
+    const int ih = 2 * h0 - a.pad + pr, sx = pc - a.pw;
+    const bool ok = pix < g.NP && (unsigned)ih < (unsigned)a.H && (unsigned)sx < (unsigned)a.W;
+    const uint32_t voff = ok ? (uint32_t)((((img * a.H + ih) * a.W + sx) << 3) * 2) : nbytes;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(dst + slice * 512), 16, voff, 0, 0, 0);
+  };
+  auto issue_tile = [&](int lt) {
+    const int tg = by + lt * gy, img = tg / g.TPI, h0 = (tg - img * g.TPI) * g.R;
+#pragma unroll
+    for (int q = 0; q < NIP; ++q) issue_piece(lt, img, h0, q);
+  };
+  int rowpix[MT];  // patch super pixel of tap (kh = 0, kwp = 0) for this lane's fragment row
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int ml = wm * 64 + i * 16 + (lane & 15);
+    const int r = ml / a.GW, w = ml - r * a.GW;
+    rowpix[i] = ml < g.TM ? 2 * r * g.PW + w : 0;
+  }
+  // B fragment of filter row kh, column group j: k = 32 kh + 8 (lane / 16) (taps kwp = lane / 16 of row kh)
+  s16x8 breg[KHMAX][NT];
+  {
+    const bf16_t* B = reinterpret_cast<const bf16_t*>(p.b.ptr);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const bf16_t* row = B + (long long)(n0 + wn * (BN / 2) + j * 16 + (lane & 15)) * p.b.ld + 8 * (lane >> 4);
+#pragma unroll
+      for (int kh = 0; kh < KHMAX; ++kh)
+        breg[kh][j] = kh < KH ? *reinterpret_cast<const s16x8*>(row + 32 * kh) : s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  constexpr int CPR = BN / 8, KC = 128 * BN / 8 / 256;
+  const int cc = tid % CPR, ncol = n0 + 8 * cc;
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // register loads retired before the first DMA (see the patch kernel)
+  issue_tile(0);
+  if (my_tiles > 1) issue_tile(1);
+
+  float b1[8], b2[8], b3[8];
+  int scnt = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b1[i] = b2[i] = b3[i] = 0.f;
+  uint4 q[KC];
+  int pm0 = 0, pmlim = 0;
+  auto process = [&](int k) {
+    const int m = pm0 + (tid + 256 * k) / CPR;
+    if (m >= pmlim) return;
+    *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + ncol) = q[k];
+    if constexpr (EPI == EPI_STATS) {
+      float v[8];
+      unpack8(q[k], v);
+      if (scnt == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) b1[i] = v[i];
+      }
+      ++scnt;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[i] - b1[i];
+        b2[i] += d;
+        b3[i] = fmaf(d, d, b3[i]);
+      }
+    }
+  };
+
+  for (int lt = 0; lt < my_tiles; ++lt) {
+    if (lt + 1 < my_tiles) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NIP));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    __builtin_amdgcn_s_barrier();
+    const bool pre = lt + 2 < my_tiles;
+    const int tg2 = by + (lt + 2) * gy, img2 = tg2 / g.TPI, h02 = (tg2 - img2 * g.TPI) * g.R;
+    const bool prev = lt > 0;
+    const bf16_t* P = Ps + (lt % RING) * PE;
+    // opaque per tile: keeps hipcc from hoisting the loop-invariant fragment addresses (registers)
+#pragma unroll
+    for (int i = 0; i < MT; ++i) asm volatile("" : "+v"(rowpix[i]));
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto unit_reads = [&](s16x8 (&f)[MT], int kh) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        f[i] = *reinterpret_cast<const s16x8*>(P + (rowpix[i] + kh * g.PW + (lane >> 4)) * 8);
+    };
+    s16x8 af[3][MT];
+    unit_reads(af[0], 0);
+    unit_reads(af[1], 1);
+#pragma unroll
+    for (int u = 0; u < KHMAX; ++u) {
+      if (u < KH) {
+        if (u + 2 < KH) unit_reads(af[(u + 2) % 3], u + 2);
+        if (u < NIP && pre) issue_piece(lt + 2, img2, h02, u);
+        if (u >= 1 && u - 1 < KC && prev) process(u - 1);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(breg[u][j], af[u % 3][i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (prev) {  // chunks not yet processed when KH - 1 < KC
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+        if (k >= KH - 1) process(k);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    bf16_t* stA = Ps + (lt % RING) * PE;
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        stage_put<BM, BN>(stA, stA, wm, wn, lane, i, j, v);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int trow = (tid + 256 * k) / CPR;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(q[k]) : "v"(lds_u32(stA + trow * BN + 8 * st_slot<BN>(trow, cc))) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pm0 = (by + lt * gy) * g.TM;
+    pmlim = pm0 + g.TM;
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k) process(k);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  if constexpr (EPI == EPI_STATS)
+    stats_finish<BM, BN>(p, reinterpret_cast<float*>(smem), scnt, b1, b2, b3, n0, by, bx, gy, (p.M + 127) / 128);
+}
+
+// Rows per stem tile (0: not the pair-packed 7x7 / 2 stem shape the stem kernel handles)
+static int stem_rows(const GemmParams& p) {
+  const char* e = getenv("VCG_NO_PATCH");
+  const OpArgs& a = p.a;
+  if ((e && e[0] == '1') || a.C != 8 || a.sw != 1 || a.KW != 4 || a.stride != 2 || a.KH > 8 || a.KH < 3 ||
+      p.K != a.KH * 32 || a.tsm_fold != 0 || p.N % 64 != 0 || p.batch_inner > 0 || p.residual || p.aux || p.bias ||
+      p.act != ACT_NONE || a.GW > 128 || a.GW + 3 > SPATCH_MAXPIX)
+    return 0;
+  for (int R = min(a.GH, 128 / a.GW); R >= 1; --R)
+    if (a.GH % R == 0 && (2 * R + a.KH - 2) * (a.GW + 3) <= SPATCH_MAXPIX) return R;
+  return 0;
+}
+
+static StemGeom stem_geom(const GemmParams& p, int R) {
+  StemGeom g{};
+  g.R = R;
+  g.TM = R * p.a.GW;
+  g.TPI = p.a.GH / R;
+  g.PW = p.a.GW + p.a.KW - 1;
+  g.NR = 2 * R + p.a.KH - 2;
+  g.NP = g.NR * g.PW;
+  g.NS = (g.NP + 63) / 64;
+  return g;
+}
+
 // Rows per patch tile (0: the patch kernel does not apply). VCG_NO_PATCH=1 keeps these convs on the im2col path.
 static int patch_rows(const GemmParams& p, int amode) {
   const char* e = getenv("VCG_NO_PATCH");  // read per call: a test compares both paths in one process
@@ -1279,6 +1487,20 @@ static int launch_patch(const GemmParams& p, int R, hipStream_t s) {
   return VCG_OK;
 }
 
+template <int EPI>
+static int launch_stem(const GemmParams& p, int R, hipStream_t s) {
+  const StemGeom g = stem_geom(p, R);
+  const int nx = p.N / 64, mtiles = p.M / g.TM;
+  int gy = min((2 * 256) / nx, min(mtiles, (p.M + 127) / 128));
+  if (gy >= 8) gy &= ~7;
+  gy = max(gy, 1);
+  const int tk = timing_begin(s);
+  hipLaunchKernelGGL((stem_patch_kernel<EPI>), dim3(nx * gy), dim3(256), 0, s, p, g);
+  timing_end(tk, s, TIMING_PATCH_CONV, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_IM2COL, EPI, false>(p, 1));
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
 // Entry from igemm.hip's dispatcher (bf16, K-contiguous A and B, no split-K).
 // VCG_STAGE_KT (default: all): largest k-step count per tile whose output goes through the LDS stage
 // (A/B in one process, tools/bench_gemm.py with VCG_BENCH_AB=1: staging never loses).
@@ -1289,6 +1511,10 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   if (amode == OP_IM2COL && p.a.C < FBK) amode = OP_IM2COL_SMALLC;
   if (amode == OP_IM2COL_TSM && p.a.C < FBK) return -1;  // (dispatcher keeps these off the fast path)
   if (amode == OP_DGRAD && p.a.C < FBK) return -1;
+  if (z == 1 && amode == OP_IM2COL_SMALLC && (epi == EPI_STATS || epi == EPI_STORE)) {
+    const int R = stem_rows(p);
+    if (R > 0) return epi == EPI_STATS ? launch_stem<EPI_STATS>(p, R, s) : launch_stem<EPI_STORE>(p, R, s);
+  }
   if (z == 1) {
     const int R = patch_rows(p, amode);
     if (R > 0) {
