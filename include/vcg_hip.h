@@ -62,6 +62,11 @@ VCG_API int vcg_fast_stamps(unsigned long long* out, int n);
  * vcg_weight_prep(transposed = 2 + pad); two stride-2 taps per 16-B chunk (GEMM K 224 instead of 392). */
 VCG_API int vcg_conv_stats_tiles(int M);
 VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
+/* vcg_conv_fwd of a 1x1 / stride-1 conv whose input is relu(x * in_scale[c] + in_shift[c]) rounded to bf16 (the
+   previous BatchNorm + ReLU, reference torchvision Bottleneck bn2 -> relu -> conv3), applied to x in LDS as each
+   tile lands instead of by a separate vcg_bn_apply pass; bf16 fast engine with BN statistics only (else
+   VCG_ERR_UNSUPPORTED). Bit-identical to vcg_bn_apply + vcg_conv_fwd. */
+VCG_API int vcg_conv_fwd_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, hipStream_t stream);
 /* autograd of conv2d: input gradient (transposed-conv gather) */
 VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, hipStream_t stream);
 /* vcg_conv_dgrad fused with the trunk backward's next steps (igemm.h BwdEpi): TSM adjoint (tsm_fold > 0:
@@ -77,6 +82,9 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
    the pair-packed stem gather (as vcg_conv_fwd) */
 VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad);
 VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
+/* vcg_conv_wgrad of the conv above: x passes BN + ReLU in LDS (bf16 fast engine, no TSM, C >= 64; else
+   VCG_ERR_UNSUPPORTED). Bit-identical to vcg_bn_apply + vcg_conv_wgrad. */
+VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* dy, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, hipStream_t stream);
 /* nn.Linear / BertSelfAttention matmuls (HF BertModel via model/lang/bert_hugface.py:20; ChapterHead
  * projections model/fusion/two_stream.py:60-61,79-85) */
 VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B, long long ldb, void* C, long long ldc, const float* bias, int act, const void* residual, long long ldr, void* aux, float alpha, hipStream_t stream);

@@ -116,6 +116,27 @@ def test_c1_bf16_fused_backward_vs_unfused():
             assert torch.equal(gf[n], gu[n]), n
 
 
+def test_c1_bf16_bn_on_load_bit_exact():
+    """VCG_BNIN's trunk path (conv3 applies bn2 + ReLU on load in its forward GEMM and its weight-gradient GEMM,
+    the bn_apply pass skipped) == the default path, bit for bit: loss, logits and every gradient."""
+    from vcg_hip import synth
+    from vcg_hip.trunk import ResNetTrunk
+    st = dict(_gold("bn_running_stats.npz"))
+    frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=123, device=DEV)
+    m = _model(4, "bf16", st)
+    saved = ResNetTrunk.fused_bnin
+    try:
+        ResNetTrunk.fused_bnin = False
+        l0, lg0, g0, _ = _step(m, frames, ids, mask, labels)
+        ResNetTrunk.fused_bnin = True
+        l1, lg1, g1, _ = _step(m, frames, ids, mask, labels)
+    finally:
+        ResNetTrunk.fused_bnin = saved
+    assert l0 == l1 and torch.equal(lg0, lg1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+
+
 def test_c1_loss_and_conditioning():
     """C1 bf16 step: loss / logits within bf16 tolerance of the exact fixture. (Its vision gradients are NOT
     compared element-wise with fp32: at C1 the BatchNorm statistics run over 8 frames of 4x4..56x56 maps and the

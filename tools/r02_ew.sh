@@ -9,4 +9,4 @@ tail -1 gpurun_out/ew_tests.log
 
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ew_bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/ew_bench.log; exit 1; }
 tail -1 gpurun_out/ew_bench.log | cut -c1-300
-bash tools/r02_prof.sh r02res
+bash tools/r02_prof.sh r02bnin

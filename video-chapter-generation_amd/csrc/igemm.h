@@ -96,6 +96,11 @@ struct GemmParams {
   long long a_so, a_si, b_so, b_si, c_so, c_si;
   int stage_kt;  // fast kernel: stage the output tile through LDS when the tile has <= stage_kt k-steps
   BwdEpi bwd;    // EPI_BWD
+  // the consuming conv applies its input's BatchNorm + ReLU on load: x -> bf16(max(fma(x, in_sc[c], in_sh[c]), 0))
+  // (vcg_bn_apply's arithmetic) for input channel c, in LDS right after the tile's DMA lands (fast dense A of
+  // igemm_fast_kernel / the x operand of wgrad_fast_kernel); in_C channels
+  const float *in_sc, *in_sh;
+  int in_C;
 };
 
 

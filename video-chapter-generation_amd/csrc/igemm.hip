@@ -501,9 +501,29 @@ VCG_API int vcg_conv_stats_tiles(int M) { return mtiles_of(M); }
 
 // y[N*OH*OW][Cout] = conv(x[N][H][W][C], w[Cout][KH][KW][C]); optional BN partial stats.
 // TSM shift (reference ops/temporal_shift.py:33-51) fused into the A gather when tsm_fold > 0.
+static int conv_fwd_impl(int dtype, const void* x, const float* in_sc, const float* in_sh, const void* w, void* y,
+                         float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad,
+                         int tsm_T, int tsm_fold, hipStream_t stream);
+
 VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W,
                          int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold,
                          hipStream_t stream) {
+  return conv_fwd_impl(dtype, x, nullptr, nullptr, w, y, stats, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T, tsm_fold,
+                       stream);
+}
+
+// The conv's input is BN + ReLU of x, applied on load (never stored): bf16, 1x1 / stride 1 with BN statistics
+// (the trunk's conv3 over bn2's input); VCG_ERR_UNSUPPORTED elsewhere.
+VCG_API int vcg_conv_fwd_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* w,
+                              void* y, float* stats, int N, int H, int W, int C, int Cout, hipStream_t stream) {
+  VCG_REQUIRE(in_scale && in_shift && stats, "in_scale / in_shift / stats required");
+  if (dtype != VCG_BF16 || !fast_gemm_enabled() || C > 1024) return VCG_ERR_UNSUPPORTED;
+  return conv_fwd_impl(dtype, x, in_scale, in_shift, w, y, stats, N, H, W, C, Cout, 1, 1, 1, 0, 0, 0, stream);
+}
+
+static int conv_fwd_impl(int dtype, const void* x, const float* in_sc, const float* in_sh, const void* w, void* y,
+                         float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad,
+                         int tsm_T, int tsm_fold, hipStream_t stream) {
   const int logC = ilog2_exact(C);
   const bool pair = stem_pair(dtype, C);
   VCG_REQUIRE(logC >= 0, "C must be a power of two");
@@ -541,7 +561,21 @@ VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float
   p.ldc = Cout;
   p.alpha = 1.f;
   p.stats = stats;
+  p.in_sc = in_sc;
+  p.in_sh = in_sh;
+  p.in_C = C;
   const int epi = stats ? EPI_STATS : EPI_STORE;
+  if (in_sc) {  // the fast engine only (no generic fallback applies the input BN)
+    if (!dense || dtype != VCG_BF16 || p.a.bytes >= 0xFFFFFF00LL || p.b.bytes >= 0xFFFFFF00LL) return VCG_ERR_UNSUPPORTED;
+    const int rc = run_fast_gemm(p, OP_DENSE_K, epi, 1, stream);
+    if (rc >= 0) {
+      if (FILE* f = gemm_log()) {
+        fprintf(f, "a=0 b=0 epi=%d M=%d N=%d K=%d z=1 fast=1 conv=1x1/1 C=%d bnin=1\n", epi, p.M, p.N, p.K, Cout);
+        fflush(f);
+      }
+    }
+    return rc < 0 ? VCG_ERR_UNSUPPORTED : rc;
+  }
   if (dtype == VCG_BF16) {
     return dense ? run_gemm<bf16_t, OP_DENSE_K, OP_DENSE_K>(p, epi, 1, stream)
                  : run_gemm<bf16_t, OP_IM2COL, OP_DENSE_K>(p, epi, 1, stream);
@@ -785,9 +819,34 @@ VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C,
 }
 
 // dw (fp32, OIHW [Cout][Cin][KH][KW]) (+)= sum_pixels dy (x) im2col(x). C = padded channels of x.
+static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const float* in_sh, const void* dy,
+                           float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cin,
+                           int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
+
 VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, int accumulate, float* ws,
                            long long ws_bytes, int N, int H, int W, int C, int Cin, int Cout, int KH, int KW,
                            int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream) {
+  return conv_wgrad_impl(dtype, x, nullptr, nullptr, dy, dw, accumulate, ws, ws_bytes, N, H, W, C, Cin, Cout, KH, KW,
+                         stride, pad, tsm_T, tsm_fold, stream);
+}
+
+// Weight gradient of a conv whose input is BN + ReLU of x (vcg_conv_fwd_bnin's conv): the transform is applied to
+// x in LDS by the fast bf16 engine (no TSM, C >= 64); VCG_ERR_UNSUPPORTED elsewhere.
+VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* dy,
+                                float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C,
+                                int Cout, int KH, int KW, int stride, int pad, hipStream_t stream) {
+  VCG_REQUIRE(in_scale && in_shift, "in_scale / in_shift required");
+  int M, Nn, K, splits, kps;
+  bool fast;
+  wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits, &kps, &fast);
+  if (dtype != VCG_BF16 || !fast || C < 64) return VCG_ERR_UNSUPPORTED;
+  return conv_wgrad_impl(dtype, x, in_scale, in_shift, dy, dw, accumulate, ws, ws_bytes, N, H, W, C, C, Cout, KH, KW,
+                         stride, pad, 0, 0, stream);
+}
+
+static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const float* in_sh, const void* dy,
+                           float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cin,
+                           int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream) {
   const int logC = ilog2_exact(C);
   VCG_REQUIRE(logC >= 0, "C must be a power of two");
   VCG_REQUIRE(Cout % 64 == 0, "Cout must be a multiple of 64");
@@ -820,6 +879,9 @@ VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, 
   p.b = b;
   p.ws = ws;
   p.alpha = 1.f;
+  p.in_sc = in_sc;
+  p.in_sh = in_sh;
+  p.in_C = C;
   FILE* f = fast ? gemm_log() : nullptr;  // the generic path logs in run_gemm
   if (f)
     fprintf(f, "a=3 b=4 epi=2 M=%d N=%d K=%d z=%d fast=2 conv=%dx%d/%d C=%d\n", M, Nn, K, splits, KH, KW, stride, C);

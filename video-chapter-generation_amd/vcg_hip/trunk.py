@@ -8,6 +8,8 @@ builds it (model/vision/resnet50_tsm.py:15-19, ops/temporal_shift.py:104-146):
 Backward is written by hand (autograd never sees the kernels) and accumulates weight / BN gradients
 straight into the parameters' flat fp32 .grad views.
 """
+import os
+
 import torch
 
 from . import ops
@@ -93,6 +95,10 @@ class ResNetTrunk:
     staged = False  # forward() input is already the stem's NHWC layout [N, H, W, Cpad] (ops.window_frames_u8)
     # backward-path census (tests: the bf16 step must run the fused conv_dgrad_bwd engine everywhere)
     path_counts = {"fused": 0, "unfused": 0}
+    # VCG_BNIN=1: conv3 applies bn2 + ReLU on load (bf16) instead of the separate bn_apply pass. Bit-identical, but
+    # measured slower (730 windows/s with it, 745 without, same box): the in-LDS transform sits between the DMA wait and the
+    # barrier of every k-step and costs the conv3 GEMMs 20-76% (fwd) and 3-56% (wgrad), more than the pass saves
+    fused_bnin = os.environ.get("VCG_BNIN") == "1"
     # False: run the bf16 backward through the unfused ops (conv_dgrad + bn_bwd_reduce / apply + tsm_unshift_add),
     # the reference path the fused conv_dgrad_bwd engine is checked against (tests/test_gpu_bf16_train.py)
     fused_bwd = True
@@ -123,13 +129,29 @@ class ResNetTrunk:
             return self.wc.bwd[id(conv)]
         return ops.weight_prep(conv.weight.data, Cin, self.dtype, transposed=True)
 
-    def _conv_bn(self, x, conv, bn, N, H, W, C, tsm_T=0, tsm_fold=0):
+    def _conv_bn(self, x, conv, bn, N, H, W, C, tsm_T=0, tsm_fold=0, in_bn=None):
+        """conv -> BN statistics (+ running-stat update). in_bn = (scale, shift): the conv's input is
+        relu(x * scale + shift) (the previous BN + ReLU), applied on load by the fused engine; returns y = None when
+        that engine does not take the shape (the caller then materialises the input)."""
         Cout, _, KH, KW, s, p = _conv_shape(conv)
         OH, OW = ops.conv_out_hw(H, W, KH, KW, s, p)
         M = N * OH * OW
         mode = bn_mode(bn)
         st = BNState(Cout, x.device, mode, M, bn)
         w = self._wprep(conv, C)
+        if in_bn is not None:
+            if mode == "running" or (KH, KW, s, p) != (1, 1, 1, 0):
+                return None, st, OH, OW
+            mt = ops.stats_tiles(M)
+            stats = ops.stats_buffer(Cout, M, x.device)
+            y = ops.conv_fwd_bnin(x, in_bn[0], in_bn[1], w, N, H, W, C, Cout, stats)
+            if y is None:
+                return None, st, OH, OW
+            upd = mode == "train"
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            ops.bn_finalize(stats, mt, M, Cout, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
+                            bn.running_mean if upd else None, bn.running_var if upd else None, mom, bn.eps)
+            return y, st, OH, OW
         if mode == "running":
             y = ops.conv_fwd(x, w, N, H, W, C, Cout, KH, KW, s, p, tsm_T, tsm_fold)
             ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, Cout, st.mean, st.invstd,
@@ -187,8 +209,15 @@ class ResNetTrunk:
         y1, b1, _, _ = self._conv_bn(x, conv1, blk.bn1, N, H, W, Cin, T, fold)
         a1 = ops.bn_apply(y1, b1.scale, b1.shift, planes, relu=True)
         y2, b2, H2, W2 = self._conv_bn(a1, blk.conv2, blk.bn2, N, H, W, planes)
-        a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
-        y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes)
+        # bn2 + ReLU applied by conv3 as its tiles land (no a2 tensor; conv3's wgrad does the same), where the
+        # fused engine takes it (bf16, batch statistics)
+        a2 = None
+        y3 = None
+        if self.dtype == torch.bfloat16 and ResNetTrunk.fused_bnin:
+            y3, b3, _, _ = self._conv_bn(y2, blk.conv3, blk.bn3, N, H2, W2, planes, in_bn=(b2.scale, b2.shift))
+        if y3 is None:
+            a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
+            y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes)
         C3 = y3.shape[-1]
         yd = bd = None
         if blk.downsample is not None:
@@ -310,7 +339,15 @@ class ResNetTrunk:
             g = torch.empty_like(dout)
             dy3 = self._bn_bwd_g(dout, r["y3"], r["b3"], C3, obits, g)
             dyd = self._bn_bwd(dout, r["yd"], r["bd"], C3, mbits=obits) if ds else None
-        self._wgrad(blk.conv3, r["a2"], dy3, N, H2, W2, planes)
+        if r["a2"] is not None:
+            self._wgrad(blk.conv3, r["a2"], dy3, N, H2, W2, planes)
+        elif blk.conv3.weight.requires_grad:  # conv3's input is bn2 + ReLU of y2, applied on load
+            Cout3, _, KH3, KW3, s3, p3 = _conv_shape(blk.conv3)
+            b2 = r["b2"]
+            if not ops.conv_wgrad_bnin(r["y2"], b2.scale, b2.shift, dy3, blk.conv3.weight.grad, N, H2, W2, planes,
+                                       Cout3, KH3, KW3, s3, p3):
+                self._wgrad(blk.conv3, ops.bn_apply(r["y2"], b2.scale, b2.shift, planes, relu=True), dy3, N, H2, W2,
+                            planes)
         dy2 = self._dgrad_bn(blk.conv3, dy3, N, H2, W2, r["y2"], r["b2"], planes)
         del dy3
         self._wgrad(blk.conv2, r["a1"], dy2, N, H, W, planes)
