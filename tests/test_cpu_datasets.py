@@ -13,43 +13,8 @@ import pytest
 import torch
 
 
-def _write_corpus(root, n_videos=2, n_frames=(40, 57), hw=32, seed=0):
-    from PIL import Image
-    from data.common_utils import write_csv
-    rng = np.random.default_rng(seed)
-    words = [f"word{i}" for i in range(50)] + ["hello", "world", "chapter", "intro"]
-    vids, timestamps, subs = [], [], {}
-    for v in range(n_videos):
-        vid = f"vid{v:02d}XyZ"
-        vids.append(vid)
-        d = os.path.join(root, "frames", vid)
-        os.makedirs(d)
-        for f in range(n_frames[v]):
-            Image.fromarray(rng.integers(0, 256, (hw, hw, 3), dtype=np.uint8)).save(os.path.join(d, "%05d.jpg" % (f + 1)),
-                                                                                    quality=95)
-        timestamps.append([f"0:{t // 60:02d}:{t % 60:02d} part {k}" if t >= 60 else f"{t // 60}:{t % 60:02d} part {k}"
-                           for k, t in enumerate([0, 9, 21, n_frames[v] - 6])])
-        sd = os.path.join(root, "subs", vid)
-        os.makedirs(sd)
-        subs[vid] = [{"start": round(float(s), 2), "text": " ".join(rng.choice(words, size=rng.integers(1, 6)))}
-                     for s in np.arange(0.0, n_frames[v], 2.7)]
-        with open(os.path.join(sd, f"subtitle_{vid}.json"), "w") as f:
-            json.dump(subs[vid], f)
-    data_file = os.path.join(root, "subs", "data.csv")
-    write_csv(data_file, vids, [f"title {v}" for v in vids], [n + 0.5 for n in n_frames], timestamps)
-    vid_file = os.path.join(root, "train.txt")
-    with open(vid_file, "w") as f:
-        f.write("\n".join(vids) + "\n")
-    vocab = os.path.join(root, "vocab.txt")
-    with open(vocab, "w") as f:
-        f.write("\n".join(["[PAD]"] + [f"[unused{i}]" for i in range(99)] + ["[UNK]", "[CLS]", "[SEP]", "[MASK]"]
-                          + words + ["##1", "##2", "word", "part"]) + "\n")
-    return os.path.join(root, "frames"), data_file, vid_file, subs, timestamps, vocab
-
-
-def _tokenizer(vocab):
-    from transformers import BertTokenizer
-    return BertTokenizer(vocab_file=vocab, do_lower_case=True)
+from corpus_util import tokenizer as _tokenizer
+from corpus_util import write_corpus as _write_corpus
 
 
 def test_parse_csv_to_list(tmp_path):
