@@ -155,6 +155,12 @@ VCG_API long long vcg_colsum_ws_bytes(int rows, int N);
 VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, float* out, int accumulate, float* ws, long long ws_bytes, hipStream_t s);
 VCG_API int vcg_attn_softmax_fwd(int dtype, const void* S, const long long* mask, void* P, void* Pd, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API int vcg_attn_softmax_bwd(int dtype, const void* dPd, const void* P, void* dS, int Z, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
+/* fused self-attention (bert_attn.hip), bf16, L <= 128, head dim 64: ctx = dropout(softmax(scale QK^T + mask)) V
+   per (sequence, head) in one workgroup, nothing L x L in HBM; stats [B*nh][128] float2 (row max, 1 / row sum)
+   for the backward, which recomputes P and writes dQ | dK | dV into dqkv [B*L][3*H]. Same semantics and dropout
+   mask as vcg_attn_softmax_fwd/bwd + the batched GEMMs (HF BertSelfAttention, bert_hugface.py:20). */
+VCG_API int vcg_bert_attn_fwd(const void* qkv, const long long* mask, void* ctx, void* stats, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_bert_attn_bwd(const void* qkv, const void* dctx, const void* ctx, const long long* mask, const void* stats, void* dqkv, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API int vcg_tanh_bwd(int dtype, const void* dy, const void* t, void* dx, long long n, hipStream_t s);
 
 /* ---- fusion head + loss (head.hip): ChapterHead mlp (two_stream.py:51-95), softmax (:189),

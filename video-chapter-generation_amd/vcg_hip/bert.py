@@ -3,11 +3,13 @@ hand-written backward.
 
 Reference use: TwoStream.forward -> lang_model(input_ids, attention_mask).pooler_output
 (model/fusion/two_stream.py:172-179) with lang_model = BertModel('bert-base-uncased')
-(model/lang/bert_hugface.py:20). Per layer: fused QKV GEMM -> batched QK^T -> masked softmax
-(+dropout) -> batched PV -> out-proj GEMM -> LN(dropout(.)+res) -> FFN1 GEMM with erf-GELU
+(model/lang/bert_hugface.py:20). Per layer: fused QKV GEMM -> attention (bf16, L <= 128: ONE fused
+kernel per direction, bert_attn.hip, nothing L x L in HBM; otherwise batched QK^T -> masked softmax (+dropout) ->
+batched PV) -> out-proj GEMM -> LN(dropout(.)+res) -> FFN1 GEMM with erf-GELU
 epilogue -> FFN2 GEMM -> LN(dropout(.)+res); pooler = tanh(W h[:,0] + b).
 """
 import math
+import os
 
 import torch
 
@@ -31,6 +33,11 @@ class BertEncoderEngine:
         self.m = model
         self.flat = flat
         self.dtype = dtype
+
+    def _fused_attn(self, L, dh):
+        # VCG_FUSED_ATTN=0: the unfused kernels (A/B and tests); the fp32 parity mode always runs unfused
+        return (self.dtype == torch.bfloat16 and L <= 128 and dh == 64
+                and os.environ.get("VCG_FUSED_ATTN", "1") != "0")
 
     def _w(self, p):
         return self.flat.compute_view(p, self.dtype)
@@ -79,19 +86,8 @@ class BertEncoderEngine:
             qkv_buf = torch.empty((rows + 8, 3 * H), dtype=dt, device=dev)  # +8 rows: padded key reads
             qkv = qkv_buf[:rows]
             ops.gemm(h, Wqkv, rows, 3 * H, H, H, H, out=qkv, ldc=3 * H, bias=bqkv)
-            Z = B * nh
-            S = torch.empty((Z, L, Lp), dtype=dt, device=dev)
-            ops.gemm_batched(qkv_buf, qkv_buf[:, H:], S, L, Lp, dh, 3 * H, 3 * H, Lp, L * 3 * H, dh, L * 3 * H, dh,
-                             nh * L * Lp, L * Lp, B, nh)
-            Pm = torch.empty_like(S)
-            Pd = torch.empty_like(S) if p_a > 0 else None
             sa = _seed(seed, i + 1, 1)
-            ops.attn_softmax_fwd(S, mask, Pm, Pd, B, nh, L, Lp, scale, p_a, sa)
-            del S
-            Pv = Pd if Pd is not None else Pm
-            ctx = torch.empty((rows, H), dtype=dt, device=dev)
-            ops.gemm_batched(Pv, qkv_buf[:, 2 * H:], ctx, L, dh, L, Lp, 3 * H, H, nh * L * Lp, L * Lp, L * 3 * H, dh,
-                             L * H, dh, B, nh, transB=True)
+            ctx, att = attention_fwd(qkv_buf, mask, B, nh, L, Lp, dh, scale, p_a, sa, self._fused_attn(L, dh))
             ao = ops.gemm(ctx, self._w(at.output.dense.weight), rows, H, H, H, H, bias=at.output.dense.bias)
             s1 = _seed(seed, i + 1, 2)
             h1, m1, r1 = ops.ln_fwd(ao, h, at.output.LayerNorm.weight, at.output.LayerNorm.bias, rows, H, eps, p_h, s1)
@@ -104,7 +100,7 @@ class BertEncoderEngine:
             h2, m2, r2 = ops.ln_fwd(fo, h1, layer.output.LayerNorm.weight, layer.output.LayerNorm.bias, rows, H, eps,
                                     p_h, s2)
             if need_grad:
-                saved_layers.append(dict(h=h, qkv_buf=qkv_buf, P=Pm, Pd=Pd, ctx=ctx, ao=ao, h1=h1, pre=pre, ff=ff,
+                saved_layers.append(dict(h=h, qkv_buf=qkv_buf, att=att, ctx=ctx, ao=ao, h1=h1, pre=pre, ff=ff,
                                          fo=fo, m1=m1, r1=r1, m2=m2, r2=r2, sa=sa, s1=s1, s2=s2))
             h = h2
         pooled = None
@@ -113,7 +109,7 @@ class BertEncoderEngine:
             pooled = ops.gemm(h, self._w(pd.weight), B, H, H, L * H, H, bias=pd.bias, act=ops.ACT_TANH)
         saved = None
         if need_grad:
-            saved = dict(ids=ids, layers=saved_layers, e_mean=e_mean, e_rstd=e_rstd, h_last=h, pooled=pooled, B=B,
+            saved = dict(ids=ids, mask=mask, layers=saved_layers, e_mean=e_mean, e_rstd=e_rstd, h_last=h, pooled=pooled, B=B,
                          L=L, Lp=Lp, H=H, nh=nh, dh=dh, p_h=p_h, p_a=p_a, scale=scale, seed=seed)
         return pooled, h, saved
 
@@ -163,24 +159,9 @@ class BertEncoderEngine:
             del dao
             # ---- attention backward
             qkv_buf = s["qkv_buf"]
-            Z = B * nh
-            dPd = torch.empty((Z, L, Lp), dtype=dt, device=dev)
-            ops.gemm_batched(dctx, qkv_buf[:, 2 * H:], dPd, L, Lp, dh, H, 3 * H, Lp, L * H, dh, L * 3 * H, dh,
-                             nh * L * Lp, L * Lp, B, nh)
-            dqkv = torch.empty((rows, 3 * H), dtype=dt, device=dev)
-            Pv = s["Pd"] if s["Pd"] is not None else s["P"]
-            # dV = Pd^T dO
-            ops.gemm_batched(Pv, dctx, dqkv[:, 2 * H:], L, dh, L, Lp, H, 3 * H, nh * L * Lp, L * Lp, L * H, dh,
-                             L * 3 * H, dh, B, nh, transA=True, transB=True)
-            dS = torch.empty_like(dPd)
-            ops.attn_softmax_bwd(dPd, s["P"], dS, Z, L, Lp, scale, p_a, s["sa"])
-            del dPd
-            # dQ = dS K ; dK = dS^T Q
-            ops.gemm_batched(dS, qkv_buf[:, H:], dqkv, L, dh, L, Lp, 3 * H, 3 * H, nh * L * Lp, L * Lp, L * 3 * H, dh,
-                             L * 3 * H, dh, B, nh, transB=True)
-            ops.gemm_batched(dS, qkv_buf, dqkv[:, H:], L, dh, L, Lp, 3 * H, 3 * H, nh * L * Lp, L * Lp, L * 3 * H, dh,
-                             L * 3 * H, dh, B, nh, transA=True, transB=True)
-            del dS, dctx
+            dqkv = attention_bwd(qkv_buf, dctx, s["ctx"], sv["mask"], s["att"], B, nh, L, Lp, dh, scale, p_a,
+                                 s["sa"])
+            del dctx
             sq, sk, svv = at.self.query, at.self.key, at.self.value
             if sq.weight.requires_grad:
                 gW = flat.contiguous_view([sq.weight, sk.weight, svv.weight], (3 * H, H), "grad")
@@ -201,3 +182,57 @@ class BertEncoderEngine:
                          pad_idx=-1 if emb.word_embeddings.padding_idx is None else emb.word_embeddings.padding_idx)
         if hooks is not None:
             hooks(list(emb.parameters()))
+
+
+def attention_fwd(qkv_buf, mask, B, nh, L, Lp, dh, scale, p_a, seed, fused):
+    """ctx [B*L, H] of HF BertSelfAttention (eager) from the fused projection qkv_buf [B*L (+8), 3H] and the
+    key mask [B, L]; returns (ctx, saved-for-backward). fused: bert_attn.hip (bf16, L <= 128, dh = 64: one kernel,
+    row statistics saved); else QK^T GEMM -> masked softmax (+dropout) -> PV GEMM with S, P, Pd in HBM."""
+    H = nh * dh
+    rows = B * L
+    dt, dev = qkv_buf.dtype, qkv_buf.device
+    ctx = torch.empty((rows, H), dtype=dt, device=dev)
+    if fused:
+        stats = torch.empty((B * nh * 128, 2), dtype=torch.float32, device=dev)
+        ops.bert_attn_fwd(qkv_buf, mask, ctx, stats, B, nh, L, Lp, scale, p_a, seed)
+        return ctx, dict(stats=stats)
+    Z = B * nh
+    S = torch.empty((Z, L, Lp), dtype=dt, device=dev)
+    ops.gemm_batched(qkv_buf, qkv_buf[:, H:], S, L, Lp, dh, 3 * H, 3 * H, Lp, L * 3 * H, dh, L * 3 * H, dh,
+                     nh * L * Lp, L * Lp, B, nh)
+    Pm = torch.empty_like(S)
+    Pd = torch.empty_like(S) if p_a > 0 else None
+    ops.attn_softmax_fwd(S, mask, Pm, Pd, B, nh, L, Lp, scale, p_a, seed)
+    del S
+    Pv = Pd if Pd is not None else Pm
+    ops.gemm_batched(Pv, qkv_buf[:, 2 * H:], ctx, L, dh, L, Lp, 3 * H, H, nh * L * Lp, L * Lp, L * 3 * H, dh,
+                     L * H, dh, B, nh, transB=True)
+    return ctx, dict(P=Pm, Pd=Pd)
+
+
+def attention_bwd(qkv_buf, dctx, ctx, mask, att, B, nh, L, Lp, dh, scale, p_a, seed):
+    """dqkv [B*L, 3H] (dQ | dK | dV) from dctx = d ctx, given attention_fwd's saved state."""
+    H = nh * dh
+    rows = B * L
+    dt, dev = qkv_buf.dtype, qkv_buf.device
+    dqkv = torch.empty((rows, 3 * H), dtype=dt, device=dev)
+    if "stats" in att:
+        ops.bert_attn_bwd(qkv_buf, dctx, ctx, mask, att["stats"], dqkv, B, nh, L, Lp, scale, p_a, seed)
+        return dqkv
+    Z = B * nh
+    dPd = torch.empty((Z, L, Lp), dtype=dt, device=dev)
+    ops.gemm_batched(dctx, qkv_buf[:, 2 * H:], dPd, L, Lp, dh, H, 3 * H, Lp, L * H, dh, L * 3 * H, dh,
+                     nh * L * Lp, L * Lp, B, nh)
+    Pv = att["Pd"] if att["Pd"] is not None else att["P"]
+    # dV = Pd^T dO
+    ops.gemm_batched(Pv, dctx, dqkv[:, 2 * H:], L, dh, L, Lp, H, 3 * H, nh * L * Lp, L * Lp, L * H, dh,
+                     L * 3 * H, dh, B, nh, transA=True, transB=True)
+    dS = torch.empty_like(dPd)
+    ops.attn_softmax_bwd(dPd, att["P"], dS, Z, L, Lp, scale, p_a, seed)
+    del dPd
+    # dQ = dS K ; dK = dS^T Q
+    ops.gemm_batched(dS, qkv_buf[:, H:], dqkv, L, dh, L, Lp, 3 * H, 3 * H, nh * L * Lp, L * Lp, L * 3 * H, dh,
+                     L * 3 * H, dh, B, nh, transB=True)
+    ops.gemm_batched(dS, qkv_buf, dqkv[:, H:], L, dh, L, Lp, 3 * H, 3 * H, nh * L * Lp, L * Lp, L * 3 * H, dh,
+                     L * 3 * H, dh, B, nh, transA=True, transB=True)
+    return dqkv

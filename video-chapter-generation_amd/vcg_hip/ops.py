@@ -508,6 +508,17 @@ def attn_softmax_bwd(dPd, Pm, dS, Z, L, Lp, scale, p=0.0, seed=0):
               int(seed) & (2**64 - 1), stream())
 
 
+def bert_attn_fwd(qkv, mask, ctx, stats, B, nh, L, Lp, scale, p=0.0, seed=0):
+    """Fused attention forward (bf16): qkv [B*L(+pad), 3H] -> ctx [B*L, H]; stats [B*nh*128, 2] f32."""
+    _lib.call("vcg_bert_attn_fwd", P(qkv), P(mask), P(ctx), P(stats), B, nh, L, Lp, float(scale), float(p),
+              int(seed) & (2**64 - 1), stream())
+
+
+def bert_attn_bwd(qkv, dctx, ctx, mask, stats, dqkv, B, nh, L, Lp, scale, p=0.0, seed=0):
+    _lib.call("vcg_bert_attn_bwd", P(qkv), P(dctx), P(ctx), P(mask), P(stats), P(dqkv), B, nh, L, Lp, float(scale),
+              float(p), int(seed) & (2**64 - 1), stream())
+
+
 def tanh_bwd(dy, t):
     dx = torch.empty_like(dy)
     _lib.call("vcg_tanh_bwd", dt_code(dy.dtype), P(dy), P(t), P(dx), dy.numel(), stream())
