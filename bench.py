@@ -304,8 +304,9 @@ def main():
     ms = max(ms, wall * 1000.0 / args.steps)
     # one extra (untimed) step with every fast-GEMM launch bracketed by HIP events; BERT runs on the trunk's
     # stream for this step, so a launch's duration is the kernel's own (not shared with a concurrent kernel)
-    overlap = model.overlap_streams
-    model.overlap_streams = False
+    from vcg_hip.trunk import ResNetTrunk
+    overlap, wside = model.overlap_streams, ResNetTrunk.wgrad_stream
+    model.overlap_streams = ResNetTrunk.wgrad_stream = False  # (and the weight gradients on the trunk's stream)
     ops.timing_enable(True)
     step()
     torch.cuda.synchronize()
@@ -313,7 +314,7 @@ def main():
     peak_tf = MFMA_PEAK_TFLOPS[args.precision]
     rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (ops.TIMING_FAST_GEMM, ops.TIMING_WGRAD)}
     ops.timing_enable(False)
-    model.overlap_streams = overlap
+    model.overlap_streams, ResNetTrunk.wgrad_stream = overlap, wside
     kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
     if world > 1:
         t = torch.tensor([ms], device=dev)

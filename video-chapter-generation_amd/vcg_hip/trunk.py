@@ -34,6 +34,9 @@ class BNState:
         self.bn = bn
 
 
+_WSTREAMS = {}  # device index -> the weight-gradient side stream
+
+
 def _conv_shape(conv):
     KH, KW = conv.kernel_size
     return conv.out_channels, conv.in_channels, KH, KW, conv.stride[0], conv.padding[0]
@@ -102,10 +105,14 @@ class ResNetTrunk:
     # False: run the bf16 backward through the unfused ops (conv_dgrad + bn_bwd_reduce / apply + tsm_unshift_add),
     # the reference path the fused conv_dgrad_bwd engine is checked against (tests/test_gpu_bf16_train.py)
     fused_bwd = True
+    # bf16 backward: the weight gradients run on a side stream (one per device, _WSTREAMS), concurrently with the
+    # input-gradient chain they branch off (each wgrad waits only for its dy); VCG_WGRAD_STREAM=0: one stream
+    wgrad_stream = os.environ.get("VCG_WGRAD_STREAM", "1") != "0"
 
     def __init__(self, net, dtype):
         self.net = net
         self.dtype = dtype
+        self._ws = None  # weight-gradient side stream of the running backward (_wside)
         self.wc = None
         flat = getattr(net, "_vcg_flat", None)
         if dtype == torch.bfloat16 and flat is not None:
@@ -249,11 +256,47 @@ class ResNetTrunk:
         return ops.bn_bwd_apply(dout, None, y, st.mean, st.invstd, bn.weight, sums[0], sums[1], C,
                                 train_stats=st.mode != "running", mbits=mbits, mscale=msc, mshift=msh)
 
+    def _wside(self, dev):
+        """The weight-gradient side stream of this backward (None: everything on the current stream)."""
+        if not (ResNetTrunk.wgrad_stream and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16 and dev.type == "cuda"):
+            return None
+        key = dev.index if dev.index is not None else torch.cuda.current_device()
+        st = _WSTREAMS.get(key)
+        if st is None:
+            st = _WSTREAMS[key] = torch.cuda.Stream(device=dev)
+        return st
+
+    def _async(self, fn, *tensors):
+        """Run fn (weight-gradient kernels) on the side stream after everything issued so far on the current
+        stream; the tensors it reads stay allocated until the side stream has used them (record_stream)."""
+        ws = self._ws
+        if ws is None:
+            return fn()
+        ws.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(ws):
+            out = fn()
+        for t in tensors:
+            if t is not None:
+                t.record_stream(ws)
+        return out
+
+    def _report(self, hooks, params):
+        """Tell the DDP reducer a group of parameters is final: on the side stream (after the current stream's
+        work), where their last weight-gradient kernels ran."""
+        if hooks is None:
+            return
+        if self._ws is None:
+            return hooks(params)
+        self._ws.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._ws):
+            hooks(params)
+
     def _wgrad(self, conv, x, dy, N, H, W, Cpad, T=0, fold=0):
         if not conv.weight.requires_grad:
             return
         Cout, Cin, KH, KW, s, p = _conv_shape(conv)
-        ops.conv_wgrad(x, dy, conv.weight.grad, N, H, W, Cpad, Cin, Cout, KH, KW, s, p, T, fold, accumulate=True)
+        self._async(lambda: ops.conv_wgrad(x, dy, conv.weight.grad, N, H, W, Cpad, Cin, Cout, KH, KW, s, p, T, fold,
+                                           accumulate=True), x, dy)
 
     def _dgrad(self, conv, dy, N, H, W):
         Cout, Cin, KH, KW, s, p = _conv_shape(conv)
@@ -271,6 +314,7 @@ class ResNetTrunk:
         downsample BN). The separate reduce / TSM-combine passes remain only where the fused engine
         does not apply (fp32 parity mode)."""
         N, Hc, Wc, C = saved["final"]
+        self._ws = self._wside(d_emb.device)
         dout = ops.avgpool_bwd(d_emb.contiguous(), N, Hc * Wc, C, self.dtype).view(N, Hc, Wc, C)
         blocks = saved["blocks"]
         gin = None  # (g, sums3, sumsd): masked output gradient of the block + its BN sums (fused path)
@@ -278,8 +322,7 @@ class ResNetTrunk:
             rec = blocks.pop()  # frees the block's activations as soon as its backward is done
             prev = blocks[-1] if blocks else None
             dout, gin = self._block_bwd(rec, dout, gin, prev)
-            if hooks is not None:
-                hooks(list(rec["blk"].parameters()))
+            self._report(hooks, list(rec["blk"].parameters()))
             del rec
         xs, y0, a0, idx, b0, N, H, W, cpad, H1, W1 = saved["stem"]
         sums0 = torch.empty((2, 64), dtype=torch.float32, device=y0.device)
@@ -291,8 +334,9 @@ class ResNetTrunk:
         dy0 = ops.maxpool_bwd_bn_apply(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift,
                                        b0.bn.weight, sums0, N * H1 * W1, b0.mode != "running")
         self._wgrad(self.net.conv1, xs, dy0, N, H, W, cpad)
-        if hooks is not None:
-            hooks(list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
+        self._report(hooks, list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
+        if self._ws is not None:  # every weight gradient is complete on the caller's stream
+            torch.cuda.current_stream().wait_stream(self._ws)
 
     def _bn_grads(self, st):
         bn = st.bn
@@ -344,8 +388,9 @@ class ResNetTrunk:
         elif blk.conv3.weight.requires_grad:  # conv3's input is bn2 + ReLU of y2, applied on load
             Cout3, _, KH3, KW3, s3, p3 = _conv_shape(blk.conv3)
             b2 = r["b2"]
-            if not ops.conv_wgrad_bnin(r["y2"], b2.scale, b2.shift, dy3, blk.conv3.weight.grad, N, H2, W2, planes,
-                                       Cout3, KH3, KW3, s3, p3):
+            if not self._async(lambda: ops.conv_wgrad_bnin(r["y2"], b2.scale, b2.shift, dy3, blk.conv3.weight.grad, N,
+                                                           H2, W2, planes, Cout3, KH3, KW3, s3, p3),
+                               r["y2"], b2.scale, b2.shift, dy3):
                 self._wgrad(blk.conv3, ops.bn_apply(r["y2"], b2.scale, b2.shift, planes, relu=True), dy3, N, H2, W2,
                             planes)
         dy2 = self._dgrad_bn(blk.conv3, dy3, N, H2, W2, r["y2"], r["b2"], planes)
