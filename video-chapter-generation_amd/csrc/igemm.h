@@ -283,6 +283,10 @@ int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
                            float* dgamma, float* dbeta, int accumulate, hipStream_t s);  // grid rows (slots of EPI_BWD partials) of a fast-kernel launch
 int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b = false);
+int wgrad_patch_rows(int dtype, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                     int tsm_fold, bool bn_in);
+int wgrad_patch_splits();
+int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int W, int R, hipStream_t s);
 int wgrad_fast_tile_m(int M);
 int wgrad_fast_tile_n(int N);
 

@@ -815,6 +815,8 @@ VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C,
   int M, Nn, K, splits, kps;
   bool fast;
   wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits, &kps, &fast);
+  if (wgrad_patch_rows(dtype, H, W, C, C, Cout, KH, KW, stride, pad, 0, false) > 0 && splits < wgrad_patch_splits())
+    splits = wgrad_patch_splits();  // the patch kernel's slabs
   return (long long)splits * M * Nn * 4;
 }
 
@@ -882,6 +884,20 @@ static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const f
   p.in_sc = in_sc;
   p.in_sh = in_sh;
   p.in_C = C;
+  const int wpr = wgrad_patch_rows(dtype, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_fold, in_sc != nullptr);
+  if (wpr > 0) {  // layer-1 3x3: im2col-free patch kernel (igemm_wgrad.hip), one slab per workgroup
+    const int wsp = wgrad_patch_splits();
+    VCG_REQUIRE(ws_bytes >= (long long)wsp * M * Nn * 4, "workspace too small");
+    if (FILE* f = gemm_log())
+      fprintf(f, "a=3 b=4 epi=2 M=%d N=%d K=%d z=%d fast=3 conv=%dx%d/%d C=%d\n", M, Nn, K, wsp, KH, KW, stride, C);
+    int rc = run_wgrad_patch(x, dy, ws, N, H, W, wpr, stream);
+    if (rc) return rc;
+    const long long MN = (long long)M * Nn;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, wsp, MN,
+                       Nn, dw, accumulate, 1, KH, KW, C, Cin, 1.f, KW, 0, pad);
+    VCG_LAUNCH_CHECK();
+    return VCG_OK;
+  }
   FILE* f = fast ? gemm_log() : nullptr;  // the generic path logs in run_gemm
   if (f)
     fprintf(f, "a=3 b=4 epi=2 M=%d N=%d K=%d z=%d fast=2 conv=%dx%d/%d C=%d\n", M, Nn, K, splits, KH, KW, stride, C);

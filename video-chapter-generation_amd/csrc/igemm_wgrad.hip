@@ -322,6 +322,147 @@ template <int BM, int BN, bool BG, bool BNI = false> int launch_wgrad(const Gemm
   return VCG_OK;
 }
 
+// ---- 3x3 / stride 1 / pad 1 weight gradient over C = Cout = 64 (layer 1) on an LDS-resident input patch ----------
+// dW[co][(kh, kw, ci)] = sum_p dy[p][co] x[p + (kh - 1, kw - 1)][ci]. An M-tile is R whole output rows of one image
+// (TM = R W <= 128 pixels, the GEMM k of 4 steps of 32; pixels TM..127 are zero dy rows). Its dy rows ([128][64]) and
+// the (R + 2) x (W + 2) input pixels the 9 taps read (zero border from the descriptor range check) go to LDS ONCE by
+// LDS-DMA; the 9 taps read shifted transposed fragments of the patch, where the im2col gather of wgrad_fast_kernel
+// fetches x once per filter tap and dy once per 128-column tile through L2 (7.5x the operand bytes). A workgroup
+// (one per CU: the 64 x 576 fp32 accumulator is 144 registers per lane) walks a contiguous range of tiles (halo rows
+// shared in L2) and writes one fp32 slab [64][576] for splitk_reduce_kernel (fixed-order sum: deterministic).
+// Wave w owns input channels 16 w .. 16 w + 15 of every tap (acc[co tile][tap]); per k-step it reads 4 dy^T
+// fragments (shared by the 9 taps) and 9 patch fragments (shared by the 4 co tiles) with ds_read_b64_tr_b16 and runs
+// 36 MFMAs, the next k-step's reads in flight under them. Tiles are DMA'd two ahead into a 3-slot ring (counted
+// vmcnt, raw barriers: the pipeline of conv3x3_patch_kernel).
+constexpr int WP_SL = 32;      // 1-KiB (8-pixel) slices of a patch slot: (R + 2)(W + 2) <= 256 pixels
+constexpr int WP_RING = 3;
+constexpr int WP_GRID = 256;   // workgroups = fp32 slabs
+constexpr int WP_NIP = 12;     // LDS-DMA instructions per wave per tile (8 patch + 4 dy)
+
+struct WPatchGeom {
+  int H, W, R, TM, PW, NP, NS, tiles, TPI;
+};
+
+__device__ __forceinline__ int wp_swz(int row, int c) { return c ^ (2 * ((row >> 1) & 3)); }  // = wswz<64>
+
+__device__ __forceinline__ void tr_read(s16x4& v, const bf16_t* p) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ ws,
+                           uint32_t xbytes, uint32_t dybytes, WPatchGeom g) {
+  constexpr int PE = WP_SL * 512, YE = 128 * 64;
+  __shared__ __attribute__((aligned(1024))) bf16_t smem[WP_RING * (PE + YE)];
+  bf16_t* Ps = smem;
+  bf16_t* Ys = smem + WP_RING * PE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const int t0 = (int)(((long long)g.tiles * blockIdx.x) / gridDim.x);
+  const int t1 = (int)(((long long)g.tiles * (blockIdx.x + 1)) / gridDim.x);
+  const int my = t1 - t0;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x), 0, xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(dy), 0, dybytes, 0x00020000);
+  const int HW = g.H * g.W;
+
+  // tile lt's DMAs: q8 < 8 patch slices wave + 4 q8 (slices >= NS repeat slice NS - 1), q8 >= 8 dy rows
+  auto issue_tile = [&](int lt) {
+    const int tg = t0 + lt, img = tg / g.TPI, h0 = (tg - img * g.TPI) * g.R;
+    bf16_t* P = Ps + (lt % WP_RING) * PE;
+    bf16_t* Y = Ys + (lt % WP_RING) * YE;
+#pragma unroll
+    for (int q8 = 0; q8 < 8; ++q8) {
+      const int slice = min(wave + 4 * q8, g.NS - 1);
+      const int pix = 8 * slice + (lane >> 3);
+      const int pr = pix / g.PW, pc = pix - pr * g.PW;
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool ok = pix < g.NP && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const int c = wp_swz(pix, lane & 7);
+      const uint32_t voff = ok ? (uint32_t)((((img * HW + h * g.W + w) << 6) + 8 * c) * 2) : xbytes;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(P + slice * 512), 16, voff, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int slice = wave + 4 * q4;
+      const int r = 8 * slice + (lane >> 3);
+      const int c = wp_swz(r, lane & 7);
+      const uint32_t voff = r < g.TM ? (uint32_t)((((img * HW + h0 * g.W + r) << 6) + 8 * c) * 2) : dybytes;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_void_t*)(Y + slice * 512), 16, voff, 0, 0, 0);
+    }
+  };
+
+  // this lane's patch pixel of tap (0, 0) for k = 32 s + 4 lg + q + 16 hh (pixels >= TM: any valid pixel, dy is 0)
+  int kpix[4][2];
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int k = 32 * st + 4 * lg + q + 16 * hh;
+      const int r = k / g.W, xx = k - r * g.W;
+      kpix[st][hh] = k < g.TM ? r * g.PW + xx : 0;
+    }
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (my > 0) issue_tile(0);
+  if (my > 1) issue_tile(1);
+  const int cb = 16 * wave + 4 * pp;  // first input channel of this lane's 8-B transposed read
+  for (int lt = 0; lt < my; ++lt) {
+    if (lt + 1 < my) __builtin_amdgcn_s_waitcnt(wvm(WP_NIP));
+    else __builtin_amdgcn_s_waitcnt(wvm(0));
+    __builtin_amdgcn_s_barrier();
+    if (lt + 2 < my) issue_tile(lt + 2);  // into the slot of tile lt - 1 (every wave is past its reads)
+    const bf16_t* P = Ps + (lt % WP_RING) * PE;
+    const bf16_t* Y = Ys + (lt % WP_RING) * YE;
+    s16x4 al[2][4], ah[2][4], bl[2][9], bh[2][9];
+    auto reads = [&](int st, int b) {
+      const int k0 = 32 * st + 4 * lg + q, k1 = k0 + 16;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int cl = 16 * ct + 4 * pp;
+        tr_read(al[b][ct], Y + k0 * 64 + 8 * wp_swz(k0, cl >> 3) + (cl & 7));
+        tr_read(ah[b][ct], Y + k1 * 64 + 8 * wp_swz(k1, cl >> 3) + (cl & 7));
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = (t / 3) * g.PW + (t % 3);
+        const int p0 = kpix[st][0] + toff, p1 = kpix[st][1] + toff;
+        tr_read(bl[b][t], P + p0 * 64 + 8 * wp_swz(p0, cb >> 3) + (cb & 7));
+        tr_read(bh[b][t], P + p1 * 64 + 8 * wp_swz(p1, cb >> 3) + (cb & 7));
+      }
+    };
+    reads(0, 0);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int b = st & 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 1 < 4) reads(st + 1, b ^ 1);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const s16x8 bf = cat8(bl[b][t], bh[b][t]);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+          acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat8(al[b][ct], ah[b][ct]), bf, acc[ct][t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (no reads outstanding: the ring slot may be refilled)
+  }
+  // acc[ct][t][r] = dW[co = 16 ct + 4 lg + r][tap t][ci = 16 wave + li] -> this workgroup's slab [64][9 * 64]
+  float* slab = ws + (long long)blockIdx.x * 64 * 576;
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[(16 * ct + 4 * lg + r) * 576 + 64 * t + 16 * wave + li] = acc[ct][t][r];
+}
+
 }  // namespace
 
 int wgrad_fast_tile_m(int M) { return M >= 128 ? 128 : 64; }
@@ -347,6 +488,40 @@ int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b)
   if (bm == 128) return launch_wgrad<128, 64, true>(p, splits, s);
   if (bn == 128) return launch_wgrad<64, 128, true>(p, splits, s);
   return launch_wgrad<64, 64, true>(p, splits, s);
+}
+
+// Rows per tile of wgrad3x3_patch_kernel (0: not eligible): bf16, x with C = 64 channels, Cout = 64, 3x3 / stride 1 /
+// pad 1, no TSM, no BN on load, R W <= 128, (R + 2)(W + 2) <= 256, H % R == 0. VCG_WGRAD_PATCH=0 disables it.
+int wgrad_patch_rows(int dtype, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                     int tsm_fold, bool bn_in) {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("VCG_WGRAD_PATCH");
+    en = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!en || dtype != VCG_BF16 || C != 64 || Cin != 64 || Cout != 64 || KH != 3 || KW != 3 || stride != 1 ||
+      pad != 1 || tsm_fold != 0 || bn_in)
+    return 0;
+  for (int R = 128 / W; R >= 1; --R)
+    if ((R + 2) * (W + 2) <= 8 * WP_SL && H % R == 0) return R;
+  return 0;
+}
+
+int wgrad_patch_splits() { return WP_GRID; }
+
+// x: NHWC [N][H][W][64] bf16, dy: [N][H][W][64] bf16 -> WP_GRID fp32 slabs [64][576] in ws
+int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int W, int R, hipStream_t s) {
+  WPatchGeom g;
+  g.H = H; g.W = W; g.R = R; g.TM = R * W; g.PW = W + 2; g.NP = (R + 2) * (W + 2); g.NS = (g.NP + 7) / 8;
+  g.TPI = H / R; g.tiles = N * g.TPI;
+  const long long xb = (long long)N * H * W * 64 * 2;
+  VCG_REQUIRE(xb < 0xFFFFFF00LL, "wgrad patch: x / dy must be below 4 GB");
+  const int tk = timing_begin(s);
+  hipLaunchKernelGGL(wgrad3x3_patch_kernel, dim3(WP_GRID), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dy, ws,
+                     (uint32_t)xb, (uint32_t)xb, g);
+  timing_end(tk, s, TIMING_WGRAD, 2.0 * 64 * 576 * (double)N * H * W, 2.0 * (double)xb + 4.0 * 64 * 576);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
 }
 
 }  // namespace vcg
