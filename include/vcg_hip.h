@@ -104,6 +104,9 @@ VCG_API long long vcg_bn_bwd_ws_bytes(long long P, int C);
    3 affine (fma(y, mscale[c], mshift[c]) > 0: the forward BN+ReLU decision recomputed from y). */
 VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, int mask_mode, const void* mask, const unsigned char* mbits, const float* mscale, const float* mshift, const void* y, const float* mean, const float* invstd, long long P, int C, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, int accumulate, hipStream_t s);
 VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, int mask_mode, const void* mask, const unsigned char* mbits, const float* mscale, const float* mshift, const void* y, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, long long count, int train_stats, void* dy, void* gout, long long P, int C, hipStream_t s);
+/* two batch-stat BN backward applies sharing one masked gradient g (bn3 + the downsample BN of a layer's first
+   bottleneck, resnet50_tsm.py:15 via torchvision Bottleneck): dy = bn3' (g, y), dyd = bn_d' (g, yd), g read once */
+VCG_API int vcg_bn_bwd_apply_dual(int dtype, const void* g, const void* y, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, const void* yd, const float* mean_d, const float* invstd_d, const float* gamma_d, const float* sum_g_d, const float* sum_gx_d, long long count, void* dy, void* dyd, long long P, int C, hipStream_t s);
 /* torchvision stem maxpool 3x3/2 and avgpool + fc=Identity (resnet50_tsm.py:19) */
 VCG_API int vcg_maxpool_fwd(int dtype, const void* x, void* y, unsigned char* idx, int N, int H, int W, int C, hipStream_t s);
 VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C, hipStream_t s);

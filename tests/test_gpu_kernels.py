@@ -261,6 +261,27 @@ def test_conv_wgrad_split(K, case):
     assert err <= 1e-4 * ref.abs().max().item() + 1e-6, f"max err {err}"
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("P,C", [(4096, 256), (777, 2048), (50, 64)])
+def test_bn_bwd_apply_dual(K, dtype, P, C):
+    """One pass over g for bn3 and the downsample BN (vcg_bn_bwd_apply_dual) == two vcg_bn_bwd_apply calls: the same
+    affine arithmetic, up to the compiler's fma contraction of the per-channel coefficients (fp32: 1e-5 relative;
+    bf16: within one output rounding)."""
+    g = _rand((P, C), dtype, 31).to(DEV)
+    ys = [_rand((P, C), dtype, 32 + k, 3.0).to(DEV) for k in range(2)]
+    prm = []
+    for k in range(2):
+        gen = torch.Generator().manual_seed(40 + k)
+        mean, invstd, gamma, sg, sgx = (torch.randn(C, generator=gen).to(DEV) for _ in range(5))
+        prm.append((mean, invstd.abs() + 0.5, gamma, sg, sgx))
+    dy, dyd = K.bn_bwd_apply_dual(g, ys[0], *prm[0], ys[1], *prm[1], C)
+    for out, y, (mean, invstd, gamma, sg, sgx) in ((dy, ys[0], prm[0]), (dyd, ys[1], prm[1])):
+        ref = K.bn_bwd_apply(g, None, y, mean, invstd, gamma, sg, sgx, C, train_stats=True)
+        o, r = out.double().cpu(), ref.double().cpu()
+        tol = 1e-5 if dtype == torch.float32 else 2.0 ** -7
+        assert ((o - r).abs() <= tol * r.abs() + 1e-6 * r.abs().max()).all()
+
+
 @pytest.mark.parametrize("case", [(8, 56, 56), (1, 56, 56), (6, 28, 28), (3, 20, 20), (2, 13, 9)])
 def test_conv_wgrad_patch(K, case):
     """The layer-1 3x3 weight gradient on the LDS patch (wgrad3x3_patch_kernel: C = Cout = 64, stride 1, pad 1; R rows

@@ -303,6 +303,67 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
+// Two batch-stat BN backward applies sharing the upstream gradient g (already masked): the first bottleneck of a
+// ResNet layer, where bn3 and the downsample BN both follow the block's output ReLU. g is read once:
+// dy = A g + B y + C (bn3) and dyd = Ad g + Bd yd + Cd (downsample BN), each with bn_bwd_apply_kernel's arithmetic.
+struct BnBwdArgs {
+  const float *mean, *invstd, *gamma, *sum_g, *sum_gx;
+};
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_dual_kernel(const T* __restrict__ g, const T* __restrict__ y,
+                                                                const T* __restrict__ yd, BnBwdArgs p1, BnBwdArgs p2,
+                                                                float inv_count, T* __restrict__ dy,
+                                                                T* __restrict__ dyd, long long TV, int cpr) {
+  constexpr int VN = V<T>::N;
+  const long long stride = (long long)gridDim.x * SB;
+  long long base = (long long)blockIdx.x * SB + threadIdx.x;
+  const bool fixed = cpr <= 256;
+  float A[2][VN], Bc[2][VN], Cc[2][VN];
+  auto params = [&](long long v) {
+    const int c0 = (int)(v & (cpr - 1)) * VN;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const BnBwdArgs& b = k ? p2 : p1;
+      float is[VN], sgx[VN], sgg[VN], mu[VN];
+      load_params<VN>(b.invstd, c0, is);
+      load_params<VN>(b.sum_gx, c0, sgx);
+      load_params<VN>(b.sum_g, c0, sgg);
+      load_params<VN>(b.mean, c0, mu);
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        A[k][e] = (b.gamma ? b.gamma[c0 + e] : 1.f) * is[e];
+        Bc[k][e] = -A[k][e] * is[e] * sgx[e] * inv_count;
+        Cc[k][e] = -A[k][e] * sgg[e] * inv_count - Bc[k][e] * mu[e];
+      }
+    }
+  };
+  params(base);
+  for (; base < TV; base += stride) {
+    float d[SU][VN], y1[SU][VN], y2[SU][VN];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {  // unconditional loads (clamped index)
+      const long long v = min(base + u * 256, TV - 1);
+      load16<T>(g + v * VN, d[u]);
+      load16<T>(y + v * VN, y1[u]);
+      load16<T>(yd + v * VN, y2[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const long long v = base + u * 256;
+      if (v >= TV) break;
+      if (!fixed) params(v);
+      float o[VN], od[VN];
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        o[e] = fmaf(A[0][e], d[u][e], fmaf(Bc[0][e], y1[u][e], Cc[0][e]));
+        od[e] = fmaf(A[1][e], d[u][e], fmaf(Bc[1][e], y2[u][e], Cc[1][e]));
+      }
+      store16<T>(dy + v * VN, o);
+      store16<T>(dyd + v * VN, od);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ max pool 3x3 / 2, pad 1
 // thread = (output pixel, 16-B channel chunk); first max in (kh, kw) scan order (torch CPU semantics);
 // the argmax bytes of a chunk are stored as one VN-byte word
@@ -808,6 +869,31 @@ VCG_API int vcg_bn_bwd_apply(int dtype, const void* dout, int mask_mode, const v
   }
 #undef VCG_BN_BAPP_M
 #undef VCG_BN_BAPP
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_bn_bwd_apply_dual(int dtype, const void* g, const void* y, const float* mean, const float* invstd,
+                                  const float* gamma, const float* sum_g, const float* sum_gx, const void* yd,
+                                  const float* mean_d, const float* invstd_d, const float* gamma_d,
+                                  const float* sum_g_d, const float* sum_gx_d, long long count, void* dy, void* dyd,
+                                  long long P, int C, hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0, "C must be a power of two multiple of the vector width");
+  const long long TV = P * C / VN;
+  if (TV == 0) return VCG_OK;
+  VCG_REQUIRE(g && y && yd && dy && dyd && mean && invstd && sum_g && sum_gx && mean_d && invstd_d && sum_g_d &&
+                  sum_gx_d,
+              "null operand");
+  const BnBwdArgs p1{mean, invstd, gamma, sum_g, sum_gx}, p2{mean_d, invstd_d, gamma_d, sum_g_d, sum_gx_d};
+  const float ic = 1.f / (float)count;
+  const unsigned gr = stream_grid(TV);
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_dual_kernel<bf16_t>, dim3(gr), dim3(256), 0, s, (const bf16_t*)g,
+                       (const bf16_t*)y, (const bf16_t*)yd, p1, p2, ic, (bf16_t*)dy, (bf16_t*)dyd, TV, C / VN);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_dual_kernel<float>, dim3(gr), dim3(256), 0, s, (const float*)g, (const float*)y,
+                       (const float*)yd, p1, p2, ic, (float*)dy, (float*)dyd, TV, C / VN);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

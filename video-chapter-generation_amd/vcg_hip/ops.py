@@ -287,6 +287,17 @@ def bn_bwd_apply(dout, mask, y, mean, invstd, gamma, sum_g, sum_gx, C, train_sta
     return dy
 
 
+def bn_bwd_apply_dual(g, y, mean, invstd, gamma, sum_g, sum_gx, yd, mean_d, invstd_d, gamma_d, sum_g_d, sum_gx_d,
+                      C):
+    """Batch-stat BN backward applies of two BNs on one (masked) gradient g: (dy, dyd), g read once."""
+    Pn = y.numel() // C
+    dy, dyd = torch.empty_like(y), torch.empty_like(yd)
+    _lib.call("vcg_bn_bwd_apply_dual", dt_code(y.dtype), P(g), P(y), P(mean), P(invstd), P(gamma), P(sum_g),
+              P(sum_gx), P(yd), P(mean_d), P(invstd_d), P(gamma_d), P(sum_g_d), P(sum_gx_d), Pn, P(dy), P(dyd), Pn, C,
+              stream())
+    return dy, dyd
+
+
 def maxpool_fwd(x, N, H, W, C):
     OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     y = torch.empty((N, OH, OW, C), dtype=x.dtype, device=x.device)

@@ -108,6 +108,8 @@ class ResNetTrunk:
     # bf16 backward: the weight gradients run on a side stream (one per device, _WSTREAMS), concurrently with the
     # input-gradient chain they branch off (each wgrad waits only for its dy); VCG_WGRAD_STREAM=0: one stream
     wgrad_stream = os.environ.get("VCG_WGRAD_STREAM", "1") != "0"
+    # the first bottleneck of a layer: bn3's and the downsample BN's backward applies in one pass over g
+    dual_bn_bwd = os.environ.get("VCG_BN_DUAL", "1") != "0"
 
     def __init__(self, net, dtype):
         self.net = net
@@ -377,8 +379,13 @@ class ResNetTrunk:
         ds = blk.downsample is not None
         if gin is not None:
             g, sums3, sumsd = gin
-            dy3 = self._bn_apply_bwd(g, r["y3"], r["b3"], C3, sums3)
-            dyd = self._bn_apply_bwd(g, r["yd"], r["bd"], C3, sumsd) if ds else None
+            b3, bd = r["b3"], r.get("bd")
+            if ResNetTrunk.dual_bn_bwd and ds and b3.mode != "running" and bd.mode != "running":  # g read once
+                dy3, dyd = ops.bn_bwd_apply_dual(g, r["y3"], b3.mean, b3.invstd, b3.bn.weight, sums3[0], sums3[1],
+                                                 r["yd"], bd.mean, bd.invstd, bd.bn.weight, sumsd[0], sumsd[1], C3)
+            else:
+                dy3 = self._bn_apply_bwd(g, r["y3"], b3, C3, sums3)
+                dyd = self._bn_apply_bwd(g, r["yd"], bd, C3, sumsd) if ds else None
         else:
             g = torch.empty_like(dout)
             dy3 = self._bn_bwd_g(dout, r["y3"], r["b3"], C3, obits, g)
