@@ -14,9 +14,15 @@ namespace {
 
 template <typename T> struct V { static constexpr int N = 16 / sizeof(T); };
 
-constexpr int SU = 4;                // 16-B vectors per thread per batch (all loads issued before use)
+#ifndef VCG_EW_SU
+#define VCG_EW_SU 4
+#endif
+#ifndef VCG_EW_GRID
+#define VCG_EW_GRID 2048
+#endif
+constexpr int SU = VCG_EW_SU;        // 16-B vectors per thread per batch (all loads issued before use)
 constexpr int SB = 256 * SU;         // vectors per block per batch
-constexpr long long GRID_MAX = 2048;  // streaming grids: 8 blocks per CU, grid-stride beyond
+constexpr long long GRID_MAX = VCG_EW_GRID;  // streaming grids: 8 blocks per CU, grid-stride beyond
 constexpr int RED_ITER_MAX = 256;  // vectors per thread of bn_bwd_reduce (adaptive: >= ~1024 blocks)
 
 template <int VN>
