@@ -305,8 +305,9 @@ def main():
     # one extra (untimed) step with every fast-GEMM launch bracketed by HIP events; BERT runs on the trunk's
     # stream for this step, so a launch's duration is the kernel's own (not shared with a concurrent kernel)
     from vcg_hip.trunk import ResNetTrunk
-    overlap, wside = model.overlap_streams, ResNetTrunk.wgrad_stream
-    model.overlap_streams = ResNetTrunk.wgrad_stream = False  # (and the weight gradients on the trunk's stream)
+    overlap, wside, dside = model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream
+    # (and the weight gradients / downsample convs on the trunk's stream)
+    model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = False
     ops.timing_enable(True)
     step()
     torch.cuda.synchronize()
@@ -314,7 +315,7 @@ def main():
     peak_tf = MFMA_PEAK_TFLOPS[args.precision]
     rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (ops.TIMING_FAST_GEMM, ops.TIMING_WGRAD)}
     ops.timing_enable(False)
-    model.overlap_streams, ResNetTrunk.wgrad_stream = overlap, wside
+    model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream = overlap, wside, dside
     kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
     if world > 1:
         t = torch.tensor([ms], device=dev)

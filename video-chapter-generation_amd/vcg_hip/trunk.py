@@ -108,6 +108,8 @@ class ResNetTrunk:
     # bf16 backward: the weight gradients run on a side stream (one per device, _WSTREAMS), concurrently with the
     # input-gradient chain they branch off (each wgrad waits only for its dy); VCG_WGRAD_STREAM=0: one stream
     wgrad_stream = os.environ.get("VCG_WGRAD_STREAM", "1") != "0"
+    # forward of a layer's first bottleneck: the downsample conv on the side stream (VCG_DS_STREAM=0: inline)
+    ds_stream = os.environ.get("VCG_DS_STREAM", "1") != "0"
     # the first bottleneck of a layer: bn3's and the downsample BN's backward applies in one pass over g
     dual_bn_bwd = os.environ.get("VCG_BN_DUAL", "1") != "0"
 
@@ -215,6 +217,19 @@ class ResNetTrunk:
         Cin = x.shape[-1]
         conv1, T, fold = _tsm_info(blk.conv1, Cin)
         planes = conv1.out_channels
+        # the downsample branch (a layer's first block) depends only on x: its conv + BN statistics run on the side
+        # stream, concurrently with conv1 -> conv2 -> conv3; the bn3 apply that adds it waits for it
+        yd = bd = side = None
+        cur = torch.cuda.current_stream() if x.is_cuda else None
+        if blk.downsample is not None:
+            side = self._wside(x.device) if ResNetTrunk.ds_stream else None
+            if side is not None:
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    yd, bd, _, _ = self._conv_bn(x, blk.downsample[0], blk.downsample[1], N, H, W, Cin)
+                x.record_stream(side)
+                yd.record_stream(cur)
+                bd.vec.record_stream(cur)
         y1, b1, _, _ = self._conv_bn(x, conv1, blk.bn1, N, H, W, Cin, T, fold)
         a1 = ops.bn_apply(y1, b1.scale, b1.shift, planes, relu=True)
         y2, b2, H2, W2 = self._conv_bn(a1, blk.conv2, blk.bn2, N, H, W, planes)
@@ -228,9 +243,11 @@ class ResNetTrunk:
             a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
             y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes)
         C3 = y3.shape[-1]
-        yd = bd = None
         if blk.downsample is not None:
-            yd, bd, _, _ = self._conv_bn(x, blk.downsample[0], blk.downsample[1], N, H, W, Cin)
+            if side is not None:
+                cur.wait_stream(side)
+            else:
+                yd, bd, _, _ = self._conv_bn(x, blk.downsample[0], blk.downsample[1], N, H, W, Cin)
             out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale,
                                       rshift=bd.shift, bits=True)
         else:
@@ -259,8 +276,9 @@ class ResNetTrunk:
                                 train_stats=st.mode != "running", mbits=mbits, mscale=msc, mshift=msh)
 
     def _wside(self, dev):
-        """The weight-gradient side stream of this backward (None: everything on the current stream)."""
-        if not (ResNetTrunk.wgrad_stream and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16 and dev.type == "cuda"):
+        """The trunk's side stream (weight gradients in the backward, downsample branches in the forward; None: bf16
+        fast engine only, otherwise everything on the current stream)."""
+        if not (ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16 and dev.type == "cuda"):
             return None
         key = dev.index if dev.index is not None else torch.cuda.current_device()
         st = _WSTREAMS.get(key)
@@ -316,7 +334,7 @@ class ResNetTrunk:
         downsample BN). The separate reduce / TSM-combine passes remain only where the fused engine
         does not apply (fp32 parity mode)."""
         N, Hc, Wc, C = saved["final"]
-        self._ws = self._wside(d_emb.device)
+        self._ws = self._wside(d_emb.device) if ResNetTrunk.wgrad_stream else None
         dout = ops.avgpool_bwd(d_emb.contiguous(), N, Hc * Wc, C, self.dtype).view(N, Hc, Wc, C)
         blocks = saved["blocks"]
         gin = None  # (g, sums3, sumsd): masked output gradient of the block + its BN sums (fused path)
