@@ -311,6 +311,24 @@ class ResNetTrunk:
         with torch.cuda.stream(self._ws):
             hooks(params)
 
+    def _ds_dgrad_side(self, cds, dyd, N, H, W, Cin, C3):
+        """The downsample conv's input gradient on the side stream: (res, res_stride, event). 1x1 / stride 2 (bf16
+        fused path): ONE dense GEMM over the output pixels, added by conv1's dgrad epilogue at the even (h, w) rows."""
+        ws, cur = self._ws, torch.cuda.current_stream()
+        ws.wait_stream(cur)
+        with torch.cuda.stream(ws):
+            if cds.stride[0] == 2:
+                wt_ds = self._wprep_t(cds, Cin)
+                Mo = dyd.numel() // C3
+                res, res_stride = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3), 2
+            else:
+                res, res_stride = self._dgrad(cds, dyd, N, H, W), 1
+            ev = torch.cuda.Event()
+            ev.record(ws)
+        dyd.record_stream(ws)
+        res.record_stream(cur)
+        return res, res_stride, ev
+
     def _wgrad(self, conv, x, dy, N, H, W, Cpad, T=0, fold=0):
         if not conv.weight.requires_grad:
             return
@@ -408,6 +426,11 @@ class ResNetTrunk:
             g = torch.empty_like(dout)
             dy3 = self._bn_bwd_g(dout, r["y3"], r["b3"], C3, obits, g)
             dyd = self._bn_bwd(dout, r["yd"], r["bd"], C3, mbits=obits) if ds else None
+        # the downsample branch's input gradient needs only dyd: on the side stream ahead of the weight gradients,
+        # joined (by its own event) just before conv1's fused dgrad adds it
+        ds_res = None
+        if ds and self._ws is not None and ResNetTrunk.ds_stream:
+            ds_res = self._ds_dgrad_side(blk.downsample[0], dyd, N, H, W, Cin, C3)
         if r["a2"] is not None:
             self._wgrad(blk.conv3, r["a2"], dy3, N, H2, W2, planes)
         elif blk.conv3.weight.requires_grad:  # conv3's input is bn2 + ReLU of y2, applied on load
@@ -425,7 +448,11 @@ class ResNetTrunk:
         del dy2
         self._wgrad(r["conv1"], r["x"], dy1, N, H, W, Cin, T, fold)
         res_stride = 1
-        if ds:
+        if ds and ds_res is not None:
+            self._wgrad(blk.downsample[0], r["x"], dyd, N, H, W, Cin)
+            res, res_stride, ev = ds_res
+            torch.cuda.current_stream().wait_event(ev)
+        elif ds:
             cds = blk.downsample[0]
             self._wgrad(cds, r["x"], dyd, N, H, W, Cin)
             if cds.stride[0] == 2 and self.dtype == torch.bfloat16 and ResNetTrunk.fused_bwd:
