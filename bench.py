@@ -292,11 +292,24 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
+    enq = []  # host time to enqueue each step (launches are asynchronous: << ms_per_step unless the host stalls)
+    import gc
+    gc0 = [g["collections"] for g in gc.get_stats()]
+    ms0 = torch.cuda.memory_stats()
     for _ in range(args.steps):
+        te = time.perf_counter()
         step()
+        enq.append(time.perf_counter() - te)
     ev1.record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    ms1 = torch.cuda.memory_stats()
+    host_diag = {"slowest_step": int(max(range(len(enq)), key=lambda i: enq[i])),
+                 "gc_collections": [g["collections"] - c for g, c in zip(gc.get_stats(), gc0)],
+                 "device_allocs": ms1.get("num_device_alloc", 0) - ms0.get("num_device_alloc", 0),
+                 "device_frees": ms1.get("num_device_free", 0) - ms0.get("num_device_free", 0),
+                 "alloc_retries": ms1.get("num_alloc_retries", 0) - ms0.get("num_alloc_retries", 0),
+                 "reserved_gb": round(torch.cuda.memory_reserved() / 2**30, 1)}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -305,9 +318,9 @@ def main():
     # one extra (untimed) step with every fast-GEMM launch bracketed by HIP events; BERT runs on the trunk's
     # stream for this step, so a launch's duration is the kernel's own (not shared with a concurrent kernel)
     from vcg_hip.trunk import ResNetTrunk
-    overlap, wside, dside = model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream
-    # (and the weight gradients / downsample convs on the trunk's stream)
-    model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = False
+    sides = (model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream, ResNetTrunk.prep_stream)
+    # (and the weight gradients / downsample convs / weight re-layout on the trunk's stream)
+    model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = ResNetTrunk.prep_stream = False
     ops.timing_enable(True)
     step()
     torch.cuda.synchronize()
@@ -315,7 +328,7 @@ def main():
     peak_tf = MFMA_PEAK_TFLOPS[args.precision]
     rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (ops.TIMING_FAST_GEMM, ops.TIMING_WGRAD)}
     ops.timing_enable(False)
-    model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream = overlap, wside, dside
+    model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream, ResNetTrunk.prep_stream = sides
     kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
     if world > 1:
         t = torch.tensor([ms], device=dev)
@@ -378,6 +391,8 @@ def main():
                        "global_batch": windows, "seq_len": L, "frames": T, "resolution": HW,
                        "parallelism": f"dp{world}"},
             "roofline": dom,
+            "host": {"enqueue_ms_per_step_median": round(1e3 * sorted(enq)[len(enq) // 2], 3),
+                     "enqueue_ms_per_step_max": round(1e3 * max(enq), 3), **host_diag},
             "roofline_step": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "scope": "whole step (all kernels) vs SURVEY App. A fused-minimum bytes "

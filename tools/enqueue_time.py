@@ -1,6 +1,8 @@
-"""Per-step wall times of the bench train step with allocator statistics (diagnosing run-to-run outliers):
-python tools/step_trace.py [steps]. Prints one line per step: ms, num_alloc_retries, reserved GB."""
+"""Host-side cost of one bench train step: wall time of step() until every launch is enqueued (no sync), and a
+cProfile of one enqueue (top functions by own time). python tools/enqueue_time.py"""
+import cProfile
 import os
+import pstats
 import sys
 import time
 
@@ -12,7 +14,6 @@ sys.path.insert(0, REPO)
 
 
 def main():
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     from vcg_hip import _lib, synth
     from vcg_hip.build import build_two_stream
     from vcg_hip.functions import cross_entropy
@@ -25,20 +26,35 @@ def main():
         weight_decay, learning_rate, betas = 0.01, 1e-5, (0.9, 0.95)
     opt = model.configure_optimizers(Cfg)
     frames, ids, mask, labels = synth.clip_batch(64, 16, 224, 224, 128, seed=123, device=dev)
-    for i in range(steps):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        c0 = time.process_time()
+
+    def step():
         opt.zero_grad()
         logits, _ = model(frames, ids, mask)
         cross_entropy(logits, labels).backward()
         opt.clip_and_step(1.0)
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    enq, tot = [], []
+    for _ in range(10):
         torch.cuda.synchronize()
-        st = torch.cuda.memory_stats()
-        load = open("/proc/loadavg").read().split()[0]
-        print(f"step {i:3d} {1e3 * (time.perf_counter() - t0):8.2f} ms  retries {st.get('num_alloc_retries', 0)}  "
-              f"reserved {torch.cuda.memory_reserved() / 2**30:6.1f} GB  peak {torch.cuda.max_memory_allocated() / 2**30:6.1f} GB"
-              f"  cpu {1e3 * (time.process_time() - c0):7.1f} ms  load {load}", flush=True)
+        t0 = time.perf_counter()
+        step()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        enq.append(1e3 * (t1 - t0))
+        tot.append(1e3 * (t2 - t0))
+    print("enqueue ms/step:", " ".join(f"{x:.1f}" for x in enq))
+    print("total   ms/step:", " ".join(f"{x:.1f}" for x in tot))
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    pr.enable()
+    step()
+    pr.disable()
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
 
 
 if __name__ == "__main__":

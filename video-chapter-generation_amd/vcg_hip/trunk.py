@@ -88,10 +88,23 @@ class _ConvWeights:
         return (flat is self.flat and stem_cpad == self.stem_cpad
                 and [c.weight.data_ptr() for c in self.convs] == self.ptrs)
 
-    def refresh(self):
-        if self.gen != self.flat.generation:
+    def refresh(self, side=None):
+        """Re-lay-out the weights after an optimizer step. side: the stem's layout (descriptor 0) on the current
+        stream, the other 52 convs' on `side` (they are first read after the stem conv + max-pool); returns the event
+        the first bottleneck waits for (None: all on the current stream)."""
+        if self.gen == self.flat.generation:
+            return None
+        self.gen = self.flat.generation
+        if side is None or self.n < 2:
             ops.weight_prep_multi(self.desc, self.n)
-            self.gen = self.flat.generation
+            return None
+        ops.weight_prep_multi(self.desc, 1)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ops.weight_prep_multi(self.desc[1:], self.n - 1)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        return ev
 
 
 class ResNetTrunk:
@@ -110,6 +123,8 @@ class ResNetTrunk:
     wgrad_stream = os.environ.get("VCG_WGRAD_STREAM", "1") != "0"
     # forward of a layer's first bottleneck: the downsample conv on the side stream (VCG_DS_STREAM=0: inline)
     ds_stream = os.environ.get("VCG_DS_STREAM", "1") != "0"
+    # the per-step bf16 weight re-layout of all convs but the stem on the side stream, under the stem conv + max-pool
+    prep_stream = os.environ.get("VCG_PREP_SIDE", "1") != "0"
     # the first bottleneck of a layer: bn3's and the downsample BN's backward applies in one pass over g
     dual_bn_bwd = os.environ.get("VCG_BN_DUAL", "1") != "0"
 
@@ -117,6 +132,8 @@ class ResNetTrunk:
         self.net = net
         self.dtype = dtype
         self._ws = None  # weight-gradient side stream of the running backward (_wside)
+        self._pending = []  # (event, tensors) the side stream still reads (_hold)
+        self._prep_ev = None  # the side-stream weight re-layout of this step (refresh), joined before layer 1
         self.wc = None
         flat = getattr(net, "_vcg_flat", None)
         if dtype == torch.bfloat16 and flat is not None:
@@ -124,7 +141,7 @@ class ResNetTrunk:
             if wc is None or not wc.valid_for(net, flat, ops.stem_cpad(dtype)):
                 wc = _ConvWeights(net, flat, ops.stem_cpad(dtype))
                 object.__setattr__(net, "_vcg_convw", wc)
-            wc.refresh()
+            self._prep_ev = wc.refresh(self._wside(flat.data.device) if ResNetTrunk.prep_stream else None)
             self.wc = wc
 
     # ---------------------------------------------------------------- helpers
@@ -201,6 +218,9 @@ class ResNetTrunk:
         if not need_grad:
             del y0, idx
         h, Hc, Wc = mp, Hm, Wm
+        if self._prep_ev is not None:
+            torch.cuda.current_stream().wait_event(self._prep_ev)
+            self._prep_ev = None
         blocks = []
         for layer in (net.layer1, net.layer2, net.layer3, net.layer4):
             for blk in layer:
@@ -227,7 +247,7 @@ class ResNetTrunk:
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):
                     yd, bd, _, _ = self._conv_bn(x, blk.downsample[0], blk.downsample[1], N, H, W, Cin)
-                x.record_stream(side)
+                # (x stays referenced here until the join below; yd / bd come from the side stream's pool)
                 yd.record_stream(cur)
                 bd.vec.record_stream(cur)
         y1, b1, _, _ = self._conv_bn(x, conv1, blk.bn1, N, H, W, Cin, T, fold)
@@ -288,17 +308,26 @@ class ResNetTrunk:
 
     def _async(self, fn, *tensors):
         """Run fn (weight-gradient kernels) on the side stream after everything issued so far on the current
-        stream; the tensors it reads stay allocated until the side stream has used them (record_stream)."""
+        stream; the tensors it reads stay referenced until the side stream has used them (_hold)."""
         ws = self._ws
         if ws is None:
             return fn()
         ws.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(ws):
             out = fn()
-        for t in tensors:
-            if t is not None:
-                t.record_stream(ws)
+        self._hold(tensors)
         return out
+
+    def _hold(self, tensors):
+        """Keep tensors that side-stream kernels read referenced until an event after those kernels has COMPLETED
+        (or the backward's final join). Not record_stream: its deferred frees are reclaimed only as the allocator
+        polls the side stream's events, and with the host running a step ahead and the side stream trailing, the
+        pool grew to ~260 GB with a 1.2-1.4 s stall in some runs (bench.py "host" diagnostics)."""
+        ev = torch.cuda.Event()
+        ev.record(self._ws)
+        self._pending.append((ev, [t for t in tensors if t is not None]))
+        while self._pending and self._pending[0][0].query():  # completed on the GPU: safe to free
+            self._pending.pop(0)
 
     def _report(self, hooks, params):
         """Tell the DDP reducer a group of parameters is final: on the side stream (after the current stream's
@@ -325,8 +354,8 @@ class ResNetTrunk:
                 res, res_stride = self._dgrad(cds, dyd, N, H, W), 1
             ev = torch.cuda.Event()
             ev.record(ws)
-        dyd.record_stream(ws)
-        res.record_stream(cur)
+        self._hold((dyd,))
+        res.record_stream(cur)  # (allocated from the side stream's pool, read by the current stream)
         return res, res_stride, ev
 
     def _wgrad(self, conv, x, dy, N, H, W, Cpad, T=0, fold=0):
@@ -375,6 +404,7 @@ class ResNetTrunk:
         self._report(hooks, list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
         if self._ws is not None:  # every weight gradient is complete on the caller's stream
             torch.cuda.current_stream().wait_stream(self._ws)
+            self._pending.clear()  # (later reuse of these blocks is ordered after the wait)
 
     def _bn_grads(self, st):
         bn = st.bn
