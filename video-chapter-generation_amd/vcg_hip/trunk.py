@@ -123,8 +123,9 @@ class ResNetTrunk:
     wgrad_stream = os.environ.get("VCG_WGRAD_STREAM", "1") != "0"
     # forward of a layer's first bottleneck: the downsample conv on the side stream (VCG_DS_STREAM=0: inline)
     ds_stream = os.environ.get("VCG_DS_STREAM", "1") != "0"
-    # the per-step bf16 weight re-layout of all convs but the stem on the side stream, under the stem conv + max-pool
-    prep_stream = os.environ.get("VCG_PREP_SIDE", "1") != "0"
+    # VCG_PREP_SIDE=1: the per-step bf16 weight re-layout of all convs but the stem on the side stream, under the stem
+    # conv + max-pool (measured neutral: 756 / 762 vs 760 / 759 windows/s, profiles/r02_bench_prep_side_ab.txt)
+    prep_stream = os.environ.get("VCG_PREP_SIDE", "0") == "1"
     # the first bottleneck of a layer: bn3's and the downsample BN's backward applies in one pass over g
     dual_bn_bwd = os.environ.get("VCG_BN_DUAL", "1") != "0"
 
