@@ -422,25 +422,32 @@ static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
 }
 
 // split-K reduction: out[m][n] (+)= sum_s ws[s][m][n], with optional conv-weight layout permutation.
-// The slabs are summed in split order (deterministic); 8 independent loads are in flight per thread
-// (a dependent one-load-per-iteration loop is latency-bound at 100-300 splits).
+// G threads per output element (G = 1 for big outputs; G = 8 when there are too few outputs to fill the chip, the
+// weight gradients' 4-64 K-element slabs): thread t of a group sums slabs t, t + G, t + 2G, ... in order (8
+// independent loads in flight), the G partials are combined by a fixed xor-shuffle tree -- deterministic.
+template <int G>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long MN,
                                                             int N, float* __restrict__ out, int accumulate,
                                                             int conv_perm, int KH, int KW, int Cpad, int Cin,
                                                             float scale, int KWp, int pwp, int pad) {
-  const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (idx >= MN) return;
+  const long long gid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long idx = gid / G;
+  const int t = (int)(gid - idx * G);
+  if (idx >= MN) return;  // (whole groups: MN * G threads, blockDim a multiple of G)
   float v = 0.f;
   const float* p = ws + idx;
-  int s = 0;
-  for (; s + 8 <= splits; s += 8) {
+  int s = t;
+  for (; s + 7 * G < splits; s += 8 * G) {
     float a[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] = p[(long long)(s + k) * MN];
+    for (int k = 0; k < 8; ++k) a[k] = p[(long long)(s + k * G) * MN];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v += a[k];
   }
-  for (; s < splits; ++s) v += p[(long long)s * MN];
+  for (; s < splits; s += G) v += p[(long long)s * MN];
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (t != 0) return;
   v *= scale;
   long long dst = idx;
   if (conv_perm == 1) {
@@ -465,6 +472,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
   if (accumulate) out[dst] += v;
   else out[dst] = v;
+}
+
+static void splitk_reduce(hipStream_t stream, const float* ws, int splits, long long MN, int N, float* out,
+                          int accumulate, int conv_perm, int KH, int KW, int Cpad, int Cin, float scale, int KWp,
+                          int pwp, int pad) {
+  if ((MN + 255) / 256 < 1024 && splits >= 16)
+    hipLaunchKernelGGL(splitk_reduce_kernel<8>, dim3((unsigned)((MN * 8 + 255) / 256)), dim3(256), 0, stream, ws,
+                       splits, MN, N, out, accumulate, conv_perm, KH, KW, Cpad, Cin, scale, KWp, pwp, pad);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel<1>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws,
+                       splits, MN, N, out, accumulate, conv_perm, KH, KW, Cpad, Cin, scale, KWp, pwp, pad);
 }
 
 static int choose_splits(int M, int N, int K, int BK) {
@@ -893,7 +911,7 @@ static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const f
     int rc = run_wgrad_patch(x, dy, ws, N, H, W, wpr, stream);
     if (rc) return rc;
     const long long MN = (long long)M * Nn;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, wsp, MN,
+    splitk_reduce(stream, ws, wsp, MN,
                        Nn, dw, accumulate, 1, KH, KW, C, Cin, 1.f, KW, 0, pad);
     VCG_LAUNCH_CHECK();
     return VCG_OK;
@@ -909,7 +927,7 @@ static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const f
                            : run_gemm<float, OP_DENSE_MN, OP_IM2COL_T>(p, EPI_SPLITK, splits, stream);
   if (rc) return rc;
   const long long MN = (long long)M * Nn;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, splits,
+  splitk_reduce(stream, ws, splits,
                      MN, Nn, dw, accumulate, pair ? 2 : 1, KH, KW, C, Cin, 1.f, KWp, pwp, pad);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -984,7 +1002,7 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
     rc = run_fast_wgrad(p, fsplits, stream, true);
     if (rc) return rc;
     const long long MN = (long long)M * N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, fsplits,
+    splitk_reduce(stream, ws, fsplits,
                        MN, N, out, accumulate, 0, 1, 1, 1, 1, 1.f, 0, 0, 0);
     VCG_LAUNCH_CHECK();
     return VCG_OK;
@@ -998,7 +1016,7 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
 #undef VCG_SK_CASE
   if (rc) return rc;
   const long long MN = (long long)M * N;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, splits,
+  splitk_reduce(stream, ws, splits,
                      MN, N, out, accumulate, 0, 1, 1, 1, 1, 1.f, 0, 0, 0);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
