@@ -261,6 +261,19 @@ def test_conv_wgrad_split(K, case):
     assert err <= 1e-4 * ref.abs().max().item() + 1e-6, f"max err {err}"
 
 
+@pytest.mark.parametrize("n,off", [(133_355_074, 0), (1_000_003, 0), (1_000_003, 1), (7, 0), (4096, 3)])
+def test_sumsq(K, n, off):
+    """Gradient-norm reduction (vcg_sumsq: 16-B loads when aligned, a 4-B path for misaligned views, tails) against
+    a float64 sum."""
+    g = torch.Generator().manual_seed(n + off)
+    x = torch.randn(n + off, generator=g).to(DEV)
+    v = x[off:]
+    out = torch.zeros(1, device=DEV)
+    K.sumsq(v, out)
+    ref = (v.double() ** 2).sum().item()
+    assert abs(out.item() - ref) <= 1e-5 * ref
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("P,C", [(4096, 256), (777, 2048), (50, 64)])
 def test_bn_bwd_apply_dual(K, dtype, P, C):

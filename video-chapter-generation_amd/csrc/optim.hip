@@ -13,9 +13,31 @@ namespace {
 __global__ void sumsq_part_kernel(const float* __restrict__ x, long long n, float* __restrict__ part) {
   __shared__ float red[16];
   double s = 0;  // per-thread double accumulation keeps the norm order-insensitive enough
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float v = x[i];
-    s += (double)v * v;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long t0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    // 16-B loads, 4 in flight per thread (the 4-B loop ran at ~2.2 TB/s on the 133 M-element flat gradient)
+    const long long n4 = n >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    long long i = t0;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+      float4 a[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = x4[i + k * stride];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        s += (double)a[k].x * a[k].x + (double)a[k].y * a[k].y + (double)a[k].z * a[k].z + (double)a[k].w * a[k].w;
+    }
+    for (; i < n4; i += stride) {
+      const float4 a = x4[i];
+      s += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
+    }
+    for (long long j = 4 * n4 + t0; j < n; j += stride) s += (double)x[j] * x[j];
+  } else {
+    for (long long i = t0; i < n; i += stride) {
+      const float v = x[i];
+      s += (double)v * v;
+    }
   }
   const float r = block_sum((float)s, red);
   if (threadIdx.x == 0) part[blockIdx.x] = r;
