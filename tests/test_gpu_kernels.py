@@ -460,6 +460,18 @@ def test_avgpool(K):
     _close(y, x.double().mean(1), torch.float32, "avgpool")
 
 
+@pytest.mark.parametrize("N,HW,C", [(64, 49, 2048), (3, 5, 8), (2, 9, 24)])
+def test_avgpool_bf16(K, N, HW, C):
+    """The trunk's global average pool and its backward in bf16 (8 channels per thread) vs float64."""
+    x = _rand((N, HW, C), torch.bfloat16, 51)
+    y = K.avgpool_fwd(x.to(DEV), N, HW, C)
+    ref = x.double().mean(1)
+    assert (y.double().cpu() - ref).abs().max().item() <= 1e-5 * (ref.abs().max().item() + 1.0)
+    dy = torch.randn(N, C)
+    dx = K.avgpool_bwd(dy.to(DEV), N, HW, C, torch.bfloat16)
+    assert torch.equal(dx.cpu(), (dy / HW).to(torch.bfloat16)[:, None, :].expand(N, HW, C))
+
+
 def test_window_frames_u8_bitexact(K):
     """Frame ingest: u8 frames gathered by the window frame table (data/clip_windows.py) and
     normalised like ToTensor + Normalize in fp32 — bit-exact in fp32, one rounding in bf16."""
