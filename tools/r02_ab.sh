@@ -19,6 +19,6 @@ for i in 1 2; do
   echo "old: $(tail -1 gpurun_out/${TAG}_old$i.log | cut -c100-200)"
 done
 rm -f gpurun_out/${TAG}_gemm.log
-VCG_OVERLAP=0 VCG_WGRAD_STREAM=0 VCG_DS_STREAM=0 VCG_GEMM_LOG=gpurun_out/${TAG}_gemm.log timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/${TAG}_prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || { echo "profile failed"; tail -20 gpurun_out/${TAG}_prof.log; exit 3; }
+VCG_OVERLAP=0 VCG_WGRAD_STREAM=0 VCG_DS_STREAM=0 VCG_PREP_SIDE=0 VCG_GEMM_LOG=gpurun_out/${TAG}_gemm.log timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/${TAG}_prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || { echo "profile failed"; tail -20 gpurun_out/${TAG}_prof.log; exit 3; }
 python tools/gemm_breakdown.py gpurun_out/${TAG}_gemm.log gpurun_out/${TAG}_prof/run_kernel_trace.csv 4 60 > gpurun_out/${TAG}_gemm_breakdown.txt
 head -8 gpurun_out/${TAG}_gemm_breakdown.txt | cut -c1-130
