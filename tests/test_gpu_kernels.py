@@ -646,7 +646,7 @@ def test_maxpool_bwd_bn(K):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("train", [True, False])
-@pytest.mark.parametrize("hw", [(13, 12), (14, 12), (16, 10)])
+@pytest.mark.parametrize("hw", [(13, 12), (14, 12), (16, 10), (112, 112)])
 def test_fused_stem_bn_relu_maxpool(K, dtype, train, hw):
     """The fused stem passes == the unfused ops, bit for bit: bn_relu_maxpool == bn_apply(relu) + maxpool_fwd
     (values and argmax); maxpool_bwd_bn(store_g=False) + maxpool_bwd_bn_apply == maxpool_bwd_bn + bn_bwd_apply.
