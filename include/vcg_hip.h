@@ -137,6 +137,9 @@ VCG_API int vcg_window_frames_u8_cpad(int dtype, const uint8_t* frames, const lo
    stem [Cout][KH][KWp][8] (bf16, Cin <= 4; element 4j + c of super tap kwp = w[.][c][kh][2 (kwp - pwp) + j + pad],
    pwp = -floor(-pad / 2), KWp = floor((KW - 1 - pad) / 2) + pwp + 1) */
 VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int KH, int KW, int Cpad, int transposed, hipStream_t s);
+/* out[r][c] = w[r][c] * scale[r] (f32 master -> dtype): a running-statistics BN (scale = gamma * invstd) folded into the
+   1x1 conv before it, for scoring (eval) forwards; the shift becomes the GEMM bias */
+VCG_API int vcg_weight_fold(int dtype, const float* w, const float* scale, void* out, int rows, int cols, hipStream_t s);
 /* every conv of the trunk in one launch: desc = DEVICE array of n x 8 int64 (src OIHW f32 ptr, dst bf16 ptr, Cout,
    Cin, KH, KW, Cpad, transposed), each as vcg_weight_prep; bf16 only, each tensor < 2^31 elements */
 VCG_API int vcg_weight_prep_multi(int dtype, const long long* desc, int n, hipStream_t s);

@@ -297,3 +297,38 @@ def test_c3_bf16_train_step_properties():
     d = (lga - lg32.float().cpu()).abs().max().item()
     print(f"C3 logits bf16 vs fp32: max diff {d:.3e}")
     assert d <= 5e-2
+
+
+def test_eval_bn3_fold_matches_unfolded():
+    """The bf16 scoring forward (running-statistics BN, no autograd) folds bn3 into conv3 (vcg_weight_fold + one GEMM
+    with bias, identity residual and ReLU; trunk._conv3_folded). Against the unfolded bf16 forward (conv3 -> y3 ->
+    bn_apply) and the fp32 parity forward on the same weights, reference-run running statistics and inputs: the
+    vision embeddings of both bf16 paths sit equally close to fp32 (rel. Frobenius error no worse than 1.25 x the
+    unfolded path's + 2e-3; both ~0.15 here: the reference-run statistics do not match random-init activations, and
+    eval BN amplifies bf16 rounding), and the folded logits no further from fp32 than 1.25 x the unfolded ones + 1e-2."""
+    from vcg_hip import synth
+    from vcg_hip.trunk import ResNetTrunk
+    st = dict(_gold("bn_running_stats.npz"))
+    frames, ids, mask, _ = synth.clip_batch(4, 4, 112, 112, 32, seed=321, device=DEV)
+    res = {}
+    saved = ResNetTrunk.fold_eval
+    try:
+        for tag, prec, fold in (("fold", "bf16", True), ("plain", "bf16", False), ("fp32", "fp32", False)):
+            ResNetTrunk.fold_eval = fold
+            m = _model(4, prec, st).eval()
+            with torch.no_grad():
+                logits, _, vis, _ = m(frames, ids, mask, return_emb=True)
+            torch.cuda.synchronize()
+            res[tag] = (logits.float().cpu().double(), vis.float().cpu().double())
+    finally:
+        ResNetTrunk.fold_eval = saved
+    ref = res["fp32"][1]
+    ef = ((res["fold"][1] - ref).norm() / ref.norm()).item()
+    ep = ((res["plain"][1] - ref).norm() / ref.norm()).item()
+    print(f"vision emb vs fp32: folded {ef:.3e}, unfolded {ep:.3e}")
+    assert torch.isfinite(res["fold"][1]).all()
+    assert ef <= 1.25 * ep + 2e-3, (ef, ep)
+    lf = (res["fold"][0] - res["fp32"][0]).abs().max().item()
+    lp = (res["plain"][0] - res["fp32"][0]).abs().max().item()
+    print(f"logits vs fp32: folded {lf:.3e}, unfolded {lp:.3e}")
+    assert lf <= 1.25 * lp + 1e-2, (lf, lp)

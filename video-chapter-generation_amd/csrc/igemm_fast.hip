@@ -350,6 +350,66 @@ __device__ __forceinline__ void unpack8(const uint4& u, float (&v)[8]) {
   }
 }
 
+// EPI_STORE + residual + ReLU through the stage (the running-statistics bn3 folded into conv3: relu(x W'^T + b + res),
+// trunk.py _conv3_folded): the GEMM value is rounded to bf16 in the stage -- as the unfolded path stores y3 -- and the
+// residual is added per 16-B row chunk in the flush, so both the residual loads and the output stores are full rows
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue_staged_res(f32x4 (&acc)[4][BN / 32], const GemmParams& p,
+                                                    const float (&bv)[BN / 32][4], bf16_t* Cout, const bf16_t* Res,
+                                                    bf16_t* stA, bf16_t* stB, int m0, int n0, int wm, int wn,
+                                                    int lane, int mlim) {
+  constexpr int MT = 4, NT = BN / 32, NTH = BM * 2, CPR = BN / 8, KC = 128 * BN / 8 / NTH;
+  static_assert(BM == 128, "128-row tiles");
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha + bv[j][r];
+      stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  uint4 q[KC], rv[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {  // residual rows first (clamped to a valid row; discarded below)
+    const int id = threadIdx.x + NTH * k;
+    const int trow = id / CPR, c = id - trow * CPR;
+    const int m = min(m0 + trow, mlim - 1), n = min(n0 + 8 * c, p.N - 8);
+    rv[k] = *reinterpret_cast<const uint4*>(Res + (long long)m * p.ldr + n);
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int id = threadIdx.x + NTH * k;
+    const int trow = id / CPR, c = id - trow * CPR;
+    const bf16_t* reg = (BN == 128 && trow >= 64) ? stB : stA;
+    const int row = BN == 128 ? (trow & 63) : trow;
+    const uint32_t addr = lds_u32(reg + row * BN + 8 * st_slot<BN>(row, c));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(q[k]) : "v"(addr) : "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int id = threadIdx.x + NTH * k;
+    const int trow = id / CPR, c = id - trow * CPR;
+    const int m = m0 + trow, n = n0 + 8 * c;
+    float a[8], r[8];
+    unpack8(q[k], a);
+    unpack8(rv[k], r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = apply_act(a[e] + r[e], p.act);
+    uint4 o;
+    o.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
+    o.y = (uint32_t)f2bf(a[2]) | ((uint32_t)f2bf(a[3]) << 16);
+    o.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
+    o.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
+    if (m < mlim && n < p.N) *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + n) = o;
+  }
+  __builtin_amdgcn_s_barrier();  // every wave has read the stage before the next step's DMA refills it
+}
+
 template <int BM, int BN, bool LIGHT>
 __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t* stB, const GemmParams& p,
                                                 bf16_t* Cout, int m0, int n0, const float* cpar, float (&s1)[8],
@@ -880,6 +940,9 @@ void igemm_fast_kernel(GemmParams p) {
         if constexpr (BM == 128) epilogue_staged_aux<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane);
       } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0)) {
         epilogue_staged<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
+      } else if (RES && staged && p.act == ACT_RELU && p.aux == nullptr && ((p.ldc | p.ldr | p.N) & 7) == 0) {
+        if constexpr (BM == 128 && RES)
+          epilogue_staged_res<BM, BN>(acc, p, bv, Cout, Res, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
       } else {
         if constexpr (BM == 128)
           gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);

@@ -476,6 +476,31 @@ VCG_API int vcg_weight_prep(int dtype, const float* w, void* out, int Cout, int 
 }
 
 namespace {
+// vcg_weight_fold: out[r][c] = w[r][c] * scale[r] -- a running-statistics BN folded into the 1x1 conv that feeds it
+template <typename T>
+__global__ void weight_fold_kernel(const float* __restrict__ w, const float* __restrict__ scale, T* __restrict__ out,
+                                   int cols, long long total) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = from_f<T>(w[i] * scale[i / cols]);
+}
+}  // namespace
+
+VCG_API int vcg_weight_fold(int dtype, const float* w, const float* scale, void* out, int rows, int cols,
+                            hipStream_t s) {
+  VCG_REQUIRE(w && scale && out && rows > 0 && cols > 0, "bad arguments");
+  const long long tot = (long long)rows * cols;
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(weight_fold_kernel<bf16_t>, dim3(grid_for(tot)), dim3(256), 0, s, w, scale, (bf16_t*)out, cols,
+                       tot);
+  else
+    hipLaunchKernelGGL(weight_fold_kernel<float>, dim3(grid_for(tot)), dim3(256), 0, s, w, scale, (float*)out, cols,
+                       tot);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+namespace {
 // vcg_weight_prep_multi: blockIdx.y = descriptor (8 int64: src, dst, Cout, Cin, KH, KW, Cpad, mode = transposed
 // as in vcg_weight_prep: 0, 1 or 2 + pad for the pair-packed stem)
 __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const long long* __restrict__ desc) {

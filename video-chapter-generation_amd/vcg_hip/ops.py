@@ -413,6 +413,16 @@ def weight_prep(w, Cpad, dtype, transposed=False, out=None, pair_pad=None):
     return out
 
 
+def weight_fold(w2d, scale, dtype, out=None):
+    """[rows, cols] f32 weight with row r scaled by scale[r], cast to dtype (vcg_weight_fold): a running-statistics BN
+    folded into the 1x1 conv before it."""
+    _chk(w2d, torch.float32, "weight")
+    rows, cols = w2d.shape
+    out = out if out is not None else torch.empty((rows, cols), dtype=dtype, device=w2d.device)
+    _lib.call("vcg_weight_fold", dt_code(dtype), P(w2d), P(scale), P(out), rows, cols, stream())
+    return out
+
+
 def weight_prep_multi(desc, n):
     """One launch of vcg_weight_prep_multi over a DEVICE int64 descriptor table [n, 8]."""
     _chk(desc, torch.int64, "desc")

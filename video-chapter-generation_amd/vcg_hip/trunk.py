@@ -128,6 +128,9 @@ class ResNetTrunk:
     prep_stream = os.environ.get("VCG_PREP_SIDE", "0") == "1"
     # the first bottleneck of a layer: bn3's and the downsample BN's backward applies in one pass over g
     dual_bn_bwd = os.environ.get("VCG_BN_DUAL", "1") != "0"
+    # bf16 scoring forward (running-statistics BN, no autograd): bn3 folded into conv3 (1x1 GEMM with the BN scale in
+    # the weight rows, the shift as bias, + identity, ReLU in the epilogue) -- no y3 tensor, no bn3 pass
+    fold_eval = os.environ.get("VCG_FOLD_BN", "1") != "0"
 
     def __init__(self, net, dtype):
         self.net = net
@@ -258,6 +261,10 @@ class ResNetTrunk:
         # fused engine takes it (bf16, batch statistics)
         a2 = None
         y3 = None
+        if (ResNetTrunk.fold_eval and not need_grad and blk.downsample is None and self.dtype == torch.bfloat16
+                and x.is_cuda and bn_mode(blk.bn3) == "running" and _conv_shape(blk.conv3)[2:] == (1, 1, 1, 0)):
+            a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
+            return self._conv3_folded(blk, a2, x, N, H2, W2, planes), None, H2, W2
         if self.dtype == torch.bfloat16 and ResNetTrunk.fused_bnin:
             y3, b3, _, _ = self._conv_bn(y2, blk.conv3, blk.bn3, N, H2, W2, planes, in_bn=(b2.scale, b2.shift))
         if y3 is None:
@@ -279,6 +286,20 @@ class ResNetTrunk:
                        bd=bd, N=N, H=H, W=W, H2=H2, W2=W2, Cin=Cin, planes=planes, C3=C3, T=T, fold=fold,
                        conv1=conv1)
         return out, rec, H2, W2
+
+    def _conv3_folded(self, blk, a2, x, N, H, W, planes):
+        """relu(bn3(conv3(a2)) + x) with running statistics, as one GEMM: rows of W3 scaled by gamma * invstd (bf16),
+        beta - mean * scale as bias, the identity x as residual (eval BN, test_video_segment_point.py:116-122)."""
+        bn, conv = blk.bn3, blk.conv3
+        C3 = conv.out_channels
+        st = BNState(C3, x.device, "running", 0, bn)
+        ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, C3, st.mean, st.invstd,
+                           st.scale, st.shift)
+        wf = ops.weight_fold(conv.weight.data.view(C3, planes), st.scale, self.dtype)
+        M = N * H * W
+        out = ops.gemm(a2.view(M, planes), wf, M, C3, planes, planes, planes, bias=st.shift, act=ops.ACT_RELU,
+                       residual=x.view(M, C3), ldr=C3)
+        return out.view(N, H, W, C3)
 
     # ---------------------------------------------------------------- backward
     def _bn_bwd(self, dout, y, st, C, mbits=None, affine=False):
