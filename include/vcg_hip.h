@@ -66,6 +66,9 @@ VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float
    previous BatchNorm + ReLU, reference torchvision Bottleneck bn2 -> relu -> conv3), applied to x in LDS as each
    tile lands instead of by a separate vcg_bn_apply pass; bf16 fast engine with BN statistics only (else
    VCG_ERR_UNSUPPORTED). Bit-identical to vcg_bn_apply + vcg_conv_fwd. */
+/* y = act(conv(x, w) + bias[col]) (act 0 none / 1 ReLU), no statistics: a conv with its running-statistics BN folded
+   into w (vcg_weight_fold) and the BN shift as bias -- the scoring (eval) forward, test_video_segment_point.py:116-122 */
+VCG_API int vcg_conv_fwd_bias_act(int dtype, const void* x, const void* w, const float* bias, int act, void* y, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
 VCG_API int vcg_conv_fwd_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, hipStream_t stream);
 /* autograd of conv2d: input gradient (transposed-conv gather) */
 VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, hipStream_t stream);

@@ -300,9 +300,10 @@ def test_c3_bf16_train_step_properties():
 
 
 def test_eval_bn3_fold_matches_unfolded():
-    """The bf16 scoring forward (running-statistics BN, no autograd) folds bn3 into conv3 (vcg_weight_fold + one GEMM
-    with bias, identity residual and ReLU; trunk._conv3_folded). Against the unfolded bf16 forward (conv3 -> y3 ->
-    bn_apply) and the fp32 parity forward on the same weights, reference-run running statistics and inputs: the
+    """The bf16 scoring forward (running-statistics BN, no autograd) folds every bottleneck BN into the conv before it
+    (vcg_weight_fold; conv1 / conv2 / downsample via vcg_conv_fwd_bias_act, conv3 as one GEMM with bias, residual and
+    ReLU; trunk._block_fwd_folded). Against the unfolded bf16 forward (conv -> y -> bn_apply) and the fp32 parity
+    forward on the same weights, reference-run running statistics and inputs: the
     vision embeddings of both bf16 paths sit equally close to fp32 (rel. Frobenius error no worse than 1.25 x the
     unfolded path's + 2e-3; both ~0.15 here: the reference-run statistics do not match random-init activations, and
     eval BN amplifies bf16 rounding), and the folded logits no further from fp32 than 1.25 x the unfolded ones + 1e-2."""

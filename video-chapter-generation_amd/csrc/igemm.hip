@@ -521,13 +521,24 @@ VCG_API int vcg_conv_stats_tiles(int M) { return mtiles_of(M); }
 // TSM shift (reference ops/temporal_shift.py:33-51) fused into the A gather when tsm_fold > 0.
 static int conv_fwd_impl(int dtype, const void* x, const float* in_sc, const float* in_sh, const void* w, void* y,
                          float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad,
-                         int tsm_T, int tsm_fold, hipStream_t stream);
+                         int tsm_T, int tsm_fold, hipStream_t stream, const float* bias = nullptr, int act = 0);
 
 VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W,
                          int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold,
                          hipStream_t stream) {
   return conv_fwd_impl(dtype, x, nullptr, nullptr, w, y, stats, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T, tsm_fold,
                        stream);
+}
+
+// y = act(conv(x) + bias[col]): a conv whose running-statistics BN was folded into its weights (vcg_weight_fold),
+// bias = the BN shift, act = ReLU (bn1 / bn2) or none (the downsample BN) -- the scoring forward's trunk.
+VCG_API int vcg_conv_fwd_bias_act(int dtype, const void* x, const void* w, const float* bias, int act, void* y, int N,
+                                  int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T,
+                                  int tsm_fold, hipStream_t stream) {
+  VCG_REQUIRE(bias, "bias required");
+  VCG_REQUIRE(act == ACT_NONE || act == ACT_RELU, "act must be none or ReLU");
+  return conv_fwd_impl(dtype, x, nullptr, nullptr, w, y, nullptr, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T,
+                       tsm_fold, stream, bias, act);
 }
 
 // The conv's input is BN + ReLU of x, applied on load (never stored): bf16, 1x1 / stride 1 with BN statistics
@@ -541,7 +552,7 @@ VCG_API int vcg_conv_fwd_bnin(int dtype, const void* x, const float* in_scale, c
 
 static int conv_fwd_impl(int dtype, const void* x, const float* in_sc, const float* in_sh, const void* w, void* y,
                          float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad,
-                         int tsm_T, int tsm_fold, hipStream_t stream) {
+                         int tsm_T, int tsm_fold, hipStream_t stream, const float* bias, int act) {
   const int logC = ilog2_exact(C);
   const bool pair = stem_pair(dtype, C);
   VCG_REQUIRE(logC >= 0, "C must be a power of two");
@@ -582,6 +593,8 @@ static int conv_fwd_impl(int dtype, const void* x, const float* in_sc, const flo
   p.in_sc = in_sc;
   p.in_sh = in_sh;
   p.in_C = C;
+  p.bias = bias;
+  p.act = act;
   const int epi = stats ? EPI_STATS : EPI_STORE;
   if (in_sc) {  // the fast engine only (no generic fallback applies the input BN)
     if (!dense || dtype != VCG_BF16 || p.a.bytes >= 0xFFFFFF00LL || p.b.bytes >= 0xFFFFFF00LL) return VCG_ERR_UNSUPPORTED;

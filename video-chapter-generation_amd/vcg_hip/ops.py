@@ -110,6 +110,18 @@ def conv_fwd(x, w, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, s
     return y
 
 
+def conv_fwd_bias_act(x, w, bias, act, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, out=None):
+    """act(conv(x, w) + bias) (vcg_conv_fwd_bias_act): w carries a folded running-statistics BN, bias its shift."""
+    _chk(x, name="x")
+    _chk(w, x.dtype, "w")
+    _chk(bias, torch.float32, "bias")
+    OH, OW = conv_out_hw(H, W, KH, KW, stride, pad)
+    y = out if out is not None else torch.empty((N, OH, OW, Cout), dtype=x.dtype, device=x.device)
+    _lib.call("vcg_conv_fwd_bias_act", dt_code(x.dtype), P(x), P(w), P(bias), int(act), P(y), N, H, W, C, Cout, KH,
+              KW, stride, pad, tsm_T, tsm_fold, stream())
+    return y
+
+
 def conv_dgrad(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, out=None):
     """dy: NHWC [N,OH,OW,Cout]; wt: [C,KH,KW,Cout]. Returns dx [N,H,W,C]."""
     _chk(dy, name="dy")

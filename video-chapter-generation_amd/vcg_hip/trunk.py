@@ -241,6 +241,8 @@ class ResNetTrunk:
         Cin = x.shape[-1]
         conv1, T, fold = _tsm_info(blk.conv1, Cin)
         planes = conv1.out_channels
+        if self._foldable(blk, x, need_grad):
+            return self._block_fwd_folded(blk, x, conv1, T, fold, N, H, W)
         # the downsample branch (a layer's first block) depends only on x: its conv + BN statistics run on the side
         # stream, concurrently with conv1 -> conv2 -> conv3; the bn3 apply that adds it waits for it
         yd = bd = side = None
@@ -261,10 +263,6 @@ class ResNetTrunk:
         # fused engine takes it (bf16, batch statistics)
         a2 = None
         y3 = None
-        if (ResNetTrunk.fold_eval and not need_grad and blk.downsample is None and self.dtype == torch.bfloat16
-                and x.is_cuda and bn_mode(blk.bn3) == "running" and _conv_shape(blk.conv3)[2:] == (1, 1, 1, 0)):
-            a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
-            return self._conv3_folded(blk, a2, x, N, H2, W2, planes), None, H2, W2
         if self.dtype == torch.bfloat16 and ResNetTrunk.fused_bnin:
             y3, b3, _, _ = self._conv_bn(y2, blk.conv3, blk.bn3, N, H2, W2, planes, in_bn=(b2.scale, b2.shift))
         if y3 is None:
@@ -287,19 +285,51 @@ class ResNetTrunk:
                        conv1=conv1)
         return out, rec, H2, W2
 
-    def _conv3_folded(self, blk, a2, x, N, H, W, planes):
-        """relu(bn3(conv3(a2)) + x) with running statistics, as one GEMM: rows of W3 scaled by gamma * invstd (bf16),
-        beta - mean * scale as bias, the identity x as residual (eval BN, test_video_segment_point.py:116-122)."""
-        bn, conv = blk.bn3, blk.conv3
-        C3 = conv.out_channels
-        st = BNState(C3, x.device, "running", 0, bn)
-        ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, C3, st.mean, st.invstd,
+    def _foldable(self, blk, x, need_grad):
+        """bf16 scoring forward with every BN of the block on running statistics and a 1x1 / stride-1 conv3."""
+        if not (ResNetTrunk.fold_eval and not need_grad and self.dtype == torch.bfloat16 and x.is_cuda):
+            return False
+        bns = [blk.bn1, blk.bn2, blk.bn3] + ([blk.downsample[1]] if blk.downsample is not None else [])
+        return all(bn_mode(b) == "running" for b in bns) and _conv_shape(blk.conv3)[2:] == (1, 1, 1, 0)
+
+    def _fold(self, conv, bn, Cpad):
+        """(folded bf16 GEMM weight [Cout][KH][KW][Cpad], bias): conv weight rows scaled by gamma * invstd of the
+        running statistics, beta - mean * scale as bias (eval BN, test_video_segment_point.py:116-122)."""
+        Cout, Cin, KH, KW, _, _ = _conv_shape(conv)
+        st = BNState(Cout, conv.weight.device, "running", 0, bn)
+        ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, Cout, st.mean, st.invstd,
                            st.scale, st.shift)
-        wf = ops.weight_fold(conv.weight.data.view(C3, planes), st.scale, self.dtype)
-        M = N * H * W
-        out = ops.gemm(a2.view(M, planes), wf, M, C3, planes, planes, planes, bias=st.shift, act=ops.ACT_RELU,
-                       residual=x.view(M, C3), ldr=C3)
-        return out.view(N, H, W, C3)
+        w2 = conv.weight.data.view(Cout, Cin * KH * KW)
+        if KH == KW == 1 and Cpad == Cin:
+            return ops.weight_fold(w2, st.scale, self.dtype), st.shift
+        wf = ops.weight_fold(w2, st.scale, torch.float32).view(Cout, Cin, KH, KW)
+        return ops.weight_prep(wf, Cpad, self.dtype), st.shift
+
+    def _block_fwd_folded(self, blk, x, conv1, T, fold, N, H, W):
+        """The bottleneck of the scoring forward with every BN folded into the conv before it: conv1 (+ TSM gather)
+        and conv2 with bias + ReLU epilogues, the downsample conv with bias, conv3 as one GEMM with bias, the
+        identity / downsample output as residual and ReLU -- no y tensors, no BN passes."""
+        Cin = x.shape[-1]
+        planes = conv1.out_channels
+        w1, c1 = self._fold(conv1, blk.bn1, Cin)
+        a1 = ops.conv_fwd_bias_act(x, w1, c1, ops.ACT_RELU, N, H, W, Cin, planes, 1, 1, 1, 0, T, fold)
+        _, _, KH, KW, s, p = _conv_shape(blk.conv2)
+        w2, c2 = self._fold(blk.conv2, blk.bn2, planes)
+        a2 = ops.conv_fwd_bias_act(a1, w2, c2, ops.ACT_RELU, N, H, W, planes, planes, KH, KW, s, p)
+        H2, W2 = a2.shape[1], a2.shape[2]
+        C3 = blk.conv3.out_channels
+        if blk.downsample is not None:
+            cd = blk.downsample[0]
+            Cd, _, KHd, KWd, sd, pd = _conv_shape(cd)
+            wd, bd = self._fold(cd, blk.downsample[1], Cin)
+            res = ops.conv_fwd_bias_act(x, wd, bd, ops.ACT_NONE, N, H, W, Cin, Cd, KHd, KWd, sd, pd)
+        else:
+            res = x
+        w3, c3 = self._fold(blk.conv3, blk.bn3, planes)
+        M = N * H2 * W2
+        out = ops.gemm(a2.view(M, planes), w3, M, C3, planes, planes, planes, bias=c3, act=ops.ACT_RELU,
+                       residual=res.view(M, C3), ldr=C3)
+        return out.view(N, H2, W2, C3), None, H2, W2
 
     # ---------------------------------------------------------------- backward
     def _bn_bwd(self, dout, y, st, C, mbits=None, affine=False):
