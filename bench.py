@@ -114,7 +114,7 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=3):
+def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=3, bn="running"):
     """The oracle (oracle/model.py: fp32 CPU restatement of the reference path, test infrastructure) timed on this
     host: train = one reference train step (fwd BN-train + CE + bwd + clip_grad_norm_ + AdamW), fwd = the eval
     forward (running-stat BN). Median of `reps` timed runs after 1 warm-up. B is a bounded sample (2 windows train,
@@ -141,13 +141,13 @@ def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=3):
             p = dict(buffers)
             p.update(params)
             with torch.no_grad():
-                om.two_stream(p, frames, ids, mask, bn_mode="running")
+                om.two_stream(p, frames, ids, mask, bn_mode=bn)
         dt = time.perf_counter() - t0
         if r > 0:
             times.append(dt)
     med = sorted(times)[len(times) // 2]
     what = ("fp32 train step (fwd + bwd + clip + AdamW, BN train, dropout 0.1)" if mode == "train"
-            else "fp32 eval forward (running-stat BN)")
+            else f"fp32 eval forward ({bn}-stat BN)")
     return {"value": round(B / med, 4), "unit": "clip-windows/sec", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"oracle/ CPU {what} on B={B} windows of {T}x{HW}^2 + {L} tokens; median of {reps} timed runs "
@@ -169,6 +169,9 @@ def long_video_bench(args):
     _lib.call("vcg_init", 0)
     T, HW, L, B, F = args.frames, args.res, args.tokens, args.batch, args.video_frames
     model = build_two_stream(clip_frame_num=T, seed=123, device=dev, precision=args.precision).eval()
+    if args.bn == "batch":
+        from test_video_segment_point import drop_bn_running_stats
+        drop_bn_running_stats(model)
     frames, timestamps, subtitles = lv.synthetic_long_video(F, HW, HW, seed=123, device=dev)
     win, idx, ids, mask = lv.window_inputs(F, T, 1, subtitles, HashTokenizer(), L)
     idx, ids, mask = (torch.from_numpy(a).to(dev) for a in (idx, ids, mask))
@@ -186,7 +189,7 @@ def long_video_bench(args):
         "value": round(n / sec, 3), "unit": "clip-windows/sec", "n_gpus": 1, "windows": n, "seconds": round(sec, 3),
         "higher_is_better": True, "dtype": args.precision,
         "data": "synthetic 1 fps video (seeded u8 frames in HBM, random-init weights)",
-        "config": {"workload": f"{F} frames {HW}^2, T={T}, L={L}, batch {B}, running-stats BN",
+        "config": {"workload": f"{F} frames {HW}^2, T={T}, L={L}, batch {B}, {args.bn}-stats BN", "bn": args.bn,
                    "frames": F, "clip_frame_num": T, "seq_len": L, "resolution": HW},
         "roofline_step": {"bound": "hbm", "achieved": round(nbytes * n / sec / 1e9, 2), "peak": HBM_PEAK_GBS,
                           "unit": "GB/s", "frac": round(nbytes * n / sec / 1e9 / HBM_PEAK_GBS, 4),
@@ -195,13 +198,54 @@ def long_video_bench(args):
                                        "f", "f_3", "f_5")}}), flush=True)
 
 
+# ----------------------------------------------------------------------------- launcher
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Run this same command as an n-rank torch.distributed.run job (rendezvous on 127.0.0.1) in a child process
+    and return its exit status. Rank 0 of the job prints the JSON line."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(args, world, rank):
+    """The launch path without the model: the ranks rendezvous (gloo), count themselves with an all-reduce and
+    rank 0 prints n_gpus and the local ranks it saw (tests/test_cpu_bench_launch.py)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([1, int(os.environ.get("LOCAL_RANK", "0"))], dtype=torch.int64)
+    seen = [torch.zeros_like(t) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(seen, t)
+    else:
+        seen = [t]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": int(sum(int(s[0]) for s in seen)),
+                          "local_ranks": [int(s[1]) for s in seen], "launch_check": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="clip windows per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="clip windows per GPU (default 64; 16 with --bn batch, the test driver's batch)")
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--res", type=int, default=224)
     ap.add_argument("--tokens", type=int, default=128)
@@ -210,10 +254,24 @@ def main():
                     help="long_video: BASELINE config 5 (1 h synthetic video, stride-1 s windows, on-GPU frame "
                          "ingest, end-to-end boundary metrics), 1 GPU")
     ap.add_argument("--video-frames", type=int, default=3600)
+    ap.add_argument("--bn", default="running", choices=["running", "batch"],
+                    help="scoring modes (fwd / long_video): BN with running statistics (model.eval(), the trainer's "
+                         "val and convert2vision_emb) or with the batch's statistics (test_video_segment_point.py:"
+                         "116-122, which scores batches of 16 windows: pass --batch 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rehearse the rank launch only (gloo, no GPU): every rank joins the process group and "
+                         "rank 0 prints the line's n_gpus / rank layout")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 16 if (args.bn == "batch" and args.mode != "train") else 64
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: start the N rank processes ourselves, one per GPU, as the
+        # reference's DDP driver does with mp.spawn (train_video_segment_ddp.py:599-608). This process has not
+        # touched the GPU (torch is not even imported yet), and the ranks are fresh child processes, not an exec.
+        return launch_ranks(args.gpus)
     import torch
     import torch.distributed as dist
 
@@ -221,6 +279,10 @@ def main():
         return long_video_bench(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
+    if args.launch_check:
+        return launch_check(args, world, rank)
     # one process per GPU; VCG_DIST_BACKEND=gloo + more ranks than GPUs only for rehearsing the DDP path on a
     # one-GPU box (ranks then share devices round-robin); the benchmark itself is RCCL ("nccl") over xGMI
     backend = os.environ.get("VCG_DIST_BACKEND", "nccl")
@@ -245,6 +307,9 @@ def main():
     torch.manual_seed(123)
     model = build_two_stream(clip_frame_num=T, seed=123, device=dev, precision=args.precision)
     model.train(args.mode == "train")
+    if args.mode == "fwd" and args.bn == "batch":
+        from test_video_segment_point import drop_bn_running_stats
+        drop_bn_running_stats(model)
 
     class Cfg:
         weight_decay = 0.01
@@ -324,9 +389,12 @@ def main():
     ops.timing_enable(True)
     step()
     torch.cuda.synchronize()
-    k_ms, k_n, k_fl = ops.timing_query(ops.TIMING_FAST_GEMM)
+    # the dominant kernel: the bf16 fast engine, or the generic engine (exact fp32 MFMA) in the parity precision
+    dom_id, dom_name = ((ops.TIMING_FAST_GEMM, "igemm_fast_kernel") if args.precision == "bf16"
+                        else (ops.TIMING_GENERIC_GEMM, "igemm_kernel"))
+    k_ms, k_n, k_fl = ops.timing_query(dom_id)
     peak_tf = MFMA_PEAK_TFLOPS[args.precision]
-    rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (ops.TIMING_FAST_GEMM, ops.TIMING_WGRAD)}
+    rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (dom_id, ops.TIMING_WGRAD)}
     ops.timing_enable(False)
     model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream, ResNetTrunk.prep_stream = sides
     kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
@@ -348,20 +416,20 @@ def main():
             with open(tf) as f:
                 tj = json.load(f)
             traffic = tj.get("hbm_bytes_per_step")
-            kern_traffic = tj.get("igemm_fast_kernel", {}).get("hbm_bytes_per_launch")
+            kern_traffic = tj.get(dom_name, {}).get("hbm_bytes_per_launch")
         mf = os.path.join(REPO, "profiles", f"mfma_{args.mode}_{args.precision}_b{B}.json")
         if os.path.exists(mf):  # PMC SQ_VALU_MFMA_BUSY_CYCLES pass (tools/mfma.sh)
             with open(mf) as f:
-                mfma_busy = json.load(f).get("igemm_fast_kernel")
+                mfma_busy = json.load(f).get(dom_name)
         dom = None
         if kern["launches"]:
             # the dominant kernel's bound from its aggregate arithmetic intensity over the step: algorithmic
             # bytes / HBM peak vs algorithmic FLOPs / MFMA peak (ridge ~312 flop/B in bf16)
-            r_ms, r_ideal, r_bytes, r_flops = rl[ops.TIMING_FAST_GEMM]
+            r_ms, r_ideal, r_bytes, r_flops = rl[dom_id]
             k_tf = kern["flops"] / (kern["ms"] / 1e3) / 1e12
             k_gbs = r_bytes / (kern["ms"] / 1e3) / 1e9
             hbm_bound = r_bytes / (HBM_PEAK_GBS * 1e9) >= r_flops / (peak_tf * 1e12)
-            dom = {"kernel": "igemm_fast_kernel", "bound": "hbm" if hbm_bound else "mfma",
+            dom = {"kernel": dom_name, "bound": "hbm" if hbm_bound else "mfma",
                    "achieved": round(k_gbs if hbm_bound else k_tf, 2),
                    "peak": HBM_PEAK_GBS if hbm_bound else peak_tf, "unit": "GB/s" if hbm_bound else "TFLOP/s",
                    "frac": round((k_gbs / HBM_PEAK_GBS) if hbm_bound else (k_tf / peak_tf), 4),
@@ -376,7 +444,7 @@ def main():
                    "share_of_step": round(kern["ms"] / ms, 4),
                    # the same launches against their own roofline: ideal = sum of max(flops / MFMA peak,
                    # algorithmic bytes / HBM peak) per launch
-                   "per_launch_roofline": _per_launch(rl[ops.TIMING_FAST_GEMM]),
+                   "per_launch_roofline": _per_launch(rl[dom_id]),
                    "wgrad_fast_kernel": _per_launch(rl[ops.TIMING_WGRAD]),
                    "timing": "HIP events around each launch on its stream, one instrumented step (no BERT side "
                              "stream in that step: unshared launch durations)"}
@@ -389,7 +457,7 @@ def main():
                                    f"B={B} windows/GPU of {T}x{HW}^2 frames + {L} tokens"
                                    + (", fused clip+AdamW" if args.mode == "train" else ""),
                        "global_batch": windows, "seq_len": L, "frames": T, "resolution": HW,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", **({"bn": args.bn} if args.mode == "fwd" else {})},
             "roofline": dom,
             "host": {"enqueue_ms_per_step_median": round(1e3 * sorted(enq)[len(enq) // 2], 3),
                      "enqueue_ms_per_step_max": round(1e3 * max(enq), 3), **host_diag},
@@ -402,7 +470,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or cpu_threads()
             try:
-                out["cpu_baseline"] = cpu_baseline(T, HW, L, threads, args.mode)
+                out["cpu_baseline"] = cpu_baseline(T, HW, L, threads, args.mode, bn=args.bn)
             except Exception as e:  # the GPU number stands on its own; report why the baseline is missing
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), flush=True)
@@ -411,4 +479,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -26,6 +26,10 @@ extern "C" {
 enum { VCG_F32 = 0, VCG_BF16 = 1 };
 enum { VCG_OK = 0, VCG_ERR_INVALID = -1, VCG_ERR_UNSUPPORTED = -2, VCG_ERR_HIP = -3 };
 enum { VCG_ACT_NONE = 0, VCG_ACT_RELU = 1, VCG_ACT_GELU = 2, VCG_ACT_TANH = 3, VCG_ACT_GELU_BWD = 4 };
+/* vcg_gemm act flag: with a residual, round alpha * AB + bias to the storage dtype BEFORE adding the residual (the
+   unfolded conv3 -> bn3 path stores y3 in bf16; the scoring forward's folded conv3 sets it to match). Without it the
+   residual is added to the f32 accumulator value. */
+enum { VCG_ACT_FLAG_ROUND_PRE = 0x100 };
 
 /* ---- library ---------------------------------------------------------------------------- */
 VCG_API const char* vcg_last_error(void);

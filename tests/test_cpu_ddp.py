@@ -93,6 +93,13 @@ def _worker(rank, world, port, q):
         bb()
         ok_bufs = bool((mb.running_mean == 10.0).all()) and bool((mb.running_var == 20.0).all()) and \
             int(mb.num_batches_tracked) == rank
+        # a buffer replaced after binding (reassignment / .to()) is re-bound and still synced; mixed float dtypes
+        # sync as one flat buffer per dtype
+        mb.running_var = torch.full((5,), 30.0 + rank)
+        mb.register_buffer("half_stat", torch.full((4,), 1.0 + rank, dtype=torch.float64))
+        bb()
+        ok_bufs = ok_bufs and bool((mb.running_var == 30.0).all()) and bool((mb.half_stat == 1.0).all()) and \
+            len(bb.flats) == 2
         # disabled reducer (accumulation micro-step) leaves the local gradient alone
         before = flat.grad.clone()
         red.enabled = False

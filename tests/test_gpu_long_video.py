@@ -147,3 +147,64 @@ def test_c5_full_size_bf16_vs_fp32_and_oracle():
     e = np.abs(pr[:, 1].numpy() - p32[pick]).max()
     print(f"C5 fp32 native vs oracle on 16 windows: max |dprob| {e:.2e}")
     assert e < 1e-3
+
+
+def test_c5_batch_stat_bn_vs_oracle():
+    """Config 5 under the reference F1 pipeline's BN semantics (test_video_segment_point.py:116-122: running
+    statistics dropped, every batch of 16 consecutive windows normalised with its own statistics, batch 16 at :41)
+    on the full 1 h video, stride 1 s: fp32 parity mode scored end to end, bf16 vs fp32 labels / F1 on every
+    window, and two whole 16-window batches (the batch partition is part of the result) against the CPU oracle in
+    its "batch" BN mode within 1e-3."""
+    import long_video as lv
+    from data.synthetic_dataset import HashTokenizer, normalize_frames
+    from oracle import model as om
+    from test_video_segment_point import drop_bn_running_stats
+    from vcg_hip import ops
+    from vcg_hip.build import build_two_stream
+    F, T, HW, L, S, BS = 3600, 16, 224, 128, 1, 16
+    frames, timestamps, subtitles = lv.synthetic_long_video(F, HW, HW, seed=123, device=DEV)
+    win, idx, ids, mask = lv.window_inputs(F, T, S, subtitles, HashTokenizer(), L)
+    idx_d, ids_d, mask_d = (torch.from_numpy(a).to(DEV) for a in (idx, ids, mask))
+    models = {p: build_two_stream(clip_frame_num=T, seed=123, device=DEV, precision=p, dropout=0.0).eval()
+              for p in ("fp32", "bf16")}
+    for m in models.values():
+        assert drop_bn_running_stats(m) == 53
+    with torch.no_grad():  # re-bias the head so that about half the windows are positive (see the test above)
+        fr = ops.window_frames_u8(frames, idx_d[:BS].contiguous(), torch.float32, cpad=ops.stem_cpad(torch.float32))
+        lg, _ = models["fp32"].forward_staged(fr, ids_d[:BS], mask_d[:BS])
+        shift = (lg[:, 0] - lg[:, 1]).median().item()
+        for m in models.values():
+            m.fusion_head.head.bias.data[1] += shift
+            m.native_flat().refresh_shadow(force=True)
+    res = {}
+    for p, m in models.items():
+        sc, lab = lv.score_windows(m, frames, idx_d, ids_d, mask_d, batch_size=BS)
+        torch.cuda.synchronize()
+        res[p] = (sc.cpu().numpy().astype(np.float64), lab.cpu().numpy())
+    p32, l32 = res["fp32"]
+    p16, l16 = res["bf16"]
+    d = np.abs(p16 - p32)
+    flips = np.nonzero(l16 != l32)[0]
+    m32 = lv.boundary_metrics(l32.tolist(), timestamps, F, T, S)
+    m16 = lv.boundary_metrics(l16.tolist(), timestamps, F, T, S)
+    print(f"C5 batch-stat BN: positive share {l32.mean():.3f}; |p16 - p32| median {np.median(d):.2e} max "
+          f"{d.max():.2e}; {len(flips)} flips")
+    print("C5 batch-stat fp32 metrics", {k: m32[k] for k in ("recall", "precision", "f", "f_3", "f_5")})
+    print("C5 batch-stat bf16 metrics", {k: m16[k] for k in ("recall", "precision", "f", "f_3", "f_5")})
+    assert 0.05 < l32.mean() < 0.95
+    assert d.max() <= 5e-2
+    share = len(flips) / len(win)
+    for k in ("f", "f_3", "f_5"):
+        assert abs(m16[k] - m32[k]) <= max(2 * share, 1e-9) + (0.0 if share == 0 else 0.05), k
+    p = {k: v.detach().cpu() for k, v in models["fp32"].state_dict().items()}
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    for b0 in (0, (len(win) // 2) // BS * BS):
+        sel = np.arange(b0, b0 + BS)
+        img = normalize_frames(frames[torch.from_numpy(idx[sel].reshape(-1)).to(DEV)].cpu().numpy().reshape(
+            BS, T, HW, HW, 3))
+        with torch.no_grad():
+            _, pr, _, _ = om.two_stream(p, img, torch.from_numpy(ids[sel]), torch.from_numpy(mask[sel]),
+                                        bn_mode="batch")
+        e = np.abs(pr[:, 1].numpy() - p32[sel]).max()
+        print(f"C5 batch-stat fp32 native vs oracle, windows {b0}..{b0 + BS - 1}: max |dprob| {e:.2e}")
+        assert e < 1e-3

@@ -11,6 +11,7 @@ enum { OP_DENSE_K = 0, OP_IM2COL = 1, OP_DGRAD = 2, OP_DENSE_MN = 3, OP_IM2COL_T
 // goes out through the LDS stage, in a round of its own
 enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 4, EPI_STORE_AUX = 5 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
+enum { ACT_FLAG_ROUND_PRE = 0x100 };  // = VCG_ACT_FLAG_ROUND_PRE (include/vcg_hip.h)
 
 template <typename T> struct Cfg;
 template <> struct Cfg<float> { static constexpr int VEC = 4, BK = 16, LDK = 20; };   // 80-B rows
@@ -95,6 +96,7 @@ struct GemmParams {
   int batch_inner;
   long long a_so, a_si, b_so, b_si, c_so, c_si;
   int stage_kt;  // fast kernel: stage the output tile through LDS when the tile has <= stage_kt k-steps
+  int res_round; // residual epilogue: round alpha*AB + bias to bf16 before adding the residual (VCG_ACT_FLAG_ROUND_PRE)
   BwdEpi bwd;    // EPI_BWD
   // the consuming conv applies its input's BatchNorm + ReLU on load: x -> bf16(max(fma(x, in_sc[c], in_sh[c]), 0))
   // (vcg_bn_apply's arithmetic) for input channel c, in LDS right after the tile's DMA lands (fast dense A of

@@ -369,7 +369,20 @@ static bool fast_gemm_enabled() {
 template <typename T, int BM, int BN, int AM, int BMD, int EPI>
 static int launch(const GemmParams& p, int splits, hipStream_t s) {
   dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
+  const int tk = timing_begin(s);
   hipLaunchKernelGGL((igemm_kernel<T, BM, BN, AM, BMD, EPI>), grid, dim3(256), 0, s, p);
+  {
+    // algorithmic bytes: each operand once (a gathered A as its source tensor), the output once (the split-K
+    // epilogue's f32 slabs count as its output), the residual once
+    const double es = (double)sizeof(T);
+    const double z = p.batch_inner > 0 ? (double)splits : 1.0;
+    const bool adense = AM == OP_DENSE_K || AM == OP_DENSE_MN, bdense = BMD == OP_DENSE_K || BMD == OP_DENSE_MN;
+    double b = (adense ? es * p.M * (double)p.K : (double)p.a.bytes) * z +
+               (bdense ? es * p.N * (double)p.K : (double)p.b.bytes) * z;
+    b += (EPI == EPI_SPLITK ? 4.0 * splits : es * z) * p.M * (double)p.N;
+    if (p.residual) b += es * p.M * (double)p.N * z;
+    timing_end(tk, s, TIMING_GENERIC_GEMM, 2.0 * p.M * p.N * (double)p.K * z, b);
+  }
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -963,7 +976,9 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
   p.b = transB ? dense_op(B, ldb, K, N, esz) : dense_op(B, ldb, N, K, esz);
   p.a.rows = M;
   p.b.rows = N;
-  p.C = C; p.ldc = ldc; p.bias = bias; p.act = act; p.residual = residual; p.ldr = ldr; p.aux = aux;
+  VCG_REQUIRE((act & ~(0xff | ACT_FLAG_ROUND_PRE)) == 0, "unknown act flags");
+  p.C = C; p.ldc = ldc; p.bias = bias; p.act = act & 0xff; p.residual = residual; p.ldr = ldr; p.aux = aux;
+  p.res_round = (act & ACT_FLAG_ROUND_PRE) != 0 && residual != nullptr;
   p.alpha = alpha;
 #define VCG_GEMM_CASE(TT)                                                                   \
   if (!transA && !transB) return run_gemm<TT, OP_DENSE_K, OP_DENSE_K>(p, EPI_STORE, 1, stream);   \

@@ -938,9 +938,11 @@ void igemm_fast_kernel(GemmParams p) {
         }
       } else if constexpr (EPI == EPI_STORE_AUX) {
         if constexpr (BM == 128) epilogue_staged_aux<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane);
-      } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0)) {
+      } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0 &&
+                               ((uintptr_t)p.C & 15) == 0)) {
         epilogue_staged<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
-      } else if (RES && staged && p.act == ACT_RELU && p.aux == nullptr && ((p.ldc | p.ldr | p.N) & 7) == 0) {
+      } else if (RES && staged && p.res_round && p.act == ACT_RELU && p.aux == nullptr &&
+                 ((p.ldc | p.ldr | p.N) & 7) == 0 && (((uintptr_t)p.residual | (uintptr_t)p.C) & 15) == 0) {
         if constexpr (BM == 128 && RES)
           epilogue_staged_res<BM, BN>(acc, p, bv, Cout, Res, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
       } else {

@@ -9,13 +9,18 @@ One decoded video (u8 frames [F, H, W, 3], 1 fps, resident in HBM) is scored end
      layout (ops.window_frames_u8) -- no host decode / upload per window;
   3. subtitles in (s - 1, e + 1) are tokenised as "[CLS] " + text, truncated / padded to L
      (`youtube_dataset.py:141-174`);
-  4. TwoStream scores the windows in batches (eval: BN running statistics), pred_label = argmax(logits),
+  4. TwoStream scores the windows in batches of consecutive windows, pred_label = argmax(logits),
      pred_score = prob[:, 1] (`test_video_segment_point.py:193-206`); optionally each window's vision
      embedding [T, 2048] is exported as vision_emb_{s}_{e}.npy (`convert2vision_emb.py:177-198`);
+     BN: `--bn_mode running` (model.eval(), as convert2vision_emb.py:123 and the trainer's validation) or `batch`
+     (test_video_segment_point.py:116-122: the running statistics are dropped and every batch of `batch_size`
+     consecutive windows -- 16 there, :41 -- is normalised with its own statistics, so the batch partition is part
+     of the result);
   5. runs of positive windows -> cut points (`eval_utils.py:3-18`, window step = stride) -> recall / precision
      at 0 / 3 / 5 s against the chapter starts (`eval_utils.py:21-92`) -> F.
 
 usage: python long_video.py [--frames 3600] [--res 224] [--clip_frame_num 16] [--stride 1] [--batch_size 64]
+                            [--bn_mode running|batch]
 """
 import argparse
 import json
@@ -114,12 +119,15 @@ def main(argv=None):
     ap.add_argument("--clip_frame_num", default=16, type=int)
     ap.add_argument("--stride", default=1, type=int)
     ap.add_argument("--max_text_len", default=128, type=int)
-    ap.add_argument("--batch_size", default=64, type=int)
+    ap.add_argument("--batch_size", default=None, type=int, help="default: 64 (running), 16 (batch, the test driver's)")
+    ap.add_argument("--bn_mode", default="running", choices=["running", "batch"])
     ap.add_argument("--head_type", default="mlp", type=str)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--export_dir", default=None, help="write vision_emb_{s}_{e}.npy per window (convert2vision_emb)")
     ap.add_argument("--seed", default=123, type=int)
     args = ap.parse_args(argv)
+    if args.batch_size is None:
+        args.batch_size = 64 if args.bn_mode == "running" else 16
 
     from convert2vision_emb import emb_path
     from data.synthetic_dataset import HashTokenizer
@@ -131,6 +139,9 @@ def main(argv=None):
     _lib.call("vcg_init", args.gpu)
     model = build_two_stream(clip_frame_num=args.clip_frame_num, head_type=args.head_type, seed=args.seed,
                              device=dev, precision=args.precision).eval()
+    if args.bn_mode == "batch":
+        from test_video_segment_point import drop_bn_running_stats
+        drop_bn_running_stats(model)
     frames, timestamps, subtitles = synthetic_long_video(args.frames, args.res, args.res, seed=args.seed, device=dev)
     win, idx, ids, mask = window_inputs(args.frames, args.clip_frame_num, args.stride, subtitles, HashTokenizer(),
                                         args.max_text_len)

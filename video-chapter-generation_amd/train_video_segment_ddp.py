@@ -17,7 +17,9 @@ averages the validation metric with `all_gather_object` (`:276-281`). Here:
 Launch: `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 train_video_segment_ddp.py`.
 """
 import argparse
+import glob
 import os
+import re
 import sys
 
 import torch
@@ -28,6 +30,34 @@ if _HERE not in sys.path:
     sys.path.insert(0, _HERE)
 
 from train_video_segment_point import TrainerConfig, lr_multiplier  # noqa: E402
+
+
+CKPT_RE = re.compile(r"_(\d+)(?:_score_[\d.]+)?\.pth$")
+
+
+def find_latest_checkpoint(ckpt_dir, rank=0):
+    """(path, epoch) of the newest `<base>_<epoch>[_score_<s>].pth` under ckpt_dir, found on rank 0 and broadcast
+    (`train_video_segment_ddp.py:176-207`); (None, 0) when there is none."""
+    info = (None, 0)
+    if rank == 0 and ckpt_dir and os.path.isdir(ckpt_dir):
+        best = (None, -1)
+        for f in glob.glob(os.path.join(ckpt_dir, "*.pth")):
+            m = CKPT_RE.search(os.path.basename(f))
+            if m and int(m.group(1)) > best[1]:
+                best = (f, int(m.group(1)))
+        if best[0] is not None:
+            info = best
+    if dist.is_initialized():
+        obj = [info]
+        dist.broadcast_object_list(obj, src=0)
+        info = obj[0]
+    return info
+
+
+def checkpoint_path(ckpt_path, epoch, best_result, is_best):
+    """`train_video_segment_ddp.py:150-173`'s names: <base>_<epoch>_score_<best:.4f>.pth or <base>_<epoch>.pth."""
+    base = os.path.splitext(ckpt_path)[0]
+    return f"{base}_{epoch}_score_{best_result:.4f}.pth" if is_best else f"{base}_{epoch}.pth"
 
 
 class DDPTrainer:
@@ -47,6 +77,51 @@ class DDPTrainer:
         # DDP(model)'s broadcast_buffers=True: rank 0's BatchNorm running stats before every training forward
         self.buffers = BufferBroadcaster(model)
         self.history = []
+        self.start_epoch, self.best_result = 0, float("-inf")
+
+    def resume(self):
+        """Continue from the newest checkpoint under config.ckpt_path (`:176-207,245-263`): rank 0 finds it and
+        broadcasts its name; every rank loads the model and optimizer state from it (the reference loads the
+        optimizer state on rank 0 only, leaving the other ranks' Adam moments at zero), then rank 0's parameters are
+        broadcast as at start."""
+        from vcg_hip.ddp import broadcast_parameters
+        path, _ = find_latest_checkpoint(self.config.ckpt_path, self.rank)
+        if path is None:
+            return None
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(ck["model_state_dict"])
+        self.optimizer.load_state_dict(ck["optimizer_state_dict"])
+        self.start_epoch, self.best_result = int(ck["epoch"]), float(ck["best_result"])
+        broadcast_parameters(self.model)
+        return path
+
+    def save_checkpoint(self, epoch, best_result, is_best=False):
+        """Rank 0 writes the reference's checkpoint dict (`:150-173`)."""
+        if self.rank != 0 or self.config.ckpt_path is None:
+            return None
+        path = checkpoint_path(self.config.ckpt_path, epoch, best_result, is_best)
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        torch.save({"epoch": epoch, "best_result": best_result, "model_state_dict": self.model.state_dict(),
+                    "optimizer_state_dict": self.optimizer.state_dict()}, path)
+        return path
+
+    def fit(self, val_every=30, save_every=10):
+        """The reference's epoch loop (`:265-290`): validation every `val_every` epochs (rank-averaged metric; a best
+        checkpoint when it improves), else a regular checkpoint every `save_every` epochs."""
+        best, result = self.best_result, None
+        for epoch in range(self.start_epoch + 1, self.config.max_epochs + 1):
+            self.run_epoch("train", epoch)
+            if self.test_dataset is not None and epoch % val_every == 0:
+                result = self.run_epoch("infer_test", epoch)
+                if self.rank == 0:
+                    print(f"epoch {epoch}: val {result}")
+                if result == result and result > best:
+                    best = result
+                    self.save_checkpoint(epoch, best, is_best=True)
+            elif epoch % save_every == 0:
+                self.save_checkpoint(epoch, best, is_best=False)
+        self.best_result = best
+        return result
 
     def run_epoch(self, split, epoch):
         from vcg_hip.ddp import all_gather_object
@@ -126,6 +201,10 @@ def main(argv=None):
                         "(two_stream_window.TwoStream over 2w+1 clips, WindowClipDataset)")
     p.add_argument("--head_type", default="cross_attn", help="window model head (reference default cross_attn)")
     p.add_argument("--data_dir", default=None, help="window model: directory for the reference-format corpus")
+    p.add_argument("--ckpt_path", default=None,
+                   help="checkpoint directory (+ name prefix); training resumes from its newest checkpoint")
+    p.add_argument("--val_every", default=1, type=int, help="validate every N epochs (the reference: 30)")
+    p.add_argument("--save_every", default=10, type=int, help="regular checkpoint every N epochs (the reference: 10)")
     args = p.parse_args(argv)
 
     from common_utils import set_random_seed
@@ -150,14 +229,15 @@ def main(argv=None):
     model = build_two_stream(clip_frame_num=args.clip_frame_num, seed=args.seed, device=device, precision=args.precision)
     conf = TrainerConfig(max_epochs=args.epoch, batch_size=args.batch_size, val_batch_size=args.batch_size * 8,
                          gradient_accumulation_steps=4, num_workers=0, lr_decay=True,
-                         warmup_epochs=args.epoch // 100, final_epochs=args.epoch // 100 * 90)
-    tr = DDPTrainer(model, train_ds, test_ds, conf, rank, world, device)
-    result = None
-    for epoch in range(1, args.epoch + 1):
-        tr.run_epoch("train", epoch)
-        result = tr.run_epoch("infer_test", epoch)
-        if rank == 0:
-            print(f"epoch {epoch}: val m_ap {result}")
+                         warmup_epochs=args.epoch // 100, final_epochs=args.epoch // 100 * 90, ckpt_path=args.ckpt_path)
+    return _fit(DDPTrainer(model, train_ds, test_ds, conf, rank, world, device), args, world)
+
+
+def _fit(tr, args, world):
+    resumed = tr.resume()
+    if resumed and tr.rank == 0:
+        print(f"resumed from {resumed} (epoch {tr.start_epoch}, best {tr.best_result})")
+    result = tr.fit(args.val_every, args.save_every)
     if world > 1:
         dist.destroy_process_group()
     return result
@@ -189,17 +269,8 @@ def _window_main(args, rank, world, device, tok):
                                     head_type=args.head_type, seed=args.seed, device=device, precision=args.precision)
     conf = TrainerConfig(max_epochs=args.epoch, batch_size=args.batch_size, val_batch_size=args.batch_size,
                          gradient_accumulation_steps=4, num_workers=0, lr_decay=True,
-                         warmup_epochs=args.epoch // 100, final_epochs=args.epoch // 100 * 90)
-    tr = DDPTrainer(model, train_ds, test_ds, conf, rank, world, device)
-    result = None
-    for epoch in range(1, args.epoch + 1):
-        tr.run_epoch("train", epoch)
-        result = tr.run_epoch("infer_test", epoch)
-        if rank == 0:
-            print(f"epoch {epoch}: val window AP {result}")
-    if world > 1:
-        dist.destroy_process_group()
-    return result
+                         warmup_epochs=args.epoch // 100, final_epochs=args.epoch // 100 * 90, ckpt_path=args.ckpt_path)
+    return _fit(DDPTrainer(model, train_ds, test_ds, conf, rank, world, device), args, world)
 
 
 if __name__ == "__main__":

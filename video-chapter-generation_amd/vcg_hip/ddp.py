@@ -166,34 +166,50 @@ class BufferBroadcaster:
     """DDP's broadcast_buffers=True (the default of the reference's DDP(model), train_video_segment_ddp.py:148):
     before every training forward, rank 0's floating-point buffers (BatchNorm running_mean / running_var) are
     copied to every rank, so the running statistics do not drift apart across ranks (each rank's BN sees only its
-    own shard). The module buffers are re-bound to views of ONE flat buffer, so a sync is one collective."""
+    own shard). The module buffers are re-bound to views of one flat buffer per dtype, so a sync is one collective
+    per dtype. A buffer that was replaced since (model.to(), reassignment) is re-bound before the sync."""
 
     def __init__(self, model, src=0, group=None, comm=None):
         self.src, self.group, self.comm = src, group, comm
-        bufs = [(m, n, b) for m in model.modules() for n, b in m._buffers.items()
+        self.model = model
+        self.flats = {}
+        self._bind()
+
+    def _bufs(self):
+        return [(m, n, b) for m in self.model.modules() for n, b in m._buffers.items()
                 if b is not None and b.is_floating_point()]
-        self.flat = None
-        if not bufs:
-            return
-        dt = bufs[0][2].dtype
-        if any(b.dtype != dt for _, _, b in bufs):
-            raise TypeError("BufferBroadcaster: floating buffers of mixed dtypes")
-        total = sum(b.numel() for _, _, b in bufs)
-        self.flat = torch.empty(total, dtype=dt, device=bufs[0][2].device)
-        o = 0
-        for m, n, b in bufs:
-            v = self.flat[o:o + b.numel()].view_as(b)
-            v.copy_(b)
-            m._buffers[n] = v
-            o += b.numel()
+
+    def _bind(self):
+        bufs = self._bufs()
+        self.flats, self.bound = {}, []
+        for dt in dict.fromkeys(b.dtype for _, _, b in bufs):
+            group = [(m, n, b) for m, n, b in bufs if b.dtype == dt]
+            flat = torch.empty(sum(b.numel() for _, _, b in group), dtype=dt, device=group[0][2].device)
+            o = 0
+            for m, n, b in group:
+                v = flat[o:o + b.numel()].view_as(b)
+                v.copy_(b)
+                m._buffers[n] = v
+                self.bound.append((m, n, v))
+                o += b.numel()
+            self.flats[dt] = flat
+
+    @property
+    def flat(self):
+        """The flat buffer of the (single) buffer dtype, None without floating buffers."""
+        return next(iter(self.flats.values())) if len(self.flats) == 1 else (None if not self.flats else self.flats)
+
+    def _intact(self):
+        return all(m._buffers.get(n) is v for m, n, v in self.bound) and len(self.bound) == len(self._bufs())
 
     def __call__(self):
-        if self.flat is None:
-            return
-        if self.comm is not None:
-            self.comm.broadcast(self.flat, root=self.src)
-        elif dist.is_initialized() and dist.get_world_size(self.group) > 1:
-            dist.broadcast(self.flat, src=self.src, group=self.group)
+        if not self._intact():
+            self._bind()
+        for flat in self.flats.values():
+            if self.comm is not None:
+                self.comm.broadcast(flat, root=self.src)
+            elif dist.is_initialized() and dist.get_world_size(self.group) > 1:
+                dist.broadcast(flat, src=self.src, group=self.group)
 
 
 def all_gather_object(obj, group=None):

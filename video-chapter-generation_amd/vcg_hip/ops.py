@@ -12,6 +12,7 @@ from . import _lib
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_GELU_BWD = 0, 1, 2, 3, 4
+ACT_FLAG_ROUND_PRE = 0x100  # gemm: round alpha*AB + bias to the storage dtype before the residual (vcg_hip.h)
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -58,7 +59,7 @@ def conv_out_hw(H, W, KH, KW, stride, pad):
     return (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
 
 
-TIMING_FAST_GEMM, TIMING_WGRAD = 0, 1
+TIMING_FAST_GEMM, TIMING_WGRAD, TIMING_GENERIC_GEMM, TIMING_PATCH_CONV = 0, 1, 2, 3
 
 
 def timing_enable(on):

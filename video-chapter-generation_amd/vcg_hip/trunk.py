@@ -222,6 +222,13 @@ class ResNetTrunk:
         if not need_grad:
             del y0, idx
         h, Hc, Wc = mp, Hm, Wm
+        self._fold_gen = None
+        if ResNetTrunk.fold_eval and not need_grad and dt == torch.bfloat16:
+            key = self._fold_key()
+            old = getattr(net, "_vcg_fold_key", None)
+            if old is None or old[0] != key:
+                object.__setattr__(net, "_vcg_fold_key", (key, object()))
+            self._fold_gen = net._vcg_fold_key[1]
         if self._prep_ev is not None:
             torch.cuda.current_stream().wait_event(self._prep_ev)
             self._prep_ev = None
@@ -292,9 +299,32 @@ class ResNetTrunk:
         bns = [blk.bn1, blk.bn2, blk.bn3] + ([blk.downsample[1]] if blk.downsample is not None else [])
         return all(bn_mode(b) == "running" for b in bns) and _conv_shape(blk.conv3)[2:] == (1, 1, 1, 0)
 
+    def _fold_key(self):
+        """What the folded weights depend on: the master weights (flat.generation moves with every optimizer step /
+        in-place write) and the BN affine + running statistics (their tensors' version counters move with every
+        load_state_dict / in-place write; a training forward's native running-stat update bumps the
+        num_batches_tracked counters, which share one version counter when they are views of one buffer)."""
+        flat = getattr(self.net, "_vcg_flat", None)
+        v = 0
+        for m in self.net.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                for t in (m.weight, m.bias, m.running_mean, m.running_var, m.num_batches_tracked):
+                    if t is not None:
+                        v += t._version
+        return (flat.generation if flat is not None else None, v)
+
     def _fold(self, conv, bn, Cpad):
-        """(folded bf16 GEMM weight [Cout][KH][KW][Cpad], bias): conv weight rows scaled by gamma * invstd of the
-        running statistics, beta - mean * scale as bias (eval BN, test_video_segment_point.py:116-122)."""
+        """(folded bf16 GEMM weight [Cout][KH][KW][Cpad], bias), cached across scoring forwards until the weights
+        or the BN state change (_fold_key)."""
+        cache = self._fold_cache
+        ent = cache.get(id(conv))
+        if ent is None:
+            ent = cache[id(conv)] = self._fold_new(conv, bn, Cpad)
+        return ent
+
+    def _fold_new(self, conv, bn, Cpad):
+        """conv weight rows scaled by gamma * invstd of the running statistics, beta - mean * scale as bias (eval BN,
+        test_video_segment_point.py:116-122)."""
         Cout, Cin, KH, KW, _, _ = _conv_shape(conv)
         st = BNState(Cout, conv.weight.device, "running", 0, bn)
         ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, Cout, st.mean, st.invstd,
@@ -304,6 +334,14 @@ class ResNetTrunk:
             return ops.weight_fold(w2, st.scale, self.dtype), st.shift
         wf = ops.weight_fold(w2, st.scale, torch.float32).view(Cout, Cin, KH, KW)
         return ops.weight_prep(wf, Cpad, self.dtype), st.shift
+
+    @property
+    def _fold_cache(self):
+        c = getattr(self.net, "_vcg_fold_cache", None)
+        if c is None or c[0] is not self._fold_gen:
+            c = (self._fold_gen, {})
+            object.__setattr__(self.net, "_vcg_fold_cache", c)
+        return c[1]
 
     def _block_fwd_folded(self, blk, x, conv1, T, fold, N, H, W):
         """The bottleneck of the scoring forward with every BN folded into the conv before it: conv1 (+ TSM gather)
@@ -327,8 +365,8 @@ class ResNetTrunk:
             res = x
         w3, c3 = self._fold(blk.conv3, blk.bn3, planes)
         M = N * H2 * W2
-        out = ops.gemm(a2.view(M, planes), w3, M, C3, planes, planes, planes, bias=c3, act=ops.ACT_RELU,
-                       residual=res.view(M, C3), ldr=C3)
+        out = ops.gemm(a2.view(M, planes), w3, M, C3, planes, planes, planes, bias=c3,
+                       act=ops.ACT_RELU | ops.ACT_FLAG_ROUND_PRE, residual=res.view(M, C3), ldr=C3)
         return out.view(N, H2, W2, C3), None, H2, W2
 
     # ---------------------------------------------------------------- backward
