@@ -206,6 +206,9 @@ VCG_API int vcg_cross_attn_fwd(const float* lang, const float* vis, const float*
  * (n % 4 == 0); out[b][r] = sum_i U[b][r][i] x[b][i] + bias[r] (nn.Bilinear's second contraction after U = x2 A^T). */
 VCG_API int vcg_mul_fwd(const float* a, const float* b, float* out, long long n, hipStream_t s);
 VCG_API int vcg_rowdot_fwd(const float* U, const float* x, const float* bias, float* out, int B, int R, int K, hipStream_t s);
+/* its backward (the bilinear window head in training): dU[b][r][i] = dy[b][r] x[b][i], dx[b][i] = sum_r dy[b][r] U[b][r][i]
+   (dx may be null) */
+VCG_API int vcg_rowdot_bwd(const float* U, const float* x, const float* dy, float* dU, float* dx, int B, int R, int K, hipStream_t s);
 /* out = act(LayerNorm(x) * gamma + beta) over `rows` rows of D f32 features (window ChapterHead's Linear -> LN -> ReLU
  * chains, two_stream_window.py:145-176); act 0 = none, 1 = ReLU, 2 = GELU (erf). */
 VCG_API int vcg_ln_act_fwd(const float* x, const float* gamma, const float* beta, float* out, int rows, int D, float eps, int act, hipStream_t s);

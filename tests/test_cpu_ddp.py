@@ -83,6 +83,13 @@ def _worker(rank, world, port, q):
             tot16 += _FakeFlat(sizes, seed=100 + r).grad.bfloat16().float()
         ok_wire = torch.allclose(flat2.grad, tot16.bfloat16().float(), rtol=1e-2, atol=1e-2) and \
             flat2.grad.dtype == torch.float32
+        # parameters no hook reports (the window model's heads) are still reduced, by finish()
+        flat3 = _FakeFlat(sizes, seed=100 + rank)
+        red3 = GradAllReducer(flat3, bucket_bytes=64 * 1024)
+        red3([flat3.params[5]])
+        red3([flat3.params[2]])
+        red3.finish()
+        ok_wire = ok_wire and torch.allclose(flat3.grad, total, rtol=0, atol=1e-5)
         # BN-buffer sync before each forward (DDP broadcast_buffers): rank 1's drifted stats become rank 0's
         mb = torch.nn.Module()
         mb.register_buffer("running_mean", torch.full((3,), 10.0 + rank))

@@ -22,7 +22,7 @@ import torch
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 DEV = "cuda"
-HEADS = ["mlp", "cross_attn", "self_attn", "multiplication"]
+HEADS = ["mlp", "cross_attn", "self_attn", "multiplication", "bilinear"]
 
 
 class _Cfg:
@@ -148,3 +148,35 @@ def test_window_attention_dropout_backward_matches_finite_difference():
     torch.manual_seed(78)
     l2, _ = m(emb)
     assert (l2 - lg).abs().max().item() > 0  # other seeds, other masks: dropout is active
+
+
+def test_window_model_ddp_buckets_overlap_backward():
+    """The window model under the DDP reducer (train_video_segment_ddp.py's configuration): BERT / trunk parameter
+    groups are reported final after the last of the 2w+1 per-clip backwards (_ClipCountingHooks), buckets go out while
+    the backward is still running, finish() reduces the heads no hook reports, and (world 1, RCCL SUM = identity) the
+    gradients equal a step without the reducer. Runs through libvcg_hip's RCCL C ABI (NativeComm)."""
+    from vcg_hip.comm import NativeComm, unique_id
+    from vcg_hip.ddp import GradAllReducer
+    torch.cuda.set_device(0)
+    ref = _model("mlp", "bf16")
+    _step(ref)
+    g_ref = ref.native_flat().grad.clone()
+    comm = NativeComm(rank=0, world=1, uid=unique_id())
+    try:
+        m = _model("mlp", "bf16")
+        red = GradAllReducer(m.native_flat(), bucket_bytes=8 << 20, comm=comm, record=True)
+        red.enabled = True
+        m.set_grad_hooks(red)
+        _step(m)
+        red.finish()
+        torch.cuda.synchronize()
+    finally:
+        comm.close()
+    kinds = [e[0] for e in red.log]
+    assert kinds.count("hook") >= 20, kinds.count("hook")
+    last_hook = max(i for i, k in enumerate(kinds) if k == "hook")
+    assert kinds.index("flush") < last_hook, "no bucket went out during the backward"
+    covered = sorted((lo, hi) for k, lo, hi in red.log if k == "flush")
+    assert covered[0][0] == 0 and all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+    assert covered[-1][1] == m.native_flat().total
+    assert torch.equal(m.native_flat().grad, g_ref)

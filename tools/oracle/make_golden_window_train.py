@@ -2,7 +2,7 @@
 (model/fusion/two_stream_window.py:291-444 with ChapterHead :134-288 and stacked_window_self_attention.py) in this
 container -- only the .npz output is committed; the reference never travels.
 
-tests/golden/window_train.npz, per head type ht in (mlp, cross_attn, self_attn, multiplication):
+tests/golden/window_train.npz, per head type ht in (mlp, cross_attn, self_attn, multiplication, bilinear):
   {ht}_loss, {ht}_logits : one step at C1 shapes (B=2 windows, window_size 1 -> 3 clips of T=4 frames 112^2 + 32
       tokens; labels [0, 1]): model.train() with every nn.Dropout at p=0 and the vision BatchNorms in eval mode on the
       calibrated running statistics of bn_running_stats.npz (a well-conditioned, deterministic step: the native
@@ -34,7 +34,10 @@ HEAD_TRACK = {"mlp": ["fusion_head.head.1.0.weight", "fusion_head.head.0.8.weigh
               "cross_attn": ["fusion_head.head.query_proj.weight", "fusion_head.head.key_proj.weight",
                              "fusion_head.head.frame_pos_encoding.weight", "fusion_head.head.lang_norm.weight"],
               "self_attn": ["fusion_head.head.query.weight", "fusion_head.head.proj.weight"],
-              "multiplication": ["fusion_head.lang_expand_layers.1.4.weight", "fusion_head.head.2.0.weight"]}
+              "multiplication": ["fusion_head.lang_expand_layers.1.4.weight", "fusion_head.head.2.0.weight"],
+              "bilinear": ["fusion_head.bilinear_layers.1.weight", "fusion_head.bilinear_layers.0.bias",
+                           "fusion_head.head.2.3.weight"]}
+HEADS = ("mlp", "cross_attn", "self_attn", "multiplication", "bilinear")
 T, B, W, L = 4, 2, 1, 32
 
 
@@ -77,9 +80,13 @@ def step(head_type, dtype):
 
 
 def main():
+    """usage: make_golden_window_train.py [head_type ...] (default: all); existing entries of other heads are kept."""
     torch.set_num_threads(os.cpu_count() or 8)
-    out = {}
-    for ht in ("mlp", "cross_attn", "self_attn", "multiplication"):
+    path = os.path.join(mg.GOLD, "window_train.npz")
+    heads = sys.argv[1:] or HEADS
+    out = dict(np.load(path, allow_pickle=False)) if os.path.exists(path) else {}
+    for ht in heads:
+        out = {k: v for k, v in out.items() if not k.startswith(ht + "_")}
         m32, l32, lg32 = step(ht, torch.float32)
         m64, l64, lg64 = step(ht, torch.float64)
         p32, p64 = dict(m32.named_parameters()), dict(m64.named_parameters())
@@ -96,7 +103,7 @@ def main():
             out[f"{ht}_g64::{n}"] = p64[n].grad.reshape(-1)[idx].numpy()
         print(ht, "loss", l32, l64, "params with grads", len(names))
         del m32, m64
-    np.savez_compressed(os.path.join(mg.GOLD, "window_train.npz"), **out)
+    np.savez_compressed(path, **out)
 
 
 if __name__ == "__main__":

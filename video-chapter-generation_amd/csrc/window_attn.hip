@@ -391,7 +391,39 @@ __global__ void __launch_bounds__(kThreads) rowdot_kernel(const float* __restric
   if (lane == 0) out[o] = s + (bias ? bias[r] : 0.f);
 }
 
+// backward of rowdot (nn.Bilinear's second contraction, training): dx[b][i] = sum_r dy[b][r] U[b][r][i] and
+// dU[b][r][i] = dy[b][r] x[b][i]; one thread per (b, i): the r loop reads / writes U rows coalesced along i.
+__global__ void __launch_bounds__(kThreads) rowdot_bwd_kernel(const float* __restrict__ U, const float* __restrict__ x,
+                                                              const float* __restrict__ dy, float* __restrict__ dU,
+                                                              float* __restrict__ dx, int B, int R, int K) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= K) return;
+  const float xi = x[(long long)b * K + i];
+  const float* u = U + (long long)b * R * K + i;
+  float* du = dU + (long long)b * R * K + i;
+  const float* g = dy + (long long)b * R;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) {
+    const float gr = g[r];
+    if (dx) s = fmaf(gr, u[(long long)r * K], s);
+    du[(long long)r * K] = gr * xi;
+  }
+  if (dx) dx[(long long)b * K + i] = s;
+}
+
 }  // namespace
+
+VCG_API int vcg_rowdot_bwd(const float* U, const float* x, const float* dy, float* dU, float* dx, int B, int R, int K,
+                           hipStream_t s) {
+  VCG_REQUIRE(B >= 0 && R >= 1 && K >= 1, "bad shape");
+  if (B == 0) return VCG_OK;
+  VCG_REQUIRE(x && dy && dU && (U || !dx), "null operand");
+  hipLaunchKernelGGL(rowdot_bwd_kernel, dim3((unsigned)((K + kThreads - 1) / kThreads), (unsigned)B), dim3(kThreads), 0,
+                     s, U, x, dy, dU, dx, B, R, K);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
 
 VCG_API int vcg_mul_fwd(const float* a, const float* b, float* out, long long n, hipStream_t s) {
   VCG_REQUIRE(n >= 0 && n % 4 == 0, "n must be a multiple of 4");

@@ -13,10 +13,11 @@ Native scope: eval-mode forward of every head type: "mlp" (train_video_segment_u
 (head_attn.hip's SelfAttention kernel, output_size = hidden), "bilinear" (x2 A^T on the GEMM path + a row-dot
 kernel), "multiplication" (elementwise kernel).
 Training (model.train()): forward and backward of "mlp", "cross_attn" (train_video_segment_ddp.py:579's default),
-"self_attn" and "multiplication" through vcg_hip/wtrain.py (every op a libvcg_hip kernel pair: GEMMs, LayerNorm +
+"self_attn", "multiplication" and "bilinear" (wtrain.BilinearFn: vcg_rowdot_fwd / _bwd + GEMMs) through
+vcg_hip/wtrain.py (every op a libvcg_hip kernel pair: GEMMs, LayerNorm +
 activation + dropout, the short-window attention core, position encodings), the per-clip BERT / trunk passes
 through the native engines with the model's flat parameter / gradient buffers (TwoStream is the NativeRoot), and
-the reference's AdamW grouping on the fused optimizer. "bilinear" trains nowhere yet (raises). No CPU / eager path.
+the reference's AdamW grouping on the fused optimizer. No CPU / eager path.
 """
 import math
 
@@ -151,6 +152,23 @@ class ChapterHead(nn.Module):
         return self._xpacked
 
 
+class _ClipCountingHooks:
+    """Forwards a parameter group to the DDP hooks at its n-th report: the per-clip BERT / trunk backwards (any
+    order) each report every group once, and the shared gradients are final after the last of the n clips."""
+
+    def __init__(self, hooks, n):
+        self.hooks, self.n, self.seen = hooks, n, {}
+
+    def __call__(self, params):
+        if isinstance(params, str) or not params:
+            return
+        key = tuple(id(p) for p in params)
+        c = self.seen.get(key, 0) + 1
+        self.seen[key] = c
+        if c == self.n:
+            self.hooks(params)
+
+
 class TwoStream(NativeRoot, nn.Module):
     """two_stream_window.py:291-444. forward(img_clips [B, 2w+1, T, 3, H, W], text_ids [B, 2w+1, L],
     attention_masks [B, 2w+1, L], clip_info) -> (logits [B, 2], prob [B, 2]) of each window's middle clip."""
@@ -183,6 +201,13 @@ class TwoStream(NativeRoot, nn.Module):
         """AdamW with the reference's decay grouping (:355-388), as one fused kernel over the flat buffers."""
         return configure_adamw(self, train_config)
 
+    def set_grad_hooks(self, hooks):
+        """hooks(params) is called from the backward as parameter groups become final (DDP bucket all-reduce,
+        vcg_hip/ddp.py). BERT and the trunk run once per window clip and share their parameters, so a group is
+        final at its (2w+1)-th report (_ClipCountingHooks); the heads' gradients are reduced by the reducer's
+        finish()."""
+        object.__setattr__(self, "_vcg_hooks", hooks)
+
     def forward(self, img_clips, text_ids, attention_masks, clip_info=None):
         if self.training:
             return self._train_forward(img_clips, text_ids, attention_masks)
@@ -211,13 +236,15 @@ class TwoStream(NativeRoot, nn.Module):
         dev = img_clips.device
         anchor = self._anchor(dev)
         embs = []
+        hooks = getattr(self, "_vcg_hooks", None)
+        counted = _ClipCountingHooks(hooks, n_clips) if (hooks is not None and need_grad) else None
         for i in range(n_clips):
             if self.vision_model.training:
                 self._bump_bn_counters()  # every BatchNorm forward of the reference counts once per clip
             lang_emb, _ = BertFn.apply(text_ids[:, i, :].contiguous(), attention_masks[:, i, :].contiguous(), anchor,
-                                       BertEncoderEngine(self.lang_model, f, dt), need_grad, new_seed(), None)
+                                       BertEncoderEngine(self.lang_model, f, dt), need_grad, new_seed(), counted)
             img = rearrange(img_clips[:, i], "b t c h w -> (b t) c h w").float().contiguous()
-            vision_emb = TrunkFn.apply(img, anchor, ResNetTrunk(self.vision_model, dt), need_grad, None)
+            vision_emb = TrunkFn.apply(img, anchor, ResNetTrunk(self.vision_model, dt), need_grad, counted)
             embs.append(self.fusion_head(lang_emb, vision_emb.view(B, self.segment_size, -1), i))
         return self.window_attn(torch.stack(embs, 1).contiguous(), None)
 

@@ -5,25 +5,15 @@ for x viewed as [n_batch, n_segment, c, h, w] with fold = c // fold_div,
     out[:, t, :fold]        = x[:, t+1, :fold]        (zero at t = T-1)
     out[:, t, fold:2*fold]  = x[:, t-1, fold:2*fold]  (zero at t = 0)
     out[:, t, 2*fold:]      = x[:, t, 2*fold:]
-It runs as the `vcg_tsm_shift` HIP kernel (bit-exact gather; the backward is the adjoint shift).
+It runs as the `vcg::tsm_shift` torch.library op over the `vcg_tsm_shift` HIP kernel (bit-exact gather; the
+backward is the adjoint shift, the same op with direction 1).
 Inside the native ResNet trunk the shift is not materialised at all: it is fused into conv1's
 input gather (see vcg_hip/trunk.py), which is why `make_temporal_shift` only tags the convs.
 """
 import torch
 import torch.nn as nn
 
-from vcg_hip import ops as vops
-
-
-class _ShiftFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, n_segment, fold_div):
-        ctx.n_segment, ctx.fold_div = n_segment, fold_div
-        return vops.tsm_shift(x.contiguous(), n_segment, fold_div, direction=0)
-
-    @staticmethod
-    def backward(ctx, g):
-        return vops.tsm_shift(g.contiguous(), ctx.n_segment, ctx.fold_div, direction=1), None, None
+from vcg_hip import torch_ops  # noqa: F401  (registers torch.ops.vcg.*)
 
 
 class TemporalShift(nn.Module):
@@ -45,7 +35,7 @@ class TemporalShift(nn.Module):
             raise RuntimeError(f"TemporalShift: {nt} frames is not a multiple of n_segment={n_segment}")
         if x.dtype not in (torch.float32, torch.bfloat16):
             raise TypeError("TemporalShift: float32 / bfloat16 tensors only")
-        return _ShiftFn.apply(x, n_segment, fold_div)
+        return torch.ops.vcg.tsm_shift(x, n_segment, fold_div, 0)  # torch.library op (vcg_hip/torch_ops.py)
 
 
 class TemporalPool(nn.Module):

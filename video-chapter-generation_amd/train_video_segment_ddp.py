@@ -69,8 +69,8 @@ class DDPTrainer:
         self.optimizer.grad_scale = 1.0 / world_size
         broadcast_parameters(model)
         self.reducer = GradAllReducer(model.native_flat())
-        # the point model reports its gradients final block by block (buckets overlap the backward); the window model
-        # (its heads are autograd Functions) is reduced in one collective after the backward
+        # both models report their gradients final block by block (buckets overlap the backward); whatever no hook
+        # reported (the window model's heads) is reduced by finish()
         self.overlap = hasattr(model, "set_grad_hooks")
         if self.overlap:
             model.set_grad_hooks(self.reducer)

@@ -55,6 +55,7 @@ class GradAllReducer:
         self._side = None    # NativeComm: the side stream the collectives run on
         self.record = record
         self.log = []        # ("hook", lo, hi) / ("flush", lo, hi) in call order (record=True)
+        self._flushed = []   # [lo, hi) ranges reduced in this backward: finish() reduces the rest of the buffer
 
     # called by the engines (autograd backward thread) with parameters whose grads are final
     def __call__(self, params):
@@ -95,6 +96,7 @@ class GradAllReducer:
         if self._lo is None:
             return
         lo, hi = self._lo, min(self._hi, self.flat.total)
+        self._flushed.append((lo, hi))
         buf = self.flat.grad[lo:hi]
         if self.record:
             self.log.append(("flush", lo, hi))
@@ -125,11 +127,30 @@ class GradAllReducer:
                 self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         self._lo = self._hi = None
 
+    def _gaps(self):
+        """[lo, hi) ranges of the flat buffer no hook reported in this backward (parameters whose gradients are
+        produced outside the native engines' reports, e.g. the window model's heads), coalesced."""
+        out, pos = [], 0
+        for lo, hi in sorted(self._flushed):
+            if lo > pos:
+                out.append((pos, lo))
+            pos = max(pos, hi)
+        if pos < self.flat.total:
+            out.append((pos, self.flat.total))
+        return out
+
     def finish(self):
-        """Flush the last bucket and make the current stream wait for every collective."""
+        """Flush the last bucket, reduce every range no hook reported (so the whole gradient is always averaged,
+        as DDP does), and make the current stream wait for every collective."""
         if not self.enabled:
             return
         self._flush()
+        self._stream = torch.cuda.current_stream() if self.flat.grad.is_cuda else None
+        for lo, hi in self._gaps():
+            for b in range(lo, hi, self.bucket_elems):
+                self._lo, self._hi = b, min(hi, b + self.bucket_elems)
+                self._flush()
+        self._flushed = []
         for w in self._works:
             w.wait()
         self._works = []

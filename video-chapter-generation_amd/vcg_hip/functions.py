@@ -86,22 +86,8 @@ class HeadFn(torch.autograd.Function):
         return dlang, dvis, None, None, None, None
 
 
-class CrossEntropyFn(torch.autograd.Function):
-    """Mean cross-entropy (F.cross_entropy, train_video_segment_point.py:165) on the native kernels."""
-
-    @staticmethod
-    def forward(ctx, logits, labels):
-        logits = logits.contiguous()
-        labels = labels.to(torch.int64).contiguous()
-        loss = ops.cross_entropy_fwd(logits, labels)
-        ctx.save_for_backward(logits, labels)
-        return loss
-
-    @staticmethod
-    def backward(ctx, dloss):
-        logits, labels = ctx.saved_tensors
-        return ops.cross_entropy_bwd(logits, labels, dloss.contiguous()), None
-
-
 def cross_entropy(logits, labels):
-    return CrossEntropyFn.apply(logits, labels)
+    """Mean cross-entropy (F.cross_entropy, train_video_segment_point.py:165): the vcg::cross_entropy torch.library
+    op (vcg_hip/torch_ops.py) over vcg_cross_entropy_fwd / _bwd."""
+    from . import torch_ops  # noqa: F401  (registers torch.ops.vcg.*)
+    return torch.ops.vcg.cross_entropy(logits, labels.to(torch.int64))

@@ -1,0 +1,104 @@
+"""libvcg_hip entry points registered as torch.library custom ops (namespace `vcg`), the op surface SURVEY §8b
+names for the model/ and ops/ wrappers: each op has a schema, a fake (meta) implementation for shape inference /
+tracing, and, where the reference op is differentiable, an autograd formula that is itself a vcg op.
+
+    vcg::tsm_shift(x, n_segment, fold_div, direction)      TemporalShift.shift (ops/temporal_shift.py:33-51) and
+                                                           its adjoint (direction 1); ops/temporal_shift.py calls it
+    vcg::cross_entropy(logits, labels) / _bwd              F.cross_entropy (train_video_segment_point.py:165);
+                                                           vcg_hip.functions.cross_entropy calls it
+    vcg::window_frames_u8(frames, idx, bf16, cpad)         the frame ingest (gather + ToTensor + Normalize into the
+                                                           stem layout, youtube_dataset.py:180-190)
+    vcg::linear(x, weight, bias, act)                      nn.Linear (+ ReLU / GELU / tanh epilogue) on the GEMM engine
+
+The encoder engines (vcg_hip/trunk.py, bert.py) issue ~2000 launches per train step and call the C ABI through
+ctypes directly: a dispatcher round trip per launch (~5-10 us of host time) would make the step host-bound.
+"""
+from typing import Optional
+
+import torch
+
+from . import ops
+
+_DT = {False: torch.float32, True: torch.bfloat16}
+
+
+@torch.library.custom_op("vcg::tsm_shift", mutates_args=())
+def tsm_shift(x: torch.Tensor, n_segment: int, fold_div: int, direction: int) -> torch.Tensor:
+    if x.dim() != 4 or x.shape[0] % n_segment != 0:
+        raise RuntimeError(f"vcg::tsm_shift: x must be [n_batch*{n_segment}, C, H, W], got {tuple(x.shape)}")
+    return ops.tsm_shift(x.contiguous(), n_segment, fold_div, direction=direction)
+
+
+@tsm_shift.register_fake
+def _(x, n_segment, fold_div, direction):
+    return torch.empty_like(x)
+
+
+def _tsm_setup(ctx, inputs, output):
+    _, ctx.n_segment, ctx.fold_div, ctx.direction = inputs
+
+
+def _tsm_backward(ctx, g):
+    return torch.ops.vcg.tsm_shift(g, ctx.n_segment, ctx.fold_div, 1 - ctx.direction), None, None, None
+
+
+tsm_shift.register_autograd(_tsm_backward, setup_context=_tsm_setup)
+
+
+@torch.library.custom_op("vcg::cross_entropy_bwd", mutates_args=())
+def cross_entropy_bwd(logits: torch.Tensor, labels: torch.Tensor, dloss: torch.Tensor) -> torch.Tensor:
+    return ops.cross_entropy_bwd(logits.contiguous(), labels.to(torch.int64).contiguous(), dloss.contiguous())
+
+
+@cross_entropy_bwd.register_fake
+def _(logits, labels, dloss):
+    return torch.empty_like(logits)
+
+
+@torch.library.custom_op("vcg::cross_entropy", mutates_args=())
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    if logits.dim() != 2 or labels.shape != logits.shape[:1]:
+        raise RuntimeError("vcg::cross_entropy: logits [B, C] and labels [B]")
+    return ops.cross_entropy_fwd(logits.contiguous(), labels.to(torch.int64).contiguous())
+
+
+@cross_entropy.register_fake
+def _(logits, labels):
+    return logits.new_empty(())
+
+
+def _ce_setup(ctx, inputs, output):
+    ctx.save_for_backward(*inputs)
+
+
+def _ce_backward(ctx, dloss):
+    logits, labels = ctx.saved_tensors
+    return torch.ops.vcg.cross_entropy_bwd(logits, labels, dloss), None
+
+
+cross_entropy.register_autograd(_ce_backward, setup_context=_ce_setup)
+
+
+@torch.library.custom_op("vcg::window_frames_u8", mutates_args=())
+def window_frames_u8(frames: torch.Tensor, idx: torch.Tensor, bf16: bool, cpad: int) -> torch.Tensor:
+    return ops.window_frames_u8(frames, idx.contiguous(), _DT[bf16], cpad=cpad)
+
+
+@window_frames_u8.register_fake
+def _(frames, idx, bf16, cpad):
+    F, H, W, _ = frames.shape
+    return frames.new_empty((idx.numel(), H, W, cpad), dtype=_DT[bf16])
+
+
+@torch.library.custom_op("vcg::linear", mutates_args=())
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], act: int) -> torch.Tensor:
+    if x.dim() != 2 or weight.dim() != 2 or x.shape[1] != weight.shape[1] or x.dtype != weight.dtype:
+        raise RuntimeError("vcg::linear: x [M, K] and weight [N, K] of one dtype")
+    M, K = x.shape
+    N = weight.shape[0]
+    return ops.gemm(x.contiguous(), weight.contiguous(), M, N, K, K, K, bias=bias, act=act)
+
+
+@linear.register_fake
+def _(x, weight, bias, act):
+    return x.new_empty((x.shape[0], weight.shape[0]))

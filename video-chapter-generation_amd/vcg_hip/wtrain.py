@@ -100,6 +100,46 @@ class LinearFn(torch.autograd.Function):
         return dx, None, None, (g if ctx.needs_input_grad[3] else None)
 
 
+class BilinearFn(torch.autograd.Function):
+    """nn.Bilinear(x1 [B, I], x2 [B, J]) -> [B, O] (the "bilinear" window ChapterHead, two_stream_window.py:187-191,
+    269-273): U = x2 A^T (A = weight viewed [O*I][J]), y[b][o] = sum_i U[b][o*I + i] x1[b][i] + bias[o]
+    (vcg_rowdot_fwd). Backward: dU = dy (x) x1 and dx1 = sum_o dy U (vcg_rowdot_bwd), dx2 = dU A (GEMM),
+    dA += dU^T x2 (split-K GEMM), dbias += colsum(dy)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, bl):
+        O, I, J = bl.weight.shape
+        B = x1.shape[0]
+        x1, x2 = x1.contiguous(), x2.contiguous()
+        U = ops.gemm(x2, bl.weight.detach().reshape(O * I, J), B, O * I, J, J, J)
+        y = torch.empty((B, O), dtype=torch.float32, device=x1.device)
+        _lib.call("vcg_rowdot_fwd", P(U), P(x1), P(bl.bias), P(y), B, O, I, stream())
+        ctx.bl = bl
+        ctx.save_for_backward(x1, x2, U)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x1, x2, U = ctx.saved_tensors
+        bl = ctx.bl
+        O, I, J = bl.weight.shape
+        B = x1.shape[0]
+        dy = dy.contiguous()
+        dU = torch.empty_like(U)
+        dx1 = torch.empty_like(x1) if ctx.needs_input_grad[0] else None
+        _lib.call("vcg_rowdot_bwd", P(U), P(x1), P(dy), P(dU), P(dx1), B, O, I, stream())
+        gw = _grad(bl.weight)
+        if gw is not None:
+            ops.gemm_splitk(dU, x2, gw.view(O * I, J), O * I, J, B, O * I, J, transA=True, transB=True)
+        gb = _grad(bl.bias)
+        if gb is not None:
+            ops.colsum(dy, O, B, O, gb, accumulate=True)
+        dx2 = None
+        if ctx.needs_input_grad[1]:
+            dx2 = ops.gemm(dU, bl.weight.detach().reshape(O * I, J), B, J, O * I, O * I, J, transB=True)
+        return dx1, dx2, None
+
+
 class LNActDropFn(torch.autograd.Function):
     """Dropout(act(LayerNorm(x))) for x [rows, D]."""
 
@@ -344,7 +384,9 @@ def chapter_head(hd, lang_emb, vision_emb, i):
         return HeadAttnFn.apply(vision_out, lang_out, hd.head, B, T, h)
     if hd.head_type == "cross_attn":                                                               # :284-286
         return cross_attention(hd.head, lang_out, vision_out, B, T)
-    raise NotImplementedError(f"training with head_type {hd.head_type!r} is not native yet (inference is)")
+    if hd.head_type == "bilinear":                                                                 # :269-273
+        return chain(BilinearFn.apply(lang_out, vision_out.view(B, T * h), hd.bilinear_layers[i]), hd.head[i])
+    raise NotImplementedError(f"head_type {hd.head_type!r}")
 
 
 # ------------------------------------------------------------------------------------------------ window transformer
