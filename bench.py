@@ -175,10 +175,11 @@ def long_video_bench(args):
     frames, timestamps, subtitles = lv.synthetic_long_video(F, HW, HW, seed=123, device=dev)
     win, idx, ids, mask = lv.window_inputs(F, T, args.stride, subtitles, HashTokenizer(), L)
     idx, ids, mask = (torch.from_numpy(a).to(dev) for a in (idx, ids, mask))
-    lv.score_windows(model, frames, idx[:B], ids[:B], mask[:B], B)
+    K = args.scoring_streams
+    lv.score_windows(model, frames, idx[:B * max(2, K)], ids[:B * max(2, K)], mask[:B * max(2, K)], B, streams=K)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scores, labels = lv.score_windows(model, frames, idx, ids, mask, B)
+    scores, labels = lv.score_windows(model, frames, idx, ids, mask, B, streams=K)
     torch.cuda.synchronize()
     sec = time.perf_counter() - t0
     m = lv.boundary_metrics(labels.cpu().tolist(), timestamps, F, T, args.stride)
@@ -213,7 +214,8 @@ def long_video_bench(args):
         "higher_is_better": True, "dtype": args.precision,
         "data": "synthetic 1 fps video (seeded u8 frames in HBM, random-init weights)",
         "config": {"workload": f"{F} frames {HW}^2, T={T}, L={L}, stride {args.stride} s, batch {B}, "
-                               f"{args.bn}-stats BN", "bn": args.bn, "stride": args.stride,
+                               f"{args.bn}-stats BN" + (f", batches on {K} streams" if K > 1 else ""),
+                   "bn": args.bn, "stride": args.stride, "scoring_streams": K,
                    "frames": F, "clip_frame_num": T, "seq_len": L, "resolution": HW},
         "cpu_baseline": cpu,
         "roofline_step": {"bound": "hbm", "achieved": round(nbytes * n / sec / 1e9, 2), "peak": HBM_PEAK_GBS,
@@ -280,12 +282,17 @@ def main():
                          "ingest, end-to-end boundary metrics), 1 GPU")
     ap.add_argument("--video-frames", type=int, default=3600)
     ap.add_argument("--stride", type=int, default=1, help="long_video: window stride in s (the reference's own: 4)")
+    ap.add_argument("--scoring-streams", type=int, default=1,
+                    help="long_video: scoring batches round-robin over this many HIP streams (long_video.score_windows)")
     ap.add_argument("--bn", default="running", choices=["running", "batch"],
                     help="scoring modes (fwd / long_video): BN with running statistics (model.eval(), the trainer's "
                          "val and convert2vision_emb) or with the batch's statistics (test_video_segment_point.py:"
                          "116-122, which scores batches of 16 windows: pass --batch 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-roofline-step", action="store_true",
+                    help="skip the instrumented step after the timed region (profiling runs: the trace then ends with "
+                         "the timed steps); the line then has no dominant-kernel roofline")
     ap.add_argument("--launch-check", action="store_true",
                     help="rehearse the rank launch only (gloo, no GPU): every rank joins the process group and "
                          "rank 0 prints the line's n_gpus / rank layout")
@@ -413,7 +420,8 @@ def main():
     # (and the weight gradients / downsample convs / weight re-layout on the trunk's stream)
     model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = ResNetTrunk.prep_stream = False
     ops.timing_enable(True)
-    step()
+    if not args.no_roofline_step:
+        step()
     torch.cuda.synchronize()
     # the dominant kernel: the bf16 fast engine, or the generic engine (exact fp32 MFMA) in the parity precision
     dom_id, dom_name = ((ops.TIMING_FAST_GEMM, "igemm_fast_kernel") if args.precision == "bf16"

@@ -208,3 +208,22 @@ def test_c5_batch_stat_bn_vs_oracle():
         e = np.abs(pr[:, 1].numpy() - p32[sel]).max()
         print(f"C5 batch-stat fp32 native vs oracle, windows {b0}..{b0 + BS - 1}: max |dprob| {e:.2e}")
         assert e < 1e-3
+
+
+def test_score_windows_streams_identical():
+    """Batch-statistics scoring with the batches spread over 4 HIP streams gives bit-identical scores / labels to
+    one stream (each batch is still one forward over exactly its own windows)."""
+    import long_video as lv
+    from data.synthetic_dataset import HashTokenizer
+    from test_video_segment_point import drop_bn_running_stats
+    from vcg_hip.build import build_two_stream
+    F, T, HW, L = 80, 4, 112, 32
+    model = build_two_stream(clip_frame_num=T, seed=123, device=DEV, precision="bf16", dropout=0.0).eval()
+    drop_bn_running_stats(model)
+    frames, _, subtitles = lv.synthetic_long_video(F, HW, HW, chapter_every=12, seed=8, device=DEV)
+    win, idx, ids, mask = lv.window_inputs(F, T, 1, subtitles, HashTokenizer(), L)
+    args = [torch.from_numpy(a).to(DEV) for a in (idx, ids, mask)]
+    s1, l1 = lv.score_windows(model, frames, *args, batch_size=16, streams=1)
+    s4, l4 = lv.score_windows(model, frames, *args, batch_size=16, streams=4)
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s4) and torch.equal(l1, l4)

@@ -40,10 +40,20 @@ def main():
             pre = torch.empty(R, N, dtype=dt, device=dev)
             t = timeit(lambda: ops.gemm(A, W, R, N, K, K, K, bias=b, act=ops.ACT_GELU, aux=pre))
             line.append(f"gelu+aux {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
+            t = timeit(lambda: ops.gemm(A, W, R, N, K, K, K, bias=b, act=ops.ACT_GELU))
+            line.append(f"gelu {t:7.1f}us")
+            t = timeit(lambda: ops.gemm(A, W, R, N, K, K, K, bias=b, act=ops.ACT_RELU))
+            line.append(f"relu {t:7.1f}us")
         # input gradient: dA [R, K] = dY [R, N] @ W [N, K]
         dY = torch.randn(R, N, device=dev).to(dt)
         t = timeit(lambda: ops.gemm(dY, W, R, K, N, N, K, transB=True))
         line.append(f"dX transB {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
+        if name == "ffn2":  # the FFN2 input gradient carries the GELU derivative of the saved pre-activation
+            pre = torch.randn(R, K, device=dev).to(dt)
+            t = timeit(lambda: ops.gemm(dY, W, R, K, N, N, K, transB=True, act=ops.ACT_GELU_BWD, residual=pre, ldr=K))
+            line.append(f"dX transB+gelu' {t:7.1f}us")
+            t = timeit(lambda: ops.gemm(dY, ops.transpose(W), R, K, N, N, N, act=ops.ACT_GELU_BWD, residual=pre, ldr=K))
+            line.append(f"dX W^T+gelu' {t:7.1f}us")
         t = timeit(lambda: ops.gemm(dY, ops.transpose(W), R, K, N, N, N))
         line.append(f"dX W^T {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
         t = timeit(lambda: ops.transpose(W))

@@ -73,24 +73,39 @@ def window_inputs(n_frames, clip_frame_num, stride, subtitles, tokenizer, max_te
 
 
 @torch.no_grad()
-def score_windows(model, frames_u8, idx, ids, mask, batch_size, export=None):
+def score_windows(model, frames_u8, idx, ids, mask, batch_size, export=None, streams=1):
     """GPU part: per batch, frame gather + normalisation (ops.window_frames_u8) and the TwoStream forward.
     idx / ids / mask are device tensors. Returns (pred_score f32 [n], pred_label i64 [n]) on the device.
-    export(b0, vision_emb [b, T, 2048]) is called per batch when given."""
+    export(b0, vision_emb [b, T, 2048]) is called per batch when given.
+    streams > 1: consecutive batches go round-robin to that many HIP streams, so the small batches of the
+    batch-statistics mode (16 windows: BN couples only the windows of one batch) run concurrently; every batch is
+    still one forward over exactly its own windows, so the results are those of streams = 1."""
     from vcg_hip import ops
     dt = model.compute_dtype()
     n = idx.shape[0]
-    scores = torch.empty(n, dtype=torch.float32, device=frames_u8.device)
-    labels = torch.empty(n, dtype=torch.int64, device=frames_u8.device)
-    for b0 in range(0, n, batch_size):
+    dev = frames_u8.device
+    scores = torch.empty(n, dtype=torch.float32, device=dev)
+    labels = torch.empty(n, dtype=torch.int64, device=dev)
+    main = torch.cuda.current_stream(dev)
+    pool = [main] if streams <= 1 or export is not None else [torch.cuda.Stream(device=dev) for _ in range(streams)]
+    for k, b0 in enumerate(range(0, n, batch_size)):
         b1 = min(n, b0 + batch_size)
-        fr = ops.window_frames_u8(frames_u8, idx[b0:b1].contiguous(), dt, cpad=ops.stem_cpad(dt))
-        out = model.forward_staged(fr, ids[b0:b1], mask[b0:b1], return_emb=export is not None)
-        logits, prob = out[0], out[1]
-        scores[b0:b1] = prob[:, 1]
-        labels[b0:b1] = logits.argmax(1)
+        if k == 1 and len(pool) > 1:
+            # batch 0 ran on the caller's stream: whatever the first forward prepares once (the bf16 weight shadow /
+            # GEMM layouts / folded weights) is ordered before every stream's batches
+            for s in pool:
+                s.wait_stream(main)
+        with torch.cuda.stream(main if k == 0 else pool[k % len(pool)]):
+            fr = ops.window_frames_u8(frames_u8, idx[b0:b1].contiguous(), dt, cpad=ops.stem_cpad(dt))
+            out = model.forward_staged(fr, ids[b0:b1], mask[b0:b1], return_emb=export is not None)
+            logits, prob = out[0], out[1]
+            scores[b0:b1] = prob[:, 1]
+            labels[b0:b1] = logits.argmax(1)
         if export is not None:
             export(b0, out[2])
+    for s in pool:
+        if s is not main:
+            main.wait_stream(s)
     return scores, labels
 
 
