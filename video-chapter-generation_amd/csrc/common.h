@@ -139,6 +139,23 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
   return cdf + x * pdf;
 }
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, ~1 fp32 ulp of 1): branch-free, one v_rcp_f32 and one
+// v_exp_f32 instead of the library erff's piecewise polynomials. Used by the bf16 GEMM epilogues (the output is
+// rounded to bf16, 2^-8); the fp32 parity mode keeps erff.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
+  float y = fmaf(t, 1.061405429f, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  return copysignf(1.f - y * t * __expf(-ax * ax), x);
+}
+__device__ __forceinline__ float gelu_erf_fast(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad_fast(float x) {
+  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f));
+  return fmaf(x * 0.39894228040143268f, __expf(-0.5f * x * x), cdf);
+}
 
 // Counter-based hash (splitmix64 finaliser), shared by dropout and the synthetic generator.
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {

@@ -97,6 +97,7 @@ struct GemmParams {
   long long a_so, a_si, b_so, b_si, c_so, c_si;
   int stage_kt;  // fast kernel: stage the output tile through LDS when the tile has <= stage_kt k-steps
   int res_round; // residual epilogue: round alpha*AB + bias to bf16 before adding the residual (VCG_ACT_FLAG_ROUND_PRE)
+  int fast_act;  // bf16 epilogues: GELU / GELU' through erf_fast (common.h) instead of erff (VCG_FAST_GELU=0: off)
   BwdEpi bwd;    // EPI_BWD
   // the consuming conv applies its input's BatchNorm + ReLU on load: x -> bf16(max(fma(x, in_sc[c], in_sh[c]), 0))
   // (vcg_bn_apply's arithmetic) for input channel c, in LDS right after the tile's DMA lands (fast dense A of
@@ -127,9 +128,9 @@ template <typename T> __device__ __forceinline__ void store4(T* p, const float (
   }
 }
 
-__device__ __forceinline__ float apply_act(float v, int act) {
+__device__ __forceinline__ float apply_act(float v, int act, bool fast = false) {
   if (act == ACT_RELU) return fmaxf(v, 0.f);
-  if (act == ACT_GELU) return gelu_erf(v);
+  if (act == ACT_GELU) return fast ? gelu_erf_fast(v) : gelu_erf(v);
   if (act == ACT_TANH) return tanhf(v);
   return v;
 }
@@ -197,7 +198,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
         load4<T>(Res + (long long)m * p.ldr + n, rv);
         if (p.act == ACT_GELU_BWD) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] *= gelu_erf_grad(rv[r]);
+          for (int r = 0; r < 4; ++r) v[r] *= (sizeof(T) == 2 && p.fast_act) ? gelu_erf_grad_fast(rv[r]) : gelu_erf_grad(rv[r]);
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += rv[r];
@@ -206,7 +207,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
       if (p.aux) store4<T>(reinterpret_cast<T*>(p.aux) + (long long)m * p.ldc + n, v);
       if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act, sizeof(T) == 2 && p.fast_act);
       }
       if constexpr (EPI == EPI_STATS) {
 #pragma unroll

@@ -409,8 +409,18 @@ static FILE* gemm_log() {
   return f;
 }
 
+static bool fast_gelu_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VCG_FAST_GELU");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 template <typename T, int AM, int BMD>
 static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
+  p.fast_act = sizeof(T) == 2 && fast_gelu_enabled();
   if (FILE* f = gemm_log()) {
     const bool fast = sizeof(T) == 2 && is_kcontig(AM) && BMD == OP_DENSE_K && fast_gemm_enabled() &&
                       epi != EPI_SPLITK && (splits == 1 || p.batch_inner > 0) && p.K % 8 == 0 &&

@@ -301,7 +301,7 @@ __device__ __forceinline__ void epilogue_staged(f32x4 (&acc)[4][BN / 32], const 
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float t = acc[i][j][r] * p.alpha + bv[j][r];
-            if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) t = apply_act(t, p.act);
+            if (p.act != ACT_NONE && p.act != ACT_GELU_BWD) t = apply_act(t, p.act, p.fast_act);
             v[r] = t;
           }
           stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
@@ -329,7 +329,7 @@ __device__ __forceinline__ void epilogue_staged_aux(f32x4 (&acc)[4][BN / 32], co
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float t = acc[i][j][r] * p.alpha + bv[j][r];
-          v[r] = pass == 0 ? t : apply_act(t, p.act);
+          v[r] = pass == 0 ? t : apply_act(t, p.act, p.fast_act);
         }
         stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
       }
