@@ -508,6 +508,8 @@ DGRAD_BWD_CASES = [
     (16, 28, 28, 128, 128, 3, 2, 1, 4),  # same, several tiles per class
     (8, 7, 7, 64, 256, 1, 1, 0, 4),    # conv3 / conv1 1x1 (dense)
     (8, 6, 6, 128, 64, 1, 1, 0, 8),    # wider C: BN = 128 tiles
+    (8, 7, 9, 256, 128, 1, 1, 0, 4),   # 1x1, K = 128 (streaming kernel, 3-deep ring), M = 504: a ragged last tile
+    (4, 14, 14, 512, 64, 1, 1, 0, 4),  # 1x1, K = 64, 8 column tiles (streaming kernel, 4-deep ring), fold 64
 ]
 
 
@@ -579,6 +581,46 @@ def test_conv_dgrad_bwd(K, case, mode):
         assert (sgx2.double() - sx2).abs().max().item() <= tol(sx2)
         assert (dgam2.double() - 0.5 - sx2).abs().max().item() <= tol(sx2)
         assert (dbet2.double() - 0.25 - sg).abs().max().item() <= tol(sg)
+
+
+# the trunk's conv1 input gradients that the streaming EPI_BWD kernel takes (layers 1-2 at 16 frames):
+# (N, H, W, C, Cout, T, res_stride)
+STREAM_CASES = [(16, 56, 56, 256, 64, 8, 1), (16, 28, 28, 512, 128, 8, 1), (16, 56, 56, 256, 128, 8, 2)]
+
+
+@pytest.mark.parametrize("case", STREAM_CASES)
+@pytest.mark.parametrize("y2", [False, True])
+def test_conv_dgrad_bwd_stream_vs_persistent(K, case, y2, monkeypatch):
+    """The streaming fused 1x1 dgrad (EPI_BWD_STREAM: A rows and residual / y / mask operands DMA'd into an LDS ring
+    tiles ahead) against the persistent engine's EPI_BWD (VCG_BWD_STREAM=0) at the trunk's shapes: g bit for bit,
+    the BN sums to float rounding (different tilings sum in different orders)."""
+    N, H, W, C, Cout, T, rs = case
+    dtype = torch.bfloat16
+    fold = C // 8
+    dy = _rand((N, H, W, Cout), dtype, 71).to(DEV)
+    wt = K.weight_prep(_rand((Cout, C, 1, 1), torch.float32, 72, 0.1).to(DEV), C, dtype, transposed=True)
+    y = _rand((N, H, W, C), dtype, 73).to(DEV)
+    y2t = _rand((N, H, W, C), dtype, 74).to(DEV) if y2 else None
+    res = _rand((N, (H + 1) // 2, (W + 1) // 2, C) if rs == 2 else (N, H, W, C), dtype, 75).to(DEV)
+    _, bits = K.bn_apply(_rand((N, H, W, C), dtype, 76).to(DEV), torch.ones(C, device=DEV),
+                         torch.zeros(C, device=DEV), C, relu=True, bits=True)
+    g0 = torch.Generator().manual_seed(77)
+    mean, inv = (torch.randn(C, generator=g0) * 0.1).to(DEV), (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    mean2, inv2 = (torch.randn(C, generator=g0) * 0.1).to(DEV), (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("VCG_BWD_STREAM", flag)
+        sums, sgx2 = torch.zeros((2, C), device=DEV), torch.zeros(C, device=DEV)
+        kw = dict(y2=y2t, mean2=mean2, invstd2=inv2, sum_gx2=sgx2) if y2 else {}
+        g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, 1, 1, 1, 0, tsm_T=T, tsm_fold=fold, res=res, res_stride=rs,
+                             bits=bits, y=y, mean=mean, invstd=inv, sums=sums, **kw)
+        assert g is not None
+        torch.cuda.synchronize()
+        outs.append((g.clone(), sums.clone(), sgx2.clone()))
+    (ga, sa, xa), (gb, sb, xb) = outs
+    assert torch.equal(ga, gb), f"g differs: max {(ga.float() - gb.float()).abs().max().item():.3e}"
+    for a, b in ((sa, sb), (xa, xb)):
+        assert (a.double() - b.double()).abs().max().item() <= 1e-4 * (b.abs().max().item() + 1.0)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)

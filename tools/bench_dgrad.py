@@ -12,18 +12,21 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from vcg_hip import _lib, ops  # noqa: E402
 
 _lib.call("vcg_init", 0)
+NOTSM = os.environ.get("VCG_BENCH_NOTSM") == "1"
 dev, bf = "cuda", torch.bfloat16
-SHAPES = [  # (name, N, H, W, C (dx channels), Cout (dy channels), T)
-    ("l1 conv1 dgrad", 1024, 56, 56, 256, 64, 16),
-    ("l2 conv1 dgrad", 1024, 28, 28, 512, 128, 16),
-    ("l3 conv1 dgrad", 1024, 14, 14, 1024, 256, 16),
+SHAPES = [  # (name, N, H, W, C (dx channels), Cout (dy channels), T, residual stride)
+    ("l1 conv1 dgrad", 1024, 56, 56, 256, 64, 16, 1),
+    ("l2 b0 conv1 dgrad", 1024, 56, 56, 256, 128, 16, 2),
+    ("l2 conv1 dgrad", 1024, 28, 28, 512, 128, 16, 1),
+    ("l3 conv1 dgrad", 1024, 14, 14, 1024, 256, 16, 1),
 ]
 
 
-def run(name, N, H, W, C, Co, T):
+def run(name, N, H, W, C, Co, T, rs=1):
     dy = torch.randn(N, H, W, Co, device=dev).to(bf)
     wt = ops.weight_prep((torch.randn(Co, C, 1, 1, device=dev) * 0.05), C, bf, transposed=True)
-    res = torch.randn(N, H, W, C, device=dev).to(bf)
+    res = torch.randn(N, (H + 1) // rs, (W + 1) // rs, C, device=dev).to(bf) if rs == 2 else \
+        torch.randn(N, H, W, C, device=dev).to(bf)
     y = torch.randn(N, H, W, C, device=dev).to(bf)
     _, bits = ops.bn_apply(y, torch.ones(C, device=dev), torch.zeros(C, device=dev), C, relu=True, bits=True)
     mean, inv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
@@ -33,7 +36,7 @@ def run(name, N, H, W, C, Co, T):
     wsb = ops.ws(_lib.query("vcg_conv_dgrad_bwd_ws_bytes", C, Co, 1, 1), dev)
 
     def f():
-        ops.conv_dgrad_bwd(dy, wt, N, H, W, C, Co, 1, 1, 1, 0, tsm_T=T, tsm_fold=C // 8, res=res, bits=bits, y=y,
+        ops.conv_dgrad_bwd(dy, wt, N, H, W, C, Co, 1, 1, 1, 0, tsm_T=T, tsm_fold=0 if NOTSM else C // 8, res=res, res_stride=rs, bits=bits, y=y,
                            mean=mean, invstd=inv, sums=sums, dgamma=dg, dbeta=db, out=out, workspace=wsb)
     for _ in range(3):
         f()
@@ -46,7 +49,7 @@ def run(name, N, H, W, C, Co, T):
     torch.cuda.synchronize()
     us = a.elapsed_time(b) / 10 * 1e3
     M = N * H * W
-    gb = (M * Co + 4 * M * C) * 2 / 1e9 + M * C / 8 / 1e9  # dy + res + y + g (read/write) + bits
+    gb = (M * Co + (2 + (0.25 if rs == 2 else 1)) * M * C) * 2 / 1e9 + M * C / 8 / 1e9  # dy + y + g + res + bits
     line = f"{name:16s} M={M} N={C} K={Co}: {us:8.1f} us  {gb / us * 1e3:6.2f} TB/s algorithmic"
     buf = (ctypes.c_ulonglong * 256)()
     if _lib.query("vcg_fast_stamps", ctypes.addressof(buf), 256) == 0:
@@ -63,5 +66,13 @@ def run(name, N, H, W, C, Co, T):
     print(line, flush=True)
 
 
-for s in SHAPES:
-    run(*s)
+# argv: [name prefix] [flags "10" / "1" / "0"]; VCG_BENCH_NOTSM=1: no TSM adjoint (A/B of the access pattern)
+sel = sys.argv[1] if len(sys.argv) > 1 else ""
+flags = sys.argv[2] if len(sys.argv) > 2 else "10"
+for s in SHAPES:  # the streaming kernel (EPI_BWD_STREAM, K <= 128) and the persistent engine, same process
+    if not s[0].startswith(sel):
+        continue
+    for flag in flags:
+        os.environ["VCG_BWD_STREAM"] = flag
+        print(f"VCG_BWD_STREAM={flag} ", end="")
+        run(*s)

@@ -9,7 +9,11 @@ enum { OP_DENSE_K = 0, OP_IM2COL = 1, OP_DGRAD = 2, OP_DENSE_MN = 3, OP_IM2COL_T
 // recomputed from y, BN sums): fewer live registers, so the 64-column kernel fits 3 workgroups per CU
 // EPI_STORE_AUX (fast kernel): EPI_STORE whose pre-activation copy `aux` (the GELU input the backward needs) also
 // goes out through the LDS stage, in a round of its own
-enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 4, EPI_STORE_AUX = 5 };
+// EPI_BWD_STREAM (fast kernel): EPI_BWD of a 1x1 conv input gradient with K <= 128 (the conv1 dgrads of layers 1-2,
+// where the epilogue's residual / y / mask operands are 4-6x the A operand): 64 x 64 tiles whose A rows AND epilogue
+// operands are DMA'd into an LDS ring several tiles ahead (igemm_fast.hip bwd_stream_body)
+enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 4, EPI_STORE_AUX = 5,
+       EPI_BWD_STREAM = 6 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
 enum { ACT_FLAG_ROUND_PRE = 0x100 };  // = VCG_ACT_FLAG_ROUND_PRE (include/vcg_hip.h)
 

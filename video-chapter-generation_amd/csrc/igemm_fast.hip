@@ -687,6 +687,7 @@ __device__ __forceinline__ void stats_finish(const GemmParams& p, float* scratch
   }
 }
 
+
 // Profiling build (make EXTRA=-DVCG_FAST_STAMPS OUT=... OBJDIR=...): s_memtime per tile phase of workgroup 0,
 // wave 0 of every igemm_fast launch (the last launch's survive): tile's first k-step, after its last MFMAs,
 // after the output staging, after the epilogue flush. vcg_fast_stamps() copies them out.
@@ -700,9 +701,297 @@ __device__ unsigned long long g_fast_stamps[64 * 4];
 #define FAST_STAMP(t, k) do {} while (0)
 #endif
 
+// ---- EPI_BWD_STREAM: the fused 1x1 conv input gradient (EPI_BWD) with K <= 128, as a streaming kernel ----------
+// For the trunk's conv1 dgrads of layers 1-2 (K = 64 / 128 input channels of dy) the GEMM is a small part of the
+// work: per 64 x 64 output tile the A rows are 8-16 KB, the epilogue reads the residual, y (the previous block's
+// bn3 input) and the mask bits (16.5 KB, + 8 KB y2 after a downsample block) and writes 8 KB of g. The persistent
+// 2-stage engine above issues those epilogue loads only after a tile's MFMAs (two dependent HBM round trips per
+// tile: 3.6-4.3 TB/s). Here every operand of a tile is DMA'd into an LDS ring NBUF - 1 tiles ahead; the weight
+// tile (64 columns x K) stays in LDS for the whole kernel.
+// Tiles are DESTINATION rows d of g: the TSM adjoint moves the dgrad value of GEMM row m to d = m + s hw for the
+// columns of shift s (+1: n < fold, -1: fold <= n < 2 fold, 0: the rest), so d's value is the product of the A row
+// d - s hw (zero when that frame is outside the clip -- the wrap row of the adjoint -- and the clip-edge rows are
+// never read, i.e. dropped). The shift is applied to the A rows (a wave's 32 columns have one shift: fold % 32 == 0;
+// a workgroup whose 64 columns straddle two shifts loads two A tiles), so the residual / y / mask / g rows of a tile
+// are plain contiguous rows (full 128-B lines; moving them instead costs 35 % at the layer-1 shape).
+// Per tile: counted vmcnt (the ring's later tiles and the previous flushes' stores stay in flight), one barrier,
+// MFMAs of a 16 x 32 block per wave, the bf16 value staged through LDS, one barrier, then each thread combines one
+// 16-B chunk of stage + LDS operands and stores it. Same products, order and rounding as stage_flush_bwd
+// (bit-identical g; per-thread column sums combined in a fixed order by bwd_finish).
+constexpr int XF_HASY = 1;  // y + mask bits present (the BN sums of the previous block's bn3)
+constexpr int XF_Y2 = 2;    // y2 present (the previous block's downsample BN)
+
+__device__ __forceinline__ int bwd_tsm_shift(const BwdEpi& e, int n) {
+  if (e.tsm_T <= 0) return 0;
+  return n < e.tsm_fold ? 1 : (n < 2 * e.tsm_fold ? -1 : 0);
+}
+
+// LDS bytes of one ring slot / of the fixed part (weights, stage, column parameters) and the ring depth
+__host__ __device__ constexpr int bwd_stream_buf(int KC, int XF) {
+  return 2 * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 + 8 * 256 : 0) + ((XF & XF_Y2) ? 8192 : 0);
+}
+__host__ __device__ constexpr int bwd_stream_nbuf(int KC, int XF) {
+  return (160 * 1024 - (KC * 8192 + 8192 + 1024)) / bwd_stream_buf(KC, XF) >= 4 ? 4
+         : (160 * 1024 - (KC * 8192 + 8192 + 1024)) / bwd_stream_buf(KC, XF);
+}
+
+template <int KC, int XF>
+__device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
+  constexpr bool HASY = (XF & XF_HASY) != 0, Y2 = (XF & XF_Y2) != 0;
+  static_assert(!Y2 || HASY, "y2 comes with y");
+  constexpr int TM = 64, TN = 64, NTH = 512, NW = 8;
+  constexpr int NBUF = bwd_stream_nbuf(KC, XF);
+  static_assert(NBUF >= 2, "LDS ring");
+  constexpr int AT = KC * TM * 64 * 2;  // one A tile ([64][64] swizzled sub-tiles, fast_frag layout); two per slot
+  constexpr int OB = TM * TN * 2;       // one row-major [64][64] bf16 epilogue operand (res / y / y2)
+  constexpr int OFF_R = 2 * AT, OFF_Y = OFF_R + OB, OFF_BITS = OFF_Y + (HASY ? OB : 0);
+  constexpr int OFF_Y2 = OFF_BITS + (HASY ? NW * 256 : 0);  // mask bytes [64][8]: 16 lanes x 4 B per wave (+ pad)
+  constexpr int BUF = OFF_Y2 + (Y2 ? OB : 0);
+  static_assert(BUF == bwd_stream_buf(KC, XF), "slot layout");
+  constexpr int BB = KC * TN * 64 * 2;
+  constexpr int SB = TM * TN * 2;
+  constexpr int TOTAL = NBUF * BUF + BB + SB + 4 * TN * 4;
+  static_assert(TOTAL <= 160 * 1024, "LDS budget");
+  static_assert(NBUF * BUF >= 3 * NTH * 8 * 4, "bwd_finish scratch");
+  // VMEM instructions per wave: one tile's DMA (A 1 per k tile and A tile, res 1, y 1 + bits 1, y2 1), one flush's
+  // stores (1)
+  constexpr int OPS1 = KC + 1 + (HASY ? 2 : 0) + (Y2 ? 1 : 0), OPS2 = OPS1 + KC;
+  constexpr int VMW1 = (NBUF - 2) * OPS1 + (NBUF - 1), VMW2 = (NBUF - 2) * OPS2 + (NBUF - 1);
+  static_assert(VMW2 < 64, "vmcnt field");
+  __shared__ __attribute__((aligned(1024))) char smem[TOTAL];  // the ONLY LDS object (see FastLoader)
+  char* ring = smem;
+  bf16_t* Bs = reinterpret_cast<bf16_t*>(smem + NBUF * BUF);
+  bf16_t* St = reinterpret_cast<bf16_t*>(smem + NBUF * BUF + BB);
+  float* cpar = reinterpret_cast<float*>(smem + NBUF * BUF + BB + SB);  // mean | mean2 | invstd | invstd2 [TN]
+
+  const BwdEpi& e = p.bwd;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nx = p.N / TN, gy = gridDim.x / nx;
+  int bx, by;
+  if ((gy & 7) == 0) {  // every column tile of an M-tile row on one XCD (the A rows come from HBM once)
+    const int sidx = blockIdx.x >> 3;
+    bx = sidx % nx;
+    by = (sidx / nx) * 8 + (blockIdx.x & 7);
+  } else {
+    bx = blockIdx.x % nx;
+    by = blockIdx.x / nx;
+  }
+  const int n0 = bx * TN;
+  const int mtiles = (p.M + TM - 1) / TM;
+  const int my_tiles = by < mtiles ? (mtiles - 1 - by) / gy + 1 : 0;
+  if (my_tiles == 0) {  // no rows: an all-zero partial slot
+    if (e.nred > 0 && tid < TN)
+      for (int r = 0; r < e.nred; ++r) e.part[((long long)by * e.nred + r) * p.N + n0 + tid] = 0.f;
+    return;
+  }
+  if (tid < TN) {
+    const int n = n0 + tid;
+    cpar[tid] = e.mean ? e.mean[n] : 0.f;
+    cpar[TN + tid] = e.mean2 ? e.mean2[n] : 0.f;
+    cpar[2 * TN + tid] = e.invstd ? e.invstd[n] : 0.f;
+    cpar[3 * TN + tid] = e.invstd2 ? e.invstd2[n] : 0.f;
+  }
+  __syncthreads();  // (no LDS-DMA issued yet)
+  const int cc = tid & 7;  // the flush's 16-B column chunk of this thread (fixed for the whole kernel)
+  float mu[8], mu2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = cpar[8 * cc + i];
+    mu2[i] = cpar[TN + 8 * cc + i];
+  }
+  // TSM shifts of the workgroup's two 32-column halves; two A tiles when they differ
+  const int sh0 = bwd_tsm_shift(e, n0), sh1 = bwd_tsm_shift(e, n0 + 32);
+  const bool two = sh0 != sh1;
+
+  // buffer descriptors of the epilogue operands (offset beyond num_records -> zeros)
+  const long long ld = p.ldc;
+  const uint32_t nb_full = (uint32_t)min((long long)p.M * ld * 2, (long long)0xFFFFFF00LL);
+  const long long rrows = e.res_s > 1 ? (long long)(p.M / e.hw) * e.rH * e.rW : (long long)p.M;
+  const uint32_t nb_res = (uint32_t)min(rrows * ld * 2, (long long)0xFFFFFF00LL);
+  const __amdgpu_buffer_rsrc_t rs_res = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.res), 0, nb_res, 0x00020000);
+  __amdgpu_buffer_rsrc_t rs_y = rs_res, rs_y2 = rs_res, rs_bits = rs_res;
+  uint32_t nb_bits = 0;
+  if constexpr (HASY) {
+    rs_y = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.y), 0, nb_full, 0x00020000);
+    nb_bits = (uint32_t)(((long long)p.M * ld) >> 3);
+    rs_bits = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(e.bits), 0, nb_bits, 0x00020000);
+  }
+  if constexpr (Y2) rs_y2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.y2), 0, nb_full, 0x00020000);
+
+  FastLoader<64, OP_DENSE_K, NW> la, lb;
+  lb.init(p.b, 0, n0, wave, lane);
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) lb.issue(p.b, kc * 64, p.K, Bs + kc * 4096, wave);
+
+  auto issue_tile = [&](int t) {
+    const int d0 = (by + t * gy) * TM;
+    char* buf = ring + (t % NBUF) * BUF;
+    // A rows of the shift(s): destination row d reads GEMM row d - s hw, zero outside the clip
+    la.init(p.a, 0, d0, wave, lane);
+    const int d = d0 + wave * 8 + (lane >> 3);  // FastLoader<64, dense, 8 waves>: one row per lane
+    int f = 0, tt = 0;
+    if (e.tsm_T > 0 && (sh0 | sh1) != 0) {
+      f = (int)fdiv((uint32_t)min(d, p.M - 1), e.fd_hw);
+      tt = f - (int)fdiv((uint32_t)f, e.fd_T) * e.tsm_T;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      if (a == 1 && !two) break;
+      const int s = a == 0 ? sh0 : sh1;
+      const bool ok = d < p.M && (unsigned)(tt - s) < (unsigned)max(e.tsm_T, 1);
+      la.off[0] = ok ? (int)((long long)(d - s * e.hw) * p.a.ld) : -1;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+        la.issue(p.a, kc * 64, p.K, reinterpret_cast<bf16_t*>(buf + a * AT) + kc * 4096, wave);
+    }
+    // residual / y / y2 rows: this wave's instruction covers tile rows 8 wave .. + 7, lane -> (row, chunk)
+    {
+      const int r = wave * 8 + (lane >> 3);
+      const int dr = d0 + r, n = n0 + 8 * (lane & 7);
+      const bool ok = dr < p.M;
+      uint32_t roff = (uint32_t)((long long)dr * ld + n) * 2u;
+      if (e.res_s > 1) {  // compact residual of a 1x1 / stride-2 conv: only even (h, w) rows carry one
+        const uint32_t f2 = fdiv((uint32_t)dr, e.fd_hw), rr = (uint32_t)dr - f2 * (uint32_t)e.hw;
+        const uint32_t h = fdiv(rr, e.fd_w), w = rr - h * e.fd_w.d;
+        roff = ((h | w) & 1u) ? nb_res : (uint32_t)((((long long)(f2 * e.rH + (h >> 1)) * e.rW + (w >> 1)) * ld + n) * 2);
+      }
+      const uint32_t yoff = (uint32_t)((long long)dr * ld + n) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_res, (lds_void_t*)(buf + OFF_R + wave * 1024), 16, ok ? roff : nb_res,
+                                               0, 0, 0);
+      if constexpr (HASY)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_y, (lds_void_t*)(buf + OFF_Y + wave * 1024), 16, ok ? yoff : nb_full,
+                                                 0, 0, 0);
+      if constexpr (Y2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_y2, (lds_void_t*)(buf + OFF_Y2 + wave * 1024), 16,
+                                                 ok ? yoff : nb_full, 0, 0, 0);
+    }
+    if constexpr (HASY) {  // mask bytes: lane < 16 -> row 8 wave + lane / 2, 32 columns (dword lane & 1)
+      const int dr = d0 + 8 * wave + ((lane & 15) >> 1), n = n0 + 32 * (lane & 1);
+      const bool ok = lane < 16 && dr < p.M;
+      const uint32_t boff = (uint32_t)(((long long)dr * ld + n) >> 3);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_bits, (lds_void_t*)(buf + OFF_BITS + wave * 256), 4,
+                                               ok ? boff : nb_bits, 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < my_tiles) issue_tile(i);
+
+  float s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s1[i] = s2[i] = s3[i] = 0.f;
+  bf16_t* Cout = reinterpret_cast<bf16_t*>(p.C);
+  const int g = lane >> 4, ci = lane & 15;
+  const int wr = wave & 3, wc = wave >> 2;  // MFMA block: rows 16 wr .. + 15, columns 32 wc .. + 31 of the tile
+
+  for (int t = 0; t < my_tiles; ++t) {
+    FAST_STAMP(t, 0);
+    // tile t has landed once only the ring's later tiles (NBUF - 2) and the stores of the NBUF - 1 flushes since
+    // its DMA are outstanding (steady state); the first / last tiles wait for everything
+    if (t >= NBUF - 1 && t + NBUF - 2 < my_tiles) {
+      if (two) __builtin_amdgcn_s_waitcnt(waitcnt_vm(VMW2));
+      else __builtin_amdgcn_s_waitcnt(waitcnt_vm(VMW1));
+    } else {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    }
+    __builtin_amdgcn_s_barrier();  // tile t visible to every wave; every wave's reads of the ring slot below retired
+    FAST_STAMP(t, 1);
+    if (t + NBUF - 1 < my_tiles) issue_tile(t + NBUF - 1);
+    const int d0 = (by + t * gy) * TM;
+    const char* buf = ring + (t % NBUF) * BUF;
+    const bf16_t* At = reinterpret_cast<const bf16_t*>(buf + ((two && wc == 1) ? AT : 0));
+    f32x4 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 af = fast_frag(At + kc * 4096, 16 * wr, lane, s);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fast_frag(Bs + kc * 4096, 32 * wc + 16 * j, lane, s), af,
+                                                           acc[j], 0, 0, 0);
+      }
+    // stage the bf16 GEMM value: row 16 wr + ci, columns 32 wc + 16 j + 4 g .. + 3
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = 16 * wr + ci, col = 32 * wc + 16 * j + 4 * g;
+      uint2 q2;
+      q2.x = (uint32_t)f2bf(acc[j][0]) | ((uint32_t)f2bf(acc[j][1]) << 16);
+      q2.y = (uint32_t)f2bf(acc[j][2]) | ((uint32_t)f2bf(acc[j][3]) << 16);
+      // (inline asm: a plain LDS store makes hipcc wait vmcnt(0) for the ring's in-flight DMA first)
+      asm volatile("ds_write_b64 %0, %1" ::"v"(lds_u32(St + row * 64 + 8 * st_slot<64>(row, col >> 3) + (col & 7))),
+                   "v"(q2) : "memory");
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    FAST_STAMP(t, 2);
+    const bf16_t* R = reinterpret_cast<const bf16_t*>(buf + OFF_R);
+    const bf16_t* Y = reinterpret_cast<const bf16_t*>(buf + OFF_Y);
+    const bf16_t* Y2p = reinterpret_cast<const bf16_t*>(buf + OFF_Y2);
+    const uint8_t* Bt = reinterpret_cast<const uint8_t*>(buf + OFF_BITS);
+    {
+      const int r = tid >> 3;
+      const int d = d0 + r, n = n0 + 8 * cc;
+      // (LDS reads as inline asm: hipcc would wait vmcnt(0) for the ring's in-flight DMA before plain ones)
+      uint4 sv, rv, yv = make_uint4(0u, 0u, 0u, 0u), y2v = yv;
+      uint32_t bits = 0xFFu;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(sv) : "v"(lds_u32(St + r * 64 + 8 * st_slot<64>(r, cc))) : "memory");
+      asm volatile("ds_read_b128 %0, %1" : "=v"(rv) : "v"(lds_u32(R + r * 64 + 8 * cc)) : "memory");
+      if constexpr (HASY) {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(yv) : "v"(lds_u32(Y + r * 64 + 8 * cc)) : "memory");
+        asm volatile("ds_read_u8 %0, %1" : "=v"(bits) : "v"(lds_u32(Bt + (r >> 3) * 256 + (r & 7) * 8 + cc)) : "memory");
+      }
+      if constexpr (Y2)
+        asm volatile("ds_read_b128 %0, %1" : "=v"(y2v) : "v"(lds_u32(Y2p + r * 64 + 8 * cc)) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (d < p.M) {
+        float v[8], rr[8];
+        unpack8(sv, v);
+        unpack8(rv, rr);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += rr[i];
+        if constexpr (HASY) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = ((bits >> i) & 1u) ? v[i] : 0.f;
+        }
+        uint4 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+        o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        *reinterpret_cast<uint4*>(Cout + (long long)d * ld + n) = o;
+        if constexpr (HASY) {
+          float yy[8];
+          unpack8(o, v);  // statistics of the stored (rounded) gradient
+          unpack8(yv, yy);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            s1[i] += v[i];
+            s2[i] = fmaf(v[i], yy[i] - mu[i], s2[i]);
+          }
+          if constexpr (Y2) {
+            float y2[8];
+            unpack8(y2v, y2);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s3[i] = fmaf(v[i], y2[i] - mu2[i], s3[i]);
+          }
+        }
+      }
+    }
+    FAST_STAMP(t, 3);
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  if constexpr (HASY) {
+    if (e.nred > 0) bwd_finish<256, 64>(p, reinterpret_cast<float*>(smem), cpar + 2 * TN, s1, s2, s3, n0, by);
+  }
+}
+
 template <int BM, int BN, int AM, int EPI, bool RES>
-__global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(EPI == EPI_BWD_AFF && BN == 64 ? 3 : 2)))
-void igemm_fast_kernel(GemmParams p) {
+__device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
   // Persistent-style grid: workgroup (bx, by) owns N-tile bx and M-tiles by, by + gy, by + 2gy, ...;
   // the (m-tile, k-tile) steps form one software pipeline, so the next tiles' loads are in flight while
   // a tile finishes its MFMAs and its epilogue. Workgroups are dealt round-robin to the 8 XCDs by
@@ -964,6 +1253,17 @@ void igemm_fast_kernel(GemmParams p) {
   if constexpr (BWD) {
     if (p.bwd.nred > 0) bwd_finish<BM, BN>(p, reinterpret_cast<float*>(smem), cpar + 4 * BN, b1, b2, b3, n0, by);
   }
+}
+
+// The kernel: EPI_BWD_STREAM has its own tile schedule (bwd_stream_body; AM = K / 64, XF = its operand flags),
+// every other epilogue runs the persistent 2-stage pipeline above.
+template <int BM, int BN, int AM, int EPI, bool RES, int XF = 0>
+__global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(EPI == EPI_BWD_AFF && BN == 64 ? 3 : 2)))
+void igemm_fast_kernel(GemmParams p) {
+  if constexpr (EPI == EPI_BWD_STREAM)
+    bwd_stream_body<AM, XF>(p);
+  else
+    igemm_fast_body<BM, BN, AM, EPI, RES>(p);
 }
 
 // One resident round of workgroups (LDS allows 2 per CU at BM = 128 / BN = 128, 3 at BN = 64, 1 at BM = 256);
@@ -1542,7 +1842,34 @@ static int patch_grid_rows(const GemmParams& p, const PatchGeom& g) {
   return max(gy, 1);
 }
 
+// EPI_BWD_STREAM applies to a full EPI_BWD (residual; mask bits with y, or neither) of a dense 1x1 dgrad with
+// K = 64 or 128; VCG_BWD_STREAM=0 keeps it on the persistent engine (read per call: tests compare both paths)
+static bool bwd_stream_ok(const GemmParams& p) {
+  const char* v = getenv("VCG_BWD_STREAM");
+  if (v && v[0] == '0') return false;
+  const BwdEpi& e = p.bwd;
+  const bool dense = p.a.KH == 0 && p.a.GH == 0;  // dense_op(): no conv geometry
+  if (!dense || (p.K != 64 && p.K != 128) || p.N % 64 != 0 || p.batch_inner > 0 || p.ldc != p.N || p.a.ld != p.K ||
+      !e.res || e.msc || e.sub || bwd_light(p))
+    return false;
+  if ((e.y != nullptr) != (e.bits != nullptr) || (e.y2 && !e.y)) return false;
+  if (e.y && e.nred < 2) return false;
+  if (e.tsm_T > 0 && e.tsm_fold % 32 != 0) return false;  // one TSM shift per wave's 32 columns
+  if (((uintptr_t)p.C | (uintptr_t)e.res | (uintptr_t)e.y | (uintptr_t)e.y2 | (uintptr_t)p.a.ptr) & 15) return false;
+  if (e.res_s > 1 && (p.M % e.hw) != 0) return false;
+  return true;
+}
+
+static int bwd_stream_rows(const GemmParams& p) {
+  const int nx = p.N / 64, mtiles = (p.M + 63) / 64;
+  int gy = 256 / nx;  // one workgroup per CU (~100-147 KB of LDS)
+  if (gy >= 8) gy &= ~7;
+  if (gy > mtiles) gy = mtiles >= 8 ? (mtiles & ~7) : mtiles;
+  return gy < 1 ? 1 : gy;
+}
+
 int fast_bwd_slots(const GemmParams& p) {
+  if (bwd_stream_ok(p)) return bwd_stream_rows(p);
   const int R = patch_rows(p, OP_DGRAD);
   if (R > 0) return patch_grid_rows(p, patch_geom(p, R));
   return fast_grid_rows(p.M, p.N, 1, bwd_light(p) ? EPI_BWD_AFF : EPI_BWD);
@@ -1577,6 +1904,23 @@ static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K * z, algorithmic_bytes<AM, EPI, RES>(p, z));
   VCG_LAUNCH_CHECK();
   return VCG_OK;
+}
+
+template <int KC, int XF>
+static int launch_bwd_stream(const GemmParams& p, hipStream_t s) {
+  const int nx = p.N / 64, gy = bwd_stream_rows(p);
+  const int tk = timing_begin(s);
+  hipLaunchKernelGGL((igemm_fast_kernel<256, 64, KC, EPI_BWD_STREAM, false, XF>), dim3(nx * gy), dim3(512), 0, s, p);
+  timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_DENSE_K, EPI_BWD, false>(p, 1));
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+template <int KC>
+static int run_bwd_stream(const GemmParams& p, hipStream_t s) {
+  if (!p.bwd.y) return launch_bwd_stream<KC, 0>(p, s);
+  if (!p.bwd.y2) return launch_bwd_stream<KC, XF_HASY>(p, s);
+  return launch_bwd_stream<KC, XF_HASY | XF_Y2>(p, s);
 }
 
 template <int AM, int EPI, bool RES = false>
@@ -1654,6 +1998,8 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
       }
     }
   }
+  if (epi == EPI_BWD && amode == OP_DENSE_K && z == 1 && bwd_stream_ok(p))
+    return p.K == 64 ? run_bwd_stream<1>(p, s) : run_bwd_stream<2>(p, s);
   if (epi == EPI_BWD && bwd_light(p)) {
     if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_BWD_AFF>(p, z, s);
     if (amode == OP_DENSE_K) return fast_bn<OP_DENSE_K, EPI_BWD_AFF>(p, z, s);
