@@ -152,6 +152,10 @@ VCG_API int vcg_weight_fold(int dtype, const float* w, const float* scale, void*
 VCG_API int vcg_weight_prep_multi(int dtype, const long long* desc, int n, hipStream_t s);
 /* out[c][r] = in[r][c] ([rows][cols], leading dims ld_in / ld_out): W^T for the BERT input-gradient GEMMs */
 VCG_API int vcg_transpose(int dtype, const void* in, void* out, int rows, int cols, long long ld_in, long long ld_out, hipStream_t s);
+/* Batched bf16 transpose: desc (DEVICE int64 [n][5]) = (src, dst, rows, cols, first tile), [rows][cols] -> [cols][rows],
+   rows and cols multiples of 8, first tile = the running sum of ceil(rows/64) * ceil(cols/64); total_tiles = the sum.
+   (BERT's Linear weights transposed once per weight generation for the input-gradient GEMMs.) */
+VCG_API int vcg_transpose_multi(const long long* desc, int n, int total_tiles, hipStream_t s);
 VCG_API int vcg_cast_from_f32(int dtype, const float* in, void* out, long long n, hipStream_t s);
 VCG_API int vcg_cast_to_f32(int dtype, const void* in, float* out, long long n, hipStream_t s);
 /* TemporalShift.shift (ops/temporal_shift.py:33-51) on NCHW; direction 1 = its adjoint */

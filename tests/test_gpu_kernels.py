@@ -499,6 +499,21 @@ def test_transpose(K, dtype, shape):
     assert torch.equal(y.cpu(), x.t().contiguous()), "transpose must be an exact copy"
 
 
+def test_transpose_multi(K):
+    """The batched bf16 transpose (BERT's W^T cache) against torch, several shapes in one launch (ragged tiles)."""
+    shapes = [(2304, 768), (768, 3072), (72, 200), (8, 8), (64, 128)]
+    xs = [_rand(s, torch.bfloat16, 30 + i).to(DEV) for i, s in enumerate(shapes)]
+    outs = [torch.empty((s[1], s[0]), dtype=torch.bfloat16, device=DEV) for s in shapes]
+    desc, tiles = [], 0
+    for x, o in zip(xs, outs):
+        r, c = x.shape
+        desc.append([x.data_ptr(), o.data_ptr(), r, c, tiles])
+        tiles += ((r + 63) // 64) * ((c + 63) // 64)
+    K.transpose_multi(torch.tensor(desc, dtype=torch.int64).to(DEV), len(desc), tiles)
+    for x, o in zip(xs, outs):
+        assert torch.equal(o, x.t().contiguous())
+
+
 # (N, H, W, C = dgrad output channels, Cout, k, stride, pad, T) of the fused trunk-backward dgrad
 DGRAD_BWD_CASES = [
     (16, 65, 71, 128, 64, 3, 1, 1, 4),  # >= 64 Ki rows, 128 columns (256-row kernel with VCG_BIG_TILE=1)

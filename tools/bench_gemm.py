@@ -23,6 +23,25 @@ def timeit(fn, iters=10):
 
 
 def main():
+    if os.environ.get("VCG_BENCH_STAMPS"):  # per-tile phase stamps of workgroup 0 (a -DVCG_FAST_STAMPS build)
+        import ctypes
+        import numpy as np
+        from vcg_hip import _lib
+        for name, fn in _ab_cases() + _dense_cases():
+            us = timeit(fn, 5)
+            buf = (ctypes.c_ulonglong * 256)()
+            if _lib.query("vcg_fast_stamps", ctypes.addressof(buf), 256) != 0:
+                print("not a stamps build")
+                return
+            st = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(64, 4)
+            n = int((st[:, 0] > 0).sum())
+            st = st[1:max(2, n - 1)]
+            per = np.diff(st[:, 0])
+            d = np.diff(st, axis=1)
+            print(f"{name:32s} {us:7.1f} us | {len(per)} tiles: per-tile {per.mean():6.0f} ticks: k-loop {d[:, 0].mean():6.0f} "
+                  f"stage {d[:, 1].mean():5.0f} flush {d[:, 2].mean():5.0f} to next tile {(per - (st[:-1, 3] - st[:-1, 0])).mean():5.0f}",
+                  flush=True)
+        return
     if os.environ.get("VCG_BENCH_AB"):  # A/B of the output staging threshold in one process
         for name, fn in _ab_cases():
             res = []
@@ -93,6 +112,17 @@ def main():
         print(f"gemm {M}x{Nn}x{K:<20d} {us:8.1f} us  {2.0 * M * Nn * K / us / 1e6:7.1f} TF/s")
 
 
+def _dense_cases():
+    dt, dev = torch.bfloat16, "cuda"
+    out = []
+    for M, Nn, K in ((8192, 3072, 768), (8192, 768, 3072), (200704, 1024, 256), (50176, 2048, 512)):
+        A = torch.randn(M, K, device=dev).to(dt)
+        B = torch.randn(Nn, K, device=dev).to(dt)
+        C = torch.empty(M, Nn, device=dev, dtype=dt)
+        out.append((f"gemm {M}x{Nn}x{K}", (lambda A=A, B=B, C=C, M=M, Nn=Nn, K=K: ops.gemm(A, B, M, Nn, K, K, K, out=C))))
+    return out
+
+
 def _ab_cases():
     dt = torch.bfloat16
     dev = "cuda"
@@ -102,7 +132,9 @@ def _ab_cases():
                                               ("l2 conv3 128->512 stats", 1024, 28, 28, 128, 512, 1, 1, 0, True),
                                               ("l3 conv1 1024->256 stats", 1024, 14, 14, 1024, 256, 1, 1, 0, True),
                                               ("l2 conv2 3x3 128 stats", 1024, 28, 28, 128, 128, 3, 1, 1, True),
-                                              ("l3 conv2 3x3 256 stats", 1024, 14, 14, 256, 256, 3, 1, 1, True)):
+                                              ("l3 conv2 3x3 256 stats", 1024, 14, 14, 256, 256, 3, 1, 1, True),
+                                              ("l3 conv3 256->1024 stats", 1024, 14, 14, 256, 1024, 1, 1, 0, True),
+                                              ("l4 conv2 3x3 512 stats", 1024, 7, 7, 512, 512, 3, 1, 1, True)):
         x = torch.randn(N, H, W, C, device=dev).to(dt)
         w = torch.randn(Co, k, k, C, device=dev).to(dt) * 0.05
         OH, OW = ops.conv_out_hw(H, W, k, k, s, p)

@@ -321,6 +321,41 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ in
   }
 }
 
+// Batched bf16 transpose (vcg_transpose_multi): descriptor i = (src, dst, rows, cols, first tile) [5 int64];
+// block b transposes the 64 x 64 tile b - first of the descriptor whose range holds b. 16-B loads and stores,
+// the tile in LDS with a 144-B row pitch. rows, cols multiples of 8.
+__global__ __launch_bounds__(256) void transpose_multi_kernel(const long long* __restrict__ desc, int n) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[64 * 72];
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < n && desc[5 * (i + 1) + 4] <= b) ++i;
+  const long long* d = desc + 5 * i;
+  const bf16_t* in = reinterpret_cast<const bf16_t*>(d[0]);
+  bf16_t* out = reinterpret_cast<bf16_t*>(d[1]);
+  const int rows = (int)d[2], cols = (int)d[3];
+  const int t = b - (int)d[4], tc = (cols + 63) / 64;
+  const int r0 = (t / tc) * 64, c0 = (t % tc) * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = tid + 256 * k, r = id >> 3, c = 8 * (id & 7);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r0 + r < rows && c0 + c < cols) v = *reinterpret_cast<const uint4*>(in + (long long)(r0 + r) * cols + c0 + c);
+    *reinterpret_cast<uint4*>(tile + r * 72 + c) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = tid + 256 * k, oc = id >> 3, r = 8 * (id & 7);
+    if (c0 + oc >= cols || r0 + r >= rows) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)tile[(r + 2 * j) * 72 + oc] | ((uint32_t)tile[(r + 2 * j + 1) * 72 + oc] << 16);
+    *reinterpret_cast<uint4*>(out + (long long)(c0 + oc) * rows + r0 + r) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 template <typename TO>
 __global__ void cast_kernel(const float* __restrict__ in, TO* __restrict__ out, long long n) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
@@ -556,6 +591,13 @@ VCG_API int vcg_transpose(int dtype, const void* in, void* out, int rows, int co
   else
     hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, s, (const float*)in, (float*)out, rows, cols,
                        ld_in, ld_out);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_transpose_multi(const long long* desc, int n, int total_tiles, hipStream_t s) {
+  VCG_REQUIRE(n > 0 && total_tiles > 0, "bad descriptor / tile count");
+  hipLaunchKernelGGL(transpose_multi_kernel, dim3(total_tiles), dim3(256), 0, s, desc, n);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

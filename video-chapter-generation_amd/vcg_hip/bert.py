@@ -28,11 +28,60 @@ def _uniform_p(mods, what):
     return ps.pop()
 
 
+class _LinearT:
+    """bf16 W^T [in][out] of the encoder's Linear weights (QKV, attention output, FFN1, FFN2), the K-contiguous B operand
+    of the backward's input-gradient GEMMs dX = dY W, written by ONE vcg_transpose_multi launch per weight generation
+    (flat.generation moves with every optimizer step) instead of a transpose per GEMM or the generic engine's
+    N-contiguous B path (FFN2 / attention-output input gradients: 112 / 37 us vs ~60 / ~25 us on the fast engine)."""
+
+    def __init__(self, model, flat, dtype):
+        self.flat = flat
+        self.gen = None
+        srcs = []
+        H = model.config.hidden_size
+        for lyr in model.encoder.layer:
+            at = lyr.attention
+            srcs.append(flat.compute_contiguous([at.self.query.weight, at.self.key.weight, at.self.value.weight],
+                                                (3 * H, H), dtype))
+            for w in (at.output.dense.weight, lyr.intermediate.dense.weight, lyr.output.dense.weight):
+                srcs.append(flat.compute_view(w, dtype))
+        total = sum(s.numel() for s in srcs)
+        dev = srcs[0].device
+        self.buf = torch.empty(total, dtype=dtype, device=dev)
+        self.t = {}
+        desc, off, tiles = [], 0, 0
+        for s in srcs:
+            rows, cols = s.shape
+            dst = self.buf[off:off + s.numel()].view(cols, rows)
+            self.t[s.data_ptr()] = dst
+            desc.append([s.data_ptr(), dst.data_ptr(), rows, cols, tiles])
+            off += s.numel()
+            tiles += ((rows + 63) // 64) * ((cols + 63) // 64)
+        self.desc = torch.tensor(desc, dtype=torch.int64).to(dev)
+        self.n, self.tiles = len(desc), tiles
+        self.ptrs = [s.data_ptr() for s in srcs]
+
+    def refresh(self):
+        if self.gen != self.flat.generation:
+            ops.transpose_multi(self.desc, self.n, self.tiles)
+            self.gen = self.flat.generation
+
+    def get(self, W):
+        return self.t.get(W.data_ptr())
+
+
 class BertEncoderEngine:
     def __init__(self, model, flat, dtype):
         self.m = model
         self.flat = flat
         self.dtype = dtype
+        self.wt = None
+        if dtype == torch.bfloat16 and flat is not None and os.environ.get("VCG_BERT_WT", "1") != "0":
+            wt = getattr(model, "_vcg_bert_wt", None)
+            if wt is None or wt.flat is not flat:
+                wt = _LinearT(model, flat, dtype)
+                object.__setattr__(model, "_vcg_bert_wt", wt)
+            self.wt = wt
 
     def _fused_attn(self, L, dh):
         # VCG_FUSED_ATTN=0: the unfused kernels (A/B and tests); the fp32 parity mode always runs unfused
@@ -47,6 +96,9 @@ class BertEncoderEngine:
         (QKV, FFN1 input gradients: K = 2304 / 3072, N = 768): W^T is materialised (tiled transpose) so the
         LDS-DMA GEMM reads both operands K-contiguous (measured 87 -> 61 us at K = 3072, 67 -> 53 us at
         K = 2304; no gain at K = 768, tools/bench_bert_gemm.py)."""
+        wt = self.wt.get(W) if self.wt is not None else None
+        if wt is not None:
+            return ops.gemm(A, wt, M, N, K, K, K, **kw)
         if self.dtype == torch.bfloat16 and K >= 2 * N:
             return ops.gemm(A, ops.transpose(W), M, N, K, K, K, **kw)
         return ops.gemm(A, W, M, N, K, K, N, transB=True, **kw)
@@ -72,6 +124,8 @@ class BertEncoderEngine:
         dev = ids.device
         ids = ids.contiguous()
         mask = mask.to(torch.int64).contiguous()
+        if need_grad and self.wt is not None:
+            self.wt.refresh()  # (read only by the backward; issued here, on BERT's stream, beside the trunk)
 
         emb = m.embeddings
         h, e_mean, e_rstd = ops.embed_ln_fwd(ids, emb.word_embeddings.weight, emb.position_embeddings.weight,

@@ -443,6 +443,14 @@ def weight_prep_multi(desc, n):
     _lib.call("vcg_weight_prep_multi", BF16, P(desc), int(n), stream())
 
 
+def transpose_multi(desc, n, total_tiles):
+    """One launch of vcg_transpose_multi over a DEVICE int64 descriptor table [n, 5] (src, dst, rows, cols, first
+    tile): bf16 [rows][cols] -> [cols][rows]."""
+    _chk(desc, torch.int64, "desc")
+    assert desc.numel() >= 5 * n
+    _lib.call("vcg_transpose_multi", P(desc), int(n), int(total_tiles), stream())
+
+
 def transpose(x, out=None):
     """[rows, cols] -> [cols, rows] (contiguous)."""
     _chk(x, None, "x")
