@@ -593,14 +593,18 @@ class ResNetTrunk:
         kw = dict(tsm_T=T if fold else 0, tsm_fold=fold, res=res, res_stride=res_stride)
         sums3 = sumsd = None
         if prev is not None:
-            sums3 = torch.empty((2, Cin), dtype=torch.float32, device=dy1.device)
+            # rows: sum g, sum g (y3 - mean3) invstd3, sum g (yd - meand) invstdd; the downsample BN's (sum g, sum gx)
+            # are rows 0 and 2 (one gradient feeds both BatchNorms)
+            s3 = torch.empty((3 if prev["blk"].downsample is not None else 2, Cin), dtype=torch.float32,
+                             device=dy1.device)
+            sums3 = s3[:2]
             dg, db = self._bn_grads(prev["b3"])
             kw.update(bits=prev["obits"], y=prev["y3"], mean=prev["b3"].mean, invstd=prev["b3"].invstd, sums=sums3,
                       dgamma=dg, dbeta=db)
             if prev["blk"].downsample is not None:
-                sumsd = torch.empty((2, Cin), dtype=torch.float32, device=dy1.device)
+                sumsd = (s3[0], s3[2])
                 dg2, db2 = self._bn_grads(prev["bd"])
-                kw.update(y2=prev["yd"], mean2=prev["bd"].mean, invstd2=prev["bd"].invstd, sum_gx2=sumsd[1],
+                kw.update(y2=prev["yd"], mean2=prev["bd"].mean, invstd2=prev["bd"].invstd, sum_gx2=s3[2],
                           dgamma2=dg2, dbeta2=db2)
         out = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, **kw) if ResNetTrunk.fused_bwd else None
         ResNetTrunk.path_counts["unfused" if out is None else "fused"] += 1
@@ -611,8 +615,6 @@ class ResNetTrunk:
         if out is not None:
             if prev is None:
                 return out, None  # the max-pool's output gradient (no mask, no BN)
-            if sumsd is not None:
-                sumsd[0].copy_(sums3[0])
             return None, (out, sums3, sumsd)
         dxs = ops.conv_dgrad(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p)
         return ops.tsm_unshift_add(dxs, res, N, T if T else 1, H * W, Cin, fold), None
