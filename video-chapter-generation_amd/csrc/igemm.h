@@ -285,6 +285,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
 }
 
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
+int run_gemm8(const GemmParams& p, int amode, int epi, int z, hipStream_t s);  // igemm8.hip (-1: n/a)
 int fast_grid_rows(int M, int N, int z, int epi);
 int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an EPI_BWD launch of run_fast_gemm
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,

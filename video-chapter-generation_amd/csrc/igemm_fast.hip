@@ -1977,6 +1977,10 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
       return -1;
     return launch_fast<128, 128, OP_DENSE_K_BN, EPI_STATS, false>(p, z, s);
   }
+  if (epi == EPI_STATS || epi == EPI_STORE) {  // the 256-row ping-pong kernel for the compute-bound shapes
+    const int rc = run_gemm8(p, amode, epi, z, s);
+    if (rc >= 0) return rc;
+  }
   if (amode == OP_IM2COL && p.a.tsm_fold > 0) amode = OP_IM2COL_TSM;
   if (amode == OP_IM2COL && p.a.C < FBK) amode = OP_IM2COL_SMALLC;
   if (amode == OP_IM2COL_TSM && p.a.C < FBK) return -1;  // (dispatcher keeps these off the fast path)
