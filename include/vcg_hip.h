@@ -92,6 +92,19 @@ VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, 
 /* vcg_conv_wgrad of the conv above: x passes BN + ReLU in LDS (bf16 fast engine, no TSM, C >= 64; else
    VCG_ERR_UNSUPPORTED). Bit-identical to vcg_bn_apply + vcg_conv_wgrad. */
 VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* dy, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, hipStream_t stream);
+/* A batch-statistics BatchNorm backward (torch BatchNorm2d autograd: dy = A g + B y + Cc per channel, as
+   vcg_bn_bwd_apply) folded into the two gradients of the 1x1 conv that consumes dy (bottleneck conv3 after
+   bn3, model/vision/resnet50_tsm.py:15 via torchvision Bottleneck), so dy is never stored (bf16 only):
+   vcg_bn_bwd_fold_weights: wt [N][K] (the dgrad's B operand) -> wfold [N][2K] = [A_k wt | B_k wt] (bf16) and the
+   per-column constant bias [N] (f32); vcg_conv_dgrad_bwd_bnfold: the input gradient of that conv as one GEMM over
+   [g | yg] (K = 2 Cout) with vcg_conv_dgrad_bwd's light epilogue (ReLU mask fma(y, mscale, mshift) > 0, sums against
+   y); vcg_conv_wgrad_bnfold: dw[Cout][C] (+)= its weight gradient, one GEMM with 2 Cout rows ([g | yg]^T x)
+   combined per row with colsum_x = the column sums of x (f32 [C]). VCG_ERR_UNSUPPORTED where the engine does not
+   apply. */
+VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, void* wfold, float* bias, hipStream_t stream);
+VCG_API int vcg_conv_dgrad_bwd_bnfold(const void* g, const void* yg, const void* wfold, const float* bias, void* out, int N, int H, int W, int C, int Cout, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t stream);
+VCG_API long long vcg_conv_wgrad_bnfold_ws_bytes(int N, int H, int W, int C, int Cout);
+VCG_API int vcg_conv_wgrad_bnfold(const void* x, const void* g, const void* yg, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_x, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cout, hipStream_t stream);
 /* nn.Linear / BertSelfAttention matmuls (HF BertModel via model/lang/bert_hugface.py:20; ChapterHead
  * projections model/fusion/two_stream.py:60-61,79-85) */
 VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B, long long ldb, void* C, long long ldc, const float* bias, int act, const void* residual, long long ldr, void* aux, float alpha, hipStream_t stream);

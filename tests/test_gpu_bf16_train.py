@@ -124,17 +124,49 @@ def test_c1_bf16_bn_on_load_bit_exact():
     st = dict(_gold("bn_running_stats.npz"))
     frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=123, device=DEV)
     m = _model(4, "bf16", st)
-    saved = ResNetTrunk.fused_bnin
+    saved = ResNetTrunk.fused_bnin, ResNetTrunk.bn_fold_bwd
     try:
+        ResNetTrunk.bn_fold_bwd = False  # (the bn3 fold needs the stored conv3 input: both paths unfolded)
         ResNetTrunk.fused_bnin = False
         l0, lg0, g0, _ = _step(m, frames, ids, mask, labels)
         ResNetTrunk.fused_bnin = True
         l1, lg1, g1, _ = _step(m, frames, ids, mask, labels)
     finally:
-        ResNetTrunk.fused_bnin = saved
+        ResNetTrunk.fused_bnin, ResNetTrunk.bn_fold_bwd = saved
     assert l0 == l1 and torch.equal(lg0, lg1)
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n
+
+
+def test_c1_bf16_bn_fold_vs_apply():
+    """bn3's batch-statistics backward folded into conv3's input / weight gradients (VCG_BN_FOLD, no dy3 tensor)
+    against the bn_bwd_apply pass, same forward: two bf16 rounding orders of the same linear backward (the fold
+    rounds A w / B w, the pass rounds dy3), held to the fused-vs-unfused bounds; both runs deterministic."""
+    from vcg_hip import synth
+    from vcg_hip.trunk import ResNetTrunk
+    st = dict(_gold("bn_running_stats.npz"))
+    frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=123, device=DEV)
+    m = _model(4, "bf16", st)
+    saved = ResNetTrunk.bn_fold_bwd
+    try:
+        ResNetTrunk.bn_fold_bwd = False
+        la, lga, ga, _ = _step(m, frames, ids, mask, labels)
+        ResNetTrunk.bn_fold_bwd = True
+        ResNetTrunk.path_counts = {"fused": 0, "unfused": 0}
+        lb, lgb, gb, _ = _step(m, frames, ids, mask, labels)
+        assert ResNetTrunk.path_counts["unfused"] == 0
+        lc, lgc, gc, _ = _step(m, frames, ids, mask, labels)
+    finally:
+        ResNetTrunk.bn_fold_bwd = saved
+    assert la == lb == lc and torch.equal(lga, lgb)
+    for n in gb:
+        assert torch.equal(gb[n], gc[n]), n
+    stats = _compare({n: v for n, v in gb.items() if n.startswith("vision_model")},
+                     {n: v for n, v in ga.items() if n.startswith("vision_model")}, "C1 bf16 bn3 fold vs apply")
+    errs = np.array([e for e, _ in stats.values()])
+    coss = np.array([c for _, c in stats.values()])
+    print(f"fold vs apply: rel err median {np.median(errs):.2e} max {errs.max():.2e}; cosine min {coss.min():.6f}")
+    assert np.median(errs) <= 2e-2 and errs.max() <= 8e-2 and coss.min() >= 0.998
 
 
 def test_c1_loss_and_conditioning():

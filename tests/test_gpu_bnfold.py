@@ -1,0 +1,163 @@
+"""The batch-statistics BN backward folded into the consuming 1x1 conv's gradients (vcg_bn_bwd_fold_weights,
+vcg_conv_dgrad_bwd_bnfold, vcg_conv_wgrad_bnfold) against the unfused path (vcg_bn_bwd_apply -> the conv's dgrad /
+wgrad) and a float64 reference of the same math (torch BatchNorm2d autograd, the bn3 -> conv3 step of the trunk
+backward). The fold rounds the scaled weights A w / B w to bf16 where the unfused path rounds dy: the two differ by
+rounding only, so the test bounds the fold's error against float64 by a small multiple of the unfused path's."""
+import pytest
+import torch
+
+from vcg_hip import _lib, ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _init():
+    _lib.call("vcg_init", 0)
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(DEV)
+
+
+def _case(N, H, W, C, Cout, seed, ymean=0.7):
+    """g, y (bf16 [M, Cout]), BN params / sums of y, conv weight w [Cout, C] (fp32), wt [C, Cout] bf16, and the
+    epilogue's bn2 (y2 [M, C], mean2, invstd2, scale / shift of its ReLU decision)."""
+    gen = torch.Generator().manual_seed(seed)
+    M = N * H * W
+    g = torch.randn(M, Cout, generator=gen) * 0.02
+    g = torch.where(torch.rand(M, Cout, generator=gen) < 0.5, g, torch.zeros_like(g))  # a ReLU-masked gradient
+    y = torch.randn(M, Cout, generator=gen) * (0.5 + torch.rand(Cout, generator=gen)) + ymean * torch.randn(Cout, generator=gen)
+    gb, yb = _bf(g), _bf(y)
+    yd = yb.double()
+    mean = yd.mean(0)
+    var = yd.var(0, unbiased=False)
+    invstd = (var + 1e-5).rsqrt()
+    gamma = 0.5 + torch.rand(Cout, generator=gen).double()
+    sum_g = gb.double().sum(0)
+    sum_gx = (gb.double() * (yd - mean) * invstd).sum(0)
+    w = torch.randn(Cout, C, generator=gen) * (1.0 / Cout ** 0.5)
+    wt = _bf(w.t().contiguous())
+    y2c = (torch.randn(M, C, generator=gen) + 0.3).to(torch.bfloat16)
+    m2 = y2c.double().mean(0)
+    is2 = (y2c.double().var(0, unbiased=False) + 1e-5).rsqrt()
+    y2 = y2c.to(DEV)
+    gam2 = 0.5 + torch.rand(C, generator=gen).double()
+    bet2 = torch.randn(C, generator=gen).double() * 0.1
+    sc2 = (gam2 * is2)
+    sh2 = bet2 - m2 * sc2
+    f = lambda t: t.float().to(DEV)
+    return dict(M=M, g=gb, y=yb, mean=f(mean), invstd=f(invstd), gamma=f(gamma), sum_g=f(sum_g), sum_gx=f(sum_gx),
+                wt=wt, y2=y2, mean2=f(m2), invstd2=f(is2), sc2=f(sc2), sh2=f(sh2))
+
+
+def _dy_ref(c):
+    """float64 dy = A g + B y + Cc (the batch-stat BN backward of the masked gradient g)."""
+    g, y = c["g"].double(), c["y"].double()
+    A = c["gamma"].double() * c["invstd"].double()
+    B = -A * c["invstd"].double() * c["sum_gx"].double() / c["M"]
+    Cc = -A * c["sum_g"].double() / c["M"] - B * c["mean"].double()
+    return A * g + B * y + Cc
+
+
+SHAPES = [(4, 28, 28, 64, 256), (8, 14, 14, 256, 1024), (3, 7, 9, 128, 512), (2, 7, 7, 512, 2048)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_bnfold_dgrad(shape):
+    N, H, W, C, Cout = shape
+    c = _case(N, H, W, C, Cout, 1)
+    M = c["M"]
+    wfold, bias = ops.bn_bwd_fold_weights(c["wt"], C, Cout, c["mean"], c["invstd"], c["gamma"], c["sum_g"],
+                                          c["sum_gx"], M)
+    kw = dict(y=c["y2"], mean=c["mean2"], invstd=c["invstd2"], mscale=c["sc2"], mshift=c["sh2"])
+    s_f = torch.zeros(2, C, device=DEV)
+    gf = ops.conv_dgrad_bwd_bnfold(c["g"], c["y"], wfold, bias, N, H, W, C, Cout, sums=s_f, **kw)
+    assert gf is not None
+    # unfused: bn_bwd_apply (dy rounded to bf16) -> fused dgrad with the same epilogue
+    dy = ops.bn_bwd_apply(c["g"], None, c["y"], c["mean"], c["invstd"], c["gamma"], c["sum_g"], c["sum_gx"], Cout,
+                          train_stats=True)
+    s_u = torch.zeros(2, C, device=DEV)
+    gu = ops.conv_dgrad_bwd(dy, c["wt"], N, H, W, C, Cout, 1, 1, 1, 0, sums=s_u, **kw)
+    torch.cuda.synchronize()
+    gf, gu = gf.view(M, C), gu.view(M, C)
+    ref = _dy_ref(c) @ c["wt"].double().t()
+    keep = (c["y2"].double() * c["sc2"].double() + c["sh2"].double()) > 0
+    ref = torch.where(keep, ref, torch.zeros_like(ref))
+    scale = ref.abs().max().item()
+    ef = (gf.double() - ref).abs().max().item() / scale
+    eu = (gu.double() - ref).abs().max().item() / scale
+    assert ef < max(2.0 * eu, 8e-3), (ef, eu)
+    assert ((gf.double() - ref).abs().mean() / ref.abs().mean()).item() < 8e-3
+    assert (gf[~keep] == 0).all()
+    # the sums against y2 of the stored gradient (what bn2's backward consumes)
+    sref = torch.stack([gf.double().sum(0), (gf.double() * (c["y2"].double() - c["mean2"].double())
+                                              * c["invstd2"].double()).sum(0)])
+    assert (s_f.double() - sref).abs().max().item() < 1e-3 * (sref.abs().max().item() + 1)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_bnfold_wgrad(shape):
+    N, H, W, C, Cout = shape
+    c = _case(N, H, W, C, Cout, 2)
+    M = c["M"]
+    x = torch.relu(c["y2"])  # a post-ReLU activation (the conv's input)
+    cs = torch.zeros(C, device=DEV)
+    ops.colsum(x, C, M, C, cs, accumulate=False)
+    dw_f = torch.full((Cout, C), 0.25, device=DEV)  # accumulate onto an existing gradient
+    ok = ops.conv_wgrad_bnfold(x, c["g"], c["y"], c["mean"], c["invstd"], c["gamma"], c["sum_g"], c["sum_gx"], M, cs,
+                               dw_f, N, H, W, C, Cout)
+    assert ok
+    dy = ops.bn_bwd_apply(c["g"], None, c["y"], c["mean"], c["invstd"], c["gamma"], c["sum_g"], c["sum_gx"], Cout,
+                          train_stats=True)
+    dw_u = torch.full((Cout, C, 1, 1), 0.25, device=DEV)
+    ops.conv_wgrad(x, dy, dw_u, N, H, W, C, C, Cout, 1, 1, 1, 0)
+    torch.cuda.synchronize()
+    ref = _dy_ref(c).t() @ x.double() + 0.25
+    d = ref - 0.25
+    scale = d.abs().max().item()
+    ef = (dw_f.double() - ref).abs().max().item() / scale
+    eu = (dw_u.view(Cout, C).double() - ref).abs().max().item() / scale
+    assert ef < max(2.0 * eu, 2e-3), (ef, eu)
+
+
+def test_bnfold_deterministic():
+    N, H, W, C, Cout = 8, 14, 14, 256, 1024
+    c = _case(N, H, W, C, Cout, 3)
+    M = c["M"]
+    outs = []
+    for _ in range(2):
+        wfold, bias = ops.bn_bwd_fold_weights(c["wt"], C, Cout, c["mean"], c["invstd"], c["gamma"], c["sum_g"],
+                                              c["sum_gx"], M)
+        s = torch.zeros(2, C, device=DEV)
+        gf = ops.conv_dgrad_bwd_bnfold(c["g"], c["y"], wfold, bias, N, H, W, C, Cout, y=c["y2"], mean=c["mean2"],
+                                       invstd=c["invstd2"], mscale=c["sc2"], mshift=c["sh2"], sums=s)
+        x = torch.relu(c["y2"])
+        cs = torch.zeros(C, device=DEV)
+        ops.colsum(x, C, M, C, cs, accumulate=False)
+        dw = torch.zeros(Cout, C, device=DEV)
+        ops.conv_wgrad_bnfold(x, c["g"], c["y"], c["mean"], c["invstd"], c["gamma"], c["sum_g"], c["sum_gx"], M, cs,
+                              dw, N, H, W, C, Cout)
+        outs.append((gf, s, dw, bias))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rows,N", [(3211264 // 8, 64), (200704, 256), (50176 + 37, 512), (802816, 128)])
+def test_colsum_tall(rows, N):
+    """vcg_colsum on the trunk's tall conv inputs (the fold's colsum(x)): fixed-order partials, vs float64."""
+    gen = torch.Generator().manual_seed(rows + N)
+    x = (torch.randn(rows, N, generator=gen) + 0.5).to(torch.bfloat16).to(DEV)
+    out = torch.full((N,), 2.0, device=DEV)
+    ops.colsum(x, N, rows, N, out, accumulate=True)
+    torch.cuda.synchronize()
+    ref = x.double().sum(0) + 2.0
+    assert ((out.double() - ref).abs() / ref.abs().clamp_min(1.0)).max().item() < 1e-5
+    out2 = torch.zeros(N, device=DEV)
+    ops.colsum(x, N, rows, N, out2, accumulate=False)
+    out3 = torch.zeros(N, device=DEV)
+    ops.colsum(x, N, rows, N, out3, accumulate=False)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out3)

@@ -663,6 +663,51 @@ __global__ __launch_bounds__(256) void colsum_rw_kernel(const T* __restrict__ x,
   }
 }
 
+// column sums of a TALL x [rows][ld] with few columns (N = 8 cpr, cpr | 256: the trunk's conv inputs, 64..512
+// channels over up to millions of pixel rows): a thread owns one 16-B column chunk of rows r0, r0 + rpi, ... (rpi =
+// 256 / cpr rows per block step, U rows in flight per thread); per-block partials part[block][N], fixed order
+template <typename T, int U>
+__global__ __launch_bounds__(256) void colsum_tall_kernel(const T* __restrict__ x, long long ld, int rows, int N,
+                                                          int cpr, float* __restrict__ part) {
+  __shared__ float red[256][9];
+  const int t = threadIdx.x, rpi = 256 / cpr;
+  const int c = t % cpr, r0 = t / cpr;
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  const long long step = (long long)gridDim.x * rpi;
+  for (long long row = (long long)blockIdx.x * rpi + r0; row < rows; row += step * U) {
+    float v[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long r = min(row + u * step, (long long)rows - 1);  // clamped: unconditional loads
+      float a[4], b[4];
+      ld4<T>(x + r * ld + 8 * c, a);
+      ld4<T>(x + r * ld + 8 * c + 4, b);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[u][i] = a[i];
+        v[u][4 + i] = b[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (row + u * step < rows) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += v[u][i];
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[t][i] = acc[i];
+  __syncthreads();
+  for (int o = t; o < N; o += 256) {  // (N = 512: two columns per thread)
+    const int cc = o >> 3, i = o & 7;
+    float a = 0.f;
+    for (int r = 0; r < rpi; ++r) a += red[r * cpr + cc][i];
+    part[(long long)blockIdx.x * N + o] = a;
+  }
+}
+
 // Column sums of partial rows, 64 columns x 16 row-stripes per block (1024 threads), fixed order:
 //   out_k[c] (+)= sum_i part[i * stride + k * N + c], k < nout
 __global__ __launch_bounds__(1024) void colred16_kernel(const float* __restrict__ part, int nblocks, long long stride,
@@ -863,10 +908,17 @@ VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* r
   return VCG_OK;
 }
 
+constexpr int COLSUM_TALL_BLOCKS = 1024;
+static bool colsum_tall(int N, long long ld, const void* x, int rows) {
+  const int cpr = N / 8;
+  return N % 8 == 0 && N <= 512 && (256 % cpr) == 0 && ld % 8 == 0 && ((uintptr_t)x & 15) == 0 &&
+         rows >= 8 * (256 / cpr) * 64;
+}
+
 VCG_API long long vcg_colsum_ws_bytes(int rows, int N) {
   int rpb;
   const int nb = row_blocks(rows, &rpb);
-  return (long long)nb * N * 4;
+  return (long long)(nb > COLSUM_TALL_BLOCKS ? nb : COLSUM_TALL_BLOCKS) * N * 4;
 }
 
 // out[c] (+)= sum_r x[r][c]  (bias gradients)
@@ -875,6 +927,18 @@ VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, 
   int rpb;
   const int nb = row_blocks(rows, &rpb);
   VCG_REQUIRE(ws_bytes >= (long long)nb * N * 4, "workspace too small");
+  if (dtype == VCG_BF16 && colsum_tall(N, ld, x, rows) && ws_bytes >= (long long)COLSUM_TALL_BLOCKS * N * 4) {
+    const int cpr = N / 8, rpi = 256 / cpr;
+    int nbx = (int)(((long long)rows + 4LL * rpi - 1) / (4LL * rpi));
+    nbx = nbx < COLSUM_TALL_BLOCKS ? nbx : COLSUM_TALL_BLOCKS;
+    hipLaunchKernelGGL((colsum_tall_kernel<bf16_t, 4>), dim3(nbx), dim3(256), 0, s, (const bf16_t*)x, ld, rows, N, cpr,
+                       ws);
+    VCG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colred16_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, ws, nbx, (long long)N, N, 1, out,
+                       (float*)nullptr, (float*)nullptr, accumulate);
+    VCG_LAUNCH_CHECK();
+    return VCG_OK;
+  }
   if (N % 8 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15) == 0 && rows > 0) {
     int nbx = (rows + 3) / 4;
     nbx = nbx < 128 ? nbx : 128;

@@ -48,6 +48,11 @@ struct OpArgs {
   // image as W/2 "super pixels" of 8 channels (two adjacent RGB0 pixels, one 16-B chunk) that a stride-2
   // tap pair reads together: sw = 1, pw = the super-pixel pad, KW = the super-pixel tap count.
   int sw, pw;
+  // second source (fast dense A, OP_DENSE_K2: k tiles k0 >= split2 read ptr2 at k - split2, same rows / ld;
+  // wgrad_fast_kernel's dense MN A: output rows m >= split2 read ptr2 at column m - split2): the BatchNorm
+  // backward folded into its consumer GEMM reads [g | y] as one operand (vcg_conv_dgrad_bwd_bnfold)
+  const void* ptr2;
+  int split2;
 };
 
 // EPI_BWD (fast kernel, conv dgrad): the epilogue of a conv input gradient inside the trunk backward.

@@ -969,6 +969,197 @@ static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const f
   return VCG_OK;
 }
 
+// ---- BatchNorm backward folded into the consuming 1x1 conv's gradients (batch statistics) --------------------
+// The trunk backward's bn3 step dy = A g + B y + Cc (bn_bwd_apply_kernel's per-channel affine map of the masked
+// gradient g and the BN input y: A = gamma invstd, B = -A invstd sum_gx / M, Cc = -A sum_g / M - B mean) feeds
+// only conv3's input gradient and weight gradient, both linear in dy:
+//   dgrad: dx[m][n] = sum_k dy[m][k] w[k][n] = sum_k g[m][k] (A_k w) + sum_k y[m][k] (B_k w) + sum_k Cc_k w
+//          -> ONE GEMM over [g | y] (K = 2 Cout) against wfold = [bf16(A w) | bf16(B w)] plus a column bias;
+//   wgrad: dW[k][n] = A_k (g^T x)[k][n] + B_k (y^T x)[k][n] + Cc_k colsum(x)[n]
+//          -> ONE GEMM with 2 Cout output rows ([g | y]^T x), combined per row by the split-K reduction.
+// dy is never stored: the bn_bwd_apply pass (read g, y; write dy) and the two GEMMs' read of dy become two reads
+// of [g | y]. The bias keeps the y term's cancellation exact: bias[n] = sum_k (-A_k sum_g_k / M) w[k][n] -
+// mean_k bf16(B_k w[k][n]), so GEMM + bias = sum g wg + sum (y - mean) wy - sum A gbar w (no |mean| / std loss).
+namespace {
+__global__ __launch_bounds__(256) void bn_fold_weights_kernel(const bf16_t* __restrict__ wt, int K,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ sum_g,
+                                                              const float* __restrict__ sum_gx, float ic,
+                                                              bf16_t* __restrict__ wf, float* __restrict__ bias) {
+  __shared__ float red[256];
+  const int n = blockIdx.x, t = threadIdx.x;
+  float acc = 0.f;
+  for (int k = t; k < K; k += 256) {
+    const float is = invstd[k], A = (gamma ? gamma[k] : 1.f) * is;
+    const float B = -A * is * sum_gx[k] * ic;
+    const float w = bf2f(wt[(long long)n * K + k]);
+    const bf16_t wy = f2bf(B * w);
+    wf[(long long)n * 2 * K + k] = f2bf(A * w);
+    wf[(long long)n * 2 * K + K + k] = wy;
+    acc += (-A * sum_g[k] * ic) * w - mean[k] * bf2f(wy);
+  }
+  red[t] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {  // fixed tree: deterministic
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  if (t == 0) bias[n] = red[0];
+}
+
+// dw[k][n] (+)= A_k S[k][n] + B_k S[Cout + k][n] + Cc_k cs[n], S = sum of the split slabs [split][2 Cout][N]
+// (G threads per output, fixed-order combine as splitk_reduce_kernel)
+template <int G>
+__global__ __launch_bounds__(256) void splitk_reduce_bnfold_kernel(const float* __restrict__ ws, int splits, int Cout,
+                                                                   int N, const float* __restrict__ mean,
+                                                                   const float* __restrict__ invstd,
+                                                                   const float* __restrict__ gamma,
+                                                                   const float* __restrict__ sum_g,
+                                                                   const float* __restrict__ sum_gx, float ic,
+                                                                   const float* __restrict__ cs, float* __restrict__ out,
+                                                                   int accumulate) {
+  const long long MN = (long long)Cout * N, slab = 2 * MN;
+  const long long gid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long idx = gid / G;
+  const int t = (int)(gid - idx * G);
+  if (idx >= MN) return;
+  float v1 = 0.f, v2 = 0.f;
+  const float* p = ws + idx;
+  for (int s = t; s < splits; s += G) {
+    v1 += p[(long long)s * slab];
+    v2 += p[(long long)s * slab + MN];
+  }
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) {
+    v1 += __shfl_xor(v1, o, 64);
+    v2 += __shfl_xor(v2, o, 64);
+  }
+  if (t != 0) return;
+  const int k = (int)(idx / N), n = (int)(idx - (long long)k * N);
+  const float is = invstd[k], A = (gamma ? gamma[k] : 1.f) * is;
+  const float B = -A * is * sum_gx[k] * ic;
+  const float Cc = -A * sum_g[k] * ic - B * mean[k];
+  const float v = fmaf(A, v1, fmaf(B, v2, Cc * cs[n]));
+  if (accumulate) out[idx] += v;
+  else out[idx] = v;
+}
+}  // namespace
+
+VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* mean, const float* invstd,
+                                    const float* gamma, const float* sum_g, const float* sum_gx, float inv_count,
+                                    void* wfold, float* bias, hipStream_t stream) {
+  VCG_REQUIRE(wt && wfold && bias && mean && invstd && sum_g && sum_gx, "null argument");
+  VCG_REQUIRE(N > 0 && K > 0, "empty weight");
+  hipLaunchKernelGGL(bn_fold_weights_kernel, dim3(N), dim3(256), 0, stream, (const bf16_t*)wt, K, mean, invstd, gamma,
+                     sum_g, sum_gx, inv_count, (bf16_t*)wfold, bias);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_conv_dgrad_bwd_bnfold(const void* g, const void* yg, const void* wfold, const float* bias, void* out,
+                                      int N, int H, int W, int C, int Cout, const void* y, const float* mean,
+                                      const float* invstd, const float* mscale, const float* mshift, float* ws,
+                                      long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta,
+                                      hipStream_t stream) {
+  VCG_REQUIRE(g && yg && wfold && bias && out, "null argument");
+  VCG_REQUIRE(C % 64 == 0 && Cout % 64 == 0, "C and Cout must be multiples of 64");
+  VCG_REQUIRE(!mscale || (mshift && y), "mscale needs mshift and y");
+  VCG_REQUIRE(!y || (mean && invstd && sum_g && sum_gx), "the reduction needs mean/invstd/sum_g/sum_gx");
+  VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C, 2 * Cout, 1, 1), "workspace too small");
+  const long long M = (long long)N * H * W;
+  if (!fast_gemm_enabled() || M * C * 2 >= 0xFFFFFF00LL || M * Cout * 2 >= 0xFFFFFF00LL || M >= (1LL << 31))
+    return VCG_ERR_UNSUPPORTED;
+  GemmParams p{};
+  p.M = (int)M;
+  p.N = C;
+  p.K = 2 * Cout;
+  p.k_per_split = p.K + 64;
+  p.a = dense_op(g, Cout, p.M, Cout, 2);
+  p.a.ptr2 = yg;
+  p.a.split2 = Cout;
+  p.b = dense_op(wfold, p.K, C, p.K, 2);
+  p.bias = bias;
+  p.C = out;
+  p.ldc = C;
+  p.alpha = 1.f;
+  BwdEpi& e = p.bwd;
+  e.hw = H * W;
+  e.fd_hw = make_fastdiv((uint32_t)(H * W));
+  e.fd_T = make_fastdiv(1u);
+  e.fd_w = make_fastdiv((uint32_t)W);
+  e.res_s = 1;
+  e.y = y; e.mean = mean; e.invstd = invstd; e.msc = mscale; e.msh = mshift;
+  e.part = ws;
+  e.nred = y ? 2 : 0;
+  if (FILE* f = gemm_log()) {
+    fprintf(f, "a=0 b=0 epi=3 M=%d N=%d K=%d z=1 fast=1 conv=1x1/1 C=%d bnfold=1\n", p.M, p.N, p.K, Cout);
+    fflush(f);
+  }
+  int rc = run_fast_gemm(p, OP_DENSE_K, EPI_BWD, 1, stream);
+  if (rc < 0) return VCG_ERR_UNSUPPORTED;
+  if (rc) return rc;
+  if (e.nred > 0) {
+    rc = bn_bwd_finalize_launch(ws, fast_bwd_slots(p), C, 2LL * C, C, sum_g, sum_gx, dgamma, dbeta, 1, stream);
+    if (rc) return rc;
+  }
+  return VCG_OK;
+}
+
+VCG_API long long vcg_conv_wgrad_bnfold_ws_bytes(int N, int H, int W, int C, int Cout) {
+  int M, Nn, K, splits, kps;
+  bool fast;
+  wgrad_geometry(VCG_BF16, N, H, W, C, 2 * Cout, 1, 1, 1, 0, &M, &Nn, &K, &splits, &kps, &fast);
+  return (long long)splits * M * Nn * 4;
+}
+
+VCG_API int vcg_conv_wgrad_bnfold(const void* x, const void* g, const void* yg, const float* mean, const float* invstd,
+                                  const float* gamma, const float* sum_g, const float* sum_gx, float inv_count,
+                                  const float* colsum_x, float* dw, int accumulate, float* ws, long long ws_bytes, int N,
+                                  int H, int W, int C, int Cout, hipStream_t stream) {
+  VCG_REQUIRE(x && g && yg && mean && invstd && sum_g && sum_gx && colsum_x && dw, "null argument");
+  const int logC = ilog2_exact(C);
+  VCG_REQUIRE(logC >= 6 && Cout % 128 == 0, "C must be a power of two >= 64, Cout a multiple of 128");
+  int M, Nn, K, splits, kps;
+  bool fast;
+  wgrad_geometry(VCG_BF16, N, H, W, C, 2 * Cout, 1, 1, 1, 0, &M, &Nn, &K, &splits, &kps, &fast);
+  if (!fast || wgrad_fast_tile_m(M) != 128 || (long long)K * Cout * 2 >= 0xFFFFFF00LL) return VCG_ERR_UNSUPPORTED;
+  VCG_REQUIRE(ws_bytes >= (long long)splits * M * Nn * 4, "workspace too small");
+  GemmParams p{};
+  p.M = M;
+  p.N = Nn;
+  p.K = K;
+  p.k_per_split = kps;
+  p.a = dense_op(g, Cout, Cout);  // A[m = row of [g | y]][k = pixel]
+  p.a.bytes = (long long)K * Cout * 2;
+  p.a.ptr2 = yg;
+  p.a.split2 = Cout;
+  OpArgs b{};
+  b.ptr = x; b.rows = Nn; b.N = N; b.H = H; b.W = W; b.C = C; b.logC = logC;
+  b.bytes = (long long)N * H * W * C * 2;
+  b.GH = H; b.GW = W; b.KH = 1; b.KW = 1; b.stride = 1; b.pad = 0;
+  b.tsm_T = 1; b.tsm_fold = 0;
+  b.fd_ghw = make_fastdiv(H * W); b.fd_gw = make_fastdiv(W); b.fd_T = make_fastdiv(1);
+  p.b = b;
+  p.ws = ws;
+  p.alpha = 1.f;
+  p.in_C = C;
+  if (FILE* f = gemm_log())
+    fprintf(f, "a=3 b=4 epi=2 M=%d N=%d K=%d z=%d fast=2 conv=1x1/1 C=%d bnfold=1\n", M, Nn, K, splits, C);
+  int rc = run_fast_wgrad(p, splits, stream);
+  if (rc) return rc;
+  const long long MN = (long long)Cout * Nn;
+  if ((MN + 255) / 256 < 1024 && splits >= 16)
+    hipLaunchKernelGGL(splitk_reduce_bnfold_kernel<8>, dim3((unsigned)((MN * 8 + 255) / 256)), dim3(256), 0, stream,
+                       ws, splits, Cout, Nn, mean, invstd, gamma, sum_g, sum_gx, inv_count, colsum_x, dw, accumulate);
+  else
+    hipLaunchKernelGGL(splitk_reduce_bnfold_kernel<1>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws,
+                       splits, Cout, Nn, mean, invstd, gamma, sum_g, sum_gx, inv_count, colsum_x, dw, accumulate);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
 // C[M][N] = act(alpha * op(A) op(B)^T + bias + residual)
 //   transA = 0: A stored [M][lda>=K];  transA = 1: A stored [K][lda>=M]
 //   transB = 0: B stored [N][ldb>=K];  transB = 1: B stored [K][ldb>=N]

@@ -28,15 +28,19 @@ constexpr int OP_IM2COL_SMALLC = 6;
 // dense A whose BatchNorm + ReLU is applied on load (p.in_sc / p.in_sh; the conv-stats GEMM of a 1x1 conv whose
 // input is a BN output that is never stored): its own instantiation, so the plain dense GEMMs carry no table
 constexpr int OP_DENSE_K_BN = 7;
+// dense A from two sources along K (OpArgs ptr2 / split2): [g | y] of a BatchNorm backward folded into the consuming
+// conv's input gradient; its own instantiation, so the plain dense loaders carry no second descriptor
+constexpr int OP_DENSE_K2 = 8;
 
 template <int ROWS, int MODE, int NW = 4> struct FastLoader {
   static constexpr int PER_WAVE = ROWS / (8 * NW);  // 1-KiB (8-row) slices per wave per tile
-  static constexpr bool GATHER = MODE != OP_DENSE_K && MODE != OP_DENSE_K_BN;
+  static constexpr bool GATHER = MODE != OP_DENSE_K && MODE != OP_DENSE_K_BN && MODE != OP_DENSE_K2;
+  static constexpr bool TWO = MODE == OP_DENSE_K2;
   static constexpr bool IM2COL = MODE == OP_IM2COL || MODE == OP_IM2COL_TSM || MODE == OP_IM2COL_SMALLC;
   static constexpr bool TSM = MODE == OP_IM2COL_TSM;
   static constexpr bool SMALLC = MODE == OP_IM2COL_SMALLC;
   static constexpr int BAD = -(1 << 28);  // spatial base of rows beyond M: every bounds test fails
-  __amdgpu_buffer_rsrc_t rsrc;
+  __amdgpu_buffer_rsrc_t rsrc, rsrc2;
   uint32_t oob;
   // element offsets fit in 31 bits: the dispatcher routes only tensors < 4 GB here (32-bit buffer range)
   // Gathers with C >= 64 (one filter tap per 64-wide k tile) keep per row: pb = element offset of the
@@ -49,6 +53,7 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
   __device__ __forceinline__ void init(const OpArgs& a, long long batch_off, int row0, int wave, int lane) {
     const uint32_t nbytes = (uint32_t)min(a.bytes, (long long)0xFFFFFF00LL);
     rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr), 0, nbytes, 0x00020000);
+    if constexpr (TWO) rsrc2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr2), 0, nbytes, 0x00020000);
     oob = nbytes;  // offset + 16 > num_records -> the load returns zeros
 #pragma clang loop unroll(full)
     for (int q = 0; q < PER_WAVE; ++q) {
@@ -189,6 +194,16 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
         return;
       }
     }
+    __amdgpu_buffer_rsrc_t rs = rsrc;
+    if constexpr (TWO) {  // the k tile lies in one source (split2 % 64 == 0): a uniform select
+      if (k0 >= a.split2) {
+        rs = rsrc2;
+        k0 -= a.split2;
+        kend -= a.split2;
+      } else {
+        kend = min(kend, a.split2);
+      }
+    }
 #pragma clang loop unroll(full)
     for (int q = 0; q < PER_WAVE; ++q) {
       const int k = k0 + kc[q];
@@ -204,7 +219,7 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
         if (ok) voff = (uint32_t)e * 2u;
       }
       bf16_t* slice = lds + (wave * PER_WAVE + q) * 512;  // 1 KiB per slice
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)slice, 16, voff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)slice, 16, voff, 0, 0, 0);
     }
   }
 };
@@ -1205,6 +1220,10 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
 #pragma unroll
               for (int i = 0; i < MT; ++i) {
                 float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                if constexpr (AM == OP_DENSE_K2) {  // the folded BN's constant term, before the bf16 rounding
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) v[r] += bv[j][r];
+                }
                 stage_put<BM, BN>(stA, stB, wm, wn, lane, i, j, v);
               }
           }
@@ -1880,7 +1899,7 @@ int fast_bwd_slots(const GemmParams& p) {
 template <int AM, int EPI, bool RES>
 static double algorithmic_bytes(const GemmParams& p, int z) {
   const double mn = (double)p.M * p.N * z;
-  double b = (AM == OP_DENSE_K || AM == OP_DENSE_K_BN ? 2.0 * p.M * (double)p.K * z : (double)p.a.bytes) + 2.0 * p.N * (double)p.K * z;
+  double b = (AM == OP_DENSE_K || AM == OP_DENSE_K_BN || AM == OP_DENSE_K2 ? 2.0 * p.M * (double)p.K * z : (double)p.a.bytes) + 2.0 * p.N * (double)p.K * z;
   b += 2.0 * mn;
   if (RES) b += 2.0 * mn;
   if (p.aux) b += 2.0 * mn;
@@ -1976,6 +1995,10 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
         fast_bn_cols(p.N) != 128 || fast_bm(p.M, p.N, z, false) != 128)
       return -1;
     return launch_fast<128, 128, OP_DENSE_K_BN, EPI_STATS, false>(p, z, s);
+  }
+  if (p.a.ptr2) {  // a BatchNorm backward folded into this input gradient: A = [g | y] (light epilogue only)
+    if (amode != OP_DENSE_K || epi != EPI_BWD || z != 1 || !bwd_light(p) || p.a.split2 % FBK != 0) return -1;
+    return fast_bn<OP_DENSE_K2, EPI_BWD_AFF>(p, z, s);
   }
   if (epi == EPI_STATS || epi == EPI_STORE) {  // the 256-row ping-pong kernel for the compute-bound shapes
     const int rc = run_gemm8(p, amode, epi, z, s);

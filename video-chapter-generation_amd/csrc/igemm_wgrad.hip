@@ -50,7 +50,19 @@ template <int COLS, bool GATHER> struct MNLoader {
 
   __device__ __forceinline__ void init(const OpArgs& a, int col0, int ncols, int kb, int wave, int lane) {
     const uint32_t nbytes = (uint32_t)min(a.bytes, (long long)0xFFFFFF00LL);
-    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr), 0, nbytes, 0x00020000);
+    const void* src = a.ptr;
+    if constexpr (!GATHER) {
+      if (a.ptr2) {  // two sources along the output rows (OpArgs::split2 % BM == 0): a uniform choice per tile
+        if (col0 >= a.split2) {
+          src = a.ptr2;
+          col0 -= a.split2;
+          ncols -= a.split2;
+        } else {
+          ncols = min(ncols, a.split2);
+        }
+      }
+    }
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(src), 0, nbytes, 0x00020000);
     oob = nbytes;
     if constexpr (GATHER) {
       const int ohw = a.GH * a.GW;

@@ -164,6 +164,59 @@ def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_f
     return g
 
 
+def bn_bwd_fold_weights(wt, N, K, mean, invstd, gamma, sum_g, sum_gx, count):
+    """(wfold [N, 2K] bf16, bias [N] f32) of a batch-statistics BN backward folded into the dgrad whose B operand is
+    wt [N, K] (vcg_bn_bwd_fold_weights)."""
+    _chk(wt, torch.bfloat16, "wt")
+    wfold = torch.empty((N, 2 * K), dtype=torch.bfloat16, device=wt.device)
+    bias = torch.empty(N, dtype=torch.float32, device=wt.device)
+    _lib.call("vcg_bn_bwd_fold_weights", P(wt), N, K, P(mean), P(invstd), P(gamma), P(sum_g), P(sum_gx),
+              float(1.0 / count), P(wfold), P(bias), stream())
+    return wfold, bias
+
+
+def conv_dgrad_bwd_bnfold(g, yg, wfold, bias, N, H, W, C, Cout, y=None, mean=None, invstd=None, mscale=None,
+                          mshift=None, sums=None, dgamma=None, dbeta=None, out=None, workspace=None):
+    """Input gradient of a 1x1 conv whose output gradient is the folded BN backward A g + B yg + Cc
+    (vcg_conv_dgrad_bwd_bnfold; the light epilogue of conv_dgrad_bwd). Returns the masked gradient, or None where
+    the engine does not apply."""
+    _chk(g, torch.bfloat16, "g")
+    _chk(yg, torch.bfloat16, "yg")
+    assert g.numel() == yg.numel() == N * H * W * Cout and wfold.numel() == C * 2 * Cout
+    gout = out if out is not None else torch.empty((N, H, W, C), dtype=g.dtype, device=g.device)
+    nbytes = _lib.query("vcg_conv_dgrad_bwd_ws_bytes", C, 2 * Cout, 1, 1)
+    if workspace is None or workspace.numel() * 4 < nbytes:
+        workspace = ws(nbytes, g.device)
+    rc = _lib.query("vcg_conv_dgrad_bwd_bnfold", P(g), P(yg), P(wfold), P(bias), P(gout), N, H, W, C, Cout, P(y),
+                    P(mean), P(invstd), P(mscale), P(mshift), P(workspace), workspace.numel() * 4,
+                    P(sums[0]) if sums is not None else None, P(sums[1]) if sums is not None else None, P(dgamma),
+                    P(dbeta), stream())
+    if rc == -2:
+        return None
+    if rc != 0:
+        raise _lib.VcgError(f"vcg_conv_dgrad_bwd_bnfold failed ({rc}): {_lib.last_error()}")
+    return gout
+
+
+def conv_wgrad_bnfold(x, g, yg, mean, invstd, gamma, sum_g, sum_gx, count, colsum_x, dw, N, H, W, C, Cout,
+                      accumulate=True, workspace=None):
+    """dw [Cout, C] (+)= weight gradient of a 1x1 conv over x whose output gradient is the folded BN backward
+    (vcg_conv_wgrad_bnfold). Returns False where the engine does not apply."""
+    _chk(x, torch.bfloat16, "x")
+    _chk(dw, torch.float32, "dw")
+    nbytes = _lib.query("vcg_conv_wgrad_bnfold_ws_bytes", N, H, W, C, Cout)
+    if workspace is None or workspace.numel() * 4 < nbytes:
+        workspace = ws(nbytes, x.device)
+    rc = _lib.query("vcg_conv_wgrad_bnfold", P(x), P(g), P(yg), P(mean), P(invstd), P(gamma), P(sum_g), P(sum_gx),
+                    float(1.0 / count), P(colsum_x), P(dw), int(accumulate), P(workspace), workspace.numel() * 4, N, H,
+                    W, C, Cout, stream())
+    if rc == -2:
+        return False
+    if rc != 0:
+        raise _lib.VcgError(f"vcg_conv_wgrad_bnfold failed ({rc}): {_lib.last_error()}")
+    return True
+
+
 def conv_wgrad(x, dy, dw, N, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, accumulate=True,
                workspace=None):
     """dw (fp32 OIHW [Cout,Cin,KH,KW]) += wgrad. x: NHWC with C (padded) channels."""

@@ -131,6 +131,13 @@ class ResNetTrunk:
     # bf16 scoring forward (running-statistics BN, no autograd): bn3 folded into conv3 (1x1 GEMM with the BN scale in
     # the weight rows, the shift as bias, + identity, ReLU in the epilogue) -- no y3 tensor, no bn3 pass
     fold_eval = os.environ.get("VCG_FOLD_BN", "1") != "0"
+    # bf16 training backward: bn3's batch-statistics backward folded into conv3's two gradients (dy3 = A g + B y3 + C
+    # is never stored: the input gradient is one GEMM over [g | y3], the weight gradient one GEMM with 2 C3 rows;
+    # ops.conv_dgrad_bwd_bnfold / conv_wgrad_bnfold); VCG_BN_FOLD=0: the bn_bwd_apply pass
+    bn_fold_bwd = os.environ.get("VCG_BN_FOLD", "1") != "0"
+    # ... for blocks with C3 <= this many channels (layers 1-2: HBM-bound conv3 gradients; the deeper layers' doubled
+    # K costs more MFMA time than the pass it removes)
+    bn_fold_max_c3 = int(os.environ.get("VCG_BN_FOLD_MAXC3", "512"))
 
     def __init__(self, net, dtype):
         self.net = net
@@ -524,6 +531,53 @@ class ResNetTrunk:
             return self._bn_bwd(da, y, st, C, affine=True)
         return self._bn_apply_bwd(g, y, st, C, sums)
 
+    def _can_fold(self, r, ds):
+        """bn3's backward folds into conv3's gradients here (bf16 fused engine, batch statistics, stored conv3 input,
+        layers up to bn_fold_max_c3 channels; a first bottleneck also needs the side stream, where its downsample
+        BN's apply pass then runs -- dyd feeds only side-stream work)."""
+        blk, b3, C3, planes = r["blk"], r["b3"], r["C3"], r["planes"]
+        if not (ResNetTrunk.bn_fold_bwd and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16):
+            return False
+        if b3.mode == "running" or r["a2"] is None or C3 > ResNetTrunk.bn_fold_max_c3 or C3 % 128 != 0:
+            return False
+        if blk.conv3.stride[0] != 1 or planes < 64 or (planes & (planes - 1)) != 0:
+            return False
+        return not ds or (r["bd"].mode != "running" and self._ws is not None and ResNetTrunk.ds_stream)
+
+    def _fold_conv3(self, r, g, sums3):
+        """conv3's weight gradient with bn3's batch-statistics backward folded in (side stream): dW = A (g^T a2) +
+        B (y3^T a2) + C colsum(a2) as one GEMM with 2 C3 rows. False where the engine does not apply."""
+        blk = r["blk"]
+        if not blk.conv3.weight.requires_grad:
+            return True
+        N, H2, W2, planes, C3 = r["N"], r["H2"], r["W2"], r["planes"], r["C3"]
+        b3, a2, y3 = r["b3"], r["a2"], r["y3"]
+        M = N * H2 * W2
+
+        def wfn():
+            cs = torch.empty(planes, dtype=torch.float32, device=a2.device)
+            ops.colsum(a2.view(M, planes), planes, M, planes, cs, accumulate=False)
+            return ops.conv_wgrad_bnfold(a2, g, y3, b3.mean, b3.invstd, b3.bn.weight, sums3[0], sums3[1], M, cs,
+                                         blk.conv3.weight.grad, N, H2, W2, planes, C3)
+        return self._async(wfn, a2, g, y3, sums3)
+
+    def _dgrad_bn_fold(self, conv, g, y3, b3, sums3, N, H, W, y, st, C, C3):
+        """_dgrad_bn of conv3 with bn3's backward folded in: one GEMM over [g | y3] against [A w | B w] plus the
+        constant column bias. None where the engine does not apply."""
+        Cout, Cin, KH, KW, s, p = _conv_shape(conv)
+        wt = self._wprep_t(conv, Cin)
+        M = N * H * W
+        wfold, bias = ops.bn_bwd_fold_weights(wt.view(Cin, C3), Cin, C3, b3.mean, b3.invstd, b3.bn.weight, sums3[0],
+                                              sums3[1], M)
+        sums = torch.empty((2, C), dtype=torch.float32, device=y.device)
+        dg, db = self._bn_grads(st)
+        g2 = ops.conv_dgrad_bwd_bnfold(g, y3, wfold, bias, N, H, W, Cin, C3, y=y, mean=st.mean, invstd=st.invstd,
+                                       mscale=st.scale, mshift=st.shift, sums=sums, dgamma=dg, dbeta=db)
+        if g2 is None:
+            return None
+        ResNetTrunk.path_counts["fused"] += 1
+        return self._bn_apply_bwd(g2, y, st, C, sums)
+
     def _block_bwd(self, r, dout, gin, prev):
         """Backward of one bottleneck. `gin` (fused path): (g, sums3, sumsd) = this block's ReLU-masked output
         gradient and its BN sums; else `dout` is the raw output gradient. `prev`: the record of the block
@@ -533,10 +587,16 @@ class ResNetTrunk:
         Cin, planes, C3, T, fold = r["Cin"], r["planes"], r["C3"], r["T"], r["fold"]
         obits = r["obits"]
         ds = blk.downsample is not None
+        bnf = None  # bn3's backward folded into conv3's gradients: (g, sums3)
         if gin is not None:
             g, sums3, sumsd = gin
             b3, bd = r["b3"], r.get("bd")
-            if ResNetTrunk.dual_bn_bwd and ds and b3.mode != "running" and bd.mode != "running":  # g read once
+            if self._can_fold(r, ds):
+                bnf = (g, sums3)
+                dy3 = dyd = None
+                if ds:  # the downsample BN's apply pass on the side stream (dyd feeds only side-stream kernels)
+                    dyd = self._async(lambda: self._bn_apply_bwd(g, r["yd"], bd, C3, sumsd), g, r["yd"], *sumsd)
+            elif ResNetTrunk.dual_bn_bwd and ds and b3.mode != "running" and bd.mode != "running":  # g read once
                 dy3, dyd = ops.bn_bwd_apply_dual(g, r["y3"], b3.mean, b3.invstd, b3.bn.weight, sums3[0], sums3[1],
                                                  r["yd"], bd.mean, bd.invstd, bd.bn.weight, sumsd[0], sumsd[1], C3)
             else:
@@ -551,7 +611,12 @@ class ResNetTrunk:
         ds_res = None
         if ds and self._ws is not None and ResNetTrunk.ds_stream:
             ds_res = self._ds_dgrad_side(blk.downsample[0], dyd, N, H, W, Cin, C3)
-        if r["a2"] is not None:
+        if bnf is not None and not self._fold_conv3(r, *bnf):  # (the engine does not apply: the pass on dy3)
+            dy3 = self._bn_apply_bwd(bnf[0], r["y3"], r["b3"], C3, bnf[1])
+            bnf = None
+        if bnf is not None:
+            pass  # (conv3's weight gradient went out with the fold)
+        elif r["a2"] is not None:
             self._wgrad(blk.conv3, r["a2"], dy3, N, H2, W2, planes)
         elif blk.conv3.weight.requires_grad:  # conv3's input is bn2 + ReLU of y2, applied on load
             Cout3, _, KH3, KW3, s3, p3 = _conv_shape(blk.conv3)
@@ -561,7 +626,14 @@ class ResNetTrunk:
                                r["y2"], b2.scale, b2.shift, dy3):
                 self._wgrad(blk.conv3, ops.bn_apply(r["y2"], b2.scale, b2.shift, planes, relu=True), dy3, N, H2, W2,
                             planes)
-        dy2 = self._dgrad_bn(blk.conv3, dy3, N, H2, W2, r["y2"], r["b2"], planes)
+        dy2 = None
+        if bnf is not None:
+            dy2 = self._dgrad_bn_fold(blk.conv3, bnf[0], r["y3"], r["b3"], bnf[1], N, H2, W2, r["y2"], r["b2"], planes,
+                                      C3)
+            if dy2 is None:  # (the fused engine does not apply: the unfused pass, and conv3's dgrad on dy3)
+                dy3 = self._bn_apply_bwd(bnf[0], r["y3"], r["b3"], C3, bnf[1])
+        if dy2 is None:
+            dy2 = self._dgrad_bn(blk.conv3, dy3, N, H2, W2, r["y2"], r["b2"], planes)
         del dy3
         self._wgrad(blk.conv2, r["a1"], dy2, N, H, W, planes)
         dy1 = self._dgrad_bn(blk.conv2, dy2, N, H, W, r["y1"], r["b1"], planes)
