@@ -101,6 +101,11 @@ VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale,
    y); vcg_conv_wgrad_bnfold: dw[Cout][C] (+)= its weight gradient, one GEMM with 2 Cout rows ([g | yg]^T x)
    combined per row with colsum_x = the column sums of x (f32 [C]). VCG_ERR_UNSUPPORTED where the engine does not
    apply. */
+/* torchvision Bottleneck's bn3 + identity + ReLU (model/vision/resnet50_tsm.py:15) as a second pass of conv3's GEMM:
+   out[M][N] = relu(bf16(x[M][K] wfold[N][K]^T + bias) + res) and the ReLU mask bits (vcg_bn_apply's layout), with
+   wfold = the conv3 weight rows scaled by the batch-statistics BN scale (vcg_weight_fold), bias = its shift: the stored
+   conv output is not read back (bf16 fast engine; VCG_ERR_UNSUPPORTED elsewhere) */
+VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const float* bias, const void* res, void* out, unsigned char* bits, int M, int N, int K, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, void* wfold, float* bias, hipStream_t stream);
 VCG_API int vcg_conv_dgrad_bwd_bnfold(const void* g, const void* yg, const void* wfold, const float* bias, void* out, int N, int H, int W, int C, int Cout, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t stream);
 VCG_API long long vcg_conv_wgrad_bnfold_ws_bytes(int N, int H, int W, int C, int Cout);

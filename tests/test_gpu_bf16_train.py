@@ -124,15 +124,16 @@ def test_c1_bf16_bn_on_load_bit_exact():
     st = dict(_gold("bn_running_stats.npz"))
     frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=123, device=DEV)
     m = _model(4, "bf16", st)
-    saved = ResNetTrunk.fused_bnin, ResNetTrunk.bn_fold_bwd
+    saved = ResNetTrunk.fused_bnin, ResNetTrunk.bn_fold_bwd, ResNetTrunk.bn3_gemm_max_c3
     try:
-        ResNetTrunk.bn_fold_bwd = False  # (the bn3 fold needs the stored conv3 input: both paths unfolded)
+        # (the bn3 fold and the bn3 GEMM pass need the stored conv3 input: both paths without them)
+        ResNetTrunk.bn_fold_bwd, ResNetTrunk.bn3_gemm_max_c3 = False, 0
         ResNetTrunk.fused_bnin = False
         l0, lg0, g0, _ = _step(m, frames, ids, mask, labels)
         ResNetTrunk.fused_bnin = True
         l1, lg1, g1, _ = _step(m, frames, ids, mask, labels)
     finally:
-        ResNetTrunk.fused_bnin, ResNetTrunk.bn_fold_bwd = saved
+        ResNetTrunk.fused_bnin, ResNetTrunk.bn_fold_bwd, ResNetTrunk.bn3_gemm_max_c3 = saved
     assert l0 == l1 and torch.equal(lg0, lg1)
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n

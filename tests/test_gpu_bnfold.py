@@ -161,3 +161,34 @@ def test_colsum_tall(rows, N):
     ops.colsum(x, N, rows, N, out3, accumulate=False)
     torch.cuda.synchronize()
     assert torch.equal(out2, out3)
+
+
+@pytest.mark.parametrize("shape", [(4, 28, 28, 64, 256), (3, 7, 9, 128, 512), (8, 14, 14, 256, 1024)])
+def test_conv1x1_bn_res_relu(shape):
+    """bn3 + identity + ReLU as a second conv3 GEMM pass (vcg_conv1x1_bn_res_relu) against conv -> bn_apply (the stored
+    bf16 y3 read back): one bf16 rounding apart (the GEMM rounds x W' + b instead of y3), mask bits = out > 0."""
+    N, H, W, C, Cout = shape
+    M = N * H * W
+    gen = torch.Generator().manual_seed(7)
+    x = _bf(torch.relu(torch.randn(M, C, generator=gen)))
+    w = (torch.randn(Cout, C, generator=gen) / C ** 0.5).to(DEV)
+    res = _bf(torch.relu(torch.randn(M, Cout, generator=gen)))
+    y = x.double() @ w.double().t()
+    sc = (0.5 + torch.rand(Cout, generator=gen)).to(DEV) / y.std(0).float()
+    sh = (torch.randn(Cout, generator=gen) * 0.3).to(DEV) - y.mean(0).float() * sc
+    wf = ops.weight_fold(w, sc, torch.bfloat16)
+    r = ops.conv1x1_bn_res_relu(x, wf, sh, res, M, Cout, C)
+    assert r is not None
+    out, bits = r
+    y3 = ops.gemm(x, ops.weight_fold(w, torch.ones(Cout, device=DEV), torch.bfloat16), M, Cout, C, C, C)
+    ref, rbits = ops.bn_apply(y3, sc, sh, Cout, relu=True, res=res, bits=True)
+    torch.cuda.synchronize()
+    exact = torch.relu(y * sc.double() + sh.double() + res.double())
+    e_new = (out.double() - exact).abs().max().item()
+    e_old = (ref.double() - exact).abs().max().item()
+    assert e_new <= max(1.5 * e_old, 3e-2 * exact.abs().max().item()), (e_new, e_old)
+    # bits: byte (m Cout + n) / 8, bit n % 8 = out > 0 of this pass
+    pos = (out.view(-1, 8) > 0).to(torch.uint8)
+    expect = (pos * (2 ** torch.arange(8, device=DEV, dtype=torch.uint8))).sum(1).to(torch.uint8)
+    assert torch.equal(bits, expect)
+    assert (bits != rbits).float().mean().item() < 0.02

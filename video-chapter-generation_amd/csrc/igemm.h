@@ -113,6 +113,9 @@ struct GemmParams {
   // igemm_fast_kernel / the x operand of wgrad_fast_kernel); in_C channels
   const float *in_sc, *in_sh;
   int in_C;
+  // EPI_STORE + residual + ReLU through the stage (epilogue_staged_res): also store the ReLU decisions as mask bits,
+  // byte (m N + n) / 8 bit n % 8 (vcg_bn_apply's bits layout; vcg_conv1x1_bn_res_relu)
+  uint8_t* obits;
 };
 
 

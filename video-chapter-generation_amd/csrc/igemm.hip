@@ -1160,6 +1160,40 @@ VCG_API int vcg_conv_wgrad_bnfold(const void* x, const void* g, const void* yg, 
   return VCG_OK;
 }
 
+// out = relu(bf16(x wfold^T + bias) + res) with the ReLU mask bits: a batch-statistics bn3 (scale folded into the
+// conv3 weight rows by vcg_weight_fold, shift as bias) applied by a second pass of conv3's GEMM instead of reading
+// the stored conv output back (trunk forward; the bn3 + residual + ReLU of vcg_bn_apply, one bf16 rounding earlier)
+VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const float* bias, const void* res, void* out,
+                                    unsigned char* bits, int M, int N, int K, hipStream_t stream) {
+  VCG_REQUIRE(x && wfold && bias && res && out && bits, "null argument");
+  VCG_REQUIRE(M > 0 && N % 64 == 0 && K % 64 == 0, "N and K must be multiples of 64");
+  VCG_REQUIRE((((uintptr_t)x | (uintptr_t)wfold | (uintptr_t)res | (uintptr_t)out) & 15) == 0, "16-B alignment");
+  if (!fast_gemm_enabled() || (long long)M * K * 2 >= 0xFFFFFF00LL || (long long)M * N * 2 >= 0xFFFFFF00LL)
+    return VCG_ERR_UNSUPPORTED;
+  GemmParams p{};
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.k_per_split = K + 64;
+  p.a = dense_op(x, K, M, K, 2);
+  p.b = dense_op(wfold, K, N, K, 2);
+  p.C = out;
+  p.ldc = N;
+  p.alpha = 1.f;
+  p.bias = bias;
+  p.act = ACT_RELU;
+  p.residual = res;
+  p.ldr = N;
+  p.res_round = 1;
+  p.obits = bits;
+  if (FILE* f = gemm_log()) {
+    fprintf(f, "a=0 b=0 epi=0 M=%d N=%d K=%d z=1 fast=1 conv=1x1/1 C=%d bnres=1\n", M, N, K, K);
+    fflush(f);
+  }
+  const int rc = run_fast_gemm(p, OP_DENSE_K, EPI_STORE, 1, stream);
+  return rc < 0 ? VCG_ERR_UNSUPPORTED : rc;
+}
+
 // C[M][N] = act(alpha * op(A) op(B)^T + bias + residual)
 //   transA = 0: A stored [M][lda>=K];  transA = 1: A stored [K][lda>=M]
 //   transB = 0: B stored [N][ldb>=K];  transB = 1: B stored [K][ldb>=N]

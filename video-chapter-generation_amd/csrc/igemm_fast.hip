@@ -413,14 +413,21 @@ __device__ __forceinline__ void epilogue_staged_res(f32x4 (&acc)[4][BN / 32], co
     float a[8], r[8];
     unpack8(q[k], a);
     unpack8(rv[k], r);
+    uint32_t mb = 0;  // ReLU mask of the output (p.obits): bit e = out > 0, as vcg_bn_apply writes it
 #pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = apply_act(a[e] + r[e], p.act);
+    for (int e = 0; e < 8; ++e) {
+      a[e] = apply_act(a[e] + r[e], p.act);
+      mb |= (a[e] > 0.f ? 1u : 0u) << e;
+    }
     uint4 o;
     o.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
     o.y = (uint32_t)f2bf(a[2]) | ((uint32_t)f2bf(a[3]) << 16);
     o.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
     o.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
-    if (m < mlim && n < p.N) *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + n) = o;
+    if (m < mlim && n < p.N) {
+      *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + n) = o;
+      if (p.obits) p.obits[((long long)m * p.N + n) >> 3] = (uint8_t)mb;
+    }
   }
   __builtin_amdgcn_s_barrier();  // every wave has read the stage before the next step's DMA refills it
 }
@@ -1249,7 +1256,7 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
       } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0 &&
                                ((uintptr_t)p.C & 15) == 0)) {
         epilogue_staged<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
-      } else if (RES && staged && p.res_round && p.act == ACT_RELU && p.aux == nullptr &&
+      } else if (RES && (staged || p.obits) && p.res_round && p.act == ACT_RELU && p.aux == nullptr &&
                  ((p.ldc | p.ldr | p.N) & 7) == 0 && (((uintptr_t)p.residual | (uintptr_t)p.C) & 15) == 0) {
         if constexpr (BM == 128 && RES)
           epilogue_staged_res<BM, BN>(acc, p, bv, Cout, Res, stA, stB, mt * BM, n0, wm, wn, lane, p.M);

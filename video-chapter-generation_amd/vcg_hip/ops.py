@@ -164,6 +164,21 @@ def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_f
     return g
 
 
+def conv1x1_bn_res_relu(x, wfold, bias, res, M, N, K):
+    """(out, bits): relu(bf16(x @ wfold^T + bias) + res) and its ReLU mask bits (vcg_conv1x1_bn_res_relu), or None
+    where the fused engine does not apply."""
+    _chk(x, torch.bfloat16, "x")
+    _chk(res, torch.bfloat16, "res")
+    out = torch.empty_like(res)
+    bits = torch.empty(res.numel() // 8, dtype=torch.uint8, device=res.device)
+    rc = _lib.query("vcg_conv1x1_bn_res_relu", P(x), P(wfold), P(bias), P(res), P(out), P(bits), M, N, K, stream())
+    if rc == -2:
+        return None
+    if rc != 0:
+        raise _lib.VcgError(f"vcg_conv1x1_bn_res_relu failed ({rc}): {_lib.last_error()}")
+    return out, bits
+
+
 def bn_bwd_fold_weights(wt, N, K, mean, invstd, gamma, sum_g, sum_gx, count):
     """(wfold [N, 2K] bf16, bias [N] f32) of a batch-statistics BN backward folded into the dgrad whose B operand is
     wt [N, K] (vcg_bn_bwd_fold_weights)."""

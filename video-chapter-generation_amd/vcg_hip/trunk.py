@@ -138,6 +138,10 @@ class ResNetTrunk:
     # ... for blocks with C3 <= this many channels (layers 1-2: HBM-bound conv3 gradients; the deeper layers' doubled
     # K costs more MFMA time than the pass it removes)
     bn_fold_max_c3 = int(os.environ.get("VCG_BN_FOLD_MAXC3", "512"))
+    # batch-statistics forward of a non-first bottleneck with C3 <= this many channels: bn3 + identity + ReLU as a
+    # second pass of conv3's GEMM (scale folded into its weight rows, shift as bias; ops.conv1x1_bn_res_relu)
+    # instead of reading y3 back in the bn_apply pass (0: off)
+    bn3_gemm_max_c3 = int(os.environ.get("VCG_BN3_GEMM_MAXC3", "512"))
 
     def __init__(self, net, dtype):
         self.net = net
@@ -291,7 +295,16 @@ class ResNetTrunk:
             out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale,
                                       rshift=bd.shift, bits=True)
         else:
-            out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=x, bits=True)
+            r2 = None
+            if (a2 is not None and self.dtype == torch.bfloat16 and C3 <= ResNetTrunk.bn3_gemm_max_c3
+                    and b3.mode != "running" and blk.conv3.stride[0] == 1):
+                M = N * H2 * W2
+                wf = ops.weight_fold(blk.conv3.weight.data.view(C3, planes), b3.scale, self.dtype)
+                r2 = ops.conv1x1_bn_res_relu(a2.view(M, planes), wf, b3.shift, x, M, C3, planes)
+            if r2 is not None:
+                out, obits = r2
+            else:
+                out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=x, bits=True)
         rec = None
         if need_grad:
             rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, y3=y3, yd=yd, obits=obits, b1=b1, b2=b2, b3=b3,
