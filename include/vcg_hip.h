@@ -97,7 +97,7 @@ VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale,
    bn3, model/vision/resnet50_tsm.py:15 via torchvision Bottleneck), so dy is never stored (bf16 only):
    vcg_bn_bwd_fold_weights: wt [N][K] (the dgrad's B operand) -> wfold [N][2K] = [A_k wt | B_k wt] (bf16) and the
    per-column constant bias [N] (f32); vcg_conv_dgrad_bwd_bnfold: the input gradient of that conv as one GEMM over
-   [g | yg] (K = 2 Cout) with vcg_conv_dgrad_bwd's light epilogue (ReLU mask fma(y, mscale, mshift) > 0, sums against
+   [g | yg] (K = Cout + Ky; yg = y, Ky = Cout) with vcg_conv_dgrad_bwd's light epilogue (ReLU mask fma(y, mscale, mshift) > 0, sums against
    y); vcg_conv_wgrad_bnfold: dw[Cout][C] (+)= its weight gradient, one GEMM with 2 Cout rows ([g | yg]^T x)
    combined per row with colsum_x = the column sums of x (f32 [C]). VCG_ERR_UNSUPPORTED where the engine does not
    apply. */
@@ -107,7 +107,14 @@ VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale,
    conv output is not read back (bf16 fast engine; VCG_ERR_UNSUPPORTED elsewhere) */
 VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const float* bias, const void* res, void* out, unsigned char* bits, int M, int N, int K, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, void* wfold, float* bias, hipStream_t stream);
-VCG_API int vcg_conv_dgrad_bwd_bnfold(const void* g, const void* yg, const void* wfold, const float* bias, void* out, int N, int H, int W, int C, int Cout, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t stream);
+/* the fold with the conv3 input a2 [M][C] as the second source instead of y3 = a2 w3^T (y3 never read):
+   vcg_bn_bwd_fold_weights_a2: wfold [C][K + C] = [A_k wt | w3^T diag(B) w3] and the bias, colsum_a = column sums of
+   a2 (f32 [C]); the dgrad then runs vcg_conv_dgrad_bwd_bnfold with yg = a2, Ky = C; vcg_bn_bwd_fold_wgrad_a2:
+   dw[K][C] (+)= A P + B (w3 G) + Cc colsum_a from P = g^T a2 and G = a2^T a2 (f32, vcg_conv_wgrad products) and
+   the f32 conv3 weight w3 [K][C]. */
+VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a, void* wfold, float* bias, hipStream_t stream);
+VCG_API int vcg_bn_bwd_fold_wgrad_a2(const float* P, const float* G, const float* w3, int K, int C, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a, float* dw, int accumulate, hipStream_t stream);
+VCG_API int vcg_conv_dgrad_bwd_bnfold(const void* g, const void* yg, int Ky, const void* wfold, const float* bias, void* out, int N, int H, int W, int C, int Cout, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t stream);
 VCG_API long long vcg_conv_wgrad_bnfold_ws_bytes(int N, int H, int W, int C, int Cout);
 VCG_API int vcg_conv_wgrad_bnfold(const void* x, const void* g, const void* yg, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_x, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cout, hipStream_t stream);
 /* nn.Linear / BertSelfAttention matmuls (HF BertModel via model/lang/bert_hugface.py:20; ChapterHead

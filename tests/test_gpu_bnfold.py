@@ -192,3 +192,64 @@ def test_conv1x1_bn_res_relu(shape):
     expect = (pos * (2 ** torch.arange(8, device=DEV, dtype=torch.uint8))).sum(1).to(torch.uint8)
     assert torch.equal(bits, expect)
     assert (bits != rbits).float().mean().item() < 0.02
+
+
+def _case_a2(N, H, W, C, Cout, seed):
+    """conv3 input a2 [M, C], master weight w3 [Cout, C] f32, its bf16 dgrad operand wt [C, Cout], the stored conv
+    output y3 = bf16(a2 bf16(w3)^T) with its batch statistics, a masked upstream gradient g and its BN sums."""
+    gen = torch.Generator().manual_seed(seed)
+    M = N * H * W
+    a2 = _bf(torch.relu(torch.randn(M, C, generator=gen) + 0.2))
+    w3 = (torch.randn(Cout, C, generator=gen) / C ** 0.5).to(DEV)
+    wt = w3.t().contiguous().to(torch.bfloat16)
+    y3 = (a2.double() @ wt.double()).to(torch.bfloat16)
+    yd = y3.double()
+    mean, invstd = yd.mean(0), (yd.var(0, unbiased=False) + 1e-5).rsqrt()
+    g = torch.randn(M, Cout, generator=gen) * 0.02
+    g = _bf(torch.where(torch.rand(M, Cout, generator=gen) < 0.5, g, torch.zeros_like(g)))
+    gamma = (0.5 + torch.rand(Cout, generator=gen)).to(DEV)
+    sum_g = g.double().sum(0)
+    sum_gx = (g.double() * (yd - mean) * invstd).sum(0)
+    f = lambda t: t.float().to(DEV)
+    return dict(M=M, a2=a2, w3=w3, wt=wt, y=y3, g=g, mean=f(mean), invstd=f(invstd), gamma=gamma, sum_g=f(sum_g),
+                sum_gx=f(sum_gx))
+
+
+@pytest.mark.parametrize("shape", [(4, 28, 28, 64, 256), (3, 7, 9, 128, 512), (8, 14, 14, 256, 1024)])
+def test_bnfold_a2_dgrad_wgrad(shape):
+    """The a2 form of the fold (y3 = a2 w3^T never read): input gradient over [g | a2] and weight gradient from
+    g^T a2 and a2^T a2, against float64 of the stored-y3 math and the unfused bn_bwd_apply path."""
+    N, H, W, C, Cout = shape
+    c = _case_a2(N, H, W, C, Cout, 5)
+    M = c["M"]
+    cs = torch.zeros(C, device=DEV)
+    ops.colsum(c["a2"], C, M, C, cs, accumulate=False)
+    wfold, bias = ops.bn_bwd_fold_weights_a2(c["wt"], C, Cout, c["invstd"], c["gamma"], c["sum_g"], c["sum_gx"], M, cs)
+    gf = ops.conv_dgrad_bwd_bnfold(c["g"], c["a2"], wfold, bias, N, H, W, C, Cout, Ky=C)
+    dy = ops.bn_bwd_apply(c["g"], None, c["y"], c["mean"], c["invstd"], c["gamma"], c["sum_g"], c["sum_gx"], Cout,
+                          train_stats=True)
+    gu = ops.conv_dgrad(dy, c["wt"], N, H, W, C, Cout, 1, 1, 1, 0)
+    Pg = torch.empty(Cout, C, 1, 1, device=DEV)
+    G = torch.empty(C, C, 1, 1, device=DEV)
+    ops.conv_wgrad(c["a2"], c["g"], Pg, N, H, W, C, C, Cout, 1, 1, 1, 0, accumulate=False)
+    ops.conv_wgrad(c["a2"], c["a2"], G, N, H, W, C, C, C, 1, 1, 1, 0, accumulate=False)
+    dw_f = torch.full((Cout, C), 0.5, device=DEV)
+    ops.bn_bwd_fold_wgrad_a2(Pg.view(Cout, C), G.view(C, C), c["w3"], Cout, C, c["mean"], c["invstd"], c["gamma"],
+                             c["sum_g"], c["sum_gx"], M, cs, dw_f)
+    dw_u = torch.full((Cout, C, 1, 1), 0.5, device=DEV)
+    ops.conv_wgrad(c["a2"], dy, dw_u, N, H, W, C, C, Cout, 1, 1, 1, 0)
+    torch.cuda.synchronize()
+    A = c["gamma"].double() * c["invstd"].double()
+    B = -A * c["invstd"].double() * c["sum_gx"].double() / M
+    Cc = -A * c["sum_g"].double() / M - B * c["mean"].double()
+    dy_ref = A * c["g"].double() + B * c["y"].double() + Cc
+    ref = dy_ref @ c["wt"].double().t()
+    sc = ref.abs().max().item()
+    ef = (gf.view(M, C).double() - ref).abs().max().item() / sc
+    eu = (gu.view(M, C).double() - ref).abs().max().item() / sc
+    assert ef < max(2.0 * eu, 8e-3), (ef, eu)
+    wref = dy_ref.t() @ c["a2"].double()
+    wsc = wref.abs().max().item()
+    ewf = (dw_f.double() - 0.5 - wref).abs().max().item() / wsc
+    ewu = (dw_u.view(Cout, C).double() - 0.5 - wref).abs().max().item() / wsc
+    assert ewf < max(2.0 * ewu, 5e-3), (ewf, ewu)

@@ -53,6 +53,7 @@ struct OpArgs {
   // backward folded into its consumer GEMM reads [g | y] as one operand (vcg_conv_dgrad_bwd_bnfold)
   const void* ptr2;
   int split2;
+  long long ld2, bytes2;  // the second source's leading dimension / extent (0: those of the first)
 };
 
 // EPI_BWD (fast kernel, conv dgrad): the epilogue of a conv input gradient inside the trunk backward.

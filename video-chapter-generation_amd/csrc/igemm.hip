@@ -1058,27 +1058,123 @@ VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* m
   return VCG_OK;
 }
 
-VCG_API int vcg_conv_dgrad_bwd_bnfold(const void* g, const void* yg, const void* wfold, const float* bias, void* out,
-                                      int N, int H, int W, int C, int Cout, const void* y, const float* mean,
+// The same fold with the conv3 INPUT a2 in place of y3 (y3 = a2 w3^T, so y3 never needs reading): the B y3 term of the
+// input gradient is a2 Q with Q = w3^T diag(B) w3 ([C][C], symmetric), the weight gradient's y3^T a2 is w3 G with
+// G = a2^T a2. wfold [C][K + C] = [A_k wt | bf16(Q)], bias[n] = sum_k (-A_k sum_g_k / M) wt[n][k] - sum_j abar_j
+// bf16(Q[j][n]) with abar = colsum(a2) / M: GEMM + bias = sum g (A w) + sum_j (a2 - abar)_j Q - sum A gbar w, centred
+// like the y3 form (B (y3 - mean) with mean = abar w3^T).
+namespace {
+__global__ __launch_bounds__(256) void bn_fold_weights_a2_kernel(const bf16_t* __restrict__ wt, int C, int K,
+                                                                 const float* __restrict__ invstd,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ sum_g,
+                                                                 const float* __restrict__ sum_gx, float ic,
+                                                                 const float* __restrict__ colsum_a,
+                                                                 bf16_t* __restrict__ wf, float* __restrict__ bias) {
+  __shared__ float bw[2048];  // B_k wt[n][k]
+  __shared__ float red[256];
+  const int n = blockIdx.x, t = threadIdx.x;
+  float acc = 0.f;
+  for (int k = t; k < K; k += 256) {
+    const float is = invstd[k], A = (gamma ? gamma[k] : 1.f) * is;
+    const float B = -A * is * sum_gx[k] * ic;
+    const float w = bf2f(wt[(long long)n * K + k]);
+    bw[k] = B * w;
+    wf[(long long)n * (K + C) + k] = f2bf(A * w);
+    acc += (-A * sum_g[k] * ic) * w;
+  }
+  __syncthreads();
+  for (int j = t; j < C; j += 256) {  // Q[j][n] = sum_k wt[j][k] B_k wt[n][k]
+    const bf16_t* row = wt + (long long)j * K;
+    float q = 0.f;
+    for (int k = 0; k < K; ++k) q = fmaf(bf2f(row[k]), bw[k], q);
+    const bf16_t qb = f2bf(q);
+    wf[(long long)n * (K + C) + K + j] = qb;
+    acc -= colsum_a[j] * ic * bf2f(qb);
+  }
+  red[t] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  if (t == 0) bias[n] = red[0];
+}
+
+// dw[k][j] (+)= A_k P[k][j] + B_k (w3 G)[k][j] + Cc_k cs[j]: P = g^T a2 [K][C], G = a2^T a2 [C][C], w3 [K][C] f32
+__global__ __launch_bounds__(256) void bn_fold_wgrad_a2_kernel(const float* __restrict__ P, const float* __restrict__ G,
+                                                               const float* __restrict__ w3, int K, int C,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ sum_g,
+                                                               const float* __restrict__ sum_gx, float ic,
+                                                               const float* __restrict__ cs, float* __restrict__ dw,
+                                                               int accumulate) {
+  __shared__ float wr[512];
+  const int k = blockIdx.x;
+  for (int i = threadIdx.x; i < C; i += 256) wr[i] = w3[(long long)k * C + i];
+  __syncthreads();
+  const float is = invstd[k], A = (gamma ? gamma[k] : 1.f) * is;
+  const float B = -A * is * sum_gx[k] * ic;
+  const float Cc = -A * sum_g[k] * ic - B * mean[k];
+  for (int j = threadIdx.x; j < C; j += 256) {
+    float wg = 0.f;
+    for (int i = 0; i < C; ++i) wg = fmaf(wr[i], G[(long long)i * C + j], wg);
+    const float v = fmaf(A, P[(long long)k * C + j], fmaf(B, wg, Cc * cs[j]));
+    float* o = dw + (long long)k * C + j;
+    *o = accumulate ? *o + v : v;
+  }
+}
+}  // namespace
+
+VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float* invstd, const float* gamma,
+                                       const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a,
+                                       void* wfold, float* bias, hipStream_t stream) {
+  VCG_REQUIRE(wt && wfold && bias && invstd && sum_g && sum_gx && colsum_a, "null argument");
+  VCG_REQUIRE(C > 0 && K > 0 && K <= 2048, "K must be <= 2048");
+  hipLaunchKernelGGL(bn_fold_weights_a2_kernel, dim3(C), dim3(256), 0, stream, (const bf16_t*)wt, C, K, invstd, gamma,
+                     sum_g, sum_gx, inv_count, colsum_a, (bf16_t*)wfold, bias);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_bn_bwd_fold_wgrad_a2(const float* P, const float* G, const float* w3, int K, int C, const float* mean,
+                                     const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx,
+                                     float inv_count, const float* colsum_a, float* dw, int accumulate,
+                                     hipStream_t stream) {
+  VCG_REQUIRE(P && G && w3 && mean && invstd && sum_g && sum_gx && colsum_a && dw, "null argument");
+  VCG_REQUIRE(C > 0 && C <= 512 && K > 0, "C must be <= 512");
+  hipLaunchKernelGGL(bn_fold_wgrad_a2_kernel, dim3(K), dim3(256), 0, stream, P, G, w3, K, C, mean, invstd, gamma,
+                     sum_g, sum_gx, inv_count, colsum_a, dw, accumulate);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+VCG_API int vcg_conv_dgrad_bwd_bnfold(const void* g, const void* yg, int Ky, const void* wfold, const float* bias,
+                                      void* out, int N, int H, int W, int C, int Cout, const void* y, const float* mean,
                                       const float* invstd, const float* mscale, const float* mshift, float* ws,
                                       long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta,
                                       hipStream_t stream) {
   VCG_REQUIRE(g && yg && wfold && bias && out, "null argument");
-  VCG_REQUIRE(C % 64 == 0 && Cout % 64 == 0, "C and Cout must be multiples of 64");
+  VCG_REQUIRE(C % 64 == 0 && Cout % 64 == 0 && Ky % 64 == 0, "C, Cout and Ky must be multiples of 64");
   VCG_REQUIRE(!mscale || (mshift && y), "mscale needs mshift and y");
   VCG_REQUIRE(!y || (mean && invstd && sum_g && sum_gx), "the reduction needs mean/invstd/sum_g/sum_gx");
-  VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C, 2 * Cout, 1, 1), "workspace too small");
+  VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C, Cout + Ky, 1, 1), "workspace too small");
   const long long M = (long long)N * H * W;
-  if (!fast_gemm_enabled() || M * C * 2 >= 0xFFFFFF00LL || M * Cout * 2 >= 0xFFFFFF00LL || M >= (1LL << 31))
+  if (!fast_gemm_enabled() || M * C * 2 >= 0xFFFFFF00LL || M * Cout * 2 >= 0xFFFFFF00LL || M * Ky * 2 >= 0xFFFFFF00LL ||
+      M >= (1LL << 31))
     return VCG_ERR_UNSUPPORTED;
   GemmParams p{};
   p.M = (int)M;
   p.N = C;
-  p.K = 2 * Cout;
+  p.K = Cout + Ky;
   p.k_per_split = p.K + 64;
   p.a = dense_op(g, Cout, p.M, Cout, 2);
   p.a.ptr2 = yg;
   p.a.split2 = Cout;
+  p.a.ld2 = Ky;
+  p.a.bytes2 = M * Ky * 2;
   p.b = dense_op(wfold, p.K, C, p.K, 2);
   p.bias = bias;
   p.C = out;

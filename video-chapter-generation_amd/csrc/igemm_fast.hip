@@ -41,19 +41,24 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
   static constexpr bool SMALLC = MODE == OP_IM2COL_SMALLC;
   static constexpr int BAD = -(1 << 28);  // spatial base of rows beyond M: every bounds test fails
   __amdgpu_buffer_rsrc_t rsrc, rsrc2;
-  uint32_t oob;
+  uint32_t oob, oob2;
   // element offsets fit in 31 bits: the dispatcher routes only tensors < 4 GB here (32-bit buffer range)
   // Gathers with C >= 64 (one filter tap per 64-wide k tile) keep per row: pb = element offset of the
   // tap (0,0) source pixel, tm = bit mask of the taps that land inside the image (and, for stride-2
   // dgrad, on a stride-2 site); the tap's own offset is then a wave-uniform scalar. Other gathers
   // (the stem, C = 8) keep the pixel coordinates ra/rb and test per lane.
   int off[PER_WAVE];  // dense: element offset of the row (-1 = invalid row); gather: image base
+  int off2[TWO ? PER_WAVE : 1];  // OP_DENSE_K2: the row's offset in the second source (its own ld2)
   int ra[PER_WAVE], rb[PER_WAVE], rc[PER_WAVE], kc[PER_WAVE];
 
   __device__ __forceinline__ void init(const OpArgs& a, long long batch_off, int row0, int wave, int lane) {
     const uint32_t nbytes = (uint32_t)min(a.bytes, (long long)0xFFFFFF00LL);
     rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr), 0, nbytes, 0x00020000);
-    if constexpr (TWO) rsrc2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr2), 0, nbytes, 0x00020000);
+    if constexpr (TWO) {
+      const uint32_t nb2 = a.bytes2 > 0 ? (uint32_t)min(a.bytes2, (long long)0xFFFFFF00LL) : nbytes;
+      rsrc2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.ptr2), 0, nb2, 0x00020000);
+      oob2 = nb2;
+    }
     oob = nbytes;  // offset + 16 > num_records -> the load returns zeros
 #pragma clang loop unroll(full)
     for (int q = 0; q < PER_WAVE; ++q) {
@@ -63,6 +68,7 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
       const bool valid = gr < a.rows;
       if constexpr (!GATHER) {
         off[q] = valid ? (int)(batch_off + (long long)gr * a.ld) : -1;
+        if constexpr (TWO) off2[q] = valid ? (int)((long long)gr * (a.ld2 > 0 ? a.ld2 : a.ld)) : -1;
       } else {
         const int n = gr / (a.GH * a.GW);
         const int rem = gr - n * a.GH * a.GW;
@@ -195,8 +201,10 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
       }
     }
     __amdgpu_buffer_rsrc_t rs = rsrc;
+    bool sec = false;
     if constexpr (TWO) {  // the k tile lies in one source (split2 % 64 == 0): a uniform select
-      if (k0 >= a.split2) {
+      sec = k0 >= a.split2;
+      if (sec) {
         rs = rsrc2;
         k0 -= a.split2;
         kend -= a.split2;
@@ -208,7 +216,11 @@ template <int ROWS, int MODE, int NW = 4> struct FastLoader {
     for (int q = 0; q < PER_WAVE; ++q) {
       const int k = k0 + kc[q];
       uint32_t voff = oob;
-      if constexpr (!GATHER) {
+      if constexpr (TWO) {
+        const int o = sec ? off2[q] : off[q];
+        voff = sec ? oob2 : oob;
+        if (o >= 0 && k < kend) voff = (uint32_t)(o + k) * 2u;
+      } else if constexpr (!GATHER) {
         if (off[q] >= 0 && k < kend) voff = (uint32_t)(off[q] + k) * 2u;
       } else {  // C < 64 (stem): per-lane tap
         const int tap = k >> a.logC;

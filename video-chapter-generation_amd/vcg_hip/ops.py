@@ -191,18 +191,20 @@ def bn_bwd_fold_weights(wt, N, K, mean, invstd, gamma, sum_g, sum_gx, count):
 
 
 def conv_dgrad_bwd_bnfold(g, yg, wfold, bias, N, H, W, C, Cout, y=None, mean=None, invstd=None, mscale=None,
-                          mshift=None, sums=None, dgamma=None, dbeta=None, out=None, workspace=None):
-    """Input gradient of a 1x1 conv whose output gradient is the folded BN backward A g + B yg + Cc
-    (vcg_conv_dgrad_bwd_bnfold; the light epilogue of conv_dgrad_bwd). Returns the masked gradient, or None where
-    the engine does not apply."""
+                          mshift=None, sums=None, dgamma=None, dbeta=None, out=None, workspace=None, Ky=None):
+    """Input gradient of a 1x1 conv whose output gradient is the folded BN backward (vcg_conv_dgrad_bwd_bnfold; the
+    light epilogue of conv_dgrad_bwd): one GEMM over [g | yg], yg = the BN input y (Ky = Cout, bn_bwd_fold_weights) or
+    the conv's input a2 (Ky = C, bn_bwd_fold_weights_a2). Returns the masked gradient, or None where the engine does
+    not apply."""
+    Ky = Cout if Ky is None else Ky
     _chk(g, torch.bfloat16, "g")
     _chk(yg, torch.bfloat16, "yg")
-    assert g.numel() == yg.numel() == N * H * W * Cout and wfold.numel() == C * 2 * Cout
+    assert g.numel() == N * H * W * Cout and yg.numel() == N * H * W * Ky and wfold.numel() == C * (Cout + Ky)
     gout = out if out is not None else torch.empty((N, H, W, C), dtype=g.dtype, device=g.device)
-    nbytes = _lib.query("vcg_conv_dgrad_bwd_ws_bytes", C, 2 * Cout, 1, 1)
+    nbytes = _lib.query("vcg_conv_dgrad_bwd_ws_bytes", C, Cout + Ky, 1, 1)
     if workspace is None or workspace.numel() * 4 < nbytes:
         workspace = ws(nbytes, g.device)
-    rc = _lib.query("vcg_conv_dgrad_bwd_bnfold", P(g), P(yg), P(wfold), P(bias), P(gout), N, H, W, C, Cout, P(y),
+    rc = _lib.query("vcg_conv_dgrad_bwd_bnfold", P(g), P(yg), int(Ky), P(wfold), P(bias), P(gout), N, H, W, C, Cout, P(y),
                     P(mean), P(invstd), P(mscale), P(mshift), P(workspace), workspace.numel() * 4,
                     P(sums[0]) if sums is not None else None, P(sums[1]) if sums is not None else None, P(dgamma),
                     P(dbeta), stream())
@@ -211,6 +213,25 @@ def conv_dgrad_bwd_bnfold(g, yg, wfold, bias, N, H, W, C, Cout, y=None, mean=Non
     if rc != 0:
         raise _lib.VcgError(f"vcg_conv_dgrad_bwd_bnfold failed ({rc}): {_lib.last_error()}")
     return gout
+
+
+def bn_bwd_fold_weights_a2(wt, C, K, invstd, gamma, sum_g, sum_gx, count, colsum_a):
+    """(wfold [C, K + C] bf16, bias [C] f32) of the BN backward folded into the dgrad with the conv input a2 as the
+    second source (vcg_bn_bwd_fold_weights_a2)."""
+    _chk(wt, torch.bfloat16, "wt")
+    wfold = torch.empty((C, K + C), dtype=torch.bfloat16, device=wt.device)
+    bias = torch.empty(C, dtype=torch.float32, device=wt.device)
+    _lib.call("vcg_bn_bwd_fold_weights_a2", P(wt), C, K, P(invstd), P(gamma), P(sum_g), P(sum_gx), float(1.0 / count),
+              P(colsum_a), P(wfold), P(bias), stream())
+    return wfold, bias
+
+
+def bn_bwd_fold_wgrad_a2(Pg, G, w3, K, C, mean, invstd, gamma, sum_g, sum_gx, count, colsum_a, dw, accumulate=True):
+    """dw [K, C] (+)= A Pg + B (w3 G) + Cc colsum_a (vcg_bn_bwd_fold_wgrad_a2)."""
+    for t, n in ((Pg, "Pg"), (G, "G"), (w3, "w3"), (dw, "dw")):
+        _chk(t, torch.float32, n)
+    _lib.call("vcg_bn_bwd_fold_wgrad_a2", P(Pg), P(G), P(w3), K, C, P(mean), P(invstd), P(gamma), P(sum_g), P(sum_gx),
+              float(1.0 / count), P(colsum_a), P(dw), int(accumulate), stream())
 
 
 def conv_wgrad_bnfold(x, g, yg, mean, invstd, gamma, sum_g, sum_gx, count, colsum_x, dw, N, H, W, C, Cout,

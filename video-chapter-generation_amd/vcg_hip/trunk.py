@@ -138,6 +138,10 @@ class ResNetTrunk:
     # ... for blocks with C3 <= this many channels (layers 1-2: HBM-bound conv3 gradients; the deeper layers' doubled
     # K costs more MFMA time than the pass it removes)
     bn_fold_max_c3 = int(os.environ.get("VCG_BN_FOLD_MAXC3", "512"))
+    # ... with conv3's input a2 (C3 / 4 channels) as the second GEMM source instead of y3 (y3 = a2 w3^T: the input
+    # gradient reads [g | a2] against [A w | w3^T diag(B) w3], the weight gradient is A (g^T a2) + B w3 (a2^T a2) + C
+    # colsum(a2)); VCG_BN_FOLD_A2=0: the y3 form
+    bn_fold_a2 = os.environ.get("VCG_BN_FOLD_A2", "1") != "0"
     # batch-statistics forward of a non-first bottleneck with C3 <= this many channels: bn3 + identity + ReLU as a
     # second pass of conv3's GEMM (scale folded into its weight rows, shift as bias; ops.conv1x1_bn_res_relu)
     # instead of reading y3 back in the bn_apply pass (0: off)
@@ -287,6 +291,11 @@ class ResNetTrunk:
             a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
             y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes)
         C3 = y3.shape[-1]
+        a2sum = None
+        if (need_grad and a2 is not None and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2
+                and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16 and b3.mode != "running"
+                and C3 <= ResNetTrunk.bn_fold_max_c3):
+            a2sum = self._colsum_side(a2, planes)  # (the a2 form of the bn3 backward fold: its mean of a2)
         if blk.downsample is not None:
             if side is not None:
                 cur.wait_stream(side)
@@ -307,10 +316,28 @@ class ResNetTrunk:
                 out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=x, bits=True)
         rec = None
         if need_grad:
-            rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, y3=y3, yd=yd, obits=obits, b1=b1, b2=b2, b3=b3,
+            rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, a2sum=a2sum, y3=y3, yd=yd, obits=obits, b1=b1, b2=b2, b3=b3,
                        bd=bd, N=N, H=H, W=W, H2=H2, W2=W2, Cin=Cin, planes=planes, C3=C3, T=T, fold=fold,
                        conv1=conv1)
         return out, rec, H2, W2
+
+    def _colsum_side(self, a, C):
+        """(column sums of a [.., C] as f32 [C], event): on the side stream when there is one."""
+        cur = torch.cuda.current_stream()
+        ws = self._wside(a.device)
+        M = a.numel() // C
+        if ws is None:
+            cs = torch.empty(C, dtype=torch.float32, device=a.device)
+            ops.colsum(a.view(M, C), C, M, C, cs, accumulate=False)
+            return cs, None
+        ws.wait_stream(cur)
+        with torch.cuda.stream(ws):
+            cs = torch.empty(C, dtype=torch.float32, device=a.device)
+            ops.colsum(a.view(M, C), C, M, C, cs, accumulate=False)
+            ev = torch.cuda.Event()
+            ev.record(ws)
+        cs.record_stream(cur)
+        return cs, ev
 
     def _foldable(self, blk, x, need_grad):
         """bf16 scoring forward with every BN of the block on running statistics and a 1x1 / stride-1 conv3."""
@@ -567,6 +594,20 @@ class ResNetTrunk:
         b3, a2, y3 = r["b3"], r["a2"], r["y3"]
         M = N * H2 * W2
 
+        a2s = r.get("a2sum")
+        if a2s is not None:  # the a2 form: g^T a2 and a2^T a2 (plain weight-gradient GEMMs), combined per row
+            def wfn():
+                Pg = torch.empty((C3, planes, 1, 1), dtype=torch.float32, device=a2.device)
+                G = torch.empty((planes, planes, 1, 1), dtype=torch.float32, device=a2.device)
+                ops.conv_wgrad(a2, g, Pg, N, H2, W2, planes, planes, C3, 1, 1, 1, 0, accumulate=False)
+                ops.conv_wgrad(a2, a2, G, N, H2, W2, planes, planes, planes, 1, 1, 1, 0, accumulate=False)
+                ops.bn_bwd_fold_wgrad_a2(Pg.view(C3, planes), G.view(planes, planes),
+                                         blk.conv3.weight.data.view(C3, planes), C3, planes, b3.mean, b3.invstd,
+                                         b3.bn.weight, sums3[0], sums3[1], M, a2s[0],
+                                         blk.conv3.weight.grad.view(C3, planes))
+                return True
+            return self._async(wfn, a2, g, sums3, a2s[0])
+
         def wfn():
             cs = torch.empty(planes, dtype=torch.float32, device=a2.device)
             ops.colsum(a2.view(M, planes), planes, M, planes, cs, accumulate=False)
@@ -574,18 +615,27 @@ class ResNetTrunk:
                                          blk.conv3.weight.grad, N, H2, W2, planes, C3)
         return self._async(wfn, a2, g, y3, sums3)
 
-    def _dgrad_bn_fold(self, conv, g, y3, b3, sums3, N, H, W, y, st, C, C3):
-        """_dgrad_bn of conv3 with bn3's backward folded in: one GEMM over [g | y3] against [A w | B w] plus the
-        constant column bias. None where the engine does not apply."""
+    def _dgrad_bn_fold(self, conv, g, y3, b3, sums3, N, H, W, y, st, C, C3, a2=None, a2sum=None):
+        """_dgrad_bn of conv3 with bn3's backward folded in: one GEMM over [g | y3] against [A w | B w] (or, with
+        a2sum = (colsum(a2), event), over [g | a2] against [A w | w^T diag(B) w]) plus the constant column bias. None
+        where the engine does not apply."""
         Cout, Cin, KH, KW, s, p = _conv_shape(conv)
         wt = self._wprep_t(conv, Cin)
         M = N * H * W
-        wfold, bias = ops.bn_bwd_fold_weights(wt.view(Cin, C3), Cin, C3, b3.mean, b3.invstd, b3.bn.weight, sums3[0],
-                                              sums3[1], M)
+        if a2sum is not None:
+            if a2sum[1] is not None:
+                torch.cuda.current_stream().wait_event(a2sum[1])
+            wfold, bias = ops.bn_bwd_fold_weights_a2(wt.view(Cin, C3), Cin, C3, b3.invstd, b3.bn.weight, sums3[0],
+                                                     sums3[1], M, a2sum[0])
+            src, Ky = a2, Cin
+        else:
+            wfold, bias = ops.bn_bwd_fold_weights(wt.view(Cin, C3), Cin, C3, b3.mean, b3.invstd, b3.bn.weight,
+                                                  sums3[0], sums3[1], M)
+            src, Ky = y3, C3
         sums = torch.empty((2, C), dtype=torch.float32, device=y.device)
         dg, db = self._bn_grads(st)
-        g2 = ops.conv_dgrad_bwd_bnfold(g, y3, wfold, bias, N, H, W, Cin, C3, y=y, mean=st.mean, invstd=st.invstd,
-                                       mscale=st.scale, mshift=st.shift, sums=sums, dgamma=dg, dbeta=db)
+        g2 = ops.conv_dgrad_bwd_bnfold(g, src, wfold, bias, N, H, W, Cin, C3, y=y, mean=st.mean, invstd=st.invstd,
+                                       mscale=st.scale, mshift=st.shift, sums=sums, dgamma=dg, dbeta=db, Ky=Ky)
         if g2 is None:
             return None
         ResNetTrunk.path_counts["fused"] += 1
@@ -642,7 +692,7 @@ class ResNetTrunk:
         dy2 = None
         if bnf is not None:
             dy2 = self._dgrad_bn_fold(blk.conv3, bnf[0], r["y3"], r["b3"], bnf[1], N, H2, W2, r["y2"], r["b2"], planes,
-                                      C3)
+                                      C3, a2=r["a2"], a2sum=r.get("a2sum"))
             if dy2 is None:  # (the fused engine does not apply: the unfused pass, and conv3's dgrad on dy3)
                 dy3 = self._bn_apply_bwd(bnf[0], r["y3"], r["b3"], C3, bnf[1])
         if dy2 is None:
