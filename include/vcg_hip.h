@@ -112,6 +112,13 @@ VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* m
    a2 (f32 [C]); the dgrad then runs vcg_conv_dgrad_bwd_bnfold with yg = a2, Ky = C; vcg_bn_bwd_fold_wgrad_a2:
    dw[K][C] (+)= A P + B (w3 G) + Cc colsum_a from P = g^T a2 and G = a2^T a2 (f32, vcg_conv_wgrad products) and
    the f32 conv3 weight w3 [K][C]. */
+/* bn3 with y3 never stored (the forward keeps only its statistics, vcg_conv1x1_stats, and applies it by
+   vcg_conv1x1_bn_res_relu): sum_gx of its backward from P = g^T a2 (vcg_conv_wgrad) and the forward's bf16 conv weight
+   w [K][C]: sum_gx[k] = invstd_k (sum_j w[k][j] P[k][j] - mean_k sum_g[k]), dgamma (optional) += sum_gx; sum_g
+   comes from the producing dgrad's epilogue run with the mask bits and no y (vcg_conv_dgrad_bwd: y NULL, bits,
+   sum_g / sum_gx given: sum_gx written as 0). */
+VCG_API int vcg_conv1x1_stats(const void* x, const void* w, float* stats, int M, int N, int K, hipStream_t stream);
+VCG_API int vcg_bn_bwd_sumgx_from_wgrad(const float* P, const void* w, int K, int C, const float* mean, const float* invstd, const float* sum_g, float* sum_gx, float* dgamma, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a, void* wfold, float* bias, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_wgrad_a2(const float* P, const float* G, const float* w3, int K, int C, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a, float* dw, int accumulate, hipStream_t stream);
 VCG_API int vcg_conv_dgrad_bwd_bnfold(const void* g, const void* yg, int Ky, const void* wfold, const float* bias, void* out, int N, int H, int W, int C, int Cout, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t stream);

@@ -253,3 +253,63 @@ def test_bnfold_a2_dgrad_wgrad(shape):
     ewf = (dw_f.double() - 0.5 - wref).abs().max().item() / wsc
     ewu = (dw_u.view(Cout, C).double() - 0.5 - wref).abs().max().item() / wsc
     assert ewf < max(2.0 * ewu, 5e-3), (ewf, ewu)
+
+
+def test_conv1x1_stats_matches_stored():
+    """Statistics-only conv3 GEMM (y3 never stored) == the storing conv's statistics, bit for bit."""
+    N, H, W, C, Cout = 4, 28, 28, 64, 256
+    M = N * H * W
+    gen = torch.Generator().manual_seed(9)
+    x = _bf(torch.relu(torch.randn(M, C, generator=gen)))
+    w = _bf(torch.randn(Cout, C, generator=gen) / C ** 0.5)
+    s1, s2 = ops.stats_buffer(Cout, M, DEV), ops.stats_buffer(Cout, M, DEV)
+    ops.conv_fwd(x.view(N, H, W, C), w, N, H, W, C, Cout, 1, 1, 1, 0, stats=s1)
+    assert ops.conv1x1_stats(x, w, s2, M, Cout, C)
+    outs = []
+    for st in (s1, s2):
+        mean, inv, sc, sh = (torch.empty(Cout, device=DEV) for _ in range(4))
+        ops.bn_finalize(st, ops.stats_tiles(M), M, Cout, torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV),
+                        mean, inv, sc, sh)
+        outs.append((mean, inv))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("shape", [(4, 28, 28, 256, 64, 4), (4, 14, 14, 512, 128, 4), (8, 14, 14, 1024, 256, 4)])
+def test_dgrad_bits_only_sums_and_sumgx(shape):
+    """The conv1 dgrad epilogue with the mask bits and no y (the previous block's y3 not stored): the same g and
+    sum g as with y, sum_gx written 0; sum_gx from g^T a2 (bn_bwd_sumgx_from_wgrad) matches the y3 reduction."""
+    N, H, W, C, Co, T = shape
+    M = N * H * W
+    gen = torch.Generator().manual_seed(11)
+    dy = _bf(torch.randn(M, Co, generator=gen) * 0.1)
+    wt = _bf(torch.randn(C, Co, generator=gen) / Co ** 0.5)
+    res = _bf(torch.randn(M, C, generator=gen) * 0.1)
+    planes = C // 4
+    a2 = _bf(torch.relu(torch.randn(M, planes, generator=gen)))
+    w3 = _bf(torch.randn(C, planes, generator=gen) / planes ** 0.5)  # the previous block's conv3 (forward layout)
+    y3 = (a2.double() @ w3.double().t()).to(torch.bfloat16)
+    bits = ((torch.rand(M * C // 8, generator=gen) * 255).to(torch.uint8)).to(DEV)
+    mean = y3.double().mean(0).float()
+    invstd = (y3.double().var(0, unbiased=False) + 1e-5).rsqrt().float()
+    fold = C // 8
+    outs = []
+    for yy in (y3, None):
+        sums = torch.zeros(2, C, device=DEV)
+        gg = ops.conv_dgrad_bwd(dy.view(N, H, W, Co), wt, N, H, W, C, Co, 1, 1, 1, 0, tsm_T=T, tsm_fold=fold,
+                                res=res.view(N, H, W, C), bits=bits, y=None if yy is None else yy.view(N, H, W, C),
+                                mean=mean, invstd=invstd, sums=sums)
+        outs.append((gg, sums))
+    torch.cuda.synchronize()
+    (g1, s1), (g2, s2) = outs
+    assert torch.equal(g1, g2)
+    assert torch.equal(s1[0], s2[0]) and (s2[1] == 0).all()
+    Pg = torch.empty(C, planes, 1, 1, device=DEV)
+    ops.conv_wgrad(a2.view(N, H, W, planes), g2.view(M, C), Pg, N, H, W, planes, planes, C, 1, 1, 1, 0,
+                   accumulate=False)
+    sgx = torch.empty(C, device=DEV)
+    ops.bn_bwd_sumgx_from_wgrad(Pg.view(C, planes), w3, C, planes, mean, invstd, s2[0], sgx)
+    torch.cuda.synchronize()
+    ref = (g2.view(M, C).double() * (a2.double() @ w3.double().t() - mean.double()) * invstd.double()).sum(0)
+    assert (sgx.double() - ref).abs().max().item() < 2e-3 * (ref.abs().max().item() + 1e-3)
+    assert (s1[1].double() - ref).abs().max().item() < 2e-2 * (ref.abs().max().item() + 1e-3)

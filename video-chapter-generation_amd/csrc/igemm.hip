@@ -763,7 +763,8 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   e.fd_w = make_fastdiv((uint32_t)W); e.y = y; e.mean = mean; e.invstd = invstd; e.msc = mscale; e.msh = mshift;
   e.y2 = y2; e.mean2 = mean2; e.invstd2 = invstd2;
   e.part = ws;
-  e.nred = y ? (y2 ? 3 : 2) : 0;
+  // (bits without y: the sums row of g only -- sum_gx comes from elsewhere, the previous block's y3 not stored)
+  e.nred = y ? (y2 ? 3 : 2) : ((bits && sum_g && sum_gx) ? 2 : 0);
   if (subpix) {
     bf16_t* wpk = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(ws) + dgrad_bwd_part_bytes(C));
     const int cH = H / 2, cW = W / 2;
@@ -1128,6 +1129,38 @@ __global__ __launch_bounds__(256) void bn_fold_wgrad_a2_kernel(const float* __re
 }
 }  // namespace
 
+namespace {
+__global__ __launch_bounds__(64) void bn_sumgx_kernel(const float* __restrict__ P, const bf16_t* __restrict__ w, int C,
+                                                      const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                      const float* __restrict__ sum_g, float* __restrict__ sum_gx,
+                                                      float* __restrict__ dgamma) {
+  const int k = blockIdx.x, t = threadIdx.x;
+  float a = 0.f;
+  for (int j = t; j < C; j += 64) a = fmaf(bf2f(w[(long long)k * C + j]), P[(long long)k * C + j], a);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if (t == 0) {
+    const float v = invstd[k] * (a - mean[k] * sum_g[k]);
+    sum_gx[k] = v;
+    if (dgamma) dgamma[k] += v;
+  }
+}
+}  // namespace
+
+// sum_gx[k] = invstd_k (sum_m g[m][k] y3[m][k] - mean_k sum_g[k]) of a BN whose input y3 = a2 w^T was never stored:
+// sum_m g y3 = sum_j w[k][j] P[k][j] with P = g^T a2 (f32 [K][C], a weight-gradient GEMM) and w the conv's bf16 forward
+// weight [K][C]; dgamma (optional) += sum_gx (as vcg_bn_bwd_finalize would have added)
+VCG_API int vcg_bn_bwd_sumgx_from_wgrad(const float* P, const void* w, int K, int C, const float* mean,
+                                        const float* invstd, const float* sum_g, float* sum_gx, float* dgamma,
+                                        hipStream_t stream) {
+  VCG_REQUIRE(P && w && mean && invstd && sum_g && sum_gx, "null argument");
+  VCG_REQUIRE(K > 0 && C > 0, "empty");
+  hipLaunchKernelGGL(bn_sumgx_kernel, dim3(K), dim3(64), 0, stream, P, (const bf16_t*)w, C, mean, invstd, sum_g,
+                     sum_gx, dgamma);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
 VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float* invstd, const float* gamma,
                                        const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a,
                                        void* wfold, float* bias, hipStream_t stream) {
@@ -1254,6 +1287,31 @@ VCG_API int vcg_conv_wgrad_bnfold(const void* x, const void* g, const void* yg, 
                        splits, Cout, Nn, mean, invstd, gamma, sum_g, sum_gx, inv_count, colsum_x, dw, accumulate);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
+}
+
+// BatchNorm statistics of a 1x1 conv output that is never stored (the EPI_STATS epilogue without its stores): the
+// bn3 of a bottleneck whose apply is a second GEMM pass (vcg_conv1x1_bn_res_relu) and whose backward needs no y3
+VCG_API int vcg_conv1x1_stats(const void* x, const void* w, float* stats, int M, int N, int K, hipStream_t stream) {
+  VCG_REQUIRE(x && w && stats, "null argument");
+  VCG_REQUIRE(M > 0 && N % 64 == 0 && K % 64 == 0, "N and K must be multiples of 64");
+  if (!fast_gemm_enabled() || (long long)M * K * 2 >= 0xFFFFFF00LL) return VCG_ERR_UNSUPPORTED;
+  GemmParams p{};
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.k_per_split = K + 64;
+  p.a = dense_op(x, K, M, K, 2);
+  p.b = dense_op(w, K, N, K, 2);
+  p.C = nullptr;
+  p.ldc = N;
+  p.alpha = 1.f;
+  p.stats = stats;
+  if (FILE* f = gemm_log()) {
+    fprintf(f, "a=0 b=0 epi=1 M=%d N=%d K=%d z=1 fast=1 conv=1x1/1 C=%d nostore=1\n", M, N, K, K);
+    fflush(f);
+  }
+  const int rc = run_fast_gemm(p, OP_DENSE_K, EPI_STATS, 1, stream);
+  return rc < 0 ? VCG_ERR_UNSUPPORTED : rc;
 }
 
 // out = relu(bf16(x wfold^T + bias) + res) with the ReLU mask bits: a batch-statistics bn3 (scale folded into the

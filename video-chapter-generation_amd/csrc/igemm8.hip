@@ -376,7 +376,8 @@ static int launch_g8(const GemmParams& p, hipStream_t s) {
 // amode: igemm.h OP_DENSE_K / OP_IM2COL (p.a.tsm_fold > 0: TSM); returns -1 where the kernel does not apply
 int run_gemm8(const GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   const int mode = g8_mode();
-  if (mode == 0 || z != 1 || p.batch_inner > 0 || p.K < 256 || p.residual || p.aux || (epi != EPI_STORE && epi != EPI_STATS))
+  if (mode == 0 || z != 1 || p.batch_inner > 0 || p.K < 256 || p.residual || p.aux || !p.C ||
+      (epi != EPI_STORE && epi != EPI_STATS))
     return -1;
   if (p.N % 128 != 0 || (p.ldc & 7) != 0 || ((uintptr_t)p.C & 15) != 0 || (p.act & ~0xFF) != 0) return -1;
   const OpArgs& a = p.a;

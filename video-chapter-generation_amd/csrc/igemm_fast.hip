@@ -567,7 +567,7 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = ((bv[kk] >> i) & 1u) ? v[i] : 0.f;
       }
-      float yy[8];
+      float yy[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (yp) {
         unpack8(yv[kk], yy);
         if (e.msc) {
@@ -586,7 +586,7 @@ __device__ __forceinline__ void stage_flush_bwd(const bf16_t* stA, const bf16_t*
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           s1[i] += v[i];
-          s2[i] = fmaf(v[i], yy[i] - mu[i], s2[i]);
+          s2[i] = yp ? fmaf(v[i], yy[i] - mu[i], s2[i]) : s2[i];
         }
         if (y2p) {
           float y2[8];
@@ -660,7 +660,7 @@ __device__ __forceinline__ void stage_flush_stats(const bf16_t* stA, const bf16_
     const int id = threadIdx.x + NTH * k;
     const int m = m0 + id / CPR;
     if (m < mlim && n < p.N) {
-      *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + n) = q[k];
+      if (Cout) *reinterpret_cast<uint4*>(Cout + (long long)m * p.ldc + n) = q[k];  // (null: statistics only)
       float v[8];
       unpack8(q[k], v);
       if (cnt == 0) {
@@ -753,6 +753,7 @@ __device__ unsigned long long g_fast_stamps[64 * 4];
 // 16-B chunk of stage + LDS operands and stores it. Same products, order and rounding as stage_flush_bwd
 // (bit-identical g; per-thread column sums combined in a fixed order by bwd_finish).
 constexpr int XF_HASY = 1;  // y + mask bits present (the BN sums of the previous block's bn3)
+constexpr int XF_BITS = 4;  // mask bits without y: sum g only (the previous block's y3 is not stored, trunk.py)
 constexpr int XF_Y2 = 2;    // y2 present (the previous block's downsample BN)
 
 __device__ __forceinline__ int bwd_tsm_shift(const BwdEpi& e, int n) {
@@ -762,7 +763,8 @@ __device__ __forceinline__ int bwd_tsm_shift(const BwdEpi& e, int n) {
 
 // LDS bytes of one ring slot / of the fixed part (weights, stage, column parameters) and the ring depth
 __host__ __device__ constexpr int bwd_stream_buf(int KC, int XF) {
-  return 2 * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 + 8 * 256 : 0) + ((XF & XF_Y2) ? 8192 : 0);
+  return 2 * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 : 0) + ((XF & (XF_HASY | XF_BITS)) ? 8 * 256 : 0) +
+         ((XF & XF_Y2) ? 8192 : 0);
 }
 __host__ __device__ constexpr int bwd_stream_nbuf(int KC, int XF) {
   return (160 * 1024 - (KC * 8192 + 8192 + 1024)) / bwd_stream_buf(KC, XF) >= 4 ? 4
@@ -772,6 +774,7 @@ __host__ __device__ constexpr int bwd_stream_nbuf(int KC, int XF) {
 template <int KC, int XF>
 __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   constexpr bool HASY = (XF & XF_HASY) != 0, Y2 = (XF & XF_Y2) != 0;
+  constexpr bool HASB = HASY || (XF & XF_BITS) != 0;  // mask bits + sum g
   static_assert(!Y2 || HASY, "y2 comes with y");
   constexpr int TM = 64, TN = 64, NTH = 512, NW = 8;
   constexpr int NBUF = bwd_stream_nbuf(KC, XF);
@@ -779,7 +782,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   constexpr int AT = KC * TM * 64 * 2;  // one A tile ([64][64] swizzled sub-tiles, fast_frag layout); two per slot
   constexpr int OB = TM * TN * 2;       // one row-major [64][64] bf16 epilogue operand (res / y / y2)
   constexpr int OFF_R = 2 * AT, OFF_Y = OFF_R + OB, OFF_BITS = OFF_Y + (HASY ? OB : 0);
-  constexpr int OFF_Y2 = OFF_BITS + (HASY ? NW * 256 : 0);  // mask bytes [64][8]: 16 lanes x 4 B per wave (+ pad)
+  constexpr int OFF_Y2 = OFF_BITS + (HASB ? NW * 256 : 0);  // mask bytes [64][8]: 16 lanes x 4 B per wave (+ pad)
   constexpr int BUF = OFF_Y2 + (Y2 ? OB : 0);
   static_assert(BUF == bwd_stream_buf(KC, XF), "slot layout");
   constexpr int BB = KC * TN * 64 * 2;
@@ -789,7 +792,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   static_assert(NBUF * BUF >= 3 * NTH * 8 * 4, "bwd_finish scratch");
   // VMEM instructions per wave: one tile's DMA (A 1 per k tile and A tile, res 1, y 1 + bits 1, y2 1), one flush's
   // stores (1)
-  constexpr int OPS1 = KC + 1 + (HASY ? 2 : 0) + (Y2 ? 1 : 0), OPS2 = OPS1 + KC;
+  constexpr int OPS1 = KC + 1 + (HASY ? 1 : 0) + (HASB ? 1 : 0) + (Y2 ? 1 : 0), OPS2 = OPS1 + KC;
   constexpr int VMW1 = (NBUF - 2) * OPS1 + (NBUF - 1), VMW2 = (NBUF - 2) * OPS2 + (NBUF - 1);
   static_assert(VMW2 < 64, "vmcnt field");
   __shared__ __attribute__((aligned(1024))) char smem[TOTAL];  // the ONLY LDS object (see FastLoader)
@@ -845,8 +848,8 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   const __amdgpu_buffer_rsrc_t rs_res = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.res), 0, nb_res, 0x00020000);
   __amdgpu_buffer_rsrc_t rs_y = rs_res, rs_y2 = rs_res, rs_bits = rs_res;
   uint32_t nb_bits = 0;
-  if constexpr (HASY) {
-    rs_y = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.y), 0, nb_full, 0x00020000);
+  if constexpr (HASY) rs_y = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.y), 0, nb_full, 0x00020000);
+  if constexpr (HASB) {
     nb_bits = (uint32_t)(((long long)p.M * ld) >> 3);
     rs_bits = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(e.bits), 0, nb_bits, 0x00020000);
   }
@@ -899,7 +902,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_y2, (lds_void_t*)(buf + OFF_Y2 + wave * 1024), 16,
                                                  ok ? yoff : nb_full, 0, 0, 0);
     }
-    if constexpr (HASY) {  // mask bytes: lane < 16 -> row 8 wave + lane / 2, 32 columns (dword lane & 1)
+    if constexpr (HASB) {  // mask bytes: lane < 16 -> row 8 wave + lane / 2, 32 columns (dword lane & 1)
       const int dr = d0 + 8 * wave + ((lane & 15) >> 1), n = n0 + 32 * (lane & 1);
       const bool ok = lane < 16 && dr < p.M;
       const uint32_t boff = (uint32_t)(((long long)dr * ld + n) >> 3);
@@ -974,10 +977,10 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
       uint32_t bits = 0xFFu;
       asm volatile("ds_read_b128 %0, %1" : "=v"(sv) : "v"(lds_u32(St + r * 64 + 8 * st_slot<64>(r, cc))) : "memory");
       asm volatile("ds_read_b128 %0, %1" : "=v"(rv) : "v"(lds_u32(R + r * 64 + 8 * cc)) : "memory");
-      if constexpr (HASY) {
+      if constexpr (HASY)
         asm volatile("ds_read_b128 %0, %1" : "=v"(yv) : "v"(lds_u32(Y + r * 64 + 8 * cc)) : "memory");
+      if constexpr (HASB)
         asm volatile("ds_read_u8 %0, %1" : "=v"(bits) : "v"(lds_u32(Bt + (r >> 3) * 256 + (r & 7) * 8 + cc)) : "memory");
-      }
       if constexpr (Y2)
         asm volatile("ds_read_b128 %0, %1" : "=v"(y2v) : "v"(lds_u32(Y2p + r * 64 + 8 * cc)) : "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -988,7 +991,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
         unpack8(rv, rr);
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] += rr[i];
-        if constexpr (HASY) {
+        if constexpr (HASB) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) v[i] = ((bits >> i) & 1u) ? v[i] : 0.f;
         }
@@ -998,6 +1001,11 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
         o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
         o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
         *reinterpret_cast<uint4*>(Cout + (long long)d * ld + n) = o;
+        if constexpr (HASB && !HASY) {
+          unpack8(o, v);  // sum of the stored (rounded) gradient
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s1[i] += v[i];
+        }
         if constexpr (HASY) {
           float yy[8];
           unpack8(o, v);  // statistics of the stored (rounded) gradient
@@ -1019,7 +1027,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
     FAST_STAMP(t, 3);
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-  if constexpr (HASY) {
+  if constexpr (HASB) {
     if (e.nred > 0) bwd_finish<256, 64>(p, reinterpret_cast<float*>(smem), cpar + 2 * TN, s1, s2, s3, n0, by);
   }
 }
@@ -1890,8 +1898,8 @@ static bool bwd_stream_ok(const GemmParams& p) {
   if (!dense || (p.K != 64 && p.K != 128) || p.N % 64 != 0 || p.batch_inner > 0 || p.ldc != p.N || p.a.ld != p.K ||
       !e.res || e.msc || e.sub || bwd_light(p))
     return false;
-  if ((e.y != nullptr) != (e.bits != nullptr) || (e.y2 && !e.y)) return false;
-  if (e.y && e.nred < 2) return false;
+  if ((e.y && !e.bits) || (e.y2 && !e.y)) return false;
+  if ((e.y || e.bits) && e.nred < 2) return false;
   if (e.tsm_T > 0 && e.tsm_fold % 32 != 0) return false;  // one TSM shift per wave's 32 columns
   if (((uintptr_t)p.C | (uintptr_t)e.res | (uintptr_t)e.y | (uintptr_t)e.y2 | (uintptr_t)p.a.ptr) & 15) return false;
   if (e.res_s > 1 && (p.M % e.hw) != 0) return false;
@@ -1956,7 +1964,7 @@ static int launch_bwd_stream(const GemmParams& p, hipStream_t s) {
 
 template <int KC>
 static int run_bwd_stream(const GemmParams& p, hipStream_t s) {
-  if (!p.bwd.y) return launch_bwd_stream<KC, 0>(p, s);
+  if (!p.bwd.y) return p.bwd.bits ? launch_bwd_stream<KC, XF_BITS>(p, s) : launch_bwd_stream<KC, 0>(p, s);
   if (!p.bwd.y2) return launch_bwd_stream<KC, XF_HASY>(p, s);
   return launch_bwd_stream<KC, XF_HASY | XF_Y2>(p, s);
 }

@@ -164,6 +164,27 @@ def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_f
     return g
 
 
+def conv1x1_stats(x, w, stats, M, N, K):
+    """BatchNorm statistics of x [M, K] @ w [N, K]^T without storing the product (vcg_conv1x1_stats). False where
+    the fused engine does not apply."""
+    _chk(x, torch.bfloat16, "x")
+    _chk(w, torch.bfloat16, "w")
+    rc = _lib.query("vcg_conv1x1_stats", P(x), P(w), P(stats), M, N, K, stream())
+    if rc == -2:
+        return False
+    if rc != 0:
+        raise _lib.VcgError(f"vcg_conv1x1_stats failed ({rc}): {_lib.last_error()}")
+    return True
+
+
+def bn_bwd_sumgx_from_wgrad(Pg, w, K, C, mean, invstd, sum_g, sum_gx, dgamma=None):
+    """sum_gx of a BN whose input y3 = a2 w^T was not stored, from Pg = g^T a2 (vcg_bn_bwd_sumgx_from_wgrad)."""
+    _chk(Pg, torch.float32, "Pg")
+    _chk(w, torch.bfloat16, "w")
+    _lib.call("vcg_bn_bwd_sumgx_from_wgrad", P(Pg), P(w), K, C, P(mean), P(invstd), P(sum_g), P(sum_gx), P(dgamma),
+              stream())
+
+
 def conv1x1_bn_res_relu(x, wfold, bias, res, M, N, K):
     """(out, bits): relu(bf16(x @ wfold^T + bias) + res) and its ReLU mask bits (vcg_conv1x1_bn_res_relu), or None
     where the fused engine does not apply."""

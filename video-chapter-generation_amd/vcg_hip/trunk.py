@@ -142,6 +142,10 @@ class ResNetTrunk:
     # gradient reads [g | a2] against [A w | w3^T diag(B) w3], the weight gradient is A (g^T a2) + B w3 (a2^T a2) + C
     # colsum(a2)); VCG_BN_FOLD_A2=0: the y3 form
     bn_fold_a2 = os.environ.get("VCG_BN_FOLD_A2", "1") != "0"
+    # ... and with both (non-first blocks): y3 is not stored at all -- conv3's forward GEMM keeps only the BN
+    # statistics (ops.conv1x1_stats), the next block's conv1 dgrad reduces only sum g, and sum_gx comes from g^T a2
+    # (ops.bn_bwd_sumgx_from_wgrad), which is also the weight gradient's first product; VCG_Y3_DROP=0: stored
+    y3_drop = os.environ.get("VCG_Y3_DROP", "1") != "0"
     # batch-statistics forward of a non-first bottleneck with C3 <= this many channels: bn3 + identity + ReLU as a
     # second pass of conv3's GEMM (scale folded into its weight rows, shift as bias; ops.conv1x1_bn_res_relu)
     # instead of reading y3 back in the bn_apply pass (0: off)
@@ -176,7 +180,16 @@ class ResNetTrunk:
             return self.wc.bwd[id(conv)]
         return ops.weight_prep(conv.weight.data, Cin, self.dtype, transposed=True)
 
-    def _conv_bn(self, x, conv, bn, N, H, W, C, tsm_T=0, tsm_fold=0, in_bn=None):
+    def _drop_y3(self, blk, planes, need_grad):
+        """This bottleneck's training forward keeps only bn3's statistics (see y3_drop)."""
+        C3 = blk.conv3.out_channels
+        return (ResNetTrunk.y3_drop and need_grad and blk.downsample is None and ResNetTrunk.bn_fold_bwd
+                and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16
+                and not ResNetTrunk.fused_bnin and C3 <= ResNetTrunk.bn_fold_max_c3
+                and C3 <= ResNetTrunk.bn3_gemm_max_c3 and C3 % 128 == 0 and planes >= 64
+                and (planes & (planes - 1)) == 0 and blk.conv3.stride[0] == 1 and bn_mode(blk.bn3) != "running")
+
+    def _conv_bn(self, x, conv, bn, N, H, W, C, tsm_T=0, tsm_fold=0, in_bn=None, store=True):
         """conv -> BN statistics (+ running-stat update). in_bn = (scale, shift): the conv's input is
         relu(x * scale + shift) (the previous BN + ReLU), applied on load by the fused engine; returns y = None when
         that engine does not take the shape (the caller then materialises the input)."""
@@ -206,7 +219,10 @@ class ResNetTrunk:
         else:
             mt = ops.stats_tiles(M)
             stats = ops.stats_buffer(Cout, M, x.device)
-            y = ops.conv_fwd(x, w, N, H, W, C, Cout, KH, KW, s, p, tsm_T, tsm_fold, stats=stats)
+            y = None
+            if store or (KH, KW, s, p, tsm_fold) != (1, 1, 1, 0, 0) or not ops.conv1x1_stats(x.view(M, C), w, stats,
+                                                                                               M, Cout, C):
+                y = ops.conv_fwd(x, w, N, H, W, C, Cout, KH, KW, s, p, tsm_T, tsm_fold, stats=stats)
             upd = mode == "train"
             mom = bn.momentum if bn.momentum is not None else 0.1
             ops.bn_finalize(stats, mt, M, Cout, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
@@ -287,10 +303,11 @@ class ResNetTrunk:
         y3 = None
         if self.dtype == torch.bfloat16 and ResNetTrunk.fused_bnin:
             y3, b3, _, _ = self._conv_bn(y2, blk.conv3, blk.bn3, N, H2, W2, planes, in_bn=(b2.scale, b2.shift))
+        drop = y3 is None and self._drop_y3(blk, planes, need_grad)
         if y3 is None:
             a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
-            y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes)
-        C3 = y3.shape[-1]
+            y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
+        C3 = blk.conv3.out_channels
         a2sum = None
         if (need_grad and a2 is not None and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2
                 and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16 and b3.mode != "running"
@@ -313,6 +330,8 @@ class ResNetTrunk:
             if r2 is not None:
                 out, obits = r2
             else:
+                if y3 is None:  # (the GEMM pass did not apply: the conv output after all)
+                    y3 = self._conv3_out(blk, a2, N, H2, W2, planes)
                 out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=x, bits=True)
         rec = None
         if need_grad:
@@ -320,6 +339,16 @@ class ResNetTrunk:
                        bd=bd, N=N, H=H, W=W, H2=H2, W2=W2, Cin=Cin, planes=planes, C3=C3, T=T, fold=fold,
                        conv1=conv1)
         return out, rec, H2, W2
+
+    def _conv3_out(self, blk, a2, N, H2, W2, planes):
+        """conv3's output y3 recomputed from its input (where a stats-only forward dropped it)"""
+        C3 = blk.conv3.out_channels
+        return ops.conv_fwd(a2, self._wprep(blk.conv3, planes), N, H2, W2, planes, C3, 1, 1, 1, 0)
+
+    def _y3(self, r):
+        if r["y3"] is None:
+            r["y3"] = self._conv3_out(r["blk"], r["a2"], r["N"], r["H2"], r["W2"], r["planes"])
+        return r["y3"]
 
     def _colsum_side(self, a, C):
         """(column sums of a [.., C] as f32 [C], event): on the side stream when there is one."""
@@ -596,17 +625,21 @@ class ResNetTrunk:
 
         a2s = r.get("a2sum")
         if a2s is not None:  # the a2 form: g^T a2 and a2^T a2 (plain weight-gradient GEMMs), combined per row
+            Pg0 = r.get("Pg")
+
             def wfn():
-                Pg = torch.empty((C3, planes, 1, 1), dtype=torch.float32, device=a2.device)
                 G = torch.empty((planes, planes, 1, 1), dtype=torch.float32, device=a2.device)
-                ops.conv_wgrad(a2, g, Pg, N, H2, W2, planes, planes, C3, 1, 1, 1, 0, accumulate=False)
+                Pg = Pg0
+                if Pg is None:
+                    Pg = torch.empty((C3, planes, 1, 1), dtype=torch.float32, device=a2.device)
+                    ops.conv_wgrad(a2, g, Pg, N, H2, W2, planes, planes, C3, 1, 1, 1, 0, accumulate=False)
                 ops.conv_wgrad(a2, a2, G, N, H2, W2, planes, planes, planes, 1, 1, 1, 0, accumulate=False)
                 ops.bn_bwd_fold_wgrad_a2(Pg.view(C3, planes), G.view(planes, planes),
                                          blk.conv3.weight.data.view(C3, planes), C3, planes, b3.mean, b3.invstd,
                                          b3.bn.weight, sums3[0], sums3[1], M, a2s[0],
                                          blk.conv3.weight.grad.view(C3, planes))
                 return True
-            return self._async(wfn, a2, g, sums3, a2s[0])
+            return self._async(wfn, a2, g, sums3, a2s[0], Pg0)
 
         def wfn():
             cs = torch.empty(planes, dtype=torch.float32, device=a2.device)
@@ -654,6 +687,12 @@ class ResNetTrunk:
         if gin is not None:
             g, sums3, sumsd = gin
             b3, bd = r["b3"], r.get("bd")
+            if r["y3"] is None and not ds:  # bn3's sum_gx from g^T a2 (the conv1 dgrad reduced only sum g)
+                Pg = torch.empty((C3, planes, 1, 1), dtype=torch.float32, device=g.device)
+                ops.conv_wgrad(r["a2"], g, Pg, N, H2, W2, planes, planes, C3, 1, 1, 1, 0, accumulate=False)
+                ops.bn_bwd_sumgx_from_wgrad(Pg.view(C3, planes), self._wprep(blk.conv3, planes), C3, planes, b3.mean,
+                                            b3.invstd, sums3[0], sums3[1], self._bn_grads(b3)[0])
+                r["Pg"] = Pg
             if self._can_fold(r, ds):
                 bnf = (g, sums3)
                 dy3 = dyd = None
@@ -663,7 +702,7 @@ class ResNetTrunk:
                 dy3, dyd = ops.bn_bwd_apply_dual(g, r["y3"], b3.mean, b3.invstd, b3.bn.weight, sums3[0], sums3[1],
                                                  r["yd"], bd.mean, bd.invstd, bd.bn.weight, sumsd[0], sumsd[1], C3)
             else:
-                dy3 = self._bn_apply_bwd(g, r["y3"], b3, C3, sums3)
+                dy3 = self._bn_apply_bwd(g, self._y3(r), b3, C3, sums3)
                 dyd = self._bn_apply_bwd(g, r["yd"], bd, C3, sumsd) if ds else None
         else:
             g = torch.empty_like(dout)
@@ -675,7 +714,7 @@ class ResNetTrunk:
         if ds and self._ws is not None and ResNetTrunk.ds_stream:
             ds_res = self._ds_dgrad_side(blk.downsample[0], dyd, N, H, W, Cin, C3)
         if bnf is not None and not self._fold_conv3(r, *bnf):  # (the engine does not apply: the pass on dy3)
-            dy3 = self._bn_apply_bwd(bnf[0], r["y3"], r["b3"], C3, bnf[1])
+            dy3 = self._bn_apply_bwd(bnf[0], self._y3(r), r["b3"], C3, bnf[1])
             bnf = None
         if bnf is not None:
             pass  # (conv3's weight gradient went out with the fold)
@@ -694,7 +733,7 @@ class ResNetTrunk:
             dy2 = self._dgrad_bn_fold(blk.conv3, bnf[0], r["y3"], r["b3"], bnf[1], N, H2, W2, r["y2"], r["b2"], planes,
                                       C3, a2=r["a2"], a2sum=r.get("a2sum"))
             if dy2 is None:  # (the fused engine does not apply: the unfused pass, and conv3's dgrad on dy3)
-                dy3 = self._bn_apply_bwd(bnf[0], r["y3"], r["b3"], C3, bnf[1])
+                dy3 = self._bn_apply_bwd(bnf[0], self._y3(r), r["b3"], C3, bnf[1])
         if dy2 is None:
             dy2 = self._dgrad_bn(blk.conv3, dy3, N, H2, W2, r["y2"], r["b2"], planes)
         del dy3
