@@ -135,9 +135,9 @@ class ResNetTrunk:
     # is never stored: the input gradient is one GEMM over [g | y3], the weight gradient one GEMM with 2 C3 rows;
     # ops.conv_dgrad_bwd_bnfold / conv_wgrad_bnfold); VCG_BN_FOLD=0: the bn_bwd_apply pass
     bn_fold_bwd = os.environ.get("VCG_BN_FOLD", "1") != "0"
-    # ... for blocks with C3 <= this many channels (layers 1-2: HBM-bound conv3 gradients; the deeper layers' doubled
-    # K costs more MFMA time than the pass it removes)
-    bn_fold_max_c3 = int(os.environ.get("VCG_BN_FOLD_MAXC3", "512"))
+    # ... for blocks with C3 <= this many channels (layers 1-3; layer 4's MFMA-bound conv3 gradients lose more to the
+    # extra K than the pass costs: measured with the y3 drop, 78.6 vs 78.0 ms per step)
+    bn_fold_max_c3 = int(os.environ.get("VCG_BN_FOLD_MAXC3", "1024"))
     # ... with conv3's input a2 (C3 / 4 channels) as the second GEMM source instead of y3 (y3 = a2 w3^T: the input
     # gradient reads [g | a2] against [A w | w3^T diag(B) w3], the weight gradient is A (g^T a2) + B w3 (a2^T a2) + C
     # colsum(a2)); VCG_BN_FOLD_A2=0: the y3 form
@@ -149,7 +149,7 @@ class ResNetTrunk:
     # batch-statistics forward of a non-first bottleneck with C3 <= this many channels: bn3 + identity + ReLU as a
     # second pass of conv3's GEMM (scale folded into its weight rows, shift as bias; ops.conv1x1_bn_res_relu)
     # instead of reading y3 back in the bn_apply pass (0: off)
-    bn3_gemm_max_c3 = int(os.environ.get("VCG_BN3_GEMM_MAXC3", "512"))
+    bn3_gemm_max_c3 = int(os.environ.get("VCG_BN3_GEMM_MAXC3", "1024"))
 
     def __init__(self, net, dtype):
         self.net = net
@@ -183,6 +183,8 @@ class ResNetTrunk:
     def _drop_y3(self, blk, planes, need_grad):
         """This bottleneck's training forward keeps only bn3's statistics (see y3_drop)."""
         C3 = blk.conv3.out_channels
+        if blk is self.net.layer4[-1]:  # (its backward starts from the raw output gradient: bn3 needs y3)
+            return False
         return (ResNetTrunk.y3_drop and need_grad and blk.downsample is None and ResNetTrunk.bn_fold_bwd
                 and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16
                 and not ResNetTrunk.fused_bnin and C3 <= ResNetTrunk.bn_fold_max_c3
@@ -706,7 +708,7 @@ class ResNetTrunk:
                 dyd = self._bn_apply_bwd(g, r["yd"], bd, C3, sumsd) if ds else None
         else:
             g = torch.empty_like(dout)
-            dy3 = self._bn_bwd_g(dout, r["y3"], r["b3"], C3, obits, g)
+            dy3 = self._bn_bwd_g(dout, self._y3(r), r["b3"], C3, obits, g)
             dyd = self._bn_bwd(dout, r["yd"], r["bd"], C3, mbits=obits) if ds else None
         # the downsample branch's input gradient needs only dyd: on the side stream ahead of the weight gradients,
         # joined (by its own event) just before conv1's fused dgrad adds it
