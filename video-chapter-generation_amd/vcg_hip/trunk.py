@@ -183,6 +183,10 @@ class ResNetTrunk:
     def _drop_y3(self, blk, planes, need_grad):
         """This bottleneck's training forward keeps only bn3's statistics (see y3_drop)."""
         C3 = blk.conv3.out_channels
+        if not need_grad:  # batch-statistics scoring: the GEMM pass is y3's only consumer
+            return (ResNetTrunk.y3_drop and blk.downsample is None and self.dtype == torch.bfloat16
+                    and not ResNetTrunk.fused_bnin and C3 <= ResNetTrunk.bn3_gemm_max_c3 and C3 % 64 == 0
+                    and planes % 64 == 0 and blk.conv3.stride[0] == 1 and bn_mode(blk.bn3) != "running")
         if blk is self.net.layer4[-1]:  # (its backward starts from the raw output gradient: bn3 needs y3)
             return False
         return (ResNetTrunk.y3_drop and need_grad and blk.downsample is None and ResNetTrunk.bn_fold_bwd
