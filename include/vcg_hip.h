@@ -102,10 +102,11 @@ VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale,
    combined per row with colsum_x = the column sums of x (f32 [C]). VCG_ERR_UNSUPPORTED where the engine does not
    apply. */
 /* torchvision Bottleneck's bn3 + identity + ReLU (model/vision/resnet50_tsm.py:15) as a second pass of conv3's GEMM:
-   out[M][N] = relu(bf16(x[M][K] wfold[N][K]^T + bias) + res) and the ReLU mask bits (vcg_bn_apply's layout), with
+   out[M][N] = relu(bf16(x[M][K] wfold[N][K]^T + bias) + res') and the ReLU mask bits (vcg_bn_apply's layout),
+   res' = res or fma(res, res_scale[n], res_shift[n]) (a layer's first block: the downsample BN's output), with
    wfold = the conv3 weight rows scaled by the batch-statistics BN scale (vcg_weight_fold), bias = its shift: the stored
    conv output is not read back (bf16 fast engine; VCG_ERR_UNSUPPORTED elsewhere) */
-VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const float* bias, const void* res, void* out, unsigned char* bits, int M, int N, int K, hipStream_t stream);
+VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const float* bias, const void* res, const float* res_scale, const float* res_shift, void* out, unsigned char* bits, int M, int N, int K, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* mean, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, void* wfold, float* bias, hipStream_t stream);
 /* the fold with the conv3 input a2 [M][C] as the second source instead of y3 = a2 w3^T (y3 never read):
    vcg_bn_bwd_fold_weights_a2: wfold [C][K + C] = [A_k wt | w3^T diag(B) w3] and the bias, colsum_a = column sums of

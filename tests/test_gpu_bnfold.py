@@ -313,3 +313,31 @@ def test_dgrad_bits_only_sums_and_sumgx(shape):
     ref = (g2.view(M, C).double() * (a2.double() @ w3.double().t() - mean.double()) * invstd.double()).sum(0)
     assert (sgx.double() - ref).abs().max().item() < 2e-3 * (ref.abs().max().item() + 1e-3)
     assert (s1[1].double() - ref).abs().max().item() < 2e-2 * (ref.abs().max().item() + 1e-3)
+
+
+def test_conv1x1_bn_res_relu_affine_residual():
+    """A layer's first block: the residual is the downsample BN's output, fma(yd, rs, rb) in the epilogue, against
+    conv -> bn_apply(res=yd, rscale, rshift)."""
+    N, H, W, C, Cout = 4, 28, 28, 128, 512
+    M = N * H * W
+    gen = torch.Generator().manual_seed(13)
+    x = _bf(torch.relu(torch.randn(M, C, generator=gen)))
+    w = (torch.randn(Cout, C, generator=gen) / C ** 0.5).to(DEV)
+    yd = _bf(torch.randn(M, Cout, generator=gen) + 0.3)
+    sc = (0.5 + torch.rand(Cout, generator=gen)).to(DEV)
+    sh = (torch.randn(Cout, generator=gen) * 0.3).to(DEV)
+    rs = (0.5 + torch.rand(Cout, generator=gen)).to(DEV)
+    rb = (torch.randn(Cout, generator=gen) * 0.3).to(DEV)
+    out, bits = ops.conv1x1_bn_res_relu(x, ops.weight_fold(w, sc, torch.bfloat16), sh, yd, M, Cout, C, res_scale=rs,
+                                        res_shift=rb)
+    y3 = ops.gemm(x, ops.weight_fold(w, torch.ones(Cout, device=DEV), torch.bfloat16), M, Cout, C, C, C)
+    ref, rbits = ops.bn_apply(y3, sc, sh, Cout, relu=True, res=yd, rscale=rs, rshift=rb, bits=True)
+    torch.cuda.synchronize()
+    exact = torch.relu((x.double() @ w.double().t()) * sc.double() + sh.double() + yd.double() * rs.double()
+                       + rb.double())
+    e_new = (out.double() - exact).abs().max().item()
+    e_old = (ref.double() - exact).abs().max().item()
+    assert e_new <= max(1.5 * e_old, 3e-2 * exact.abs().max().item()), (e_new, e_old)
+    pos = (out.view(-1, 8) > 0).to(torch.uint8)
+    assert torch.equal(bits, (pos * (2 ** torch.arange(8, device=DEV, dtype=torch.uint8))).sum(1).to(torch.uint8))
+    assert (bits != rbits).float().mean().item() < 0.02

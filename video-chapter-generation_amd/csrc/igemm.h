@@ -117,6 +117,7 @@ struct GemmParams {
   // EPI_STORE + residual + ReLU through the stage (epilogue_staged_res): also store the ReLU decisions as mask bits,
   // byte (m N + n) / 8 bit n % 8 (vcg_bn_apply's bits layout; vcg_conv1x1_bn_res_relu)
   uint8_t* obits;
+  const float *res_sc, *res_sh;  // epilogue_staged_res: residual r -> fma(r, res_sc[n], res_sh[n]) (a BN'd residual)
 };
 
 

@@ -1317,8 +1317,9 @@ VCG_API int vcg_conv1x1_stats(const void* x, const void* w, float* stats, int M,
 // out = relu(bf16(x wfold^T + bias) + res) with the ReLU mask bits: a batch-statistics bn3 (scale folded into the
 // conv3 weight rows by vcg_weight_fold, shift as bias) applied by a second pass of conv3's GEMM instead of reading
 // the stored conv output back (trunk forward; the bn3 + residual + ReLU of vcg_bn_apply, one bf16 rounding earlier)
-VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const float* bias, const void* res, void* out,
-                                    unsigned char* bits, int M, int N, int K, hipStream_t stream) {
+VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const float* bias, const void* res,
+                                    const float* res_scale, const float* res_shift, void* out, unsigned char* bits,
+                                    int M, int N, int K, hipStream_t stream) {
   VCG_REQUIRE(x && wfold && bias && res && out && bits, "null argument");
   VCG_REQUIRE(M > 0 && N % 64 == 0 && K % 64 == 0, "N and K must be multiples of 64");
   VCG_REQUIRE((((uintptr_t)x | (uintptr_t)wfold | (uintptr_t)res | (uintptr_t)out) & 15) == 0, "16-B alignment");
@@ -1340,6 +1341,9 @@ VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const floa
   p.ldr = N;
   p.res_round = 1;
   p.obits = bits;
+  VCG_REQUIRE(!res_scale == !res_shift, "res_scale and res_shift go together");
+  p.res_sc = res_scale;
+  p.res_sh = res_shift;
   if (FILE* f = gemm_log()) {
     fprintf(f, "a=0 b=0 epi=0 M=%d N=%d K=%d z=1 fast=1 conv=1x1/1 C=%d bnres=1\n", M, N, K, K);
     fflush(f);

@@ -415,6 +415,15 @@ __device__ __forceinline__ void epilogue_staged_res(f32x4 (&acc)[4][BN / 32], co
     const uint32_t addr = lds_u32(reg + row * BN + 8 * st_slot<BN>(row, c));
     asm volatile("ds_read_b128 %0, %1" : "=v"(q[k]) : "v"(addr) : "memory");
   }
+  float rsc[8], rsh[8];  // an affine residual (p.res_sc): this thread's 8 columns are the same for every k
+  if (p.res_sc) {
+    const int nc = min(n0 + 8 * (int)(threadIdx.x % CPR), p.N - 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      rsc[e] = p.res_sc[nc + e];
+      rsh[e] = p.res_sh[nc + e];
+    }
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -425,6 +434,10 @@ __device__ __forceinline__ void epilogue_staged_res(f32x4 (&acc)[4][BN / 32], co
     float a[8], r[8];
     unpack8(q[k], a);
     unpack8(rv[k], r);
+    if (p.res_sc) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r[e] = fmaf(r[e], rsc[e], rsh[e]);
+    }
     uint32_t mb = 0;  // ReLU mask of the output (p.obits): bit e = out > 0, as vcg_bn_apply writes it
 #pragma unroll
     for (int e = 0; e < 8; ++e) {

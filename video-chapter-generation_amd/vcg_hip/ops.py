@@ -185,14 +185,15 @@ def bn_bwd_sumgx_from_wgrad(Pg, w, K, C, mean, invstd, sum_g, sum_gx, dgamma=Non
               stream())
 
 
-def conv1x1_bn_res_relu(x, wfold, bias, res, M, N, K):
-    """(out, bits): relu(bf16(x @ wfold^T + bias) + res) and its ReLU mask bits (vcg_conv1x1_bn_res_relu), or None
-    where the fused engine does not apply."""
+def conv1x1_bn_res_relu(x, wfold, bias, res, M, N, K, res_scale=None, res_shift=None):
+    """(out, bits): relu(bf16(x @ wfold^T + bias) + res') and its ReLU mask bits (vcg_conv1x1_bn_res_relu), res' =
+    res or res * res_scale + res_shift per column; None where the fused engine does not apply."""
     _chk(x, torch.bfloat16, "x")
     _chk(res, torch.bfloat16, "res")
     out = torch.empty_like(res)
     bits = torch.empty(res.numel() // 8, dtype=torch.uint8, device=res.device)
-    rc = _lib.query("vcg_conv1x1_bn_res_relu", P(x), P(wfold), P(bias), P(res), P(out), P(bits), M, N, K, stream())
+    rc = _lib.query("vcg_conv1x1_bn_res_relu", P(x), P(wfold), P(bias), P(res), P(res_scale), P(res_shift), P(out),
+                    P(bits), M, N, K, stream())
     if rc == -2:
         return None
     if rc != 0:

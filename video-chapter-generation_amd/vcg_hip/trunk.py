@@ -150,6 +150,9 @@ class ResNetTrunk:
     # second pass of conv3's GEMM (scale folded into its weight rows, shift as bias; ops.conv1x1_bn_res_relu)
     # instead of reading y3 back in the bn_apply pass (0: off)
     bn3_gemm_max_c3 = int(os.environ.get("VCG_BN3_GEMM_MAXC3", "1024"))
+    # ... and of a layer's first block (the residual is the downsample BN's output, applied in the epilogue):
+    # measured neutral (805.3 vs 807.5 windows/s same box), opt-in VCG_BN3_GEMM_FIRST=1
+    bn3_gemm_first = os.environ.get("VCG_BN3_GEMM_FIRST", "0") == "1"
 
     def __init__(self, net, dtype):
         self.net = net
@@ -324,8 +327,18 @@ class ResNetTrunk:
                 cur.wait_stream(side)
             else:
                 yd, bd, _, _ = self._conv_bn(x, blk.downsample[0], blk.downsample[1], N, H, W, Cin)
-            out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale,
-                                      rshift=bd.shift, bits=True)
+            r2 = None
+            if (a2 is not None and self.dtype == torch.bfloat16 and C3 <= ResNetTrunk.bn3_gemm_max_c3
+                    and b3.mode != "running" and blk.conv3.stride[0] == 1 and ResNetTrunk.bn3_gemm_first):
+                M = N * H2 * W2  # bn3 + the downsample BN'd residual + ReLU as a second conv3 GEMM pass
+                wf = ops.weight_fold(blk.conv3.weight.data.view(C3, planes), b3.scale, self.dtype)
+                r2 = ops.conv1x1_bn_res_relu(a2.view(M, planes), wf, b3.shift, yd, M, C3, planes,
+                                             res_scale=bd.scale, res_shift=bd.shift)
+            if r2 is not None:
+                out, obits = r2
+            else:
+                out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale,
+                                          rshift=bd.shift, bits=True)
         else:
             r2 = None
             if (a2 is not None and self.dtype == torch.bfloat16 and C3 <= ResNetTrunk.bn3_gemm_max_c3
