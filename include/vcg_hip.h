@@ -118,6 +118,10 @@ VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* m
    w [K][C]: sum_gx[k] = invstd_k (sum_j w[k][j] P[k][j] - mean_k sum_g[k]), dgamma (optional) += sum_gx; sum_g
    comes from the producing dgrad's epilogue run with the mask bits and no y (vcg_conv_dgrad_bwd: y NULL, bits,
    sum_g / sum_gx given: sum_gx written as 0). */
+/* vcg_bn_apply without a residual (bf16) that also writes the column sums of the stored output (f32 [C]): conv3's
+   input a2 and its colsum for the bn3 fold's centring in one pass */
+VCG_API long long vcg_bn_apply_colsum_ws_bytes(long long P, int C);
+VCG_API int vcg_bn_apply_colsum(const void* y, const float* scale, const float* shift, int relu, void* out, float* colsum, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
 VCG_API int vcg_conv1x1_stats(const void* x, const void* w, float* stats, int M, int N, int K, hipStream_t stream);
 VCG_API int vcg_bn_bwd_sumgx_from_wgrad(const float* P, const void* w, int K, int C, const float* mean, const float* invstd, const float* sum_g, float* sum_gx, float* dgamma, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a, void* wfold, float* bias, hipStream_t stream);

@@ -341,3 +341,19 @@ def test_conv1x1_bn_res_relu_affine_residual():
     pos = (out.view(-1, 8) > 0).to(torch.uint8)
     assert torch.equal(bits, (pos * (2 ** torch.arange(8, device=DEV, dtype=torch.uint8))).sum(1).to(torch.uint8))
     assert (bits != rbits).float().mean().item() < 0.02
+
+
+@pytest.mark.parametrize("rows,C", [(3211264 // 4, 64), (802816 // 2 + 13, 128), (200704, 256), (50176, 512)])
+def test_bn_apply_colsum(rows, C):
+    """bn_apply + the column sums of its stored output in one pass == bn_apply (bit for bit) and colsum."""
+    gen = torch.Generator().manual_seed(rows % 97 + C)
+    y = _bf(torch.randn(rows, C, generator=gen))
+    sc = (0.5 + torch.rand(C, generator=gen)).to(DEV)
+    sh = (torch.randn(C, generator=gen) * 0.2).to(DEV)
+    a, cs = ops.bn_apply_colsum(y, sc, sh, C)  # (VCG_A2SUM_FUSED=1 in the trunk)
+    ref = ops.bn_apply(y, sc, sh, C, relu=True)
+    csr = torch.zeros(C, device=DEV)
+    ops.colsum(ref, C, rows, C, csr, accumulate=False)
+    torch.cuda.synchronize()
+    assert torch.equal(a, ref)
+    assert ((cs.double() - csr.double()).abs() / csr.double().abs().clamp_min(1.0)).max().item() < 1e-5

@@ -73,18 +73,21 @@ __host__ __device__ inline int ilog2i(int x) {
 // out = act(fma(y, scale, shift) + [fma(res, rscale, rshift) | res]); bits (optional): ReLU mask of
 // out, one byte per 16-B vector (the backward's VCG_MASK_BITS). Grid-stride over batches of SU
 // vectors per thread; every load of a batch is issued before the first use.
-template <typename T, bool RES, bool RAFF>
+template <typename T, bool RES, bool RAFF, bool CS = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const T* __restrict__ res,
                                                        const float* __restrict__ rscale,
                                                        const float* __restrict__ rshift, int relu,
                                                        T* __restrict__ out, uint8_t* __restrict__ bits, long long TV,
-                                                       int cpr) {
+                                                       int cpr, float* __restrict__ colpart = nullptr) {
   constexpr int VN = V<T>::N;
   const long long stride = (long long)gridDim.x * SB;
   long long base = (long long)blockIdx.x * SB + threadIdx.x;
   const bool fixed = cpr <= 256;
   float sc[VN], sh[VN], rs[VN], rb[VN];
+  float csum[VN];  // colpart: this thread's column sums of the stored output (its channel chunk is fixed, cpr | 256)
+#pragma unroll
+  for (int e = 0; e < VN; ++e) csum[e] = 0.f;
   auto params = [&](long long v) {
     const int c0 = (int)(v & (cpr - 1)) * VN;
     load_params<VN>(scale, c0, sc);
@@ -120,8 +123,44 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, 
         for (int e = 0; e < VN; ++e) b |= (a[u][e] > 0.f ? 1u : 0u) << e;
         bits[v] = (uint8_t)b;
       }
+      if constexpr (CS) {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) csum[e] += to_f<T>(from_f<T>(a[u][e]));  // the stored (rounded) value
+      }
       store16<T>(out + v * VN, a[u]);
     }
+  }
+  if constexpr (CS) {  // per-block column partials [block][C], threads of one chunk combined in a fixed order
+    __shared__ float red[256][VN + 1];
+#pragma unroll
+    for (int e = 0; e < VN; ++e) red[threadIdx.x][e] = csum[e];
+    __syncthreads();
+    const int C = cpr * VN;
+    for (int o = threadIdx.x; o < C; o += 256) {
+      const int ch = o / VN, i = o - ch * VN;
+      float acc = 0.f;
+      for (int t = ch; t < 256; t += cpr) acc += red[t][i];
+      colpart[(long long)blockIdx.x * C + o] = acc;
+    }
+  }
+}
+
+// out[c] = sum_b part[b][c] (fixed order: 16 row stripes per channel in double, then the stripes in order)
+__global__ __launch_bounds__(1024) void colpart_reduce_kernel(const float* __restrict__ part, int nb, int C,
+                                                              float* __restrict__ out) {
+  __shared__ double sa[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  double a = 0;
+  if (c < C)
+    for (int b = ty; b < nb; b += 16) a += part[(long long)b * C + c];
+  sa[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    a = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a += sa[k][tx];
+    out[c] = (float)a;
   }
 }
 
@@ -801,6 +840,29 @@ int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, in
 }  // namespace vcg
 
 // ==================================================================== C ABI
+
+// vcg_bn_apply (no residual) that also returns the column sums of the stored output (the bn3 fold's colsum(a2)
+// without a pass of its own); ws: vcg_bn_apply_colsum_ws_bytes
+VCG_API long long vcg_bn_apply_colsum_ws_bytes(long long P, int C) {
+  return (long long)stream_grid(P * C / 8) * C * 4 + 256;
+}
+
+VCG_API int vcg_bn_apply_colsum(const void* y, const float* scale, const float* shift, int relu, void* out,
+                                float* colsum, float* ws, long long ws_bytes, long long P, int C, hipStream_t s) {
+  VCG_REQUIRE(y && scale && shift && out && colsum && ws, "null argument");
+  VCG_REQUIRE(C % 8 == 0 && (C & (C - 1)) == 0 && C / 8 <= 256, "C must be a power of two in [8, 2048]");
+  const long long TV = P * C / 8;
+  if (TV == 0) return VCG_OK;
+  const unsigned g = stream_grid(TV);
+  VCG_REQUIRE(ws_bytes >= (long long)g * C * 4, "workspace too small");
+  hipLaunchKernelGGL((bn_apply_kernel<bf16_t, false, false, true>), dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
+                     (const bf16_t*)nullptr, (const float*)nullptr, (const float*)nullptr, relu, (bf16_t*)out,
+                     (uint8_t*)nullptr, TV, C / 8, ws);
+  VCG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colpart_reduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)g, C, colsum);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
 
 VCG_API int vcg_bn_apply(int dtype, const void* y, const float* scale, const float* shift, const void* res,
                          const float* rscale, const float* rshift, int relu, void* out, unsigned char* bits,

@@ -164,6 +164,18 @@ def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_f
     return g
 
 
+def bn_apply_colsum(y, scale, shift, C, relu=True):
+    """(bn_apply(y, scale, shift, relu), its column sums f32 [C]) in one pass (vcg_bn_apply_colsum, bf16)."""
+    _chk(y, torch.bfloat16, "y")
+    out = torch.empty_like(y)
+    cs = torch.empty(C, dtype=torch.float32, device=y.device)
+    P_ = y.numel() // C
+    w = ws(_lib.query("vcg_bn_apply_colsum_ws_bytes", P_, C), y.device)
+    _lib.call("vcg_bn_apply_colsum", P(y), P(scale), P(shift), int(relu), P(out), P(cs), P(w), w.numel() * 4, P_, C,
+              stream())
+    return out, cs
+
+
 def conv1x1_stats(x, w, stats, M, N, K):
     """BatchNorm statistics of x [M, K] @ w [N, K]^T without storing the product (vcg_conv1x1_stats). False where
     the fused engine does not apply."""

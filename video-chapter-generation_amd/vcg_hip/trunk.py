@@ -313,15 +313,23 @@ class ResNetTrunk:
         if self.dtype == torch.bfloat16 and ResNetTrunk.fused_bnin:
             y3, b3, _, _ = self._conv_bn(y2, blk.conv3, blk.bn3, N, H2, W2, planes, in_bn=(b2.scale, b2.shift))
         drop = y3 is None and self._drop_y3(blk, planes, need_grad)
-        if y3 is None:
-            a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
-            y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
         C3 = blk.conv3.out_channels
         a2sum = None
-        if (need_grad and a2 is not None and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2
-                and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16 and b3.mode != "running"
-                and C3 <= ResNetTrunk.bn_fold_max_c3):
-            a2sum = self._colsum_side(a2, planes)  # (the a2 form of the bn3 backward fold: its mean of a2)
+        if y3 is None:
+            if (need_grad and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd
+                    and self.dtype == torch.bfloat16 and bn_mode(blk.bn3) != "running"
+                    and C3 <= ResNetTrunk.bn_fold_max_c3 and planes <= 2048):
+                # (the a2 form of the bn3 backward fold needs colsum(a2): by default a column-sum pass on the side
+                # stream, which contends with conv3's GEMMs; VCG_A2SUM_FUSED=1: written by the bn2 apply pass itself)
+                if os.environ.get("VCG_A2SUM_FUSED", "0") == "1":
+                    a2, cs = ops.bn_apply_colsum(y2, b2.scale, b2.shift, planes)
+                    a2sum = (cs, None)
+                else:
+                    a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
+                    a2sum = self._colsum_side(a2, planes)
+            else:
+                a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
+            y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
         if blk.downsample is not None:
             if side is not None:
                 cur.wait_stream(side)
