@@ -225,6 +225,71 @@ def long_video_bench(args):
                                        "f", "f_3", "f_5")}}), flush=True)
 
 
+# ----------------------------------------------------------------------------- multi-GPU evidence
+def ddp_evidence(reducer, flat, exposed_ms, transport):
+    """Collective over all ranks (every rank calls it after the timed steps): what rank 0's line carries for a
+    world > 1 run so that the run validates itself -- the process group as seen from inside (backend, world size),
+    cross-rank parameter agreement (max |param - rank-0 param| over the whole flat buffer, all-reduced with MAX:
+    0 when the ranks stayed in lockstep, as DDP guarantees), and the gradient exchange (buckets and bytes one
+    backward put on the wire, wire dtype, and the exposed communication time: from the end of the backward's
+    work on the step's stream to the reducer's finish() having joined every collective, timed on that stream).
+    Replaces the reference's DDP wiring, train_video_segment_ddp.py:148,261-263,339."""
+    import torch.distributed as dist
+    from vcg_hip.ddp import params_max_divergence
+    div = params_max_divergence(flat)
+    ex = sorted(exposed_ms) or [float("nan")]
+    return {"dist": {"backend": str(dist.get_backend()), "world_size": dist.get_world_size()},
+            "params_consistent": div == 0.0, "params_max_abs_diff": div,
+            "allreduce": {"transport": transport, "op": "sum (1/world folded into AdamW)",
+                          "bucket_bytes": reducer.bucket_elems * 4,
+                          "buckets_per_step": reducer.last_step["buckets"],
+                          "bytes_per_step": reducer.last_step["bytes"],
+                          "wire_dtype": "bf16" if reducer.wire is not None else "fp32",
+                          "exposed_ms_per_step_median": round(ex[len(ex) // 2], 4),
+                          "exposed_ms_per_step_max": round(ex[-1], 4),
+                          "exposed_timing": "stream events: backward done -> finish() joined (timed steps)"}}
+
+
+def cpu_ddp_rehearsal(steps=3):
+    """--launch-check's model-free DDP step on the CPU (gloo): a small Linear stack in a FlatParams buffer, each
+    rank on its own inputs, gradients reported to GradAllReducer in backward order with small buckets, a plain SGD
+    update with the 1/world average -- the same reducer and ddp_evidence() the GPU bench line uses."""
+    import torch
+    import torch.distributed as dist
+    from vcg_hip.ddp import GradAllReducer, broadcast_parameters
+    from vcg_hip.flat import FlatParams
+    torch.manual_seed(dist.get_rank())  # ranks start apart: broadcast_parameters must align them
+    net = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 256), torch.nn.ReLU(),
+                              torch.nn.Linear(256, 8))
+    flat = FlatParams(list(net.named_parameters()), "cpu")
+
+    class _M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.net = net
+
+        def native_flat(self):
+            return flat
+    broadcast_parameters(_M())
+    red = GradAllReducer(flat, bucket_bytes=64 << 10)
+    world = dist.get_world_size()
+    gen = torch.Generator().manual_seed(1000 + dist.get_rank())
+    exposed = []
+    layers = [m for m in net if isinstance(m, torch.nn.Linear)]
+    for _ in range(steps):
+        flat.zero_grad()
+        x = torch.randn(32, 64, generator=gen)
+        net(x).square().mean().backward()
+        for lin in reversed(layers):  # the engines' backward-order reports
+            red([lin.weight, lin.bias])
+        t0 = time.perf_counter()
+        red.finish()
+        exposed.append(1e3 * (time.perf_counter() - t0))
+        with torch.no_grad():
+            flat.data.add_(flat.grad, alpha=-0.1 / world)
+    return ddp_evidence(red, flat, exposed, "torch.distributed")
+
+
 # ----------------------------------------------------------------------------- launcher
 def _free_port():
     import socket
@@ -258,9 +323,10 @@ def launch_check(args, world, rank):
         dist.all_gather(seen, t)
     else:
         seen = [t]
+    ev = cpu_ddp_rehearsal() if world > 1 else {}
     if rank == 0:
         print(json.dumps({"metric": METRIC, "n_gpus": int(sum(int(s[0]) for s in seen)),
-                          "local_ranks": [int(s[1]) for s in seen], "launch_check": True}), flush=True)
+                          "local_ranks": [int(s[1]) for s in seen], "launch_check": True, **ev}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -300,6 +366,8 @@ def main():
     if args.batch is None:
         args.batch = 16 if (args.bn == "batch" and args.mode != "train") else 64
 
+    if args.mode == "long_video" and args.gpus > 1:
+        raise SystemExit("bench.py: --mode long_video is a one-GPU benchmark (config 5); run it with --gpus 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `bench.py --gpus N` without a launcher: start the N rank processes ourselves, one per GPU, as the
         # reference's DDP driver does with mp.spawn (train_video_segment_ddp.py:599-608). This process has not
@@ -365,6 +433,7 @@ def main():
         opt.grad_scale = 1.0 / world
         bufsync = BufferBroadcaster(model, comm=comm)  # DDP broadcast_buffers: rank 0's BN stats each forward
     frames, ids, mask, labels = synth.clip_batch(B, T, HW, HW, L, seed=123 + rank, device=dev)
+    comm_events = None  # [(backward done, finish joined)] per timed step (world > 1)
 
     def step():
         if args.mode == "fwd":
@@ -377,7 +446,14 @@ def main():
         logits, prob = model(frames, ids, mask)
         loss = cross_entropy(logits, labels)
         loss.backward()
-        reducer.finish()
+        if comm_events is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            reducer.finish()
+            e1.record()
+            comm_events.append((e0, e1))
+        else:
+            reducer.finish()
         opt.clip_and_step(1.0)
 
     for _ in range(args.warmup):
@@ -394,6 +470,8 @@ def main():
     import gc
     gc0 = [g["collections"] for g in gc.get_stats()]
     ms0 = torch.cuda.memory_stats()
+    if world > 1 and args.mode == "train":
+        comm_events = []
     for _ in range(args.steps):
         te = time.perf_counter()
         step()
@@ -402,6 +480,8 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ms1 = torch.cuda.memory_stats()
+    exposed = [a.elapsed_time(b) for a, b in comm_events] if comm_events else []
+    comm_events = None
     host_diag = {"slowest_step": int(max(range(len(enq)), key=lambda i: enq[i])),
                  "gc_collections": [g["collections"] - c for g, c in zip(gc.get_stats(), gc0)],
                  "device_allocs": ms1.get("num_device_alloc", 0) - ms0.get("num_device_alloc", 0),
@@ -432,10 +512,14 @@ def main():
     ops.timing_enable(False)
     model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream, ResNetTrunk.prep_stream = sides
     kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
+    ddp = {}
     if world > 1:
         t = torch.tensor([ms], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
+        if args.mode == "train":
+            ddp = ddp_evidence(reducer, flat, exposed, "libvcg_hip RCCL C ABI" if comm is not None else
+                               "torch.distributed")
 
     if rank == 0:
         windows = B * world
@@ -493,6 +577,7 @@ def main():
                        "global_batch": windows, "seq_len": L, "frames": T, "resolution": HW,
                        "parallelism": f"dp{world}", **({"bn": args.bn} if args.mode == "fwd" else {})},
             "roofline": dom,
+            **ddp,
             "host": {"enqueue_ms_per_step_median": round(1e3 * sorted(enq)[len(enq) // 2], 3),
                      "enqueue_ms_per_step_max": round(1e3 * max(enq), 3), **host_diag},
             "roofline_step": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

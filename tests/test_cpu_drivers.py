@@ -1,6 +1,7 @@
 """CPU tests of the driver-side host logic: LR schedule, per-video metric pipelines (with the
 reference's quirks), synthetic datasets (sample tuples through the real window logic)."""
 import math
+import os
 import random
 
 import numpy as np
@@ -88,3 +89,20 @@ def test_synthetic_datasets_produce_reference_tuples():
     assert label == info["clip_label"]
     # deterministic frames (rebuilt anywhere from the seed)
     assert np.array_equal(corpus.frames("synvid0000", [3]), SyntheticVideoCorpus(3, 40, 60, H=16, W=16, seed=5).frames("synvid0000", [3]))
+
+
+@pytest.mark.parametrize("ckpt", ["ck/", "ck/run", "ck/run.pth"])
+def test_ddp_checkpoint_search_matches_save_names(tmp_path, ckpt):
+    """find_latest_checkpoint looks where checkpoint_path writes, for a directory ("DIR/") and a name prefix
+    ("DIR/run", "DIR/run.pth") alike; other prefixes and non-checkpoint names are ignored."""
+    import train_video_segment_ddp as drv
+    path = str(tmp_path / ckpt)
+    os.makedirs(tmp_path / "ck", exist_ok=True)
+    for ep, best in ((1, None), (3, 0.25), (2, None)):
+        p = drv.checkpoint_path(path, ep, best or 0.0, best is not None)
+        open(p, "w").close()
+    open(tmp_path / "ck" / "other_9.pth", "w").close()
+    open(tmp_path / "ck" / "run_7.pth.tmp", "w").close()
+    found, ep = drv.find_latest_checkpoint(path)
+    assert ep == 3 and found == drv.checkpoint_path(path, 3, 0.25, True)
+    assert drv.find_latest_checkpoint(str(tmp_path / "none" / "x"))[0] is None

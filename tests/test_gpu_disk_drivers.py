@@ -131,3 +131,9 @@ def test_bench_gpus2_rehearsal():
     assert len(lines) == 1, out.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4 and d["value"] > 0
+    # the self-validating multi-GPU fields: process group, cross-rank parameter agreement, the exchange
+    assert d["dist"] == {"backend": "gloo", "world_size": 2}
+    assert d["params_consistent"] is True and d["params_max_abs_diff"] == 0.0
+    ar = d["allreduce"]
+    assert ar["buckets_per_step"] >= 5 and ar["bytes_per_step"] >= 4 * 133_000_000
+    assert ar["wire_dtype"] == "fp32" and ar["exposed_ms_per_step_median"] >= 0.0

@@ -80,12 +80,14 @@ def test_bench_script_small():
     assert 0 < d["roofline"]["per_launch_roofline"]["frac"] <= 1
 
 
-def test_ddp_driver_window_model_world1(tmp_path):
-    """The reference DDP driver's own configuration: the window model (window_size 1, cross_attn head) trained from
-    WindowClipDataset batches read from a reference-format corpus on disk (JPEG frames, subtitle JSON, CSV)."""
+@pytest.mark.parametrize("head_type", ["cross_attn", "self_attn"])
+def test_ddp_driver_window_model_world1(tmp_path, head_type):
+    """The reference DDP driver's own configuration: the window model (window_size 1, cross_attn head -- and the
+    self_attn head at the reference's default dropout) trained from WindowClipDataset batches read from a
+    reference-format corpus on disk (JPEG frames, subtitle JSON, CSV)."""
     import train_video_segment_ddp as drv
     os.environ.pop("WORLD_SIZE", None)
     r = drv.main(TINY + ["--epoch", "1", "--batch_size", "2", "--videos", "4", "--window_size", "1",
-                         "--data_dir", str(tmp_path)])
+                         "--head_type", head_type, "--data_dir", str(tmp_path)])
     assert r is None or r != r or 0.0 <= r <= 1.0
     assert (tmp_path / "train" / "subtitles" / "data.csv").exists()

@@ -180,3 +180,31 @@ def test_window_model_ddp_buckets_overlap_backward():
     assert covered[0][0] == 0 and all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
     assert covered[-1][1] == m.native_flat().total
     assert torch.equal(m.native_flat().grad, g_ref)
+
+
+@pytest.mark.parametrize("head_type", ["mlp", "cross_attn", "self_attn", "multiplication"])
+def test_window_train_at_reference_defaults(head_type):
+    """The window model as the reference constructs it (every Dropout at its default p, SelfAttention's resid_drop
+    0.1 included -- declared but never applied, two_stream_window.py:108,114-131 -- and BatchNorm in training mode):
+    one step has a finite loss and moves every fusion-head parameter it reaches."""
+    from test_cpu_oracle import _window_two_stream
+    m = _window_two_stream(device=DEV, head_type=head_type)
+    m.train()
+    drops = [mod.p for mod in m.modules() if isinstance(mod, torch.nn.Dropout)]
+    assert drops and max(drops) > 0.0
+    if head_type == "self_attn":
+        assert m.fusion_head.head.resid_drop.p == 0.1 and m.fusion_head.head.attn_drop.p == 0.1
+    loss, lg, pr, opt = _step(m)
+    assert np.isfinite(loss) and np.isfinite(lg).all()
+    # the heads the forward reaches (the ModuleList entries of the window positions in use) get gradients
+    params = {n: p for n, p in m.named_parameters() if n.startswith("fusion_head") and p.grad is not None
+              and p.grad.abs().max().item() > 0}
+    assert len(params) >= 4
+    if head_type == "self_attn":
+        assert {f"fusion_head.head.{l}.{w}" for l in ("query", "key", "value", "proj")
+                for w in ("weight", "bias")} <= set(params)
+    before = {n: p.detach().clone() for n, p in params.items()}
+    opt.clip_and_step(1.0)
+    torch.cuda.synchronize()
+    still = [n for n, p in params.items() if torch.equal(p.detach(), before[n])]
+    assert not still, f"fusion-head parameters that did not move: {still}"

@@ -35,14 +35,20 @@ from train_video_segment_point import TrainerConfig, lr_multiplier  # noqa: E402
 CKPT_RE = re.compile(r"_(\d+)(?:_score_[\d.]+)?\.pth$")
 
 
-def find_latest_checkpoint(ckpt_dir, rank=0):
-    """(path, epoch) of the newest `<base>_<epoch>[_score_<s>].pth` under ckpt_dir, found on rank 0 and broadcast
-    (`train_video_segment_ddp.py:176-207`); (None, 0) when there is none."""
+def find_latest_checkpoint(ckpt_path, rank=0):
+    """(path, epoch) of the newest `<base>_<epoch>[_score_<s>].pth` that `checkpoint_path(ckpt_path, ...)` would have
+    written, found on rank 0 and broadcast (`train_video_segment_ddp.py:176-207`); (None, 0) when there is none.
+    The search looks where the saves go: `<base>` = splitext(ckpt_path)[0], so "DIR/" finds DIR/_<e>.pth and "DIR/run"
+    finds DIR/run_<e>.pth (the reference globs ckpt_path as a directory, which only agrees with its own save names
+    for a trailing "/"). The epoch rule is the reference's `_(\\d+)(?:_score_[\\d.]+)?\\.pth$`."""
     info = (None, 0)
-    if rank == 0 and ckpt_dir and os.path.isdir(ckpt_dir):
+    if rank == 0 and ckpt_path:
+        base = os.path.splitext(ckpt_path)[0]
+        folder, prefix = os.path.dirname(base) or ".", os.path.basename(base)
+        name_re = re.compile(re.escape(prefix) + CKPT_RE.pattern)
         best = (None, -1)
-        for f in glob.glob(os.path.join(ckpt_dir, "*.pth")):
-            m = CKPT_RE.search(os.path.basename(f))
+        for f in glob.glob(os.path.join(glob.escape(folder), "*.pth")):
+            m = name_re.fullmatch(os.path.basename(f))
             if m and int(m.group(1)) > best[1]:
                 best = (f, int(m.group(1)))
         if best[0] is not None:
@@ -107,10 +113,14 @@ class DDPTrainer:
 
     def fit(self, val_every=30, save_every=10):
         """The reference's epoch loop (`:265-290`): validation every `val_every` epochs (rank-averaged metric; a best
-        checkpoint when it improves), else a regular checkpoint every `save_every` epochs."""
+        checkpoint when it improves) and a regular checkpoint every `save_every` epochs. The reference takes the
+        regular save only on non-validation epochs (an `elif`); here it is taken on every `save_every` epoch that did
+        not already write a best checkpoint, so a validation epoch with a NaN or non-improving metric does not lose
+        the epoch's progress for a resume."""
         best, result = self.best_result, None
         for epoch in range(self.start_epoch + 1, self.config.max_epochs + 1):
             self.run_epoch("train", epoch)
+            saved = False
             if self.test_dataset is not None and epoch % val_every == 0:
                 result = self.run_epoch("infer_test", epoch)
                 if self.rank == 0:
@@ -118,7 +128,8 @@ class DDPTrainer:
                 if result == result and result > best:
                     best = result
                     self.save_checkpoint(epoch, best, is_best=True)
-            elif epoch % save_every == 0:
+                    saved = True
+            if not saved and epoch % save_every == 0:
                 self.save_checkpoint(epoch, best, is_best=False)
         self.best_result = best
         return result

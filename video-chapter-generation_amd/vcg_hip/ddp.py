@@ -56,6 +56,8 @@ class GradAllReducer:
         self.record = record
         self.log = []        # ("hook", lo, hi) / ("flush", lo, hi) in call order (record=True)
         self._flushed = []   # [lo, hi) ranges reduced in this backward: finish() reduces the rest of the buffer
+        self._buckets = self._bytes = 0
+        self.last_step = {"buckets": 0, "bytes": 0}  # collectives issued by the last finish()ed backward
 
     # called by the engines (autograd backward thread) with parameters whose grads are final
     def __call__(self, params):
@@ -98,6 +100,8 @@ class GradAllReducer:
         lo, hi = self._lo, min(self._hi, self.flat.total)
         self._flushed.append((lo, hi))
         buf = self.flat.grad[lo:hi]
+        self._buckets += 1
+        self._bytes += (hi - lo) * (2 if self.wire is not None else 4)
         if self.record:
             self.log.append(("flush", lo, hi))
         if _DEBUG:
@@ -163,11 +167,25 @@ class GradAllReducer:
             else:
                 dst.copy_(src)
         self._pending_casts = []
+        self.last_step = {"buckets": self._buckets, "bytes": self._bytes}
+        self._buckets = self._bytes = 0
 
     def reduce_all(self):
         """Synchronous fallback: one all-reduce of the whole flat gradient buffer."""
         if self.enabled:
             dist.all_reduce(self.flat.grad, op=dist.ReduceOp.SUM, group=self.group)
+
+
+def params_max_divergence(flat, src=0, group=None):
+    """max over ranks and elements of |param - rank src's param| over the flat parameter buffer (0.0: every rank
+    holds bit-identical parameters, as DDP guarantees after each synchronised step)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return 0.0
+    ref = flat.data.clone()
+    dist.broadcast(ref, src=src, group=group)
+    d = (flat.data - ref).abs().max().reshape(1).to(torch.float64)
+    dist.all_reduce(d, op=dist.ReduceOp.MAX, group=group)
+    return float(d.item())
 
 
 def broadcast_parameters(model, src=0, group=None):

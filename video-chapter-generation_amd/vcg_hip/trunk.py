@@ -655,6 +655,8 @@ class ResNetTrunk:
             Pg0 = r.get("Pg")
 
             def wfn():
+                if a2s[1] is not None:  # colsum(a2) came from a side-stream pass: order it before its reader, on
+                    torch.cuda.current_stream().wait_event(a2s[1])  # whichever stream wfn runs (inline without _ws)
                 G = torch.empty((planes, planes, 1, 1), dtype=torch.float32, device=a2.device)
                 Pg = Pg0
                 if Pg is None:

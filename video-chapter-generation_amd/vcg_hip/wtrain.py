@@ -270,8 +270,8 @@ class HeadAttnFn(torch.autograd.Function):
     def forward(ctx, vis, lang, at, B, T, hid):
         p = _drop_p(at.attn_drop)
         seed = new_seed() if p > 0.0 else 0
-        if _drop_p(at.resid_drop) > 0.0:
-            raise NotImplementedError("SelfAttention resid_drop > 0 in training (the head kernel applies attn_drop)")
+        # resid_drop is declared but never applied by the reference (two_stream_window.py:108 vs :114-131), so it is
+        # ignored here too at any p.
         out, _, saved = ops.head_attn_fwd(vis, lang, at.query, at.key, at.value, at.proj, B, T, hid, at.n_head, p, seed)
         ctx.at, ctx.dims, ctx.p, ctx.seed, ctx.saved_state = at, (B, T, hid), p, seed, saved
         ctx.save_for_backward(vis, lang)
