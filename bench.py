@@ -496,9 +496,9 @@ def main():
     # one extra (untimed) step with every fast-GEMM launch bracketed by HIP events; BERT runs on the trunk's
     # stream for this step, so a launch's duration is the kernel's own (not shared with a concurrent kernel)
     from vcg_hip.trunk import ResNetTrunk
-    sides = (model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream, ResNetTrunk.prep_stream)
+    sides = (model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream)
     # (and the weight gradients / downsample convs / weight re-layout on the trunk's stream)
-    model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = ResNetTrunk.prep_stream = False
+    model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = False
     ops.timing_enable(True)
     if not args.no_roofline_step:
         step()
@@ -510,7 +510,7 @@ def main():
     peak_tf = MFMA_PEAK_TFLOPS[args.precision]
     rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (dom_id, ops.TIMING_WGRAD)}
     ops.timing_enable(False)
-    model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream, ResNetTrunk.prep_stream = sides
+    model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream = sides
     kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
     ddp = {}
     if world > 1:

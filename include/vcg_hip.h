@@ -66,14 +66,9 @@ VCG_API int vcg_fast_stamps(unsigned long long* out, int n);
  * vcg_weight_prep(transposed = 2 + pad); two stride-2 taps per 16-B chunk (GEMM K 224 instead of 392). */
 VCG_API int vcg_conv_stats_tiles(int M);
 VCG_API int vcg_conv_fwd(int dtype, const void* x, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
-/* vcg_conv_fwd of a 1x1 / stride-1 conv whose input is relu(x * in_scale[c] + in_shift[c]) rounded to bf16 (the
-   previous BatchNorm + ReLU, reference torchvision Bottleneck bn2 -> relu -> conv3), applied to x in LDS as each
-   tile lands instead of by a separate vcg_bn_apply pass; bf16 fast engine with BN statistics only (else
-   VCG_ERR_UNSUPPORTED). Bit-identical to vcg_bn_apply + vcg_conv_fwd. */
 /* y = act(conv(x, w) + bias[col]) (act 0 none / 1 ReLU), no statistics: a conv with its running-statistics BN folded
    into w (vcg_weight_fold) and the BN shift as bias -- the scoring (eval) forward, test_video_segment_point.py:116-122 */
 VCG_API int vcg_conv_fwd_bias_act(int dtype, const void* x, const void* w, const float* bias, int act, void* y, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
-VCG_API int vcg_conv_fwd_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* w, void* y, float* stats, int N, int H, int W, int C, int Cout, hipStream_t stream);
 /* autograd of conv2d: input gradient (transposed-conv gather) */
 VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, hipStream_t stream);
 /* vcg_conv_dgrad fused with the trunk backward's next steps (igemm.h BwdEpi): TSM adjoint (tsm_fold > 0:
@@ -89,9 +84,6 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
    the pair-packed stem gather (as vcg_conv_fwd) */
 VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad);
 VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream);
-/* vcg_conv_wgrad of the conv above: x passes BN + ReLU in LDS (bf16 fast engine, no TSM, C >= 64; else
-   VCG_ERR_UNSUPPORTED). Bit-identical to vcg_bn_apply + vcg_conv_wgrad. */
-VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* dy, float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, hipStream_t stream);
 /* A batch-statistics BatchNorm backward (torch BatchNorm2d autograd: dy = A g + B y + Cc per channel, as
    vcg_bn_bwd_apply) folded into the two gradients of the 1x1 conv that consumes dy (bottleneck conv3 after
    bn3, model/vision/resnet50_tsm.py:15 via torchvision Bottleneck), so dy is never stored (bf16 only):

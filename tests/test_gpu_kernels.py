@@ -733,39 +733,6 @@ def test_fused_stem_bn_relu_maxpool(K, dtype, train, hw):
     assert torch.equal(dx, dx_ref)
 
 
-@pytest.mark.parametrize("case", [(8, 14, 14, 64, 256), (4, 7, 7, 512, 2048), (16, 28, 28, 128, 512),
-                                  (3, 9, 11, 256, 1024)])
-def test_conv_bn_on_load(K, case):
-    """conv3 with bn2 + ReLU applied to its input in LDS (vcg_conv_fwd_bnin / vcg_conv_wgrad_bnin) == bn_apply then
-    the plain conv, bit for bit (same bf16 operand values, same products in the same order)."""
-    N, H, W, C, Cout = case
-    dtype = torch.bfloat16
-    y = _rand((N, H, W, C), dtype, 101).to(DEV)
-    g0 = torch.Generator().manual_seed(102)
-    sc = (torch.rand(C, generator=g0) * 2 - 0.5).to(DEV)
-    sh = (torch.randn(C, generator=g0) * 0.3).to(DEV)
-    w = _rand((Cout, C, 1, 1), torch.float32, 103, 0.05).to(DEV)
-    wd = K.weight_prep(w, C, dtype)
-    M = N * H * W
-    a = K.bn_apply(y, sc, sh, C, relu=True)
-    st0, st1 = K.stats_buffer(Cout, M, DEV), K.stats_buffer(Cout, M, DEV)
-    ref = K.conv_fwd(a, wd, N, H, W, C, Cout, 1, 1, 1, 0, stats=st0)
-    out = K.conv_fwd_bnin(y, sc, sh, wd, N, H, W, C, Cout, st1)
-    assert out is not None, "the fused engine must take this shape"
-    assert torch.equal(out, ref)
-    m0, m1 = (torch.empty(Cout, device=DEV) for _ in range(2))
-    z = [torch.empty(Cout, device=DEV) for _ in range(6)]
-    K.bn_finalize(st0, K.stats_tiles(M), M, Cout, None, None, m0, z[0], z[1], z[2], None, None, 0.1, 1e-5)
-    K.bn_finalize(st1, K.stats_tiles(M), M, Cout, None, None, m1, z[3], z[4], z[5], None, None, 0.1, 1e-5)
-    assert torch.allclose(m0, m1, rtol=1e-5, atol=1e-6)
-    dy = _rand((N, H, W, Cout), dtype, 104).to(DEV)
-    dw0 = torch.full((Cout, C, 1, 1), 0.5, device=DEV)
-    dw1 = dw0.clone()
-    K.conv_wgrad(a, dy, dw0, N, H, W, C, C, Cout, 1, 1, 1, 0, accumulate=True)
-    assert K.conv_wgrad_bnin(y, sc, sh, dy, dw1, N, H, W, C, Cout, 1, 1, 1, 0)
-    assert torch.equal(dw0, dw1)
-
-
 def test_attention_softmax_dropout(K):
     """Masked softmax + dropout: P matches torch softmax over the valid keys; Pd = P / (1 - p) on kept
     entries and 0 on dropped ones (drop rate ~ p); the backward regenerates the same mask."""

@@ -42,15 +42,6 @@ def main():
                   f"stage {d[:, 1].mean():5.0f} flush {d[:, 2].mean():5.0f} to next tile {(per - (st[:-1, 3] - st[:-1, 0])).mean():5.0f}",
                   flush=True)
         return
-    if os.environ.get("VCG_BENCH_G8"):  # A/B of the 256-row ping-pong kernel (VCG_G8) in one process
-        for name, fn in _ab_cases() + _dense_cases():
-            res = []
-            for st in ("1", "0", "1b", "1", "0"):  # (1b: 256 x 128 tiles)
-                os.environ["VCG_G8"] = st[0]
-                os.environ["VCG_G8_BN128"] = "1" if st.endswith("b") else "0"
-                res.append(f"{st}: {timeit(fn, 20):7.1f}us")
-            print(f"{name:32s} " + "  ".join(res), flush=True)
-        return
     if os.environ.get("VCG_BENCH_AB"):  # A/B of the output staging threshold in one process
         for name, fn in _ab_cases():
             res = []

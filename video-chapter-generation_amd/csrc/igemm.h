@@ -109,11 +109,6 @@ struct GemmParams {
   int res_round; // residual epilogue: round alpha*AB + bias to bf16 before adding the residual (VCG_ACT_FLAG_ROUND_PRE)
   int fast_act;  // bf16 epilogues: GELU / GELU' through erf_fast (common.h) instead of erff (VCG_FAST_GELU=0: off)
   BwdEpi bwd;    // EPI_BWD
-  // the consuming conv applies its input's BatchNorm + ReLU on load: x -> bf16(max(fma(x, in_sc[c], in_sh[c]), 0))
-  // (vcg_bn_apply's arithmetic) for input channel c, in LDS right after the tile's DMA lands (fast dense A of
-  // igemm_fast_kernel / the x operand of wgrad_fast_kernel); in_C channels
-  const float *in_sc, *in_sh;
-  int in_C;
   // EPI_STORE + residual + ReLU through the stage (epilogue_staged_res): also store the ReLU decisions as mask bits,
   // byte (m N + n) / 8 bit n % 8 (vcg_bn_apply's bits layout; vcg_conv1x1_bn_res_relu)
   uint8_t* obits;
@@ -295,14 +290,13 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
 }
 
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
-int run_gemm8(const GemmParams& p, int amode, int epi, int z, hipStream_t s);  // igemm8.hip (-1: n/a)
 int fast_grid_rows(int M, int N, int z, int epi);
 int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an EPI_BWD launch of run_fast_gemm
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
                            float* dgamma, float* dbeta, int accumulate, hipStream_t s);  // grid rows (slots of EPI_BWD partials) of a fast-kernel launch
 int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b = false);
 int wgrad_patch_rows(int dtype, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                     int tsm_fold, bool bn_in);
+                     int tsm_fold);
 int wgrad_patch_splits();
 int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int W, int R, hipStream_t s);
 int wgrad_fast_tile_m(int M);

@@ -564,15 +564,6 @@ VCG_API int vcg_conv_fwd_bias_act(int dtype, const void* x, const void* w, const
                        tsm_fold, stream, bias, act);
 }
 
-// The conv's input is BN + ReLU of x, applied on load (never stored): bf16, 1x1 / stride 1 with BN statistics
-// (the trunk's conv3 over bn2's input); VCG_ERR_UNSUPPORTED elsewhere.
-VCG_API int vcg_conv_fwd_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* w,
-                              void* y, float* stats, int N, int H, int W, int C, int Cout, hipStream_t stream) {
-  VCG_REQUIRE(in_scale && in_shift && stats, "in_scale / in_shift / stats required");
-  if (dtype != VCG_BF16 || !fast_gemm_enabled() || C > 1024) return VCG_ERR_UNSUPPORTED;
-  return conv_fwd_impl(dtype, x, in_scale, in_shift, w, y, stats, N, H, W, C, Cout, 1, 1, 1, 0, 0, 0, stream);
-}
-
 static int conv_fwd_impl(int dtype, const void* x, const float* in_sc, const float* in_sh, const void* w, void* y,
                          float* stats, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad,
                          int tsm_T, int tsm_fold, hipStream_t stream, const float* bias, int act) {
@@ -613,23 +604,9 @@ static int conv_fwd_impl(int dtype, const void* x, const float* in_sc, const flo
   p.ldc = Cout;
   p.alpha = 1.f;
   p.stats = stats;
-  p.in_sc = in_sc;
-  p.in_sh = in_sh;
-  p.in_C = C;
   p.bias = bias;
   p.act = act;
   const int epi = stats ? EPI_STATS : EPI_STORE;
-  if (in_sc) {  // the fast engine only (no generic fallback applies the input BN)
-    if (!dense || dtype != VCG_BF16 || p.a.bytes >= 0xFFFFFF00LL || p.b.bytes >= 0xFFFFFF00LL) return VCG_ERR_UNSUPPORTED;
-    const int rc = run_fast_gemm(p, OP_DENSE_K, epi, 1, stream);
-    if (rc >= 0) {
-      if (FILE* f = gemm_log()) {
-        fprintf(f, "a=0 b=0 epi=%d M=%d N=%d K=%d z=1 fast=1 conv=1x1/1 C=%d bnin=1\n", epi, p.M, p.N, p.K, Cout);
-        fflush(f);
-      }
-    }
-    return rc < 0 ? VCG_ERR_UNSUPPORTED : rc;
-  }
   if (dtype == VCG_BF16) {
     return dense ? run_gemm<bf16_t, OP_DENSE_K, OP_DENSE_K>(p, epi, 1, stream)
                  : run_gemm<bf16_t, OP_IM2COL, OP_DENSE_K>(p, epi, 1, stream);
@@ -870,7 +847,7 @@ VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C,
   int M, Nn, K, splits, kps;
   bool fast;
   wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits, &kps, &fast);
-  if (wgrad_patch_rows(dtype, H, W, C, C, Cout, KH, KW, stride, pad, 0, false) > 0 && splits < wgrad_patch_splits())
+  if (wgrad_patch_rows(dtype, H, W, C, C, Cout, KH, KW, stride, pad, 0) > 0 && splits < wgrad_patch_splits())
     splits = wgrad_patch_splits();  // the patch kernel's slabs
   return (long long)splits * M * Nn * 4;
 }
@@ -885,20 +862,6 @@ VCG_API int vcg_conv_wgrad(int dtype, const void* x, const void* dy, float* dw, 
                            int stride, int pad, int tsm_T, int tsm_fold, hipStream_t stream) {
   return conv_wgrad_impl(dtype, x, nullptr, nullptr, dy, dw, accumulate, ws, ws_bytes, N, H, W, C, Cin, Cout, KH, KW,
                          stride, pad, tsm_T, tsm_fold, stream);
-}
-
-// Weight gradient of a conv whose input is BN + ReLU of x (vcg_conv_fwd_bnin's conv): the transform is applied to
-// x in LDS by the fast bf16 engine (no TSM, C >= 64); VCG_ERR_UNSUPPORTED elsewhere.
-VCG_API int vcg_conv_wgrad_bnin(int dtype, const void* x, const float* in_scale, const float* in_shift, const void* dy,
-                                float* dw, int accumulate, float* ws, long long ws_bytes, int N, int H, int W, int C,
-                                int Cout, int KH, int KW, int stride, int pad, hipStream_t stream) {
-  VCG_REQUIRE(in_scale && in_shift, "in_scale / in_shift required");
-  int M, Nn, K, splits, kps;
-  bool fast;
-  wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits, &kps, &fast);
-  if (dtype != VCG_BF16 || !fast || C < 64) return VCG_ERR_UNSUPPORTED;
-  return conv_wgrad_impl(dtype, x, in_scale, in_shift, dy, dw, accumulate, ws, ws_bytes, N, H, W, C, C, Cout, KH, KW,
-                         stride, pad, 0, 0, stream);
 }
 
 static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const float* in_sh, const void* dy,
@@ -936,10 +899,7 @@ static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const f
   p.b = b;
   p.ws = ws;
   p.alpha = 1.f;
-  p.in_sc = in_sc;
-  p.in_sh = in_sh;
-  p.in_C = C;
-  const int wpr = wgrad_patch_rows(dtype, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_fold, in_sc != nullptr);
+  const int wpr = wgrad_patch_rows(dtype, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_fold);
   if (wpr > 0) {  // layer-1 3x3: im2col-free patch kernel (igemm_wgrad.hip), one slab per workgroup
     const int wsp = wgrad_patch_splits();
     VCG_REQUIRE(ws_bytes >= (long long)wsp * M * Nn * 4, "workspace too small");
@@ -1273,7 +1233,6 @@ VCG_API int vcg_conv_wgrad_bnfold(const void* x, const void* g, const void* yg, 
   p.b = b;
   p.ws = ws;
   p.alpha = 1.f;
-  p.in_C = C;
   if (FILE* f = gemm_log())
     fprintf(f, "a=3 b=4 epi=2 M=%d N=%d K=%d z=%d fast=2 conv=1x1/1 C=%d bnfold=1\n", M, Nn, K, splits, C);
   int rc = run_fast_wgrad(p, splits, stream);

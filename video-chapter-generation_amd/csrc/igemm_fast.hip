@@ -25,16 +25,13 @@ __device__ __forceinline__ int fswz(int row, int chunk) { return chunk ^ ((row >
 // k tile), OP_IM2COL_TSM (the same with the TSM shift fused), OP_IM2COL_SMALLC (C < 64: the stem)
 constexpr int OP_IM2COL_TSM = 5;
 constexpr int OP_IM2COL_SMALLC = 6;
-// dense A whose BatchNorm + ReLU is applied on load (p.in_sc / p.in_sh; the conv-stats GEMM of a 1x1 conv whose
-// input is a BN output that is never stored): its own instantiation, so the plain dense GEMMs carry no table
-constexpr int OP_DENSE_K_BN = 7;
 // dense A from two sources along K (OpArgs ptr2 / split2): [g | y] of a BatchNorm backward folded into the consuming
 // conv's input gradient; its own instantiation, so the plain dense loaders carry no second descriptor
 constexpr int OP_DENSE_K2 = 8;
 
 template <int ROWS, int MODE, int NW = 4> struct FastLoader {
   static constexpr int PER_WAVE = ROWS / (8 * NW);  // 1-KiB (8-row) slices per wave per tile
-  static constexpr bool GATHER = MODE != OP_DENSE_K && MODE != OP_DENSE_K_BN && MODE != OP_DENSE_K2;
+  static constexpr bool GATHER = MODE != OP_DENSE_K && MODE != OP_DENSE_K2;
   static constexpr bool TWO = MODE == OP_DENSE_K2;
   static constexpr bool IM2COL = MODE == OP_IM2COL || MODE == OP_IM2COL_TSM || MODE == OP_IM2COL_SMALLC;
   static constexpr bool TSM = MODE == OP_IM2COL_TSM;
@@ -1069,17 +1066,11 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
   constexpr bool BWD = EPI == EPI_BWD || EPI == EPI_BWD_AFF;
   constexpr int CPAR = BWD ? 6 * BN : 0;  // EPI_BWD per-column parameters
   constexpr int RED = 2 * WM * BN + WM + 4;
-  // input BN + ReLU applied on load (p.in_sc, dense A of the conv-stats GEMM): [in_sc | in_sh][K <= BNIN_MAX]
-  constexpr bool BNIN = AM == OP_DENSE_K_BN;
-  static_assert(!BNIN || (EPI == EPI_STATS && BM == 128 && BN == 128), "BN on load: conv-stats 128 x 128 only");
-  constexpr int BNIN_MAX = 1024;
-  constexpr int TBL = BNIN ? 2 * BNIN_MAX : 0;
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * (AE + BE) * 2 + (RED + CPAR + TBL) * 4];
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * (AE + BE) * 2 + (RED + CPAR) * 4];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
   bf16_t* Bs = As + STAGES * AE;
   float* red = reinterpret_cast<float*>(smem + STAGES * (AE + BE) * 2);
   float* cpar = red + RED;  // [mean, msc, msh, mean2, invstd, invstd2][BN]
-  float* tbl = cpar + CPAR;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -1137,13 +1128,6 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
     for (int j = 0; j < NT; ++j) asm volatile("" ::"v"(bv[j][0]), "v"(bv[j][1]), "v"(bv[j][2]), "v"(bv[j][3]));
   }
 
-  if constexpr (BNIN) {  // the input BN table, before the first DMA (plain loads + barrier; no LDS-DMA in flight yet)
-    for (int c = tid; c < p.K; c += BM * 2) {
-      tbl[c] = p.in_sc[c];
-      tbl[BNIN_MAX + c] = p.in_sh[c];
-    }
-    __syncthreads();
-  }
   FastLoader<BM, AM, NW> la;
   FastLoader<BN, OP_DENSE_K, NW> lb;
   la.init(p.a, aoff, by * BM, wave, lane);
@@ -1185,45 +1169,6 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
     if (STAGES == 3 && ahead >= 2) __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * NLD));
     else if (ahead >= 1) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NLD));
     else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-    if constexpr (BNIN) {
-      {
-        // this wave's own A chunks of the step (its DMA has landed: the wait above) -> BN + ReLU in place,
-        // before the barrier that publishes the stage (lane-linear slot l of slice q = row 8 q' + l / 8,
-        // 16-B chunk fswz(row, l % 8) of the 64-wide k tile)
-        constexpr int PW = BM / (8 * NW);
-        bf16_t* Ast = As + cur * AE;
-#pragma unroll
-        for (int q = 0; q < PW; ++q) {
-          const int sl = wave * PW + q;
-          const int r = sl * 8 + (lane >> 3);
-          const int k = kt * FBK + 8 * fswz(r, lane & 7);
-          if (k < p.K) {
-            const uint32_t addr = lds_u32(Ast + sl * 512 + lane * 8);
-            uint4 v;
-            asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
-            float sc8[8], sh8[8], x[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              sc8[i] = tbl[k + i];
-              sh8[i] = tbl[BNIN_MAX + k + i];
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            unpack8(v, x);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = fmaxf(fmaf(x[i], sc8[i], sh8[i]), 0.f);
-            v.x = (uint32_t)f2bf(x[0]) | ((uint32_t)f2bf(x[1]) << 16);
-            v.y = (uint32_t)f2bf(x[2]) | ((uint32_t)f2bf(x[3]) << 16);
-            v.z = (uint32_t)f2bf(x[4]) | ((uint32_t)f2bf(x[5]) << 16);
-            v.w = (uint32_t)f2bf(x[6]) | ((uint32_t)f2bf(x[7]) << 16);
-            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 w4 = {v.x, v.y, v.z, v.w};
-            asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(w4) : "memory");
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-    }
     __builtin_amdgcn_s_barrier();
     if (kt == 0) FAST_STAMP(tile, 0);
     const bf16_t* Ac = As + cur * AE;
@@ -1939,7 +1884,7 @@ int fast_bwd_slots(const GemmParams& p) {
 template <int AM, int EPI, bool RES>
 static double algorithmic_bytes(const GemmParams& p, int z) {
   const double mn = (double)p.M * p.N * z;
-  double b = (AM == OP_DENSE_K || AM == OP_DENSE_K_BN || AM == OP_DENSE_K2 ? 2.0 * p.M * (double)p.K * z : (double)p.a.bytes) + 2.0 * p.N * (double)p.K * z;
+  double b = (AM == OP_DENSE_K || AM == OP_DENSE_K2 ? 2.0 * p.M * (double)p.K * z : (double)p.a.bytes) + 2.0 * p.N * (double)p.K * z;
   b += 2.0 * mn;
   if (RES) b += 2.0 * mn;
   if (p.aux) b += 2.0 * mn;
@@ -2030,19 +1975,9 @@ static int launch_stem(const GemmParams& p, int R, hipStream_t s) {
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   const char* e = getenv("VCG_STAGE_KT");
   p.stage_kt = e && e[0] ? atoi(e) : 1 << 30;
-  if (p.in_sc) {  // input BN + ReLU on load: the dense conv-stats GEMM on 128 x 128 tiles only
-    if (amode != OP_DENSE_K || epi != EPI_STATS || z != 1 || p.K > 1024 || p.K % 8 != 0 ||
-        fast_bn_cols(p.N) != 128 || fast_bm(p.M, p.N, z, false) != 128)
-      return -1;
-    return launch_fast<128, 128, OP_DENSE_K_BN, EPI_STATS, false>(p, z, s);
-  }
   if (p.a.ptr2) {  // a BatchNorm backward folded into this input gradient: A = [g | y] (light epilogue only)
     if (amode != OP_DENSE_K || epi != EPI_BWD || z != 1 || !bwd_light(p) || p.a.split2 % FBK != 0) return -1;
     return fast_bn<OP_DENSE_K2, EPI_BWD_AFF>(p, z, s);
-  }
-  if (epi == EPI_STATS || epi == EPI_STORE) {  // the 256-row ping-pong kernel for the compute-bound shapes
-    const int rc = run_gemm8(p, amode, epi, z, s);
-    if (rc >= 0) return rc;
   }
   if (amode == OP_IM2COL && p.a.tsm_fold > 0) amode = OP_IM2COL_TSM;
   if (amode == OP_IM2COL && p.a.C < FBK) amode = OP_IM2COL_SMALLC;

@@ -171,9 +171,7 @@ __device__ __forceinline__ constexpr int wvm(int n) { return (n & 0xF) | (0x7 <<
 
 // BG: B is the im2col gather of x (conv wgrad); !BG: B is a dense [K][ld] operand (the Linear weight gradients
 // dW = dY^T X of BERT / the head: a 1x1 "conv" whose pixels are the token rows, any column count).
-// BNI (with BG): x's BatchNorm + ReLU applied on load (p.in_sc / p.in_sh), its own instantiation so the plain
-// gathers keep their register budget
-template <int BM, int BN, bool BG, bool BNI = false>
+template <int BM, int BN, bool BG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_fast_kernel(GemmParams p) {
   constexpr int MT = BM / 32, NT = BN / 32;
   constexpr int AE = WBK * BM, BE = WBK * BN;
@@ -200,32 +198,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   const int ke = min(p.K, kb + p.k_per_split);
   const int ntiles = (ke - kb + WBK - 1) / WBK;
 
-  static_assert(BG || !BNI, "BN on load needs the gathered x operand");
-  constexpr bool bnin = BNI;
   MNLoader<BM, false> la;
   MNLoader<BN, BG> lb;
   la.init(p.a, m0, p.M, kb, wave, lane);
   lb.init(p.b, n0, p.N, kb, wave, lane);
-  uint32_t okb[2] = {0u, 0u};  // pieces of the x stage that hold real pixels (bnin: transformed in place)
-  // x's BatchNorm + ReLU applied on load (p.in_sc: the consuming conv's input is the BN output, not stored): a
-  // lane's x pieces keep their channels for the whole kernel, so their scale / shift live in registers (loaded
-  // before the first DMA: no VGPR-destination load inside the LDS-DMA loop)
-  constexpr int NIB = MNLoader<BN, BG>::NI;
-  float bsc[BNI ? NIB : 1][8], bsh[BNI ? NIB : 1][8];
-  if constexpr (BNI) {
-    {
-#pragma unroll
-      for (int q = 0; q < NIB; ++q) {
-        const int c0 = max(lb.col[q], 0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          bsc[q][i] = p.in_sc[c0 + i];
-          bsh[q][i] = p.in_sh[c0 + i];
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(wvm(0));
-    }
-  }
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -235,47 +211,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
 
   if (ntiles > 0) {
     la.issue(p.a, kb, ke, As, wave);
-    okb[0] = lb.issue(p.b, kb, ke, Bs, wave);
+    lb.issue(p.b, kb, ke, Bs, wave);
   }
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     if (t + 1 < ntiles) {
       la.issue(p.a, kb + (t + 1) * WBK, ke, As + (cur ^ 1) * AE, wave);
-      okb[cur ^ 1] = lb.issue(p.b, kb + (t + 1) * WBK, ke, Bs + (cur ^ 1) * BE, wave);
+      lb.issue(p.b, kb + (t + 1) * WBK, ke, Bs + (cur ^ 1) * BE, wave);
       __builtin_amdgcn_s_waitcnt(wvm(NLD));
     } else {
       __builtin_amdgcn_s_waitcnt(wvm(0));
-    }
-    if constexpr (bnin) {
-      // this wave's own x pieces of the stage (landed: the wait above): BN + ReLU in place before the barrier
-      // that publishes the stage; zero-filled pieces (padding, pixels past the split) stay zero
-      const uint32_t okm = okb[cur];
-#pragma unroll
-      for (int q = 0; q < NIB; ++q) {
-        if ((okm >> q) & 1u) {
-          const uint32_t addr = lds_addr(Bs + cur * BE + (wave * NIB + q) * 512 + lane * 8);
-          uint4 v;
-          asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
-          float x[8];
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            x[2 * i] = __uint_as_float(w4[i] << 16);
-            x[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
-          }
-#pragma unroll
-          for (int i = 0; i < 8; ++i) x[i] = fmaxf(fmaf(x[i], bsc[q][i], bsh[q][i]), 0.f);
-          typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-          const u32x4 o = {(uint32_t)f2bf(x[0]) | ((uint32_t)f2bf(x[1]) << 16),
-                           (uint32_t)f2bf(x[2]) | ((uint32_t)f2bf(x[3]) << 16),
-                           (uint32_t)f2bf(x[4]) | ((uint32_t)f2bf(x[5]) << 16),
-                           (uint32_t)f2bf(x[6]) | ((uint32_t)f2bf(x[7]) << 16)};
-          asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(o) : "memory");
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     const bf16_t* Ac = As + cur * AE;
@@ -319,14 +264,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   }
 }
 
-template <int BM, int BN, bool BG, bool BNI = false> int launch_wgrad(const GemmParams& p0, int splits, hipStream_t s) {
+template <int BM, int BN, bool BG> int launch_wgrad(const GemmParams& p0, int splits, hipStream_t s) {
   GemmParams p = p0;
   p.batch_inner = splits;
   const long long per = (long long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   const long long wgs = (splits + 7) / 8 * 8 * per;
   VCG_REQUIRE(wgs < (1LL << 31), "wgrad grid too large");
   const int tk = timing_begin(s);
-  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, BG, BNI>), dim3((unsigned)wgs), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, BG>), dim3((unsigned)wgs), dim3(256), 0, s, p);
   // algorithmic bytes: dy and x read once, the fp32 weight gradient written once (the split slabs are not)
   timing_end(tk, s, TIMING_WGRAD, 2.0 * p.M * p.N * (double)p.K,
              (double)p.a.bytes + (double)p.b.bytes + 4.0 * p.M * (double)p.N);
@@ -490,12 +435,6 @@ int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b)
     if (bn == 128) return launch_wgrad<64, 128, false>(p, splits, s);
     return launch_wgrad<64, 64, false>(p, splits, s);
   }
-  if (p.in_sc) {
-    if (bm == 128 && bn == 128) return launch_wgrad<128, 128, true, true>(p, splits, s);
-    if (bm == 128) return launch_wgrad<128, 64, true, true>(p, splits, s);
-    if (bn == 128) return launch_wgrad<64, 128, true, true>(p, splits, s);
-    return launch_wgrad<64, 64, true, true>(p, splits, s);
-  }
   if (bm == 128 && bn == 128) return launch_wgrad<128, 128, true>(p, splits, s);
   if (bm == 128) return launch_wgrad<128, 64, true>(p, splits, s);
   if (bn == 128) return launch_wgrad<64, 128, true>(p, splits, s);
@@ -503,16 +442,16 @@ int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b)
 }
 
 // Rows per tile of wgrad3x3_patch_kernel (0: not eligible): bf16, x with C = 64 channels, Cout = 64, 3x3 / stride 1 /
-// pad 1, no TSM, no BN on load, R W <= 128, (R + 2)(W + 2) <= 256, H % R == 0. VCG_WGRAD_PATCH=0 disables it.
+// pad 1, no TSM, R W <= 128, (R + 2)(W + 2) <= 256, H % R == 0. VCG_WGRAD_PATCH=0 disables it.
 int wgrad_patch_rows(int dtype, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                     int tsm_fold, bool bn_in) {
+                     int tsm_fold) {
   static int en = -1;
   if (en < 0) {
     const char* e = getenv("VCG_WGRAD_PATCH");
     en = (e && e[0] == '0') ? 0 : 1;
   }
   if (!en || dtype != VCG_BF16 || C != 64 || Cin != 64 || Cout != 64 || KH != 3 || KW != 3 || stride != 1 ||
-      pad != 1 || tsm_fold != 0 || bn_in)
+      pad != 1 || tsm_fold != 0)
     return 0;
   for (int R = 128 / W; R >= 1; --R)
     if ((R + 2) * (W + 2) <= 8 * WP_SL && H % R == 0) return R;

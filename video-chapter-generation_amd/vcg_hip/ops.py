@@ -301,39 +301,6 @@ def conv_wgrad(x, dy, dw, N, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_T=0, t
     return workspace
 
 
-def conv_fwd_bnin(x, in_scale, in_shift, w, N, H, W, C, Cout, stats, out=None):
-    """1x1 conv (with BN statistics) of relu(x * in_scale + in_shift) -- the input BN + ReLU applied on load
-    (vcg_conv_fwd_bnin). Returns y, or None where the fused engine does not apply (then bn_apply + conv_fwd)."""
-    _chk(x, name="x")
-    _chk(w, x.dtype, "w")
-    y = out if out is not None else torch.empty((N, H, W, Cout), dtype=x.dtype, device=x.device)
-    rc = _lib.query("vcg_conv_fwd_bnin", dt_code(x.dtype), P(x), P(in_scale), P(in_shift), P(w), P(y), P(stats), N, H,
-                    W, C, Cout, stream())
-    if rc == -2:  # VCG_ERR_UNSUPPORTED
-        return None
-    if rc != 0:
-        raise _lib.VcgError(f"vcg_conv_fwd_bnin failed ({rc}): {_lib.last_error()}")
-    return y
-
-
-def conv_wgrad_bnin(x, in_scale, in_shift, dy, dw, N, H, W, C, Cout, KH, KW, stride, pad, workspace=None):
-    """dw += wgrad of the conv whose input is relu(x * in_scale + in_shift) (vcg_conv_wgrad_bnin). Returns False
-    where the fused engine does not apply."""
-    _chk(x, name="x")
-    _chk(dy, x.dtype, "dy")
-    _chk(dw, torch.float32, "dw")
-    nbytes = _lib.query("vcg_conv_wgrad_ws_bytes", dt_code(x.dtype), N, H, W, C, Cout, KH, KW, stride, pad)
-    if workspace is None or workspace.numel() * 4 < nbytes:
-        workspace = ws(nbytes, x.device)
-    rc = _lib.query("vcg_conv_wgrad_bnin", dt_code(x.dtype), P(x), P(in_scale), P(in_shift), P(dy), P(dw), 1,
-                    P(workspace), workspace.numel() * 4, N, H, W, C, Cout, KH, KW, stride, pad, stream())
-    if rc == -2:  # VCG_ERR_UNSUPPORTED
-        return False
-    if rc != 0:
-        raise _lib.VcgError(f"vcg_conv_wgrad_bnin failed ({rc}): {_lib.last_error()}")
-    return True
-
-
 def conv_wgrad_ws_bytes(dtype, N, H, W, C, Cout, KH, KW, stride, pad):
     return _lib.query("vcg_conv_wgrad_ws_bytes", dt_code(dtype), N, H, W, C, Cout, KH, KW, stride, pad)
 

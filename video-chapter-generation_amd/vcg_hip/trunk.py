@@ -88,33 +88,22 @@ class _ConvWeights:
         return (flat is self.flat and stem_cpad == self.stem_cpad
                 and [c.weight.data_ptr() for c in self.convs] == self.ptrs)
 
-    def refresh(self, side=None):
-        """Re-lay-out the weights after an optimizer step. side: the stem's layout (descriptor 0) on the current
-        stream, the other 52 convs' on `side` (they are first read after the stem conv + max-pool); returns the event
-        the first bottleneck waits for (None: all on the current stream)."""
+    def refresh(self):
+        """Re-lay-out the weights after an optimizer step (one launch for all 53 convs). (Splitting it -- the stem's
+        layout first, the rest on a side stream under the stem conv + max-pool -- measured neutral, round 2.)"""
         if self.gen == self.flat.generation:
-            return None
+            return
         self.gen = self.flat.generation
-        if side is None or self.n < 2:
-            ops.weight_prep_multi(self.desc, self.n)
-            return None
-        ops.weight_prep_multi(self.desc, 1)
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            ops.weight_prep_multi(self.desc[1:], self.n - 1)
-            ev = torch.cuda.Event()
-            ev.record(side)
-        return ev
+        ops.weight_prep_multi(self.desc, self.n)
 
 
 class ResNetTrunk:
     staged = False  # forward() input is already the stem's NHWC layout [N, H, W, Cpad] (ops.window_frames_u8)
     # backward-path census (tests: the bf16 step must run the fused conv_dgrad_bwd engine everywhere)
     path_counts = {"fused": 0, "unfused": 0}
-    # VCG_BNIN=1: conv3 applies bn2 + ReLU on load (bf16) instead of the separate bn_apply pass. Bit-identical, but
-    # measured slower (730 windows/s with it, 745 without, same box): the in-LDS transform sits between the DMA wait and the
-    # barrier of every k-step and costs the conv3 GEMMs 20-76% (fwd) and 3-56% (wgrad), more than the pass saves
-    fused_bnin = os.environ.get("VCG_BNIN") == "1"
+    # per-block path census (tests): a list to append to, or None. Forward entries ("fwd", C3, ds, {a2sum, y3_drop,
+    # bn3_gemm}), backward entries ("bwd", C3, ds, {fold_wgrad, fold_dgrad}), in execution order
+    census = None
     # False: run the bf16 backward through the unfused ops (conv_dgrad + bn_bwd_reduce / apply + tsm_unshift_add),
     # the reference path the fused conv_dgrad_bwd engine is checked against (tests/test_gpu_bf16_train.py)
     fused_bwd = True
@@ -123,9 +112,6 @@ class ResNetTrunk:
     wgrad_stream = os.environ.get("VCG_WGRAD_STREAM", "1") != "0"
     # forward of a layer's first bottleneck: the downsample conv on the side stream (VCG_DS_STREAM=0: inline)
     ds_stream = os.environ.get("VCG_DS_STREAM", "1") != "0"
-    # VCG_PREP_SIDE=1: the per-step bf16 weight re-layout of all convs but the stem on the side stream, under the stem
-    # conv + max-pool (measured neutral: 756 / 762 vs 760 / 759 windows/s, profiles/r02_bench_prep_side_ab.txt)
-    prep_stream = os.environ.get("VCG_PREP_SIDE", "0") == "1"
     # the first bottleneck of a layer: bn3's and the downsample BN's backward applies in one pass over g
     dual_bn_bwd = os.environ.get("VCG_BN_DUAL", "1") != "0"
     # bf16 scoring forward (running-statistics BN, no autograd): bn3 folded into conv3 (1x1 GEMM with the BN scale in
@@ -150,16 +136,12 @@ class ResNetTrunk:
     # second pass of conv3's GEMM (scale folded into its weight rows, shift as bias; ops.conv1x1_bn_res_relu)
     # instead of reading y3 back in the bn_apply pass (0: off)
     bn3_gemm_max_c3 = int(os.environ.get("VCG_BN3_GEMM_MAXC3", "1024"))
-    # ... and of a layer's first block (the residual is the downsample BN's output, applied in the epilogue):
-    # measured neutral (805.3 vs 807.5 windows/s same box), opt-in VCG_BN3_GEMM_FIRST=1
-    bn3_gemm_first = os.environ.get("VCG_BN3_GEMM_FIRST", "0") == "1"
 
     def __init__(self, net, dtype):
         self.net = net
         self.dtype = dtype
         self._ws = None  # weight-gradient side stream of the running backward (_wside)
         self._pending = []  # (event, tensors) the side stream still reads (_hold)
-        self._prep_ev = None  # the side-stream weight re-layout of this step (refresh), joined before layer 1
         self.wc = None
         flat = getattr(net, "_vcg_flat", None)
         if dtype == torch.bfloat16 and flat is not None:
@@ -167,7 +149,7 @@ class ResNetTrunk:
             if wc is None or not wc.valid_for(net, flat, ops.stem_cpad(dtype)):
                 wc = _ConvWeights(net, flat, ops.stem_cpad(dtype))
                 object.__setattr__(net, "_vcg_convw", wc)
-            self._prep_ev = wc.refresh(self._wside(flat.data.device) if ResNetTrunk.prep_stream else None)
+            wc.refresh()
             self.wc = wc
 
     # ---------------------------------------------------------------- helpers
@@ -188,39 +170,25 @@ class ResNetTrunk:
         C3 = blk.conv3.out_channels
         if not need_grad:  # batch-statistics scoring: the GEMM pass is y3's only consumer
             return (ResNetTrunk.y3_drop and blk.downsample is None and self.dtype == torch.bfloat16
-                    and not ResNetTrunk.fused_bnin and C3 <= ResNetTrunk.bn3_gemm_max_c3 and C3 % 64 == 0
+                    and C3 <= ResNetTrunk.bn3_gemm_max_c3 and C3 % 64 == 0
                     and planes % 64 == 0 and blk.conv3.stride[0] == 1 and bn_mode(blk.bn3) != "running")
         if blk is self.net.layer4[-1]:  # (its backward starts from the raw output gradient: bn3 needs y3)
             return False
         return (ResNetTrunk.y3_drop and need_grad and blk.downsample is None and ResNetTrunk.bn_fold_bwd
                 and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16
-                and not ResNetTrunk.fused_bnin and C3 <= ResNetTrunk.bn_fold_max_c3
+                and C3 <= ResNetTrunk.bn_fold_max_c3
                 and C3 <= ResNetTrunk.bn3_gemm_max_c3 and C3 % 128 == 0 and planes >= 64
                 and (planes & (planes - 1)) == 0 and blk.conv3.stride[0] == 1 and bn_mode(blk.bn3) != "running")
 
-    def _conv_bn(self, x, conv, bn, N, H, W, C, tsm_T=0, tsm_fold=0, in_bn=None, store=True):
-        """conv -> BN statistics (+ running-stat update). in_bn = (scale, shift): the conv's input is
-        relu(x * scale + shift) (the previous BN + ReLU), applied on load by the fused engine; returns y = None when
-        that engine does not take the shape (the caller then materialises the input)."""
+    def _conv_bn(self, x, conv, bn, N, H, W, C, tsm_T=0, tsm_fold=0, store=True):
+        """conv -> BN statistics (+ running-stat update). store=False: a 1x1 conv keeps only the statistics (y =
+        None, ops.conv1x1_stats)."""
         Cout, _, KH, KW, s, p = _conv_shape(conv)
         OH, OW = ops.conv_out_hw(H, W, KH, KW, s, p)
         M = N * OH * OW
         mode = bn_mode(bn)
         st = BNState(Cout, x.device, mode, M, bn)
         w = self._wprep(conv, C)
-        if in_bn is not None:
-            if mode == "running" or (KH, KW, s, p) != (1, 1, 1, 0):
-                return None, st, OH, OW
-            mt = ops.stats_tiles(M)
-            stats = ops.stats_buffer(Cout, M, x.device)
-            y = ops.conv_fwd_bnin(x, in_bn[0], in_bn[1], w, N, H, W, C, Cout, stats)
-            if y is None:
-                return None, st, OH, OW
-            upd = mode == "train"
-            mom = bn.momentum if bn.momentum is not None else 0.1
-            ops.bn_finalize(stats, mt, M, Cout, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
-                            bn.running_mean if upd else None, bn.running_var if upd else None, mom, bn.eps)
-            return y, st, OH, OW
         if mode == "running":
             y = ops.conv_fwd(x, w, N, H, W, C, Cout, KH, KW, s, p, tsm_T, tsm_fold)
             ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, Cout, st.mean, st.invstd,
@@ -269,9 +237,6 @@ class ResNetTrunk:
             if old is None or old[0] != key:
                 object.__setattr__(net, "_vcg_fold_key", (key, object()))
             self._fold_gen = net._vcg_fold_key[1]
-        if self._prep_ev is not None:
-            torch.cuda.current_stream().wait_event(self._prep_ev)
-            self._prep_ev = None
         blocks = []
         for layer in (net.layer1, net.layer2, net.layer3, net.layer4):
             for blk in layer:
@@ -306,50 +271,31 @@ class ResNetTrunk:
         y1, b1, _, _ = self._conv_bn(x, conv1, blk.bn1, N, H, W, Cin, T, fold)
         a1 = ops.bn_apply(y1, b1.scale, b1.shift, planes, relu=True)
         y2, b2, H2, W2 = self._conv_bn(a1, blk.conv2, blk.bn2, N, H, W, planes)
-        # bn2 + ReLU applied by conv3 as its tiles land (no a2 tensor; conv3's wgrad does the same), where the
-        # fused engine takes it (bf16, batch statistics)
-        a2 = None
-        y3 = None
-        if self.dtype == torch.bfloat16 and ResNetTrunk.fused_bnin:
-            y3, b3, _, _ = self._conv_bn(y2, blk.conv3, blk.bn3, N, H2, W2, planes, in_bn=(b2.scale, b2.shift))
-        drop = y3 is None and self._drop_y3(blk, planes, need_grad)
+        drop = self._drop_y3(blk, planes, need_grad)
         C3 = blk.conv3.out_channels
         a2sum = None
-        if y3 is None:
-            if (need_grad and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd
-                    and self.dtype == torch.bfloat16 and bn_mode(blk.bn3) != "running"
-                    and C3 <= ResNetTrunk.bn_fold_max_c3 and planes <= 2048):
-                # (the a2 form of the bn3 backward fold needs colsum(a2): by default a column-sum pass on the side
-                # stream, which contends with conv3's GEMMs; VCG_A2SUM_FUSED=1: written by the bn2 apply pass itself)
-                if os.environ.get("VCG_A2SUM_FUSED", "0") == "1":
-                    a2, cs = ops.bn_apply_colsum(y2, b2.scale, b2.shift, planes)
-                    a2sum = (cs, None)
-                else:
-                    a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
-                    a2sum = self._colsum_side(a2, planes)
-            else:
-                a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
-            y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
+        if (need_grad and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd
+                and self.dtype == torch.bfloat16 and bn_mode(blk.bn3) != "running"
+                and C3 <= ResNetTrunk.bn_fold_max_c3 and planes <= 2048):
+            # (the a2 form of the bn3 backward fold needs colsum(a2): written by the bn2 apply pass itself. A
+            # separate column-sum pass on the side stream contended with conv3's GEMMs -- ~4 ms of kernel time per
+            # step -- for the same step time, profiles/r04_a2sum_ab.txt)
+            a2, a2sum = ops.bn_apply_colsum(y2, b2.scale, b2.shift, planes)
+        else:
+            a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
+        y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
+        r2 = None
         if blk.downsample is not None:
             if side is not None:
                 cur.wait_stream(side)
             else:
                 yd, bd, _, _ = self._conv_bn(x, blk.downsample[0], blk.downsample[1], N, H, W, Cin)
-            r2 = None
-            if (a2 is not None and self.dtype == torch.bfloat16 and C3 <= ResNetTrunk.bn3_gemm_max_c3
-                    and b3.mode != "running" and blk.conv3.stride[0] == 1 and ResNetTrunk.bn3_gemm_first):
-                M = N * H2 * W2  # bn3 + the downsample BN'd residual + ReLU as a second conv3 GEMM pass
-                wf = ops.weight_fold(blk.conv3.weight.data.view(C3, planes), b3.scale, self.dtype)
-                r2 = ops.conv1x1_bn_res_relu(a2.view(M, planes), wf, b3.shift, yd, M, C3, planes,
-                                             res_scale=bd.scale, res_shift=bd.shift)
-            if r2 is not None:
-                out, obits = r2
-            else:
-                out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale,
-                                          rshift=bd.shift, bits=True)
+            # (bn3 + the downsample BN'd residual as a second conv3 GEMM pass measured neutral here, 805.3 vs 807.5
+            # windows/s same box: the bn_apply pass over y3)
+            out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=yd, rscale=bd.scale,
+                                      rshift=bd.shift, bits=True)
         else:
-            r2 = None
-            if (a2 is not None and self.dtype == torch.bfloat16 and C3 <= ResNetTrunk.bn3_gemm_max_c3
+            if (self.dtype == torch.bfloat16 and C3 <= ResNetTrunk.bn3_gemm_max_c3
                     and b3.mode != "running" and blk.conv3.stride[0] == 1):
                 M = N * H2 * W2
                 wf = ops.weight_fold(blk.conv3.weight.data.view(C3, planes), b3.scale, self.dtype)
@@ -360,6 +306,9 @@ class ResNetTrunk:
                 if y3 is None:  # (the GEMM pass did not apply: the conv output after all)
                     y3 = self._conv3_out(blk, a2, N, H2, W2, planes)
                 out, obits = ops.bn_apply(y3, b3.scale, b3.shift, C3, relu=True, res=x, bits=True)
+        if ResNetTrunk.census is not None:
+            ResNetTrunk.census.append(("fwd", C3, blk.downsample is not None,
+                                       {"a2sum": a2sum is not None, "y3_drop": y3 is None, "bn3_gemm": r2 is not None}))
         rec = None
         if need_grad:
             rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, a2sum=a2sum, y3=y3, yd=yd, obits=obits, b1=b1, b2=b2, b3=b3,
@@ -376,24 +325,6 @@ class ResNetTrunk:
         if r["y3"] is None:
             r["y3"] = self._conv3_out(r["blk"], r["a2"], r["N"], r["H2"], r["W2"], r["planes"])
         return r["y3"]
-
-    def _colsum_side(self, a, C):
-        """(column sums of a [.., C] as f32 [C], event): on the side stream when there is one."""
-        cur = torch.cuda.current_stream()
-        ws = self._wside(a.device)
-        M = a.numel() // C
-        if ws is None:
-            cs = torch.empty(C, dtype=torch.float32, device=a.device)
-            ops.colsum(a.view(M, C), C, M, C, cs, accumulate=False)
-            return cs, None
-        ws.wait_stream(cur)
-        with torch.cuda.stream(ws):
-            cs = torch.empty(C, dtype=torch.float32, device=a.device)
-            ops.colsum(a.view(M, C), C, M, C, cs, accumulate=False)
-            ev = torch.cuda.Event()
-            ev.record(ws)
-        cs.record_stream(cur)
-        return cs, ev
 
     def _foldable(self, blk, x, need_grad):
         """bf16 scoring forward with every BN of the block on running statistics and a 1x1 / stride-1 conv3."""
@@ -655,8 +586,6 @@ class ResNetTrunk:
             Pg0 = r.get("Pg")
 
             def wfn():
-                if a2s[1] is not None:  # colsum(a2) came from a side-stream pass: order it before its reader, on
-                    torch.cuda.current_stream().wait_event(a2s[1])  # whichever stream wfn runs (inline without _ws)
                 G = torch.empty((planes, planes, 1, 1), dtype=torch.float32, device=a2.device)
                 Pg = Pg0
                 if Pg is None:
@@ -665,10 +594,10 @@ class ResNetTrunk:
                 ops.conv_wgrad(a2, a2, G, N, H2, W2, planes, planes, planes, 1, 1, 1, 0, accumulate=False)
                 ops.bn_bwd_fold_wgrad_a2(Pg.view(C3, planes), G.view(planes, planes),
                                          blk.conv3.weight.data.view(C3, planes), C3, planes, b3.mean, b3.invstd,
-                                         b3.bn.weight, sums3[0], sums3[1], M, a2s[0],
+                                         b3.bn.weight, sums3[0], sums3[1], M, a2s,
                                          blk.conv3.weight.grad.view(C3, planes))
                 return True
-            return self._async(wfn, a2, g, sums3, a2s[0], Pg0)
+            return self._async(wfn, a2, g, sums3, a2s, Pg0)
 
         def wfn():
             cs = torch.empty(planes, dtype=torch.float32, device=a2.device)
@@ -679,16 +608,14 @@ class ResNetTrunk:
 
     def _dgrad_bn_fold(self, conv, g, y3, b3, sums3, N, H, W, y, st, C, C3, a2=None, a2sum=None):
         """_dgrad_bn of conv3 with bn3's backward folded in: one GEMM over [g | y3] against [A w | B w] (or, with
-        a2sum = (colsum(a2), event), over [g | a2] against [A w | w^T diag(B) w]) plus the constant column bias. None
+        a2sum = colsum(a2), over [g | a2] against [A w | w^T diag(B) w]) plus the constant column bias. None
         where the engine does not apply."""
         Cout, Cin, KH, KW, s, p = _conv_shape(conv)
         wt = self._wprep_t(conv, Cin)
         M = N * H * W
         if a2sum is not None:
-            if a2sum[1] is not None:
-                torch.cuda.current_stream().wait_event(a2sum[1])
             wfold, bias = ops.bn_bwd_fold_weights_a2(wt.view(Cin, C3), Cin, C3, b3.invstd, b3.bn.weight, sums3[0],
-                                                     sums3[1], M, a2sum[0])
+                                                     sums3[1], M, a2sum)
             src, Ky = a2, Cin
         else:
             wfold, bias = ops.bn_bwd_fold_weights(wt.view(Cin, C3), Cin, C3, b3.mean, b3.invstd, b3.bn.weight,
@@ -745,24 +672,17 @@ class ResNetTrunk:
         if bnf is not None and not self._fold_conv3(r, *bnf):  # (the engine does not apply: the pass on dy3)
             dy3 = self._bn_apply_bwd(bnf[0], self._y3(r), r["b3"], C3, bnf[1])
             bnf = None
-        if bnf is not None:
-            pass  # (conv3's weight gradient went out with the fold)
-        elif r["a2"] is not None:
+        if bnf is None:  # (with the fold, conv3's weight gradient went out with it)
             self._wgrad(blk.conv3, r["a2"], dy3, N, H2, W2, planes)
-        elif blk.conv3.weight.requires_grad:  # conv3's input is bn2 + ReLU of y2, applied on load
-            Cout3, _, KH3, KW3, s3, p3 = _conv_shape(blk.conv3)
-            b2 = r["b2"]
-            if not self._async(lambda: ops.conv_wgrad_bnin(r["y2"], b2.scale, b2.shift, dy3, blk.conv3.weight.grad, N,
-                                                           H2, W2, planes, Cout3, KH3, KW3, s3, p3),
-                               r["y2"], b2.scale, b2.shift, dy3):
-                self._wgrad(blk.conv3, ops.bn_apply(r["y2"], b2.scale, b2.shift, planes, relu=True), dy3, N, H2, W2,
-                            planes)
         dy2 = None
         if bnf is not None:
             dy2 = self._dgrad_bn_fold(blk.conv3, bnf[0], r["y3"], r["b3"], bnf[1], N, H2, W2, r["y2"], r["b2"], planes,
                                       C3, a2=r["a2"], a2sum=r.get("a2sum"))
             if dy2 is None:  # (the fused engine does not apply: the unfused pass, and conv3's dgrad on dy3)
                 dy3 = self._bn_apply_bwd(bnf[0], self._y3(r), r["b3"], C3, bnf[1])
+        if ResNetTrunk.census is not None:
+            ResNetTrunk.census.append(("bwd", C3, ds, {"fold_wgrad": bnf is not None, "fold_dgrad": dy2 is not None,
+                                                       "a2_form": bnf is not None and r.get("a2sum") is not None}))
         if dy2 is None:
             dy2 = self._dgrad_bn(blk.conv3, dy3, N, H2, W2, r["y2"], r["b2"], planes)
         del dy3
