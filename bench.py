@@ -114,17 +114,20 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=3, bn="running"):
+def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=None, bn="running"):
     """The oracle (oracle/model.py: fp32 CPU restatement of the reference path, test infrastructure) timed on this
-    host: train = one reference train step (fwd BN-train + CE + bwd + clip_grad_norm_ + AdamW), fwd = the eval
-    forward (running-stat BN). Median of `reps` timed runs after 1 warm-up. B is a bounded sample (2 windows train,
-    4 fwd: 10-30 s of CPU work in all) so the default bench finishes in minutes; clip-windows/sec does not depend
-    on B on a CPU (the CPU path has no batch-level parallelism beyond the threads)."""
+    host: train = one reference train step (fwd BN-train with BERT dropout 0.1 as the GPU step runs it + CE + bwd +
+    clip_grad_norm_ + AdamW), fwd = the eval forward. Median of `reps` timed runs after 1 warm-up. B is a bounded
+    sample (train: 4 windows x 2 timed runs, fwd: 4 windows x 3; 15-30 s of CPU work in all) so the default bench
+    finishes in minutes. The per-window CPU rate barely depends on B (the CPU path has no batch-level parallelism
+    beyond the threads; the round-3 sweep, profiles/r03_cpu_sweep_*.jsonl: the forward at B 64 is ~20 % SLOWER per
+    window than at B 4), so a small B does not understate the CPU."""
     import torch
     from oracle import model as om
     from vcg_hip.build import build_two_stream
     from vcg_hip import synth
-    B = B or (2 if mode == "train" else 4)
+    B = B or 4
+    reps = reps or (2 if mode == "train" else 3)
     torch.set_num_threads(threads)
     m = build_two_stream(clip_frame_num=T, dropout=0.1)
     sd = m.state_dict()
@@ -136,7 +139,7 @@ def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=3, bn="running"):
         buffers = {n: sd[n].detach().clone() for n in sd if n not in params}
         t0 = time.perf_counter()
         if mode == "train":
-            om.train_step(params, buffers, frames, ids, mask, labels, lr=1e-5)
+            om.train_step(params, buffers, frames, ids, mask, labels, lr=1e-5, p_drop=0.1)
         else:
             p = dict(buffers)
             p.update(params)
@@ -159,6 +162,7 @@ def long_video_bench(args):
     """Config 5: one 1 h synthetic video (u8 frames resident in HBM), stride-1 s windows, frame gather +
     normalisation on the GPU, TwoStream scoring (eval), cut points and boundary metrics. value = windows/s of
     the GPU part (gather + forward + labels); host tokenisation is done before the timed region."""
+    import numpy as np
     import torch
     import long_video as lv
     from data.synthetic_dataset import HashTokenizer
@@ -176,13 +180,23 @@ def long_video_bench(args):
     win, idx, ids, mask = lv.window_inputs(F, T, args.stride, subtitles, HashTokenizer(), L)
     idx, ids, mask = (torch.from_numpy(a).to(dev) for a in (idx, ids, mask))
     K = args.scoring_streams
+    # re-bias the random-init 2-way head (untimed, as tests/test_gpu_long_video.py does) so its decisions split
+    # about evenly: otherwise every window sits on one side of 0.5, no cut point is predicted and F is 0 / undefined
+    samp = torch.from_numpy(np.linspace(0, len(win) - 1, 256).astype(np.int64)).to(dev)
+    with torch.no_grad():
+        sc, _ = lv.score_windows(model, frames, idx[samp], ids[samp], mask[samp], B)
+        pr = sc.double().clamp(1e-12, 1 - 1e-12)
+        shift = -torch.log(pr / (1 - pr)).median().item()
+        model.fusion_head.head.bias.data[1] += shift
+        model.native_flat().refresh_shadow(force=True)
     lv.score_windows(model, frames, idx[:B * max(2, K)], ids[:B * max(2, K)], mask[:B * max(2, K)], B, streams=K)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     scores, labels = lv.score_windows(model, frames, idx, ids, mask, B, streams=K)
     torch.cuda.synchronize()
     sec = time.perf_counter() - t0
-    m = lv.boundary_metrics(labels.cpu().tolist(), timestamps, F, T, args.stride)
+    lab = labels.cpu().tolist()
+    m = lv.boundary_metrics(lab, timestamps, F, T, args.stride)
     n = len(win)
     nbytes, nflops = window_costs(T, HW, L, B, 2 if args.precision == "bf16" else 4, False)
     cpu = None
@@ -222,7 +236,11 @@ def long_video_bench(args):
                           "unit": "GB/s", "frac": round(nbytes * n / sec / 1e9 / HBM_PEAK_GBS, 4),
                           "mfma_tflops": round(nflops * n / sec / 1e12, 2)},
         "boundary": {k: m[k] for k in ("recall", "recall_3", "recall_5", "precision", "precision_3", "precision_5",
-                                       "f", "f_3", "f_5")}}), flush=True)
+                                       "f", "f_3", "f_5")},
+        "head_calibration": {"logit1_bias_shift": round(shift, 5), "sample_windows": 256,
+                             "positive_share": round(sum(lab) / max(len(lab), 1), 4),
+                             "note": "random-init head re-biased (untimed) so about half the windows score positive"}}),
+        flush=True)
 
 
 # ----------------------------------------------------------------------------- multi-GPU evidence
@@ -349,7 +367,8 @@ def main():
     ap.add_argument("--video-frames", type=int, default=3600)
     ap.add_argument("--stride", type=int, default=1, help="long_video: window stride in s (the reference's own: 4)")
     ap.add_argument("--scoring-streams", type=int, default=1,
-                    help="long_video: scoring batches round-robin over this many HIP streams (long_video.score_windows)")
+                    help="long_video: scoring batches round-robin over this many HIP streams (long_video.score_windows); "
+                         "fwd: a step scores this many batches of --batch windows, one per HIP stream")
     ap.add_argument("--bn", default="running", choices=["running", "batch"],
                     help="scoring modes (fwd / long_video): BN with running statistics (model.eval(), the trainer's "
                          "val and convert2vision_emb) or with the batch's statistics (test_video_segment_point.py:"
@@ -432,13 +451,35 @@ def main():
         model.set_grad_hooks(reducer)
         opt.grad_scale = 1.0 / world
         bufsync = BufferBroadcaster(model, comm=comm)  # DDP broadcast_buffers: rank 0's BN stats each forward
-    frames, ids, mask, labels = synth.clip_batch(B, T, HW, HW, L, seed=123 + rank, device=dev)
+    # fwd with --scoring-streams K > 1: a step scores K batches of B windows, batch k on HIP stream k (batch 0 on the
+    # main stream first in the first step, so one-time weight preparation is ordered before the others): the
+    # batch-statistics mode scores batches of 16 (BN couples only the windows of one batch), which underfill the chip
+    K = args.scoring_streams if args.mode == "fwd" else 1
+    frames, ids, mask, labels = synth.clip_batch(B * K, T, HW, HW, L, seed=123 + rank, device=dev)
+    chunks = [(frames[k * B:(k + 1) * B], ids[k * B:(k + 1) * B], mask[k * B:(k + 1) * B]) for k in range(K)]
+    pool = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(K - 1)]
     comm_events = None  # [(backward done, finish joined)] per timed step (world > 1)
+    prepared = []
 
     def step():
         if args.mode == "fwd":
             with torch.no_grad():
-                model(frames, ids, mask)
+                if K == 1:
+                    model(frames, ids, mask)
+                    return
+                main = pool[0]
+                if not prepared:  # the first forward prepares the weights on the main stream
+                    model(*chunks[0])
+                for s_ in pool[1:]:
+                    s_.wait_stream(main)
+                for k, (f_, i_, m_) in enumerate(chunks):
+                    if k == 0 and not prepared:
+                        continue
+                    with torch.cuda.stream(pool[k]):
+                        model(f_, i_, m_)
+                prepared.append(True)
+                for s_ in pool[1:]:
+                    main.wait_stream(s_)
             return
         opt.zero_grad()
         if bufsync is not None:
@@ -522,12 +563,12 @@ def main():
                                "torch.distributed")
 
     if rank == 0:
-        windows = B * world
+        windows = B * K * world
         value = windows / (ms / 1000.0)
         s_bytes = 2 if args.precision == "bf16" else 4
         nbytes, nflops = window_costs(T, HW, L, B, s_bytes, args.mode == "train")
-        achieved = nbytes * B / (ms / 1000.0) / 1e9  # per GPU
-        tflops = nflops * B / (ms / 1000.0) / 1e12
+        achieved = nbytes * B * K / (ms / 1000.0) / 1e9  # per GPU
+        tflops = nflops * B * K / (ms / 1000.0) / 1e12
         traffic = kern_traffic = mfma_busy = None
         tf = os.path.join(REPO, "profiles", f"traffic_{args.mode}_{args.precision}_b{B}.json")
         if os.path.exists(tf):
@@ -575,6 +616,7 @@ def main():
                                    f"B={B} windows/GPU of {T}x{HW}^2 frames + {L} tokens"
                                    + (", fused clip+AdamW" if args.mode == "train" else ""),
                        "global_batch": windows, "seq_len": L, "frames": T, "resolution": HW,
+                       **({"batches_per_step": K, "batch": B, "scoring_streams": K} if K > 1 else {}),
                        "parallelism": f"dp{world}", **({"bn": args.bn} if args.mode == "fwd" else {})},
             "roofline": dom,
             **ddp,

@@ -114,6 +114,16 @@ VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* m
    input a2 and its colsum for the bn3 fold's centring in one pass */
 VCG_API long long vcg_bn_apply_colsum_ws_bytes(long long P, int C);
 VCG_API int vcg_bn_apply_colsum(const void* y, const float* scale, const float* shift, int relu, void* out, float* colsum, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
+/* vcg_bn_apply_colsum (ReLU, bf16, C = 64 / 128 / 256) that also returns gram = out^T out (f32 [C][C], summed in a
+   fixed order: deterministic): the bottleneck's bn2 -> relu -> a2 with the a2 statistics that bn3's batch statistics
+   (vcg_bn_stats_from_gram) and the a2 form of the bn3 backward fold need, so that neither reads a2 again. */
+VCG_API long long vcg_bn_apply_gram_ws_bytes(long long P, int C);
+VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* shift, void* out, float* colsum, float* gram, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
+/* Batch statistics of y = x w^T (w bf16 [N][C], the conv's forward GEMM weights; M rows) from x's (gram, colsum):
+   mean_n = w_n . colsum / M, var_n = w_n^T (gram / M - mu mu^T) w_n in double -- torchvision Bottleneck bn3 over
+   conv3's output (model/vision/resnet50_tsm.py:15) without a statistics pass over a2. Writes the vcg_conv_fwd
+   stats layout (one used slot) for vcg_bn_finalize. */
+VCG_API int vcg_bn_stats_from_gram(const float* gram, const float* colsum, const void* w, long long M, int N, int C, float* stats, int mtiles, hipStream_t s);
 VCG_API int vcg_conv1x1_stats(const void* x, const void* w, float* stats, int M, int N, int K, hipStream_t stream);
 VCG_API int vcg_bn_bwd_sumgx_from_wgrad(const float* P, const void* w, int K, int C, const float* mean, const float* invstd, const float* sum_g, float* sum_gx, float* dgamma, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a, void* wfold, float* bias, hipStream_t stream);

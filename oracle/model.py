@@ -156,13 +156,15 @@ def param_groups(named, weight_decay):
 
 
 def train_step(params, buffers, img, ids, mask, labels, lr, betas=(0.9, 0.95), weight_decay=0.01, max_norm=1.0,
-               head_type="mlp"):
+               head_type="mlp", p_drop=0.0):
     """One reference train step (train_video_segment_point.py:161-206 with accumulation 1):
-    forward (BN train mode, dropout 0) -> CE -> backward -> clip_grad_norm_ -> AdamW.step.
+    forward (BN train mode; BERT dropout p_drop in training mode, 0 by default: the parity fixtures) -> CE ->
+    backward -> clip_grad_norm_ -> AdamW.step.
     params: {name: leaf tensor requiring grad}; buffers: {name: running stats} (updated in place)."""
     p = dict(buffers)
     p.update(params)
-    logits, prob, _, _ = two_stream(p, img, ids, mask, bn_mode="train", head_type=head_type)
+    logits, prob, _, _ = two_stream(p, img, ids, mask, bn_mode="train", head_type=head_type, p_drop=p_drop,
+                                    training=p_drop > 0.0)
     loss = F.cross_entropy(logits, labels)
     loss.backward()
     total_norm = torch.nn.utils.clip_grad_norm_(list(params.values()), max_norm)

@@ -125,8 +125,11 @@ def test_c1_bf16_bn_fold_vs_apply():
     st = dict(_gold("bn_running_stats.npz"))
     frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=123, device=DEV)
     m = _model(4, "bf16", st)
-    saved = ResNetTrunk.bn_fold_bwd
+    saved = ResNetTrunk.bn_fold_bwd, ResNetTrunk.gram_stats
     try:
+        # (bn3's statistics from the conv3 GEMM in both runs: the Gram statistics of the fold's forward are not
+        # bit-identical to them, and this comparison needs the same forward -- test_gram_stats_forward covers them)
+        ResNetTrunk.gram_stats = False
         ResNetTrunk.bn_fold_bwd = False
         la, lga, ga, _ = _step(m, frames, ids, mask, labels)
         ResNetTrunk.bn_fold_bwd = True
@@ -135,7 +138,7 @@ def test_c1_bf16_bn_fold_vs_apply():
         assert ResNetTrunk.path_counts["unfused"] == 0
         lc, lgc, gc, _ = _step(m, frames, ids, mask, labels)
     finally:
-        ResNetTrunk.bn_fold_bwd = saved
+        ResNetTrunk.bn_fold_bwd, ResNetTrunk.gram_stats = saved
     assert la == lb == lc and torch.equal(lga, lgb)
     for n in gb:
         assert torch.equal(gb[n], gc[n]), n
@@ -145,6 +148,37 @@ def test_c1_bf16_bn_fold_vs_apply():
     coss = np.array([c for _, c in stats.values()])
     print(f"fold vs apply: rel err median {np.median(errs):.2e} max {errs.max():.2e}; cosine min {coss.min():.6f}")
     assert np.median(errs) <= 2e-2 and errs.max() <= 8e-2 and coss.min() >= 0.998
+
+
+def test_gram_stats_forward():
+    """bn3's batch statistics from the bn2 apply pass's (a2^T a2, colsum(a2)) (ResNetTrunk.gram_stats, the exact y3
+    statistics) against the conv3 statistics GEMM (of the bf16-rounded y3), C1 shapes, BN in training mode: the
+    bf16 train forward's vision embeddings and logits sit as close to the fp32 native forward with either (rel. error
+    no worse than 1.25 x + 2e-3 / logits 1.25 x + 1e-2), and the Gram path's backward is deterministic and finite."""
+    from vcg_hip import synth
+    from vcg_hip.trunk import ResNetTrunk
+    st = dict(_gold("bn_running_stats.npz"))
+    frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=77, device=DEV)
+    res = {}
+    saved = ResNetTrunk.gram_stats
+    try:
+        for tag, prec, gram in (("gram", "bf16", True), ("gemm", "bf16", False), ("fp32", "fp32", False)):
+            ResNetTrunk.gram_stats = gram
+            m = _model(4, prec, st)
+            lg, _, ve, _ = m(frames, ids, mask, return_emb=True)
+            res[tag] = (lg.detach().double().cpu(), ve.detach().double().cpu())
+            if tag == "gram":
+                l1, _, g1, _ = _step(m, frames, ids, mask, labels)
+                l2, _, g2, _ = _step(m, frames, ids, mask, labels)
+                assert l1 == l2 and all(torch.equal(g1[n], g2[n]) for n in g1)
+                assert all(torch.isfinite(v).all() for v in g1.values())
+    finally:
+        ResNetTrunk.gram_stats = saved
+    lg32, ve32 = res["fp32"]
+    e = {t: (_rel(res[t][1], ve32), (res[t][0] - lg32).abs().max().item()) for t in ("gram", "gemm")}
+    print("vision emb rel err / logits max err vs fp32:", e)
+    assert e["gram"][0] <= 1.25 * e["gemm"][0] + 2e-3
+    assert e["gram"][1] <= 1.25 * e["gemm"][1] + 1e-2
 
 
 def test_c1_loss_and_conditioning():

@@ -350,10 +350,65 @@ def test_bn_apply_colsum(rows, C):
     y = _bf(torch.randn(rows, C, generator=gen))
     sc = (0.5 + torch.rand(C, generator=gen)).to(DEV)
     sh = (torch.randn(C, generator=gen) * 0.2).to(DEV)
-    a, cs = ops.bn_apply_colsum(y, sc, sh, C)  # (VCG_A2SUM_FUSED=1 in the trunk)
+    a, cs = ops.bn_apply_colsum(y, sc, sh, C)  # (the trunk's bn2 apply where the Gram pass does not apply)
     ref = ops.bn_apply(y, sc, sh, C, relu=True)
     csr = torch.zeros(C, device=DEV)
     ops.colsum(ref, C, rows, C, csr, accumulate=False)
     torch.cuda.synchronize()
     assert torch.equal(a, ref)
     assert ((cs.double() - csr.double()).abs() / csr.double().abs().clamp_min(1.0)).max().item() < 1e-5
+
+
+@pytest.mark.parametrize("rows,C", [(3211264 // 4 + 5, 64), (802816 // 2 + 13, 128), (200704, 256), (77, 64)])
+def test_bn_apply_gram(rows, C):
+    """bn_apply + colsum + the Gram matrix a^T a of the stored output in one pass: a == bn_apply bit for bit, colsum
+    and gram against float64 sums of the same bf16 values (fixed-order fp32 / MFMA accumulation: ~1e-6 relative),
+    deterministic; ragged row counts (tail rows contribute nothing)."""
+    gen = torch.Generator().manual_seed(rows % 89 + C)
+    y = _bf(torch.randn(rows, C, generator=gen) + 0.2)
+    sc = (0.5 + torch.rand(C, generator=gen)).to(DEV)
+    sh = (torch.randn(C, generator=gen) * 0.2).to(DEV)
+    a, cs, G = ops.bn_apply_gram(y, sc, sh, C)
+    ref = ops.bn_apply(y, sc, sh, C, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a, ref)
+    ad = ref.double()
+    csr = ad.sum(0)
+    Gr = ad.t() @ ad
+    assert ((cs.double() - csr).abs() / csr.abs().clamp_min(1.0)).max().item() < 1e-5
+    assert ((G.double() - Gr).abs().max() / Gr.abs().max()).item() < 1e-5
+    assert torch.equal(G, G.t())
+    a2, cs2, G2 = ops.bn_apply_gram(y, sc, sh, C)
+    assert torch.equal(cs, cs2) and torch.equal(G, G2)
+
+
+@pytest.mark.parametrize("M,C,N", [(3211264 // 8, 64, 256), (802816 // 4, 128, 512), (50176, 256, 1024)])
+def test_bn_stats_from_gram(M, C, N):
+    """conv3's batch statistics from its input's Gram matrix and column sums (bn_stats_from_gram -> bn_finalize)
+    against float64 statistics of the exact product x w^T (x >= 0 after the ReLU, w the bf16 GEMM weights): mean and
+    invstd within 1e-4 relative; also within bf16 rounding of the statistics of the stored bf16 product (the
+    conv1x1_stats path it replaces)."""
+    gen = torch.Generator().manual_seed(M % 101 + C)
+    y = _bf(torch.randn(M, C, generator=gen))
+    sc = (0.5 + torch.rand(C, generator=gen)).to(DEV)
+    sh = (torch.randn(C, generator=gen) * 0.3 + 0.2).to(DEV)
+    a, cs, G = ops.bn_apply_gram(y, sc, sh, C)
+    w = _bf(torch.randn(N, C, generator=gen) * (1.0 / C ** 0.5))
+    stats = ops.stats_buffer(N, M, DEV)
+    ops.bn_stats_from_gram(G, cs, w, M, N, C, stats)
+    out = [torch.empty(N, device=DEV) for _ in range(4)]
+    ops.bn_finalize(stats, stats.shape[1], M, N, None, None, *out, None, None, 0.1, 1e-5)
+    st2 = ops.stats_buffer(N, M, DEV)
+    assert ops.conv1x1_stats(a, w, st2, M, N, C)
+    out2 = [torch.empty(N, device=DEV) for _ in range(4)]
+    ops.bn_finalize(st2, ops.stats_tiles(M), M, N, None, None, *out2, None, None, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    yx = a.double() @ w.double().t()
+    mean = yx.mean(0)
+    inv = (yx.var(0, unbiased=False) + 1e-5).rsqrt()
+    e_mean = ((out[0].double() - mean).abs() / yx.std(0)).max().item()
+    e_inv = ((out[1].double() - inv).abs() / inv).max().item()
+    print(f"gram stats: mean err {e_mean:.2e} (of std), invstd rel err {e_inv:.2e}; GEMM stats of bf16 y: "
+          f"{((out2[0].double() - mean).abs() / yx.std(0)).max().item():.2e}, "
+          f"{((out2[1].double() - inv).abs() / inv).max().item():.2e}")
+    assert e_mean < 1e-4 and e_inv < 1e-4

@@ -176,6 +176,28 @@ def bn_apply_colsum(y, scale, shift, C, relu=True):
     return out, cs
 
 
+def bn_apply_gram(y, scale, shift, C):
+    """(relu(bn_apply(y)), its column sums f32 [C], its Gram matrix out^T out f32 [C, C]) in one pass
+    (vcg_bn_apply_gram, bf16, C in 64 / 128 / 256)."""
+    _chk(y, torch.bfloat16, "y")
+    out = torch.empty_like(y)
+    cs = torch.empty(C, dtype=torch.float32, device=y.device)
+    gram = torch.empty((C, C), dtype=torch.float32, device=y.device)
+    P_ = y.numel() // C
+    w = ws(_lib.query("vcg_bn_apply_gram_ws_bytes", P_, C), y.device)
+    _lib.call("vcg_bn_apply_gram", P(y), P(scale), P(shift), P(out), P(cs), P(gram), P(w), w.numel() * 4, P_, C,
+              stream())
+    return out, cs, gram
+
+
+def bn_stats_from_gram(gram, colsum, w, M, N, C, stats):
+    """BN statistics of x w^T (w bf16 [N, C]) from x's Gram matrix and column sums into a stats_buffer(N, M)
+    (vcg_bn_stats_from_gram; one used slot, for bn_finalize)."""
+    _chk(w, torch.bfloat16, "w")
+    _lib.call("vcg_bn_stats_from_gram", P(gram), P(colsum), P(w), M, N, C, P(stats), stats.shape[1], stream())
+    return stats
+
+
 def conv1x1_stats(x, w, stats, M, N, K):
     """BatchNorm statistics of x [M, K] @ w [N, K]^T without storing the product (vcg_conv1x1_stats). False where
     the fused engine does not apply."""

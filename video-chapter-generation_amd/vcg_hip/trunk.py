@@ -136,6 +136,10 @@ class ResNetTrunk:
     # second pass of conv3's GEMM (scale folded into its weight rows, shift as bias; ops.conv1x1_bn_res_relu)
     # instead of reading y3 back in the bn_apply pass (0: off)
     bn3_gemm_max_c3 = int(os.environ.get("VCG_BN3_GEMM_MAXC3", "1024"))
+    # bf16 batch statistics: the bn2 apply pass also returns colsum(a2) and a2^T a2 (ops.bn_apply_gram), from which
+    # bn3's statistics follow where y3 is not stored (no statistics-only conv3 pass over a2) and the a2-form fold
+    # takes its Gram term (no a2^T a2 GEMM in the backward); False: the conv3 statistics GEMM (tests compare both)
+    gram_stats = os.environ.get("VCG_GRAM_STATS", "1") != "0"
 
     def __init__(self, net, dtype):
         self.net = net
@@ -200,11 +204,25 @@ class ResNetTrunk:
             if store or (KH, KW, s, p, tsm_fold) != (1, 1, 1, 0, 0) or not ops.conv1x1_stats(x.view(M, C), w, stats,
                                                                                                M, Cout, C):
                 y = ops.conv_fwd(x, w, N, H, W, C, Cout, KH, KW, s, p, tsm_T, tsm_fold, stats=stats)
-            upd = mode == "train"
-            mom = bn.momentum if bn.momentum is not None else 0.1
-            ops.bn_finalize(stats, mt, M, Cout, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
-                            bn.running_mean if upd else None, bn.running_var if upd else None, mom, bn.eps)
+            self._finalize(stats, mt, M, Cout, bn, st)
         return y, st, OH, OW
+
+    @staticmethod
+    def _finalize(stats, mt, M, Cout, bn, st):
+        upd = st.mode == "train"
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        ops.bn_finalize(stats, mt, M, Cout, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
+                        bn.running_mean if upd else None, bn.running_var if upd else None, mom, bn.eps)
+
+    def _bn_from_gram(self, conv, bn, gram, colsum, M, C):
+        """BN state of conv's (1x1) output from its input's Gram matrix and column sums (ops.bn_stats_from_gram:
+        y = x w^T is linear, so its batch mean / variance follow from x^T x and colsum(x) -- no pass over x or y)."""
+        Cout = conv.out_channels
+        st = BNState(Cout, gram.device, bn_mode(bn), M, bn)
+        stats = ops.stats_buffer(Cout, M, gram.device)
+        ops.bn_stats_from_gram(gram, colsum, self._wprep(conv, C).view(Cout, C), M, Cout, C, stats)
+        self._finalize(stats, stats.shape[1], M, Cout, bn, st)
+        return st
 
     # ---------------------------------------------------------------- forward
     def forward(self, x, need_grad):
@@ -273,17 +291,27 @@ class ResNetTrunk:
         y2, b2, H2, W2 = self._conv_bn(a1, blk.conv2, blk.bn2, N, H, W, planes)
         drop = self._drop_y3(blk, planes, need_grad)
         C3 = blk.conv3.out_channels
-        a2sum = None
-        if (need_grad and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd
-                and self.dtype == torch.bfloat16 and bn_mode(blk.bn3) != "running"
-                and C3 <= ResNetTrunk.bn_fold_max_c3 and planes <= 2048):
+        a2sum = a2gram = None
+        fold_a2 = (need_grad and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd
+                   and self.dtype == torch.bfloat16 and bn_mode(blk.bn3) != "running"
+                   and C3 <= ResNetTrunk.bn_fold_max_c3 and planes <= 2048)
+        if (fold_a2 or drop) and ResNetTrunk.gram_stats and planes in (64, 128, 256) and bn_mode(blk.bn3) != "running":
+            # a2 with colsum(a2) and a2^T a2 from the bn2 apply pass: bn3's statistics follow from them (no conv3
+            # statistics pass over a2 when y3 is not stored), and so does the Gram term of the a2-form backward fold
+            a2, a2sum, a2gram = ops.bn_apply_gram(y2, b2.scale, b2.shift, planes)
+        elif fold_a2:
             # (the a2 form of the bn3 backward fold needs colsum(a2): written by the bn2 apply pass itself. A
             # separate column-sum pass on the side stream contended with conv3's GEMMs -- ~4 ms of kernel time per
             # step -- for the same step time, profiles/r04_a2sum_ab.txt)
             a2, a2sum = ops.bn_apply_colsum(y2, b2.scale, b2.shift, planes)
         else:
             a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
-        y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
+        if drop and a2gram is not None:
+            y3, b3 = None, self._bn_from_gram(blk.conv3, blk.bn3, a2gram, a2sum, N * H2 * W2, planes)
+        else:
+            y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
+        if not fold_a2:  # (the backward's a2-form fold reads these only where it applies)
+            a2sum = a2gram = None
         r2 = None
         if blk.downsample is not None:
             if side is not None:
@@ -311,7 +339,7 @@ class ResNetTrunk:
                                        {"a2sum": a2sum is not None, "y3_drop": y3 is None, "bn3_gemm": r2 is not None}))
         rec = None
         if need_grad:
-            rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, a2sum=a2sum, y3=y3, yd=yd, obits=obits, b1=b1, b2=b2, b3=b3,
+            rec = dict(blk=blk, x=x, y1=y1, a1=a1, y2=y2, a2=a2, a2sum=a2sum, a2gram=a2gram, y3=y3, yd=yd, obits=obits, b1=b1, b2=b2, b3=b3,
                        bd=bd, N=N, H=H, W=W, H2=H2, W2=W2, Cin=Cin, planes=planes, C3=C3, T=T, fold=fold,
                        conv1=conv1)
         return out, rec, H2, W2
@@ -585,19 +613,23 @@ class ResNetTrunk:
         if a2s is not None:  # the a2 form: g^T a2 and a2^T a2 (plain weight-gradient GEMMs), combined per row
             Pg0 = r.get("Pg")
 
+            G0 = r.get("a2gram")
+
             def wfn():
-                G = torch.empty((planes, planes, 1, 1), dtype=torch.float32, device=a2.device)
+                G = G0
+                if G is None:
+                    G = torch.empty((planes, planes, 1, 1), dtype=torch.float32, device=a2.device)
+                    ops.conv_wgrad(a2, a2, G, N, H2, W2, planes, planes, planes, 1, 1, 1, 0, accumulate=False)
                 Pg = Pg0
                 if Pg is None:
                     Pg = torch.empty((C3, planes, 1, 1), dtype=torch.float32, device=a2.device)
                     ops.conv_wgrad(a2, g, Pg, N, H2, W2, planes, planes, C3, 1, 1, 1, 0, accumulate=False)
-                ops.conv_wgrad(a2, a2, G, N, H2, W2, planes, planes, planes, 1, 1, 1, 0, accumulate=False)
                 ops.bn_bwd_fold_wgrad_a2(Pg.view(C3, planes), G.view(planes, planes),
                                          blk.conv3.weight.data.view(C3, planes), C3, planes, b3.mean, b3.invstd,
                                          b3.bn.weight, sums3[0], sums3[1], M, a2s,
                                          blk.conv3.weight.grad.view(C3, planes))
                 return True
-            return self._async(wfn, a2, g, sums3, a2s, Pg0)
+            return self._async(wfn, a2, g, sums3, a2s, Pg0, G0)
 
         def wfn():
             cs = torch.empty(planes, dtype=torch.float32, device=a2.device)
