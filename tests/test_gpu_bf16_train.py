@@ -96,12 +96,18 @@ def test_c1_bf16_fused_backward_vs_unfused():
     st = dict(_gold("bn_running_stats.npz"))
     frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=123, device=DEV)
     m = _model(4, "bf16", st)
+    saved = ResNetTrunk.gram_stats
     try:
+        # (bn3's statistics from the conv3 GEMM in both runs: the unfused path has no Gram pass, and this comparison
+        # needs the same forward -- test_gram_stats_forward covers the Gram statistics)
+        ResNetTrunk.gram_stats = False
         ResNetTrunk.fused_bwd = False
         lu, lgu, gu, _ = _step(m, frames, ids, mask, labels)
+        ResNetTrunk.fused_bwd = True
+        lf, lgf, gf, _ = _step(m, frames, ids, mask, labels)
     finally:
         ResNetTrunk.fused_bwd = True
-    lf, lgf, gf, _ = _step(m, frames, ids, mask, labels)
+        ResNetTrunk.gram_stats = saved
     assert lu == lf and torch.equal(lgu, lgf), "the forward is not deterministic"
     stats = _compare({n: v for n, v in gf.items() if n.startswith("vision_model")},
                      {n: v for n, v in gu.items() if n.startswith("vision_model")}, "C1 bf16 fused vs unfused")
