@@ -412,3 +412,24 @@ def test_bn_stats_from_gram(M, C, N):
           f"{((out2[0].double() - mean).abs() / yx.std(0)).max().item():.2e}, "
           f"{((out2[1].double() - inv).abs() / inv).max().item():.2e}")
     assert e_mean < 1e-4 and e_inv < 1e-4
+
+
+@pytest.mark.parametrize("M,C,N", [(3211264 // 8 + 7, 64, 256), (802816 // 4 + 3, 128, 512), (50176 + 9, 256, 1024),
+                                   (5, 64, 256)])
+def test_conv1x1_bn_res_relu_streaming_vs_persistent(monkeypatch, M, C, N):
+    """The register-streaming bnres kernel (stream1x1.hip) against the persistent LDS-staged engine (VCG_RS1X1=0):
+    bit-identical output and mask bits (same products, order and roundings), ragged row counts included."""
+    gen = torch.Generator().manual_seed(M % 113 + C)
+    x = _bf(torch.relu(torch.randn(M, C, generator=gen)))
+    wf = _bf(torch.randn(N, C, generator=gen) / C ** 0.5)
+    bias = (torch.randn(N, generator=gen) * 0.3).to(DEV)
+    res = _bf(torch.relu(torch.randn(M, N, generator=gen)) - 0.3)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("VCG_RS1X1", flag)
+        r = ops.conv1x1_bn_res_relu(x, wf, bias, res, M, N, C)
+        assert r is not None
+        out[flag] = r
+    torch.cuda.synchronize()
+    assert torch.equal(out["0"][0], out["1"][0])
+    assert torch.equal(out["0"][1], out["1"][1])

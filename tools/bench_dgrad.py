@@ -13,6 +13,7 @@ from vcg_hip import _lib, ops  # noqa: E402
 
 _lib.call("vcg_init", 0)
 NOTSM = os.environ.get("VCG_BENCH_NOTSM") == "1"
+NOY = os.environ.get("VCG_BENCH_NOY") == "1"  # mask bits without y (the trunk's y3-drop blocks: XF_BITS)
 dev, bf = "cuda", torch.bfloat16
 SHAPES = [  # (name, N, H, W, C (dx channels), Cout (dy channels), T, residual stride)
     ("l1 conv1 dgrad", 1024, 56, 56, 256, 64, 16, 1),
@@ -36,7 +37,7 @@ def run(name, N, H, W, C, Co, T, rs=1):
     wsb = ops.ws(_lib.query("vcg_conv_dgrad_bwd_ws_bytes", C, Co, 1, 1), dev)
 
     def f():
-        ops.conv_dgrad_bwd(dy, wt, N, H, W, C, Co, 1, 1, 1, 0, tsm_T=T, tsm_fold=0 if NOTSM else C // 8, res=res, res_stride=rs, bits=bits, y=y,
+        ops.conv_dgrad_bwd(dy, wt, N, H, W, C, Co, 1, 1, 1, 0, tsm_T=T, tsm_fold=0 if NOTSM else C // 8, res=res, res_stride=rs, bits=bits, y=None if NOY else y,
                            mean=mean, invstd=inv, sums=sums, dgamma=dg, dbeta=db, out=out, workspace=wsb)
     for _ in range(3):
         f()
@@ -49,7 +50,7 @@ def run(name, N, H, W, C, Co, T, rs=1):
     torch.cuda.synchronize()
     us = a.elapsed_time(b) / 10 * 1e3
     M = N * H * W
-    gb = (M * Co + (2 + (0.25 if rs == 2 else 1)) * M * C) * 2 / 1e9 + M * C / 8 / 1e9  # dy + y + g + res + bits
+    gb = (M * Co + (1 + (0 if NOY else 1) + (0.25 if rs == 2 else 1)) * M * C) * 2 / 1e9 + M * C / 8 / 1e9  # dy + y + g + res + bits
     line = f"{name:16s} M={M} N={C} K={Co}: {us:8.1f} us  {gb / us * 1e3:6.2f} TB/s algorithmic"
     buf = (ctypes.c_ulonglong * 256)()
     if _lib.query("vcg_fast_stamps", ctypes.addressof(buf), 256) == 0:

@@ -298,6 +298,9 @@ int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b 
 int wgrad_patch_rows(int dtype, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad,
                      int tsm_fold);
 int wgrad_patch_splits();
+// stream1x1.hip: relu(bf16(x wfold^T + bias) + res) + mask bits on the register-streaming kernel (-1: not eligible)
+int run_rs1x1_bnres(const void* x, const void* wfold, const float* bias, const void* res, void* out, uint8_t* bits,
+                    long long M, int N, int K, hipStream_t s);
 int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int W, int R, hipStream_t s);
 int wgrad_fast_tile_m(int M);
 int wgrad_fast_tile_n(int N);

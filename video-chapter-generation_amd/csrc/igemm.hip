@@ -1282,6 +1282,17 @@ VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const floa
   VCG_REQUIRE(x && wfold && bias && res && out && bits, "null argument");
   VCG_REQUIRE(M > 0 && N % 64 == 0 && K % 64 == 0, "N and K must be multiples of 64");
   VCG_REQUIRE((((uintptr_t)x | (uintptr_t)wfold | (uintptr_t)res | (uintptr_t)out) & 15) == 0, "16-B alignment");
+  VCG_REQUIRE(!res_scale == !res_shift, "res_scale and res_shift go together");
+  if (!res_scale) {  // the register-streaming kernel (stream1x1.hip) where it applies
+    const int rc = run_rs1x1_bnres(x, wfold, bias, res, out, bits, M, N, K, stream);
+    if (rc >= 0) {
+      if (FILE* f = gemm_log()) {
+        fprintf(f, "a=0 b=0 epi=0 M=%d N=%d K=%d z=1 fast=4 conv=1x1/1 C=%d bnres=1\n", M, N, K, K);
+        fflush(f);
+      }
+      return rc;
+    }
+  }
   if (!fast_gemm_enabled() || (long long)M * K * 2 >= 0xFFFFFF00LL || (long long)M * N * 2 >= 0xFFFFFF00LL)
     return VCG_ERR_UNSUPPORTED;
   GemmParams p{};
@@ -1300,7 +1311,6 @@ VCG_API int vcg_conv1x1_bn_res_relu(const void* x, const void* wfold, const floa
   p.ldr = N;
   p.res_round = 1;
   p.obits = bits;
-  VCG_REQUIRE(!res_scale == !res_shift, "res_scale and res_shift go together");
   p.res_sc = res_scale;
   p.res_sh = res_shift;
   if (FILE* f = gemm_log()) {

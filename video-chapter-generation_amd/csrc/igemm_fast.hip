@@ -776,8 +776,11 @@ __host__ __device__ constexpr int bwd_stream_buf(int KC, int XF) {
   return 2 * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 : 0) + ((XF & (XF_HASY | XF_BITS)) ? 8 * 256 : 0) +
          ((XF & XF_Y2) ? 8192 : 0);
 }
+#ifndef VCG_STREAM_NBUF
+#define VCG_STREAM_NBUF 4  // ring slots at most (build knob for A/B builds)
+#endif
 __host__ __device__ constexpr int bwd_stream_nbuf(int KC, int XF) {
-  return (160 * 1024 - (KC * 8192 + 8192 + 1024)) / bwd_stream_buf(KC, XF) >= 4 ? 4
+  return (160 * 1024 - (KC * 8192 + 8192 + 1024)) / bwd_stream_buf(KC, XF) >= VCG_STREAM_NBUF ? VCG_STREAM_NBUF
          : (160 * 1024 - (KC * 8192 + 8192 + 1024)) / bwd_stream_buf(KC, XF);
 }
 
