@@ -638,6 +638,36 @@ def test_conv_dgrad_bwd_stream_vs_persistent(K, case, y2, monkeypatch):
         assert (a.double() - b.double()).abs().max().item() <= 1e-4 * (b.abs().max().item() + 1.0)
 
 
+@pytest.mark.parametrize("case", [(16, 56, 56, 256, 64, 8, 1), (16, 28, 28, 512, 128, 8, 1), (5, 7, 7, 256, 64, 5, 1),
+                                  (4, 14, 14, 1024, 128, 4, 1), (16, 56, 56, 256, 128, 8, 2), (5, 7, 7, 256, 64, 5, 2)])
+def test_conv_dgrad_bwd_register_stream(K, case, monkeypatch):
+    """The register-streaming fused 1x1 dgrad with mask bits and no y (stream1x1.hip, the trunk's conv1 input
+    gradients after a block whose y3 is not stored) against the LDS-ring / persistent engines (VCG_RS_DGRAD=0):
+    g bit for bit (TSM adjoint with clip edges, tiles straddling frames, ragged rows, 1-3 shift variants per column
+    block, the compact stride-2 residual of a layer's first block), sum_g to float rounding."""
+    N, H, W, C, Cout, T, rs = case
+    dtype = torch.bfloat16
+    fold = C // 8
+    dy = _rand((N, H, W, Cout), dtype, 81).to(DEV)
+    wt = K.weight_prep(_rand((Cout, C, 1, 1), torch.float32, 82, 0.1).to(DEV), C, dtype, transposed=True)
+    res = _rand((N, (H + 1) // 2, (W + 1) // 2, C) if rs == 2 else (N, H, W, C), dtype, 85).to(DEV)
+    _, bits = K.bn_apply(_rand((N, H, W, C), dtype, 86).to(DEV), torch.ones(C, device=DEV),
+                         torch.zeros(C, device=DEV), C, relu=True, bits=True)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("VCG_RS_DGRAD", flag)
+        sums = torch.zeros((2, C), device=DEV)
+        g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, 1, 1, 1, 0, tsm_T=T, tsm_fold=fold, res=res, res_stride=rs,
+                             bits=bits, sums=sums)
+        assert g is not None
+        torch.cuda.synchronize()
+        outs.append((g.clone(), sums.clone()))
+    (ga, sa), (gb, sb) = outs
+    assert torch.equal(ga, gb), f"g differs: max {(ga.float() - gb.float()).abs().max().item():.3e}"
+    assert (sa[0].double() - sb[0].double()).abs().max().item() <= 1e-4 * (sb[0].abs().max().item() + 1.0)
+    assert torch.equal(sa[1], sb[1])  # (no y: no sum against it)
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("H", [768, 200])
 def test_layernorm_fwd_bwd(K, dtype, H):

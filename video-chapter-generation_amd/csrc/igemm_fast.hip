@@ -1876,6 +1876,7 @@ static int bwd_stream_rows(const GemmParams& p) {
 }
 
 int fast_bwd_slots(const GemmParams& p) {
+  if (rs_dgrad_ok(p)) return rs_dgrad_slots(p);
   if (bwd_stream_ok(p)) return bwd_stream_rows(p);
   const int R = patch_rows(p, OP_DGRAD);
   if (R > 0) return patch_grid_rows(p, patch_geom(p, R));
@@ -2002,6 +2003,12 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
         if (epi == EPI_STORE) return launch_patch<EPI_STORE, false>(p, R, s);
       }
     }
+  }
+  if (epi == EPI_BWD && amode == OP_DENSE_K && z == 1 && rs_dgrad_ok(p)) {  // the register-streaming kernel
+    const int tk = timing_begin(s);
+    const int rc = run_rs1x1_dgrad(p, s);
+    timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_DENSE_K, EPI_BWD, false>(p, 1));
+    return rc;
   }
   if (epi == EPI_BWD && amode == OP_DENSE_K && z == 1 && bwd_stream_ok(p))
     return p.K == 64 ? run_bwd_stream<1>(p, s) : run_bwd_stream<2>(p, s);
