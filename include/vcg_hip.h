@@ -161,6 +161,11 @@ VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx,
    only (for vcg_maxpool_bwd_bn_apply) */
 VCG_API long long vcg_maxpool_bwd_bn_ws_bytes(int C);
 VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* idx, void* g, int N, int H, int W, int C, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t s);
+/* the sums of vcg_maxpool_bwd_bn (g = NULL) from the pooled activation mp [N][OH][OW][C] (vcg_bn_relu_maxpool's
+   output) instead of the pre-pool y: a window's gradient reaches its argmax pixel, whose ReLU output is mp, so the
+   mask is mp > 0 and y - mean = (mp - mshift) / mscale - mean there (mscale != 0). The stem BN + ReLU + max-pool
+   backward of Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15, torchvision bn1 -> relu -> maxpool). */
+VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void* mp, int N, int OH, int OW, int C, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t s);
 /* the stem backward in two streaming passes (reference resnet50_tsm.py:19 torchvision stem: conv1 -> bn1 -> relu ->
    maxpool): dx = BN-backward-apply(g) with g = mask(maxpool_bwd(dy)) recomputed (rounded to dtype), sums from
    vcg_maxpool_bwd_bn(g = NULL) -- vcg_maxpool_bwd_bn + vcg_bn_bwd_apply without the g tensor */

@@ -187,6 +187,36 @@ def test_gram_stats_forward():
     assert e["gram"][1] <= 1.25 * e["gemm"][1] + 1e-2
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_pooled_stem_sums_step(prec):
+    """The stem BN-backward sums from the pooled activation (ResNetTrunk.pooled_stem_sums) against the per-pixel
+    pass over the pre-pool conv output, one C1-shape train step: the same loss; gradients the same up to the
+    rounding of the recovered activation (fp32: every tensor within 1e-4 relative; bf16: the stem conv / BN
+    gradients, the only ones the sums reach, within 2e-2 relative, cosine >= 0.999)."""
+    from vcg_hip import synth
+    from vcg_hip.trunk import ResNetTrunk
+    st = dict(_gold("bn_running_stats.npz"))
+    frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=78, device=DEV)
+    res = {}
+    saved = ResNetTrunk.pooled_stem_sums
+    try:
+        for pooled in (True, False):
+            ResNetTrunk.pooled_stem_sums = pooled
+            res[pooled] = _step(_model(4, prec, st), frames, ids, mask, labels)
+    finally:
+        ResNetTrunk.pooled_stem_sums = saved
+    (la, _, ga, _), (lb, _, gb, _) = res[True], res[False]
+    assert la == lb
+    for n in gb:
+        e = _rel(ga[n].cpu(), gb[n].double().cpu())
+        if prec == "fp32":
+            assert e <= 1e-4, (n, e)
+        elif e > 2e-2:
+            raise AssertionError((n, e))
+        cos = torch.nn.functional.cosine_similarity(ga[n].double().flatten(), gb[n].double().flatten(), 0).item()
+        assert gb[n].abs().max() == 0 or cos >= 0.999, (n, cos)
+
+
 def test_c1_loss_and_conditioning():
     """C1 bf16 step: loss / logits within bf16 tolerance of the exact fixture. (Its vision gradients are NOT
     compared element-wise with fp32: at C1 the BatchNorm statistics run over 8 frames of 4x4..56x56 maps and the

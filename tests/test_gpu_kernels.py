@@ -763,6 +763,35 @@ def test_fused_stem_bn_relu_maxpool(K, dtype, train, hw):
     assert torch.equal(dx, dx_ref)
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("hw", [(13, 12), (16, 10), (112, 112)])
+def test_maxpool_bwd_bn_sums_pooled(K, dtype, hw):
+    """The stem BN-backward sums from the pooled activation (a window's gradient reaches its argmax pixel, whose
+    activation is mp) == the per-pixel pass over y, up to rounding: the per-pixel pass sums g rounded to dtype per
+    pixel (after adding the <= 4 windows' dy), and for g*xhat recovers nothing (y is read), while the pooled pass
+    recovers y as (mp - shift) / scale, exact up to mp's rounding to dtype (bf16: 2^-9 relative per term)."""
+    N, C = 3, 64
+    H, W = hw
+    y = _rand((N, H, W, C), dtype, 88).to(DEV)
+    g0 = torch.Generator().manual_seed(89)
+    sc = (torch.rand(C, generator=g0) * 2 - 0.5).to(DEV)
+    sc = torch.where(sc.abs() < 0.05, torch.full_like(sc, 0.05), sc)
+    sh = (torch.randn(C, generator=g0) * 0.3).to(DEV)
+    mp, idx = K.bn_relu_maxpool(y, sc, sh, N, H, W, C)
+    dys = _rand(mp.shape, dtype, 90).to(DEV)
+    mean = (torch.randn(C, generator=g0) * 0.1).to(DEV)
+    inv = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    s_ref, s_new = torch.zeros((2, C), device=DEV), torch.zeros((2, C), device=DEV)
+    dg, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), 0.25, device=DEV)
+    K.maxpool_bwd_bn(dys, idx, N, H, W, C, y, mean, inv, sc, sh, s_ref, store_g=False)
+    K.maxpool_bwd_bn_sums_pooled(dys, mp, N, mp.shape[1], mp.shape[2], C, mean, inv, sc, sh, s_new, dg, db)
+    tol = 1e-5 if dtype == torch.float32 else 4e-3
+    for k in range(2):
+        scale = s_ref[k].abs().max().item() + 1
+        assert (s_new[k] - s_ref[k]).abs().max().item() <= tol * scale, k
+    assert torch.allclose(db - 0.25, s_new[0], atol=1e-6) and torch.allclose(dg - 0.5, s_new[1], atol=1e-6)
+
+
 def test_attention_softmax_dropout(K):
     """Masked softmax + dropout: P matches torch softmax over the valid keys; Pd = P / (1 - p) on kept
     entries and 0 on dropped ones (drop rate ~ p); the backward regenerates the same mask."""

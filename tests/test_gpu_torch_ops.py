@@ -77,3 +77,28 @@ def test_linear_op(dt, tol):
     y = torch.ops.vcg.linear(x, w, b, 1)
     ref = (x.double() @ w.double().T + b.double()).clamp_min(0)
     assert (y.double() - ref).abs().max().item() <= tol * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("dt,act,tol", [(torch.float32, 0, 1e-5), (torch.float32, 1, 1e-5), (torch.bfloat16, 0, 3e-2)])
+def test_linear_op_autograd(dt, act, tol):
+    """vcg::linear's backward (dX = dY' W, dW = dY'^T X, db = colsum(dY') on the GEMM / column-sum kernels) against
+    float64 autograd of x W^T + b (+ ReLU); opcheck of the registration."""
+    gen = torch.Generator().manual_seed(5)
+    x0 = torch.randn(100, 64, generator=gen).to(DEV).to(dt)
+    w0 = (torch.randn(48, 64, generator=gen) * 0.1).to(DEV).to(dt)
+    b0 = torch.randn(48, generator=gen).to(DEV)
+    g = torch.randn(100, 48, generator=gen).to(DEV).to(dt)
+    x, w, b = (t.clone().requires_grad_() for t in (x0, w0, b0))
+    y = torch.ops.vcg.linear(x, w, b, act)
+    y.backward(g)
+    xr, wr, br = (t.detach().double().requires_grad_() for t in (x0, w0, b0))
+    yr = xr @ wr.T + br
+    if act == 1:
+        yr = yr.clamp_min(0)
+    yr.backward(g.double())
+    for a, r in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert a.dtype == (torch.float32 if r is br.grad else dt)
+        assert (a.double() - r).abs().max().item() <= tol * (r.abs().max().item() + 1e-12)
+    if dt == torch.float32:
+        torch.library.opcheck(torch.ops.vcg.linear, (x0.clone().requires_grad_(), w0.clone().requires_grad_(),
+                                                     b0.clone().requires_grad_(), act))

@@ -425,7 +425,7 @@ void rs1x1_dgrad_kernel(const bf16_t* __restrict__ W, RdArgs q) {
 
 int rs_grid(int N) {
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int ncb = N / RS_TN;
   return (cus / ncb) * ncb;
 }

@@ -773,6 +773,68 @@ __global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const T* __restrict__
   }
 }
 
+// The stem BatchNorm-backward sums from the POOLED activation instead of y: every window's gradient goes to one
+// pixel (its argmax), whose ReLU output is the window's max mp -- so the pixel passes the ReLU mask iff mp > 0, and
+// its normalised value is recovered from mp (z = y msc + msh => y - mean = (mp - msh) / msc - mean for mp > 0).
+// Both sums are linear in the per-pixel gradient, so they are sums over windows: sum_g = sum [mp > 0] dy,
+// sum_gx = invstd * sum [mp > 0] dy (y - mean). Reads dy and mp once (1/2 of the output rows' bytes each) instead
+// of dy, the argmax bytes and the whole pre-pool y (the stem's conv output, 4x the pooled size). mp is the bf16
+// max, so y - mean carries one bf16 rounding of the activation (the per-pixel path carries that of y).
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bn_sums_pooled_kernel(const T* __restrict__ dy, const T* __restrict__ mp,
+                                                                     long long TV, int lcpr, MpBn bn) {
+  constexpr int VN = V<T>::N;
+  __shared__ float red[2][256][VN];
+  const int cpr = 1 << lcpr;
+  const int chunk = threadIdx.x & (cpr - 1);
+  const int c0 = chunk * VN;
+  float mu[VN], sc[VN], sh[VN], rsc[VN], off[VN], s1[VN], s2[VN];
+  load_params<VN>(bn.mean, c0, mu);
+  load_params<VN>(bn.msc, c0, sc);
+  load_params<VN>(bn.msh, c0, sh);
+#pragma unroll
+  for (int e = 0; e < VN; ++e) {
+    rsc[e] = 1.f / sc[e];
+    off[e] = -sh[e] * rsc[e] - mu[e];  // y - mean = mp / msc + off
+    s1[e] = s2[e] = 0.f;
+  }
+  const long long stride = (long long)gridDim.x * SB;
+  for (long long base = (long long)blockIdx.x * SB + threadIdx.x; base < TV; base += stride) {
+    float g[SU][VN], m[SU][VN];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {  // unconditional (clamped) loads, as bn_apply_kernel
+      const long long v = min(base + u * 256, TV - 1);
+      load16<T>(dy + v * VN, g[u]);
+      load16<T>(mp + v * VN, m[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      if (base + u * 256 >= TV) break;
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        const float d = m[u][e] > 0.f ? g[u][e] : 0.f;
+        s1[e] += d;
+        s2[e] = fmaf(d, fmaf(m[u][e], rsc[e], off[e]), s2[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VN; ++e) {
+    red[0][threadIdx.x][e] = s1[e];
+    red[1][threadIdx.x][e] = s2[e];
+  }
+  __syncthreads();
+  const int C = cpr * VN;
+  for (int i = threadIdx.x; i < 2 * C; i += 256) {
+    const int which = i >= C, c = i - which * C;
+    const int ch = c / VN, e = c - ch * VN;
+    float a = 0.f;
+    for (int kk = ch; kk < 256; kk += cpr) a += red[which][kk][e];
+    if (which) a *= bn.invstd[c];
+    bn.part[(long long)blockIdx.x * 2 * C + i] = a;
+  }
+}
+
 // ------------------------------------------------------------------ TSM gradient combine
 // dx = unshift(dshift) + other over NHWC [N*T][H][W][C] (adjoint of ops/temporal_shift.py:45-47)
 template <typename T, bool OTHER, bool BITS>
@@ -1100,6 +1162,36 @@ VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* i
   } else {
     if (g) VCG_MPB(float, MP_RED, g); else VCG_MPB(float, MP_RED_ONLY, g);
   }
+  VCG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
+                     sum_g, sum_gx, dgamma, dbeta, 1);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+// The sums of vcg_maxpool_bwd_bn (g == NULL) from the pooled activation mp [N][OH][OW][C] (the fused stem's
+// vcg_bn_relu_maxpool output) instead of the pre-pool y: see maxpool_bn_sums_pooled_kernel. mscale must be nonzero
+// (the BatchNorm weight times invstd).
+VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void* mp, int N, int OH, int OW, int C,
+                                           const float* mean, const float* invstd, const float* mscale,
+                                           const float* mshift, float* ws, long long ws_bytes, float* sum_g,
+                                           float* sum_gx, float* dgamma, float* dbeta, hipStream_t s) {
+  const int VN = dtype == VCG_BF16 ? 8 : 4;
+  VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && C / VN <= 256, "C must be a power of two multiple of the vector width");
+  VCG_REQUIRE(dy && mp && mean && invstd && mscale && mshift && sum_g && sum_gx, "BN arguments required");
+  VCG_REQUIRE(ws_bytes >= vcg_maxpool_bwd_bn_ws_bytes(C), "workspace too small");
+  const int lcpr = ilog2i(C / VN);
+  const long long TV = (long long)N * OH * OW * (C / VN);
+  if (TV == 0) return VCG_OK;
+  const unsigned nb = stream_grid(TV);
+  MpBn bn{};
+  bn.mean = mean; bn.invstd = invstd; bn.msc = mscale; bn.msh = mshift; bn.part = ws;
+  if (dtype == VCG_BF16)
+    hipLaunchKernelGGL(maxpool_bn_sums_pooled_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dy,
+                       (const bf16_t*)mp, TV, lcpr, bn);
+  else
+    hipLaunchKernelGGL(maxpool_bn_sums_pooled_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dy,
+                       (const float*)mp, TV, lcpr, bn);
   VCG_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
                      sum_g, sum_gx, dgamma, dbeta, 1);

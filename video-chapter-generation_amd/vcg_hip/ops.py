@@ -448,6 +448,14 @@ def maxpool_bwd_bn(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, sums, d
     return g
 
 
+def maxpool_bwd_bn_sums_pooled(dy, mp, N, OH, OW, C, mean, invstd, mscale, mshift, sums, dgamma=None, dbeta=None):
+    """The stem BN-backward sums of maxpool_bwd_bn(store_g=False) from the pooled activation mp (no pass over the
+    pre-pool y; vcg_maxpool_bwd_bn_sums_pooled)."""
+    w = ws(_lib.query("vcg_maxpool_bwd_bn_ws_bytes", C), dy.device)
+    _lib.call("vcg_maxpool_bwd_bn_sums_pooled", dt_code(dy.dtype), P(dy), P(mp), N, OH, OW, C, P(mean), P(invstd),
+              P(mscale), P(mshift), P(w), w.numel() * 4, P(sums[0]), P(sums[1]), P(dgamma), P(dbeta), stream())
+
+
 def maxpool_bwd_bn_apply(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, gamma, sums, count, train_stats):
     """The stem's BN-backward apply on g = mask(maxpool_bwd(dy)) recomputed in the same pass (sums from
     maxpool_bwd_bn(store_g=False)): returns the gradient of the stem conv output y."""

@@ -8,7 +8,10 @@ tracing, and, where the reference op is differentiable, an autograd formula that
                                                            vcg_hip.functions.cross_entropy calls it
     vcg::window_frames_u8(frames, idx, bf16, cpad)         the frame ingest (gather + ToTensor + Normalize into the
                                                            stem layout, youtube_dataset.py:180-190)
-    vcg::linear(x, weight, bias, act)                      nn.Linear (+ ReLU / GELU / tanh epilogue) on the GEMM engine
+    vcg::linear(x, weight, bias, act)                      nn.Linear (+ ReLU / GELU / tanh epilogue) on the GEMM engine;
+                                                           differentiable without an activation (any dtype) and with
+                                                           ReLU (fp32): dX = dY' W, dW = dY'^T X, db = colsum(dY');
+                                                           GELU / tanh epilogues are forward-only (backward raises)
 
 The encoder engines (vcg_hip/trunk.py, bert.py) issue ~2000 launches per train step and call the C ABI through
 ctypes directly: a dispatcher round trip per launch (~5-10 us of host time) would make the step host-bound.
@@ -31,7 +34,7 @@ def tsm_shift(x: torch.Tensor, n_segment: int, fold_div: int, direction: int) ->
 
 @tsm_shift.register_fake
 def _(x, n_segment, fold_div, direction):
-    return torch.empty_like(x)
+    return x.new_empty(x.shape)  # (contiguous, as the real op returns)
 
 
 def _tsm_setup(ctx, inputs, output):
@@ -102,3 +105,37 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], 
 @linear.register_fake
 def _(x, weight, bias, act):
     return x.new_empty((x.shape[0], weight.shape[0]))
+
+
+def _linear_setup(ctx, inputs, output):
+    x, weight, bias, act = inputs
+    ctx.act, ctx.has_bias = act, bias is not None
+    ctx.bias_dtype = bias.dtype if bias is not None else None
+    ctx.save_for_backward(x, weight, output if act == ops.ACT_RELU else None)
+
+
+def _linear_backward(ctx, dy):
+    x, weight, out = ctx.saved_tensors
+    M, K = x.shape
+    N = weight.shape[0]
+    dy = dy.contiguous()
+    if ctx.act == ops.ACT_RELU:
+        if dy.dtype != torch.float32:
+            raise NotImplementedError("vcg::linear backward through ReLU: fp32 only (vcg_act_drop_bwd)")
+        dpre = torch.empty_like(dy)
+        ops._lib.call("vcg_act_drop_bwd", ops.P(dy), ops.P(out.contiguous()), ops.P(dpre), dy.numel(), ops.ACT_RELU,
+                      0.0, 0, ops.stream())
+        dy = dpre
+    elif ctx.act != ops.ACT_NONE:
+        raise NotImplementedError(f"vcg::linear backward: act {ctx.act} is forward-only (no pre-activation saved)")
+    dx = ops.gemm(dy, weight.contiguous(), M, K, N, N, K, transB=True)
+    dw = ops.gemm(dy, x.contiguous(), N, K, M, N, K, transA=True, transB=True)
+    db = None
+    if ctx.has_bias:
+        db = torch.empty(N, dtype=torch.float32, device=dy.device)
+        ops.colsum(dy, N, M, N, db, accumulate=False)
+        db = db.to(ctx.bias_dtype)
+    return dx, dw, db, None
+
+
+linear.register_autograd(_linear_backward, setup_context=_linear_setup)

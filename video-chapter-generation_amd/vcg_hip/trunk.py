@@ -140,6 +140,9 @@ class ResNetTrunk:
     # bn3's statistics follow where y3 is not stored (no statistics-only conv3 pass over a2) and the a2-form fold
     # takes its Gram term (no a2^T a2 GEMM in the backward); False: the conv3 statistics GEMM (tests compare both)
     gram_stats = os.environ.get("VCG_GRAM_STATS", "1") != "0"
+    # the stem BN-backward sums from the pooled activation (ops.maxpool_bwd_bn_sums_pooled) instead of a pass over
+    # the pre-pool conv output; False: the per-pixel pass (tests compare both)
+    pooled_stem_sums = os.environ.get("VCG_POOLED_STEM_SUMS", "1") != "0"
 
     def __init__(self, net, dtype):
         self.net = net
@@ -244,7 +247,7 @@ class ResNetTrunk:
         # decision from y0)
         mp, idx = ops.bn_relu_maxpool(y0, b0.scale, b0.shift, N, H1, W1, 64)
         Hm, Wm = mp.shape[1], mp.shape[2]
-        saved = {"stem": (xs, y0, None, idx, b0, N, H, W, cpad, H1, W1)} if need_grad else None
+        saved = {"stem": (xs, y0, mp, idx, b0, N, H, W, cpad, H1, W1)} if need_grad else None
         if not need_grad:
             del y0, idx
         h, Hc, Wc = mp, Hm, Wm
@@ -543,13 +546,19 @@ class ResNetTrunk:
             dout, gin = self._block_bwd(rec, dout, gin, prev)
             self._report(hooks, list(rec["blk"].parameters()))
             del rec
-        xs, y0, a0, idx, b0, N, H, W, cpad, H1, W1 = saved["stem"]
-        sums0 = torch.empty((2, 64), dtype=torch.float32, device=y0.device)
+        xs, y0, mp, idx, b0, N, H, W, cpad, H1, W1 = saved["stem"]
+        sums0 = torch.zeros((2, 64), dtype=torch.float32, device=y0.device)
         dg0, db0 = self._bn_grads(b0)
-        # two passes over (dout, idx, y0): the BN sums, then the BN-backward apply with g recomputed -- no g tensor
-        # (1.34 ms vs 0.77 + 0.88 ms for storing g and applying it, tools/bench_stem.py)
-        ops.maxpool_bwd_bn(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift, sums0, dg0, db0,
-                           store_g=False)
+        # the BN sums, then the BN-backward apply over (dout, idx, y0) with g recomputed -- no g tensor (1.34 ms vs
+        # 0.77 + 0.88 ms for storing g and applying it, tools/bench_stem.py). The sums come from the pooled
+        # activation mp (a window's gradient reaches its argmax pixel, whose activation is mp): dout and mp instead of
+        # dout, idx and the 4x larger y0
+        if ResNetTrunk.pooled_stem_sums:
+            ops.maxpool_bwd_bn_sums_pooled(dout, mp, N, mp.shape[1], mp.shape[2], 64, b0.mean, b0.invstd, b0.scale,
+                                           b0.shift, sums0, dg0, db0)
+        else:
+            ops.maxpool_bwd_bn(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift, sums0, dg0, db0,
+                               store_g=False)
         dy0 = ops.maxpool_bwd_bn_apply(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift,
                                        b0.bn.weight, sums0, N * H1 * W1, b0.mode != "running")
         self._wgrad(self.net.conv1, xs, dy0, N, H, W, cpad)
