@@ -170,6 +170,14 @@ VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void
    maxpool): dx = BN-backward-apply(g) with g = mask(maxpool_bwd(dy)) recomputed (rounded to dtype), sums from
    vcg_maxpool_bwd_bn(g = NULL) -- vcg_maxpool_bwd_bn + vcg_bn_bwd_apply without the g tensor */
 VCG_API int vcg_maxpool_bwd_bn_apply(int dtype, const void* dy, const unsigned char* idx, void* dx, int N, int H, int W, int C, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, const float* gamma, const float* sum_g, const float* sum_gx, long long count, int train_stats, hipStream_t s);
+/* the stem backward from the pooled-output gradient to the stem conv's weight gradient in ONE pass (bf16; reference
+   resnet50_tsm.py:19 torchvision stem conv1 7x7/2 -> bn1 -> relu -> maxpool): vcg_maxpool_bwd_bn_apply's dy0 of each
+   conv-output row pair computed into LDS and contracted at once with the pair-packed frames x [N][2H][2W][4] into
+   dW [64][3][7][7] (fp32, added to when accumulate) -- dy0 never reaches HBM. y [N][H][W][64], dy / idx
+   [N][H/2][W/2][64]; H even, W % 8 == 0, W <= 112. Equals vcg_maxpool_bwd_bn_apply + vcg_conv_wgrad up to the
+   fp32 summation order (fixed: deterministic). */
+VCG_API long long vcg_stem_bwd_fused_ws_bytes(void);
+VCG_API int vcg_stem_bwd_fused(const void* dy, const unsigned char* idx, const void* y, const void* x, int N, int H, int W, const float* mean, const float* invstd, const float* mscale, const float* mshift, const float* gamma, const float* sum_g, const float* sum_gx, long long count, int train_stats, float* ws, long long ws_bytes, float* dw, int accumulate, hipStream_t s);
 /* the stem forward's BN + ReLU + maxpool 3x3/2 in one pass: out / idx = maxpool(relu(fma(y, scale, shift))) with the
    activation rounded to dtype (bit-identical to vcg_bn_apply then vcg_maxpool_fwd; no activation tensor) */
 VCG_API int vcg_bn_relu_maxpool(int dtype, const void* y, const float* scale, const float* shift, void* out, unsigned char* idx, int N, int H, int W, int C, hipStream_t s);

@@ -68,3 +68,12 @@ def test_ffn_gelu_fwd_and_bwd(K, M):
     cdf = 0.5 * (1 + torch.erf(pr / 2 ** 0.5))
     d64 = (dfo.double() @ W2.double()) * (cdf + pr * torch.exp(-0.5 * pr * pr) / (2 * torch.pi) ** 0.5)
     assert (dpre.double().cpu() - d64).abs().max().item() <= 2e-2 * d64.abs().max().item()
+    # the same with W2^T materialised (the BERT backward's B operand, _LinearT): the fast engine's staged GELU'
+    # epilogue (dh rounded to bf16, then times GELU'(pre), full-row residual reads)
+    W2t = W2.T.contiguous().to(DEV)
+    dpre2 = K.gemm(dfo.to(DEV), W2t, M, I, H, H, H, act=K.ACT_GELU_BWD, residual=pre, ldr=I)
+    assert (dpre2.double().cpu() - d64).abs().max().item() <= 2e-2 * d64.abs().max().item()
+    dh = (dfo.to(DEV) @ W2.to(DEV)).double()  # the rounded dh (torch bf16 GEMM), then the fp64 GELU' product
+    ref2 = (dh.cpu() * (cdf + pr * torch.exp(-0.5 * pr * pr) / (2 * torch.pi) ** 0.5))
+    rel = (dpre2.double().cpu() - ref2).abs().max().item() / ref2.abs().max().item()
+    assert rel <= 1e-2, rel

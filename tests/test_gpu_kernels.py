@@ -763,6 +763,69 @@ def test_fused_stem_bn_relu_maxpool(K, dtype, train, hw):
     assert torch.equal(dx, dx_ref)
 
 
+@pytest.mark.parametrize("train", [True, False])
+@pytest.mark.parametrize("shape", [(2, 32, 32), (3, 24, 40), (2, 56, 56), (1, 112, 112)])
+def test_stem_bwd_fused(K, train, shape):
+    """The one-pass stem backward (max-pool + BN + ReLU backward contracted with the frames into the 7x7 / 2 conv's
+    weight gradient, dy0 only in LDS) == maxpool_bwd_bn_apply + conv_wgrad (the pair-packed stem engine): the same
+    dy0 (bit-exact arithmetic), products summed in another order, so 1e-4 relative; accumulate adds."""
+    N, H1, W1 = shape
+    C = 64
+    g0 = torch.Generator().manual_seed(92)
+    y = _rand((N, H1, W1, C), torch.bfloat16, 93).to(DEV)
+    sc = (torch.rand(C, generator=g0) * 2 - 0.5).to(DEV)
+    sh = (torch.randn(C, generator=g0) * 0.3).to(DEV)
+    mp, idx = K.bn_relu_maxpool(y, sc, sh, N, H1, W1, C)
+    dys = _rand(mp.shape, torch.bfloat16, 94).to(DEV)
+    mean = (torch.randn(C, generator=g0) * 0.1).to(DEV)
+    inv = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    gamma = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    sums = torch.zeros((2, C), device=DEV)
+    K.maxpool_bwd_bn(dys, idx, N, H1, W1, C, y, mean, inv, sc, sh, sums, store_g=False)
+    xs = torch.zeros((N, 2 * H1, 2 * W1, 4), dtype=torch.bfloat16)
+    xs[..., :3] = _rand((N, 2 * H1, 2 * W1, 3), torch.bfloat16, 95)
+    xs = xs.to(DEV)
+    dy0 = K.maxpool_bwd_bn_apply(dys, idx, N, H1, W1, C, y, mean, inv, sc, sh, gamma, sums, N * H1 * W1, train)
+    ref = torch.zeros((C, 3, 7, 7), device=DEV)
+    K.conv_wgrad(xs, dy0, ref, N, 2 * H1, 2 * W1, 4, 3, C, 7, 7, 2, 3)
+    out = torch.full((C, 3, 7, 7), 0.5, device=DEV)
+    K.stem_bwd_fused(dys, idx, y, xs, N, H1, W1, mean, inv, sc, sh, gamma, sums, N * H1 * W1, train, out)
+    torch.cuda.synchronize()
+    err = (out - 0.5 - ref).abs().max().item()
+    assert err <= 1e-4 * (ref.abs().max().item() + 1e-6), err
+    # exact-arithmetic cross-check of the reference path itself: dy0 (as stored) contracted in fp64
+    ref64 = torch.nn.grad.conv2d_weight(xs[..., :3].permute(0, 3, 1, 2).double().cpu(), (C, 3, 7, 7),
+                                        dy0.permute(0, 3, 1, 2).double().cpu(), stride=2, padding=3)
+    assert (out.double().cpu() - 0.5 - ref64).abs().max().item() <= 1e-4 * ref64.abs().max().item()
+    out2 = torch.zeros_like(out)
+    K.stem_bwd_fused(dys, idx, y, xs, N, H1, W1, mean, inv, sc, sh, gamma, sums, N * H1 * W1, train, out2)
+    assert torch.equal(out2, out - 0.5) or (out2 - (out - 0.5)).abs().max().item() <= 1e-6 * ref.abs().max().item()
+
+
+def test_weight_prep_multi(K):
+    """One vcg_weight_prep_multi launch (LDS-tiled transposes) == vcg_weight_prep per weight and layout, bit for
+    bit: 1x1 / 3x3 / 7x7 shapes, Cout and Cin*KH*KW not multiples of 64, channel padding, the pair-packed stem."""
+    shapes = [(64, 64, 3, 3, 64, 0), (64, 64, 3, 3, 64, 1), (256, 64, 1, 1, 64, 0), (256, 64, 1, 1, 64, 1),
+              (512, 512, 3, 3, 512, 0), (512, 512, 3, 3, 512, 1), (2048, 1024, 1, 1, 1024, 1), (70, 37, 3, 3, 40, 0),
+              (70, 37, 3, 3, 37, 1), (64, 3, 7, 7, 8, 0), (64, 3, 7, 7, 4, 5), (24, 600, 3, 3, 600, 0)]
+    g = torch.Generator().manual_seed(91)
+    desc, outs, refs = [], [], []
+    for Cout, Cin, KH, KW, cpad, mode in shapes:
+        w = (torch.randn((Cout, Cin, KH, KW), generator=g) * 0.1).to(DEV)
+        if mode >= 2:
+            ref = K.weight_prep(w, cpad, torch.bfloat16, pair_pad=mode - 2)
+        else:
+            ref = K.weight_prep(w, cpad, torch.bfloat16, transposed=bool(mode))
+        out = torch.full_like(ref, float("nan"))
+        desc.append([w.data_ptr(), out.data_ptr(), Cout, Cin, KH, KW, cpad, mode])
+        outs.append((w, out))
+        refs.append(ref)
+    K.weight_prep_multi(torch.tensor(desc, dtype=torch.int64).to(DEV), len(desc))
+    torch.cuda.synchronize()
+    for (w, out), ref, sh in zip(outs, refs, shapes):
+        assert torch.equal(out.view(torch.int16), ref.view(torch.int16)), sh
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("hw", [(13, 12), (16, 10), (112, 112)])
 def test_maxpool_bwd_bn_sums_pooled(K, dtype, hw):

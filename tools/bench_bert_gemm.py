@@ -54,6 +54,9 @@ def main():
             line.append(f"dX transB+gelu' {t:7.1f}us")
             t = timeit(lambda: ops.gemm(dY, ops.transpose(W), R, K, N, N, N, act=ops.ACT_GELU_BWD, residual=pre, ldr=K))
             line.append(f"dX W^T+gelu' {t:7.1f}us")
+            Wt = ops.transpose(W)
+            t = timeit(lambda: ops.gemm(dY, Wt, R, K, N, N, N, act=ops.ACT_GELU_BWD, residual=pre, ldr=K))
+            line.append(f"dX (W^T resident)+gelu' {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
         t = timeit(lambda: ops.gemm(dY, ops.transpose(W), R, K, N, N, N))
         line.append(f"dX W^T {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
         t = timeit(lambda: ops.transpose(W))

@@ -376,7 +376,9 @@ __device__ __forceinline__ void unpack8(const uint4& u, float (&v)[8]) {
 
 // EPI_STORE + residual + ReLU through the stage (the running-statistics bn3 folded into conv3: relu(x W'^T + b + res),
 // trunk.py _conv3_folded): the GEMM value is rounded to bf16 in the stage -- as the unfolded path stores y3 -- and the
-// residual is added per 16-B row chunk in the flush, so both the residual loads and the output stores are full rows
+// residual is added per 16-B row chunk in the flush, so both the residual loads and the output stores are full rows.
+// ACT_GELU_BWD: the residual is the pre-activation and the output dh * GELU'(pre), dh rounded to bf16 first (as
+// torch autocast's bf16 matmul output feeding gelu_backward)
 template <int BM, int BN>
 __device__ __forceinline__ void epilogue_staged_res(f32x4 (&acc)[4][BN / 32], const GemmParams& p,
                                                     const float (&bv)[BN / 32][4], bf16_t* Cout, const bf16_t* Res,
@@ -436,10 +438,15 @@ __device__ __forceinline__ void epilogue_staged_res(f32x4 (&acc)[4][BN / 32], co
       for (int e = 0; e < 8; ++e) r[e] = fmaf(r[e], rsc[e], rsh[e]);
     }
     uint32_t mb = 0;  // ReLU mask of the output (p.obits): bit e = out > 0, as vcg_bn_apply writes it
+    if (p.act == ACT_GELU_BWD) {  // BERT FFN2's input gradient: dh * GELU'(pre), dh rounded as stored
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      a[e] = apply_act(a[e] + r[e], p.act);
-      mb |= (a[e] > 0.f ? 1u : 0u) << e;
+      for (int e = 0; e < 8; ++e) a[e] *= p.fast_act ? gelu_erf_grad_fast(r[e]) : gelu_erf_grad(r[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[e] = apply_act(a[e] + r[e], p.act);
+        mb |= (a[e] > 0.f ? 1u : 0u) << e;
+      }
     }
     uint4 o;
     o.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
@@ -1237,7 +1244,8 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
       } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0 &&
                                ((uintptr_t)p.C & 15) == 0)) {
         epilogue_staged<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
-      } else if (RES && (staged || p.obits) && p.res_round && p.act == ACT_RELU && p.aux == nullptr &&
+      } else if (RES && (staged || p.obits) && p.aux == nullptr && !(p.act == ACT_GELU_BWD && p.res_sc) &&
+                 ((p.res_round && p.act == ACT_RELU) || (staged && p.act == ACT_GELU_BWD)) &&
                  ((p.ldc | p.ldr | p.N) & 7) == 0 && (((uintptr_t)p.residual | (uintptr_t)p.C) & 15) == 0) {
         if constexpr (BM == 128 && RES)
           epilogue_staged_res<BM, BN>(acc, p, bv, Cout, Res, stA, stB, mt * BM, n0, wm, wn, lane, p.M);

@@ -537,37 +537,74 @@ VCG_API int vcg_weight_fold(int dtype, const float* w, const float* scale, void*
 
 namespace {
 // vcg_weight_prep_multi: blockIdx.y = descriptor (8 int64: src, dst, Cout, Cin, KH, KW, Cpad, mode = transposed
-// as in vcg_weight_prep: 0, 1 or 2 + pad for the pair-packed stem)
+// as in vcg_weight_prep: 0, 1 or 2 + pad for the pair-packed stem). Both GEMM layouts are transposes of the fp32
+// [Cout][Cin][KH][KW] weight, done through LDS so that reads and writes are both coalesced:
+//   mode 1 (dgrad B operand [Cin][KH][KW][Cout]): the [Cout][R = Cin KH KW] matrix transposed, 64 x 64 tiles;
+//   mode 0 ([Cout][KH][KW][Cpad]): per output channel, [Cin][T = KH KW] -> [T][Cpad] (zero pad), one row per unit.
+// (The per-element gather this replaces read the fp32 weight with a Cin KH KW stride: 338 us per step.)
+constexpr int WP_ROW_MAX = 4608;  // Cin * KH * KW of one output channel staged in LDS (18 KiB)
+
 __global__ __launch_bounds__(256) void weight_prep_multi_kernel(const long long* __restrict__ desc) {
+  __shared__ float tile[WP_ROW_MAX + 64];
   const long long* d = desc + 8 * blockIdx.y;
   const float* w = reinterpret_cast<const float*>(d[0]);
   bf16_t* out = reinterpret_cast<bf16_t*>(d[1]);
   const int Cout = (int)d[2], Cin = (int)d[3], KH = (int)d[4], KW = (int)d[5], Cpad = (int)d[6];
   const int mode = (int)d[7];
-  const bool tr = mode == 1;
-  int KWp = 0, pwp = 0;
-  if (mode >= 2) pair_geom(KW, mode - 2, KWp, pwp);
-  const int total = mode >= 2 ? Cout * KH * KWp * 8 : tr ? Cin * KH * KW * Cout : Cout * KH * KW * Cpad;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-    float v;
-    if (mode >= 2) {
-      v = pair_weight(w, i, Cin, KH, KW, mode - 2);
-    } else if (!tr) {
-      const int ci = i % Cpad;
-      int r = i / Cpad;
-      const int kw = r % KW; r /= KW;
-      const int kh = r % KH;
-      const int co = r / KH;
-      v = ci < Cin ? w[((co * Cin + ci) * KH + kh) * KW + kw] : 0.f;
-    } else {
-      const int co = i % Cout;
-      int r = i / Cout;
-      const int kw = r % KW; r /= KW;
-      const int kh = r % KH;
-      const int ci = r / KH;
-      v = w[((co * Cin + ci) * KH + kh) * KW + kw];
+  const int T = KH * KW, R = Cin * T;
+  const int tid = threadIdx.x;
+  if (mode >= 2 || (mode == 0 && R > WP_ROW_MAX)) {  // the pair-packed stem (and any oversized row): per element
+    int KWp = 0, pwp = 0;
+    if (mode >= 2) pair_geom(KW, mode - 2, KWp, pwp);
+    const int total = mode >= 2 ? Cout * KH * KWp * 8 : Cout * T * Cpad;
+    for (int i = blockIdx.x * 256 + tid; i < total; i += gridDim.x * 256) {
+      float v;
+      if (mode >= 2) {
+        v = pair_weight(w, i, Cin, KH, KW, mode - 2);
+      } else {
+        const int ci = i % Cpad, r = i / Cpad, t = r % T, co = r / T;
+        v = ci < Cin ? w[((long long)co * Cin + ci) * T + t] : 0.f;
+      }
+      out[i] = f2bf(v);
     }
-    out[i] = f2bf(v);
+    return;
+  }
+  if (mode == 1) {  // out[r][co] = w[co][r]
+    const int tr = (R + 63) / 64, tc = (Cout + 63) / 64;
+    const int tx = tid & 63, ty = tid >> 6;  // 64 x 4 threads
+    for (int tl = blockIdx.x; tl < tr * tc; tl += gridDim.x) {
+      const int r0 = (tl % tr) * 64, c0 = (tl / tr) * 64;
+      __syncthreads();
+#pragma unroll 4
+      for (int k = ty; k < 64; k += 4) {  // rows co = c0 + k, columns r0 + tx: coalesced reads
+        const int co = c0 + k, r = r0 + tx;
+        tile[k * 65 + tx] = (co < Cout && r < R) ? w[(long long)co * R + r] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int k = ty; k < 64; k += 4) {  // rows r = r0 + k, columns co = c0 + tx: coalesced writes
+        const int r = r0 + k, co = c0 + tx;
+        if (r < R && co < Cout) out[(long long)r * Cout + co] = f2bf(tile[tx * 65 + k]);
+      }
+    }
+    return;
+  }
+  // mode 0: out[co][t][ci] = w[co][ci][t] (ci < Cin), 0 for Cin <= ci < Cpad
+  const int orow = T * Cpad;
+  for (int co = blockIdx.x; co < Cout; co += gridDim.x) {
+    const float* src = w + (long long)co * R;
+    bf16_t* dst = out + (long long)co * orow;
+    if (T == 1) {
+      for (int ci = tid; ci < Cpad; ci += 256) dst[ci] = f2bf(ci < Cin ? src[ci] : 0.f);
+      continue;
+    }
+    __syncthreads();
+    for (int i = tid; i < R; i += 256) tile[i] = src[i];
+    __syncthreads();
+    for (int i = tid; i < orow; i += 256) {
+      const int t = i / Cpad, ci = i - t * Cpad;
+      dst[i] = f2bf(ci < Cin ? tile[ci * T + t] : 0.f);
+    }
   }
 }
 }  // namespace
@@ -576,7 +613,7 @@ VCG_API int vcg_weight_prep_multi(int dtype, const long long* desc, int n, hipSt
   VCG_REQUIRE(dtype == VCG_BF16, "the batched weight prep writes bf16 GEMM layouts");
   VCG_REQUIRE(n >= 0 && n <= 65535, "bad descriptor count");
   if (n == 0) return VCG_OK;
-  hipLaunchKernelGGL(weight_prep_multi_kernel, dim3(64, n), dim3(256), 0, s, desc);
+  hipLaunchKernelGGL(weight_prep_multi_kernel, dim3(128, n), dim3(256), 0, s, desc);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

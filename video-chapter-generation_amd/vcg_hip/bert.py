@@ -29,7 +29,7 @@ def _uniform_p(mods, what):
 
 
 class _LinearT:
-    """bf16 W^T [in][out] of the encoder's Linear weights (QKV, attention output, FFN1), the K-contiguous B operand
+    """bf16 W^T [in][out] of the encoder's Linear weights (QKV, attention output, FFN1, FFN2), the K-contiguous B operand
     of the backward's input-gradient GEMMs dX = dY W, written by ONE vcg_transpose_multi launch per weight generation
     (flat.generation moves with every optimizer step) instead of a transpose per GEMM (QKV, FFN1) or the generic
     engine's N-contiguous B path (attention output: 37 -> 24 us per layer)."""
@@ -43,7 +43,7 @@ class _LinearT:
             at = lyr.attention
             srcs.append(flat.compute_contiguous([at.self.query.weight, at.self.key.weight, at.self.value.weight],
                                                 (3 * H, H), dtype))
-            for w in (at.output.dense.weight, lyr.intermediate.dense.weight):
+            for w in (at.output.dense.weight, lyr.intermediate.dense.weight, lyr.output.dense.weight):
                 srcs.append(flat.compute_view(w, dtype))
         total = sum(s.numel() for s in srcs)
         dev = srcs[0].device
@@ -96,9 +96,8 @@ class BertEncoderEngine:
         (QKV, FFN1 input gradients: K = 2304 / 3072, N = 768): W^T is materialised (tiled transpose) so the
         LDS-DMA GEMM reads both operands K-contiguous (measured 87 -> 61 us at K = 3072, 67 -> 53 us at
         K = 2304; no gain at K = 768, tools/bench_bert_gemm.py)."""
-        # (the FFN2 input gradient's GELU' x residual epilogue stays on the generic engine: on the fast engine that
-        # epilogue is the unstaged per-fragment one, 123 vs 112 us, profiles/r03_final_gemm_breakdown.txt)
-        wt = self.wt.get(W) if self.wt is not None and kw.get("act") != ops.ACT_GELU_BWD else None
+        # (FFN2's input gradient: the fast engine's staged GELU' epilogue, the pre-activation read as full rows)
+        wt = self.wt.get(W) if self.wt is not None else None
         if wt is not None:
             return ops.gemm(A, wt, M, N, K, K, K, **kw)
         if self.dtype == torch.bfloat16 and K >= 2 * N:

@@ -466,6 +466,21 @@ def maxpool_bwd_bn_apply(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, g
     return dx
 
 
+def stem_bwd_fused(dy, idx, y, x, N, H, W, mean, invstd, mscale, mshift, gamma, sums, count, train_stats, dw,
+                   accumulate=True):
+    """The stem backward after the max-pool in one pass (bf16): maxpool_bwd_bn_apply's dy0 contracted with the
+    pair-packed frames x [N][2H][2W][4] into dw [64][3][7][7] (vcg_stem_bwd_fused; dy0 is never stored)."""
+    for t, n in ((dy, "dy"), (y, "y"), (x, "x")):
+        _chk(t, torch.bfloat16, n)
+    _chk(dw, torch.float32, "dw")
+    assert tuple(y.shape) == (N, H, W, 64) and tuple(x.shape) == (N, 2 * H, 2 * W, 4) and dw.numel() == 64 * 147
+    assert tuple(dy.shape) == (N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 64) and idx.shape == dy.shape
+    w = ws(_lib.query("vcg_stem_bwd_fused_ws_bytes"), dy.device)
+    _lib.call("vcg_stem_bwd_fused", P(dy), P(idx), P(y), P(x), N, H, W, P(mean), P(invstd), P(mscale), P(mshift),
+              P(gamma), P(sums[0]), P(sums[1]), int(count), int(bool(train_stats)), P(w), w.numel() * 4, P(dw),
+              int(bool(accumulate)), stream())
+
+
 def bn_relu_maxpool(y, scale, shift, N, H, W, C):
     """maxpool3x3/2(relu(y * scale + shift)) with the activation rounded to y's dtype (the values and argmax of
     bn_apply + maxpool_fwd, without the activation tensor). Returns (pooled, idx)."""

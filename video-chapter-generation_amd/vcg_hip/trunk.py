@@ -143,6 +143,9 @@ class ResNetTrunk:
     # the stem BN-backward sums from the pooled activation (ops.maxpool_bwd_bn_sums_pooled) instead of a pass over
     # the pre-pool conv output; False: the per-pixel pass (tests compare both)
     pooled_stem_sums = os.environ.get("VCG_POOLED_STEM_SUMS", "1") != "0"
+    # the stem's BN-backward apply and conv1 weight gradient as one pass (ops.stem_bwd_fused); False: the apply pass
+    # writes dy0 and the im2col weight-gradient GEMM reads it (tests compare both)
+    fused_stem_bwd = os.environ.get("VCG_FUSED_STEM_BWD", "1") != "0"
 
     def __init__(self, net, dtype):
         self.net = net
@@ -559,13 +562,28 @@ class ResNetTrunk:
         else:
             ops.maxpool_bwd_bn(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift, sums0, dg0, db0,
                                store_g=False)
-        dy0 = ops.maxpool_bwd_bn_apply(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift,
-                                       b0.bn.weight, sums0, N * H1 * W1, b0.mode != "running")
-        self._wgrad(self.net.conv1, xs, dy0, N, H, W, cpad)
+        conv1 = self.net.conv1
+        if self._stem_fused_ok(conv1, xs, N, H, W, cpad, H1, W1):
+            # the apply and the conv1 weight gradient in one pass: dy0 stays in LDS (ops.stem_bwd_fused)
+            ops.stem_bwd_fused(dout, idx, y0, xs, N, H1, W1, b0.mean, b0.invstd, b0.scale, b0.shift, b0.bn.weight,
+                               sums0, N * H1 * W1, b0.mode != "running", conv1.weight.grad)
+        else:
+            dy0 = ops.maxpool_bwd_bn_apply(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift,
+                                           b0.bn.weight, sums0, N * H1 * W1, b0.mode != "running")
+            self._wgrad(conv1, xs, dy0, N, H, W, cpad)
         self._report(hooks, list(self.net.conv1.parameters()) + list(self.net.bn1.parameters()))
         if self._ws is not None:  # every weight gradient is complete on the caller's stream
             torch.cuda.current_stream().wait_stream(self._ws)
             self._pending.clear()  # (later reuse of these blocks is ordered after the wait)
+
+    def _stem_fused_ok(self, conv1, xs, N, H, W, cpad, H1, W1):
+        """ops.stem_bwd_fused applies: bf16 pair-packed frames (C = 4), the 7x7 / 2 / pad 3 stem, even conv-output
+        height, width a multiple of 8 up to 112, a weight gradient to add to."""
+        w = conv1.weight
+        return (ResNetTrunk.fused_stem_bwd and self.dtype == torch.bfloat16 and cpad == 4 and w.requires_grad
+                and w.grad is not None and tuple(w.shape) == (64, 3, 7, 7) and conv1.stride == (2, 2)
+                and conv1.padding == (3, 3) and H == 2 * H1 and W == 2 * W1 and H1 % 2 == 0 and W1 % 8 == 0
+                and W1 <= 112)
 
     def _bn_grads(self, st):
         bn = st.bn
