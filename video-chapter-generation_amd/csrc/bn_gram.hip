@@ -210,15 +210,50 @@ __global__ __launch_bounds__(256) void bn_apply_gram_kernel(const bf16_t* __rest
   }
 }
 
-// out[i] = sum over nb slabs of slab[b][i] in slab order, in double (deterministic)
-__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ slab, int nb, int n,
+// out[i] = sum over nb slabs of slab[b][i], in double (deterministic): a thread owns 4 consecutive entries (16-B
+// loads) and G threads split the slabs (thread t sums slabs t, t + G, ... in order, the G partials are combined in
+// t order through LDS). (One thread per entry over all 256-512 slabs ran latency-bound: 100 us per call at C = 64.)
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ slab, int nb, int n, int G,
                                                          float* __restrict__ gram, float* __restrict__ colsum, int C) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += (double)slab[(long long)b * n + i];
-  if (i < C * C) gram[i] = (float)s;
-  else colsum[i - C * C] = (float)s;
+  __shared__ double red[4][256];
+  const int QB = 256 / G;
+  const int t = threadIdx.x / QB, ql = threadIdx.x - t * QB;
+  const int quad = blockIdx.x * QB + ql, nq = n >> 2;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (quad < nq) {
+    const float4* p = reinterpret_cast<const float4*>(slab) + quad;
+    int b = t;
+    for (; b + 3 * G < nb; b += 4 * G) {
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = p[(long long)(b + k * G) * nq];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s0 += (double)v[k].x; s1 += (double)v[k].y; s2 += (double)v[k].z; s3 += (double)v[k].w;
+      }
+    }
+    for (; b < nb; b += G) {
+      const float4 v = p[(long long)b * nq];
+      s0 += (double)v.x; s1 += (double)v.y; s2 += (double)v.z; s3 += (double)v.w;
+    }
+  }
+  if (G > 1) {
+    red[0][threadIdx.x] = s0; red[1][threadIdx.x] = s1; red[2][threadIdx.x] = s2; red[3][threadIdx.x] = s3;
+    __syncthreads();
+    if (t != 0) return;
+    for (int u = 1; u < G; ++u) {
+      const int o = u * QB + ql;
+      s0 += red[0][o]; s1 += red[1][o]; s2 += red[2][o]; s3 += red[3][o];
+    }
+  }
+  if (quad >= nq) return;
+  const double sv[4] = {s0, s1, s2, s3};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int i = 4 * quad + e;
+    if (i < C * C) gram[i] = (float)sv[e];
+    else colsum[i - C * C] = (float)sv[e];
+  }
 }
 
 // bn3's batch statistics from (G, colsum) and conv3's bf16 weights w [N][C]: 8 output columns per workgroup,
@@ -314,7 +349,11 @@ VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* sh
     hipLaunchKernelGGL(bn_apply_gram_kernel<256>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
                        (bf16_t*)out, ws, P);
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ws, g, (int)n, gram,
+  const int nq = (int)(n / 4);  // (n = C (C + 1), C a power of two >= 64: a multiple of 4)
+  int G = 1;
+  while (G < 64 && G * 2 <= g && (long long)nq * G < 65536) G *= 2;
+  const int QB = 256 / G;
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((nq + QB - 1) / QB)), dim3(256), 0, s, ws, g, (int)n, G, gram,
                      colsum, C);
   VCG_LAUNCH_CHECK();
   return VCG_OK;

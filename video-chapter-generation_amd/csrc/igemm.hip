@@ -445,44 +445,25 @@ static int run_gemm(GemmParams& p, int epi, int splits, hipStream_t s) {
 }
 
 // split-K reduction: out[m][n] (+)= sum_s ws[s][m][n], with optional conv-weight layout permutation.
-// G threads per output element (G = 1 for big outputs; G = 8 when there are too few outputs to fill the chip, the
-// weight gradients' 4-64 K-element slabs): thread t of a group sums slabs t, t + G, t + 2G, ... in order (8
-// independent loads in flight), the G partials are combined by a fixed xor-shuffle tree -- deterministic.
-template <int G>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long MN,
-                                                            int N, float* __restrict__ out, int accumulate,
-                                                            int conv_perm, int KH, int KW, int Cpad, int Cin,
-                                                            float scale, int KWp, int pwp, int pad) {
-  const long long gid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  const long long idx = gid / G;
-  const int t = (int)(gid - idx * G);
-  if (idx >= MN) return;  // (whole groups: MN * G threads, blockDim a multiple of G)
-  float v = 0.f;
-  const float* p = ws + idx;
-  int s = t;
-  for (; s + 7 * G < splits; s += 8 * G) {
-    float a[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] = p[(long long)(s + k * G) * MN];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v += a[k];
-  }
-  for (; s < splits; s += G) v += p[(long long)s * MN];
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (t != 0) return;
-  v *= scale;
-  long long dst = idx;
+// A thread owns 4 consecutive outputs (16-B loads: the slabs stream at HBM rate) and G threads share them when there
+// are too few outputs to fill the chip (the weight gradients' 16 K - 2 M-element slabs x 8-512 splits): thread t of
+// a group sums slabs t, t + G, ... in order, 4 loads in flight, and the G partials are combined in t order through
+// LDS -- deterministic. The threads of one t read consecutive quads: every slab read is contiguous.
+// (The first version, 4-B loads and G lanes of one wave per output on 8 different slabs, ran the ~120 reductions of
+// a train step at ~1 TB/s: 5 ms/step.)
+__device__ __forceinline__ long long splitk_dst(long long idx, int N, int conv_perm, int KH, int KW, int Cpad, int Cin,
+                                                int KWp, int pwp, int pad) {
   if (conv_perm == 1) {
     // idx = m * N + n, m = cout, n = (kh*KW + kw)*Cpad + ci  ->  OIHW [cout][ci][kh][kw]  (MN < 2^31)
     const int m = (int)idx / N;
     const int n = (int)idx - m * N;
     const int tap = n / Cpad;
     const int ci = n - tap * Cpad;
-    if (ci >= Cin) return;
+    if (ci >= Cin) return -1;
     const int kh = tap / KW, kw = tap - kh * KW;
-    dst = (((long long)m * Cin + ci) * KH + kh) * KW + kw;
-  } else if (conv_perm == 2) {
+    return (((long long)m * Cin + ci) * KH + kh) * KW + kw;
+  }
+  if (conv_perm == 2) {
     // pair-packed stem: n = (kh*KWp + kwp)*8 + 4j + ci, tap kw = 2 (kwp - pwp) + j + pad (outside the kernel:
     // the GEMM's zero-weight half of an edge pair, dropped)
     const int m = (int)idx / N;
@@ -490,9 +471,81 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     const int tap = n >> 3, j = (n >> 2) & 1, ci = n & 3;
     const int kh = tap / KWp, kwp = tap - kh * KWp;
     const int kw = 2 * (kwp - pwp) + j + pad;
-    if (ci >= Cin || kw < 0 || kw >= KW) return;
-    dst = (((long long)m * Cin + ci) * KH + kh) * KW + kw;
+    if (ci >= Cin || kw < 0 || kw >= KW) return -1;
+    return (((long long)m * Cin + ci) * KH + kh) * KW + kw;
   }
+  return idx;
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, long long MN,
+                                                            int G, int N, float* __restrict__ out, int accumulate,
+                                                            int conv_perm, int KH, int KW, int Cpad, int Cin,
+                                                            float scale, int KWp, int pwp, int pad) {
+  __shared__ float4 red[256];
+  const int QB = 256 / G;  // quads per block
+  const int t = threadIdx.x / QB, ql = threadIdx.x - t * QB;
+  const long long quad = (long long)blockIdx.x * QB + ql;
+  const long long nq = MN >> 2;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (quad < nq) {
+    const float4* p = reinterpret_cast<const float4*>(ws) + quad;
+    int s = t;
+    for (; s + 3 * G < splits; s += 4 * G) {
+      float4 a[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = p[(long long)(s + k * G) * nq];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v.x += a[k].x; v.y += a[k].y; v.z += a[k].z; v.w += a[k].w;
+      }
+    }
+    for (; s < splits; s += G) {
+      const float4 a = p[(long long)s * nq];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+  }
+  if (G > 1) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    if (t != 0) return;
+    for (int u = 1; u < G; ++u) {
+      const float4 a = red[u * QB + ql];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+  }
+  if (quad >= nq) return;
+  const float r[4] = {v.x * scale, v.y * scale, v.z * scale, v.w * scale};
+  if (conv_perm == 0) {
+    float4* o = reinterpret_cast<float4*>(out) + quad;
+    if (accumulate) {
+      const float4 c = *o;
+      *o = make_float4(c.x + r[0], c.y + r[1], c.z + r[2], c.w + r[3]);
+    } else {
+      *o = make_float4(r[0], r[1], r[2], r[3]);
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long long dst = splitk_dst(4 * quad + e, N, conv_perm, KH, KW, Cpad, Cin, KWp, pwp, pad);
+    if (dst < 0) continue;
+    if (accumulate) out[dst] += r[e];
+    else out[dst] = r[e];
+  }
+}
+
+// scalar fallback (MN or a pointer not 16-B aligned): one thread per output, slabs in order
+__global__ __launch_bounds__(256) void splitk_reduce1_kernel(const float* __restrict__ ws, int splits, long long MN,
+                                                             int N, float* __restrict__ out, int accumulate,
+                                                             int conv_perm, int KH, int KW, int Cpad, int Cin,
+                                                             float scale, int KWp, int pwp, int pad) {
+  const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (idx >= MN) return;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += ws[(long long)s * MN + idx];
+  v *= scale;
+  const long long dst = splitk_dst(idx, N, conv_perm, KH, KW, Cpad, Cin, KWp, pwp, pad);
+  if (dst < 0) return;
   if (accumulate) out[dst] += v;
   else out[dst] = v;
 }
@@ -500,17 +553,35 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 static void splitk_reduce(hipStream_t stream, const float* ws, int splits, long long MN, int N, float* out,
                           int accumulate, int conv_perm, int KH, int KW, int Cpad, int Cin, float scale, int KWp,
                           int pwp, int pad) {
-  if ((MN + 255) / 256 < 1024 && splits >= 16)
-    hipLaunchKernelGGL(splitk_reduce_kernel<8>, dim3((unsigned)((MN * 8 + 255) / 256)), dim3(256), 0, stream, ws,
-                       splits, MN, N, out, accumulate, conv_perm, KH, KW, Cpad, Cin, scale, KWp, pwp, pad);
-  else
-    hipLaunchKernelGGL(splitk_reduce_kernel<1>, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws,
-                       splits, MN, N, out, accumulate, conv_perm, KH, KW, Cpad, Cin, scale, KWp, pwp, pad);
+  const bool vec = (MN & 3) == 0 && (((uintptr_t)ws | (conv_perm ? 0 : (uintptr_t)out)) & 15) == 0;
+  if (!vec) {
+    hipLaunchKernelGGL(splitk_reduce1_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, stream, ws, splits,
+                       MN, N, out, accumulate, conv_perm, KH, KW, Cpad, Cin, scale, KWp, pwp, pad);
+    return;
+  }
+  // G: enough threads for the chip (~256 K) without more groups than slabs
+  const long long nq = MN >> 2;
+  int G = 1;
+  while (G < 64 && G * 2 <= splits && nq * G < 262144) G *= 2;
+  const int QB = 256 / G;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nq + QB - 1) / QB)), dim3(256), 0, stream, ws, splits, MN,
+                     G, N, out, accumulate, conv_perm, KH, KW, Cpad, Cin, scale, KWp, pwp, pad);
+}
+
+// Split-K target: tiles x splits ~ this many workgroups (VCG_SPLITK_WG, read once; default 1024 = 2 rounds of 2
+// workgroups per CU). Fewer splits write and re-read fewer fp32 slabs.
+static int splitk_target() {
+  static int t = 0;
+  if (t == 0) {
+    const char* e = getenv("VCG_SPLITK_WG");
+    t = e && atoi(e) > 0 ? atoi(e) : 1024;
+  }
+  return t;
 }
 
 static int choose_splits(int M, int N, int K, int BK) {
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  int splits = (1024 + tiles - 1) / tiles;
+  int splits = (splitk_target() + tiles - 1) / tiles;
   const int max_splits = (K + 16 * BK - 1) / (16 * BK);  // at least 16 k-tiles per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -828,7 +899,7 @@ static void wgrad_geometry(int dtype, int N, int H, int W, int C, int Cout, int 
     BK = 64;
     const int tiles = ((*Nn + wgrad_fast_tile_n(*Nn) - 1) / wgrad_fast_tile_n(*Nn)) *
                       ((*M + wgrad_fast_tile_m(*M) - 1) / wgrad_fast_tile_m(*M));
-    sp = (1024 + tiles - 1) / tiles;
+    sp = (splitk_target() + tiles - 1) / tiles;
     const int max_sp = (*K + 8 * BK - 1) / (8 * BK);  // at least 8 k-steps (512 pixels) per split
     sp = sp > max_sp ? max_sp : sp;
     sp = sp < 1 ? 1 : sp;

@@ -1339,8 +1339,13 @@ static bool bwd_light(const GemmParams& p) {
 // DG (dgrad): dx pixel (y, x) reads dy (y + 1 - kh, x + 1 - kw), the flipped tap map over the same patch.
 // Measured history (trunk shape M = 1024 x 56 x 56): B through a 2-stage LDS ring with a barrier per tap 586 us
 // fwd (im2col: 451-495); register B at 2 workgroups per CU spills (256 VGPRs) and lost to im2col.
-constexpr int PATCH_MAXPIX = 232;               // (R + 2)(W + 2) <= 232 pixels: 29 KiB per patch buffer
+constexpr int PATCH_MAXPIX = 256;               // (R + 2) PW <= 256 pixels: 32 KiB per patch buffer
 constexpr int PATCH_SLICES = PATCH_MAXPIX / 8;  // 1-KiB (8-pixel) LDS-DMA slices per patch
+// Patch rows have a fixed pitch PW (32 or 64 pixels >= W + 2; the kernel's template parameter): the chunk swizzle
+// depends on the pixel index mod 8 only, so a tap's row offset kh * PW moves a fragment address by a compile-time
+// constant (the ds_read offset field) and a lane's 12 fragment addresses per tile (4 row blocks x 3 column taps) are
+// computed once per tile. (With PW = W + 2 every fragment read of the 144-MFMA tile loop recomputed its swizzled
+// address -- ~5 VALU per read, more vector issue than the MFMAs leave: the MFMA phase ran at 2.45x its issue time.)
 constexpr int PATCH_RING = 3;
 
 struct PatchGeom {
@@ -1363,9 +1368,12 @@ __device__ __forceinline__ s16x8 patch_frag(const bf16_t* P, int pix, int lane, 
   return *reinterpret_cast<const s16x8*>(P + pix * 64 + 8 * pswz(pix, 4 * s2 + (lane >> 4)));
 }
 
-template <int EPI, bool DG>
+typedef __attribute__((address_space(3))) const char patch_lds_t;
+
+template <int EPI, bool DG, int PW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void conv3x3_patch_kernel(GemmParams p, PatchGeom g) {
+  static_assert(PW == 32 || PW == 64, "patch row pitch");
   constexpr int BM = 128, BN = 64, NW = 4, MT = 4, NT = 2;
   constexpr int PE = PATCH_SLICES * 512;  // elements per patch buffer
   constexpr int YE = 128 * 64;            // elements per y tile (EPI_BWD_AFF)
@@ -1417,7 +1425,7 @@ void conv3x3_patch_kernel(GemmParams p, PatchGeom g) {
       bf16_t* dst = Ps + (lt % PATCH_RING) * PE;
       const int slice = min(wave + NW * q, g.NS - 1);
       const int pix = 8 * slice + (lane >> 3);
-      const int pr = pix / g.PW, pc = pix - pr * g.PW;
+      const int pr = pix / PW, pc = pix % PW;
       const int h = h0 - 1 + pr, w = pc - 1;
       const bool ok = pix < g.NP && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
       const int csrc = ((lane & 7) - (pix & ~1)) & 7;  // pswz(pix, csrc) == lane & 7
@@ -1443,7 +1451,7 @@ void conv3x3_patch_kernel(GemmParams p, PatchGeom g) {
   for (int i = 0; i < MT; ++i) {
     const int ml = wm * 64 + i * 16 + (lane & 15);
     const int r = ml / a.W, w = ml - r * a.W;
-    rowpix[i] = ml < g.TM ? r * g.PW + w : 0;
+    rowpix[i] = ml < g.TM ? r * PW + w : 0;
   }
   // B fragment (tap t, k-step s2, column group j): row n0 + wn*32 + 16j + lane%16, k = 64t + 32 s2 + 8 (lane/16)
   s16x8 breg[9][2][NT];
@@ -1550,11 +1558,24 @@ void conv3x3_patch_kernel(GemmParams p, PatchGeom g) {
     // 18 units (tap t = u / 2, k-step u % 2) of 4 fragment reads + 8 MFMAs, reads issued two units ahead (a ring
     // of 3 fragment sets; the scheduler barriers keep hipcc from regrouping them into read-wait-MFMA pairs, whose
     // exposed LDS latency made the first build of this loop 4x slower than its MFMA time)
+    // fragment addresses of this tile: column tap c (= kw, dgrad 2 - kw), k-step s2; row taps add kh' PW pixels
+    uint32_t fa[MT][3][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int pix = rowpix[i] + c;
+        const uint32_t a0 = lds_u32(P + pix * 64 + 8 * pswz(pix, lane >> 4));
+        fa[i][c][0] = a0;
+        fa[i][c][1] = a0 ^ 64u;  // chunk + 4: slot (c + 4 + x) & 7 = ((c + x) & 7) ^ 4
+      }
     auto unit_reads = [&](s16x8 (&f)[MT], int u) {
       const int t = u >> 1, kh = t / 3, kw = t - 3 * (t / 3);
-      const int toff = DG ? (2 - kh) * g.PW + (2 - kw) : kh * g.PW + kw;
+      const int rh = DG ? 2 - kh : kh, cw = DG ? 2 - kw : kw;
 #pragma unroll
-      for (int i = 0; i < MT; ++i) f[i] = patch_frag(P, rowpix[i] + toff, lane, u & 1);
+      for (int i = 0; i < MT; ++i)
+        f[i] = *reinterpret_cast<const __attribute__((address_space(3))) s16x8*>(
+            (patch_lds_t*)(uintptr_t)fa[i][cw][u & 1] + rh * PW * 128);
     };
     s16x8 af[3][MT];
     unit_reads(af[0], 0);
@@ -1822,6 +1843,9 @@ static StemGeom stem_geom(const GemmParams& p, int R) {
   return g;
 }
 
+// Patch row pitch in pixels (the kernel's PW): 32 or 64 >= W + 2 (the two zero border columns)
+static int patch_pitch(int W) { return W + 2 <= 32 ? 32 : 64; }
+
 // Rows per patch tile (0: the patch kernel does not apply). VCG_NO_PATCH=1 keeps these convs on the im2col path.
 static int patch_rows(const GemmParams& p, int amode) {
   const char* e = getenv("VCG_NO_PATCH");  // read per call: a test compares both paths in one process
@@ -1829,11 +1853,11 @@ static int patch_rows(const GemmParams& p, int amode) {
   const OpArgs& a = p.a;
   if (off || (amode != OP_IM2COL && amode != OP_DGRAD) || a.C != 64 || a.KH != 3 || a.KW != 3 || a.stride != 1 ||
       a.pad != 1 || a.tsm_fold != 0 || a.tKW != 0 || a.sw != 0 || a.GH != a.H || a.GW != a.W || p.N % 64 != 0 ||
-      p.K != 9 * 64 || p.batch_inner > 0 || p.residual || p.aux || p.bias || p.act != ACT_NONE || a.W > 128 ||
+      p.K != 9 * 64 || p.batch_inner > 0 || p.residual || p.aux || p.bias || p.act != ACT_NONE || a.W + 2 > 64 ||
       !bwd_light(p) || p.bwd.nred > 2)
     return 0;
   for (int R = min(a.H, 128 / a.W); R >= 1; --R)
-    if (a.H % R == 0 && (R + 2) * (a.W + 2) <= PATCH_MAXPIX) return R;
+    if (a.H % R == 0 && (R + 2) * patch_pitch(a.W) <= PATCH_MAXPIX) return R;
   return 0;
 }
 
@@ -1842,7 +1866,7 @@ static PatchGeom patch_geom(const GemmParams& p, int R) {
   g.R = R;
   g.TM = R * p.a.W;
   g.TPI = p.a.H / R;
-  g.PW = p.a.W + 2;
+  g.PW = patch_pitch(p.a.W);
   g.NP = (R + 2) * g.PW;
   g.NS = (g.NP + 7) / 8;
   return g;
@@ -1950,7 +1974,7 @@ static int fast_bn(const GemmParams& p, int z, hipStream_t s) {
 
 static unsigned long long* g_patch_stamps = nullptr;
 
-template <int EPI, bool DG>
+template <int EPI, bool DG, int PW>
 static int launch_patch(const GemmParams& p, int R, hipStream_t s) {
   const PatchGeom g = patch_geom(p, R);
   const int gy = patch_grid_rows(p, g);
@@ -1961,7 +1985,7 @@ static int launch_patch(const GemmParams& p, int R, hipStream_t s) {
     if (!g_patch_stamps && hipMalloc(&g_patch_stamps, 64 * 6 * 8) != hipSuccess) g_patch_stamps = nullptr;
     gs.stamps = g_patch_stamps;
   }
-  hipLaunchKernelGGL((conv3x3_patch_kernel<EPI, DG>), dim3((p.N / 64) * gy), dim3(256), 0, s, p, gs);
+  hipLaunchKernelGGL((conv3x3_patch_kernel<EPI, DG, PW>), dim3((p.N / 64) * gy), dim3(256), 0, s, p, gs);
   timing_end(tk, s, TIMING_PATCH_CONV, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_IM2COL, EPI, false>(p, 1));
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -2002,13 +2026,19 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   if (z == 1) {
     const int R = patch_rows(p, amode);
     if (R > 0) {
+      const bool w64 = patch_pitch(p.a.W) == 64;
       if (amode == OP_DGRAD) {
-        if (epi == EPI_BWD) return launch_patch<EPI_BWD_AFF, true>(p, R, s);  // (patch_rows: light epilogues only)
-        if (epi == EPI_STATS) return launch_patch<EPI_STATS, true>(p, R, s);
-        if (epi == EPI_STORE) return launch_patch<EPI_STORE, true>(p, R, s);
+        if (epi == EPI_BWD)  // (patch_rows: light epilogues only)
+          return w64 ? launch_patch<EPI_BWD_AFF, true, 64>(p, R, s) : launch_patch<EPI_BWD_AFF, true, 32>(p, R, s);
+        if (epi == EPI_STATS)
+          return w64 ? launch_patch<EPI_STATS, true, 64>(p, R, s) : launch_patch<EPI_STATS, true, 32>(p, R, s);
+        if (epi == EPI_STORE)
+          return w64 ? launch_patch<EPI_STORE, true, 64>(p, R, s) : launch_patch<EPI_STORE, true, 32>(p, R, s);
       } else {
-        if (epi == EPI_STATS) return launch_patch<EPI_STATS, false>(p, R, s);
-        if (epi == EPI_STORE) return launch_patch<EPI_STORE, false>(p, R, s);
+        if (epi == EPI_STATS)
+          return w64 ? launch_patch<EPI_STATS, false, 64>(p, R, s) : launch_patch<EPI_STATS, false, 32>(p, R, s);
+        if (epi == EPI_STORE)
+          return w64 ? launch_patch<EPI_STORE, false, 64>(p, R, s) : launch_patch<EPI_STORE, false, 32>(p, R, s);
       }
     }
   }

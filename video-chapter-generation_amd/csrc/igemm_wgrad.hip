@@ -302,10 +302,14 @@ struct WPatchGeom {
 
 __device__ __forceinline__ int wp_swz(int row, int c) { return c ^ (2 * ((row >> 1) & 3)); }  // = wswz<64>
 
-__device__ __forceinline__ void tr_read(s16x4& v, const bf16_t* p) {
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+template <int OFF> __device__ __forceinline__ void tr_read_at(s16x4& v, uint32_t addr) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
 }
 
+// Patch rows at a fixed pitch PW (32 / 64 pixels >= W + 2, as conv3x3_patch_kernel): the swizzle depends on the
+// pixel row index mod 8, so a tap's row offset kh * PW is an immediate of the transposed read and the lane's
+// addresses (8 dy^T + 6 patch per k-step) are computed once per tile instead of per read.
+template <int PW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ ws,
                            uint32_t xbytes, uint32_t dybytes, WPatchGeom g) {
@@ -331,7 +335,7 @@ void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restric
     for (int q8 = 0; q8 < 8; ++q8) {
       const int slice = min(wave + 4 * q8, g.NS - 1);
       const int pix = 8 * slice + (lane >> 3);
-      const int pr = pix / g.PW, pc = pix - pr * g.PW;
+      const int pr = pix / PW, pc = pix % PW;
       const int h = h0 - 1 + pr, w = pc - 1;
       const bool ok = pix < g.NP && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       const int c = wp_swz(pix, lane & 7);
@@ -356,7 +360,7 @@ void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restric
     for (int hh = 0; hh < 2; ++hh) {
       const int k = 32 * st + 4 * lg + q + 16 * hh;
       const int r = k / g.W, xx = k - r * g.W;
-      kpix[st][hh] = k < g.TM ? r * g.PW + xx : 0;
+      kpix[st][hh] = k < g.TM ? r * PW + xx : 0;
     }
 
   f32x4 acc[4][9];
@@ -378,18 +382,32 @@ void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restric
     s16x4 al[2][4], ah[2][4], bl[2][9], bh[2][9];
     auto reads = [&](int st, int b) {
       const int k0 = 32 * st + 4 * lg + q, k1 = k0 + 16;
+      uint32_t ya[4][2], pa[3][2];  // (the same per tile: the compiler keeps them across the k-steps' reads)
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         const int cl = 16 * ct + 4 * pp;
-        tr_read(al[b][ct], Y + k0 * 64 + 8 * wp_swz(k0, cl >> 3) + (cl & 7));
-        tr_read(ah[b][ct], Y + k1 * 64 + 8 * wp_swz(k1, cl >> 3) + (cl & 7));
+        ya[ct][0] = lds_addr(Y + k0 * 64 + 8 * wp_swz(k0, cl >> 3) + (cl & 7));
+        ya[ct][1] = lds_addr(Y + k1 * 64 + 8 * wp_swz(k1, cl >> 3) + (cl & 7));
       }
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int toff = (t / 3) * g.PW + (t % 3);
-        const int p0 = kpix[st][0] + toff, p1 = kpix[st][1] + toff;
-        tr_read(bl[b][t], P + p0 * 64 + 8 * wp_swz(p0, cb >> 3) + (cb & 7));
-        tr_read(bh[b][t], P + p1 * 64 + 8 * wp_swz(p1, cb >> 3) + (cb & 7));
+      for (int kw = 0; kw < 3; ++kw) {
+        const int p0 = kpix[st][0] + kw, p1 = kpix[st][1] + kw;
+        pa[kw][0] = lds_addr(P + p0 * 64 + 8 * wp_swz(p0, cb >> 3) + (cb & 7));
+        pa[kw][1] = lds_addr(P + p1 * 64 + 8 * wp_swz(p1, cb >> 3) + (cb & 7));
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        tr_read_at<0>(al[b][ct], ya[ct][0]);
+        tr_read_at<0>(ah[b][ct], ya[ct][1]);
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {  // tap t = 3 kh + kw: + kh PW pixels = kh PW 128 bytes
+        tr_read_at<0>(bl[b][kw], pa[kw][0]);
+        tr_read_at<0>(bh[b][kw], pa[kw][1]);
+        tr_read_at<PW * 128>(bl[b][3 + kw], pa[kw][0]);
+        tr_read_at<PW * 128>(bh[b][3 + kw], pa[kw][1]);
+        tr_read_at<2 * PW * 128>(bl[b][6 + kw], pa[kw][0]);
+        tr_read_at<2 * PW * 128>(bh[b][6 + kw], pa[kw][1]);
       }
     };
     reads(0, 0);
@@ -453,8 +471,10 @@ int wgrad_patch_rows(int dtype, int H, int W, int C, int Cin, int Cout, int KH, 
   if (!en || dtype != VCG_BF16 || C != 64 || Cin != 64 || Cout != 64 || KH != 3 || KW != 3 || stride != 1 ||
       pad != 1 || tsm_fold != 0)
     return 0;
+  if (W + 2 > 64) return 0;
+  const int pw = W + 2 <= 32 ? 32 : 64;
   for (int R = 128 / W; R >= 1; --R)
-    if ((R + 2) * (W + 2) <= 8 * WP_SL && H % R == 0) return R;
+    if ((R + 2) * pw <= 8 * WP_SL && H % R == 0) return R;
   return 0;
 }
 
@@ -463,13 +483,18 @@ int wgrad_patch_splits() { return WP_GRID; }
 // x: NHWC [N][H][W][64] bf16, dy: [N][H][W][64] bf16 -> WP_GRID fp32 slabs [64][576] in ws
 int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int W, int R, hipStream_t s) {
   WPatchGeom g;
-  g.H = H; g.W = W; g.R = R; g.TM = R * W; g.PW = W + 2; g.NP = (R + 2) * (W + 2); g.NS = (g.NP + 7) / 8;
+  const int pw = W + 2 <= 32 ? 32 : 64;
+  g.H = H; g.W = W; g.R = R; g.TM = R * W; g.PW = pw; g.NP = (R + 2) * pw; g.NS = (g.NP + 7) / 8;
   g.TPI = H / R; g.tiles = N * g.TPI;
   const long long xb = (long long)N * H * W * 64 * 2;
   VCG_REQUIRE(xb < 0xFFFFFF00LL, "wgrad patch: x / dy must be below 4 GB");
   const int tk = timing_begin(s);
-  hipLaunchKernelGGL(wgrad3x3_patch_kernel, dim3(WP_GRID), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dy, ws,
-                     (uint32_t)xb, (uint32_t)xb, g);
+  if (pw == 64)
+    hipLaunchKernelGGL(wgrad3x3_patch_kernel<64>, dim3(WP_GRID), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dy,
+                       ws, (uint32_t)xb, (uint32_t)xb, g);
+  else
+    hipLaunchKernelGGL(wgrad3x3_patch_kernel<32>, dim3(WP_GRID), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dy,
+                       ws, (uint32_t)xb, (uint32_t)xb, g);
   timing_end(tk, s, TIMING_WGRAD, 2.0 * 64 * 576 * (double)N * H * W, 2.0 * (double)xb + 4.0 * 64 * 576);
   VCG_LAUNCH_CHECK();
   return VCG_OK;

@@ -15,10 +15,10 @@
 //            (igemm.hip pair_taps: K = 7 x 4 x 8 = 224), both operands read with ds_read_b64_tr_b16 (4
 //            consecutive pixels per lane); v_mfma_f32_16x16x32_bf16, 8 waves = 4 channel tiles x 2 halves of the
 //            14 n-tiles, fp32 accumulators for the whole range.
-// Two LDS buffers: tile t + 1's phase 1 writes the other buffer while slower waves still read tile t, so one barrier
-// per tile; tile t + 1's global loads are issued into registers before tile t's MFMAs. Each workgroup writes its
-// [64][224] fp32 slab; stem_wgrad_reduce_kernel sums the slabs in a fixed order (deterministic) into the OIHW
-// weight gradient.
+// Every operand of a tile arrives by LDS-DMA into one of two slots, issued a whole tile ahead (both phases of the
+// current tile cover its latency; the first version loaded the next tile into registers under the MFMA phase only
+// and ran latency-bound at 1.43 ms). Each workgroup writes its [64][224] fp32 slab; stem_wgrad_reduce_kernel sums
+// the slabs in a fixed order (deterministic) into the OIHW weight gradient.
 #include "igemm.h"
 
 namespace vcg {
@@ -30,9 +30,32 @@ constexpr int SB_N = 224;      // pair-packed 7x7 taps: 7 rows x 4 super pixels 
 constexpr int SB_MAXW = 112;   // conv-output width (the tile's 2W pixels are the MFMA k)
 
 typedef __attribute__((address_space(3))) char sb_lds_char;
+typedef __attribute__((address_space(3))) void lds_void_t;
 __device__ __forceinline__ uint32_t sb_addr(const bf16_t* p) { return (uint32_t)(uintptr_t)(const sb_lds_char*)p; }
 __device__ __forceinline__ void sb_tr(s16x4& v, const bf16_t* p) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(sb_addr(p)) : "memory");
+}
+// phase 1's LDS accesses are inline asm too: a plain LDS load while the next tile's LDS-DMA is in flight makes the
+// compiler drain that DMA (vmcnt(0)) first -- the overlap this kernel is built on. Ordering is explicit instead.
+typedef unsigned int sb_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int sb_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 sb_ld16(const void* p) {
+  sb_u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(sb_addr(reinterpret_cast<const bf16_t*>(p))) : "memory");
+  return uint4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ uint2 sb_ld8(const void* p) {
+  sb_u32x2 v;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(sb_addr(reinterpret_cast<const bf16_t*>(p))) : "memory");
+  return uint2{v[0], v[1]};
+}
+__device__ __forceinline__ void sb_st16(void* p, uint4 u) {
+  const sb_u32x4 v = {u.x, u.y, u.z, u.w};
+  asm volatile("ds_write_b128 %0, %1" : : "v"(sb_addr(reinterpret_cast<const bf16_t*>(p))), "v"(v) : "memory");
+}
+__device__ __forceinline__ void sb_lgkm0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 __device__ __forceinline__ s16x8 sb_cat(const s16x4& lo, const s16x4& hi) {
   return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -53,18 +76,21 @@ struct StemBwdArgs {
   int N, H, W, OH, OW, tiles;
 };
 
-struct SbRegs {  // one phase-1 item (block column j, chunk c8) and this thread's super-pixel chunks
-  uint4 g[4];
-  uint2 w[4];
-  uint4 yv[4];
-  uint4 xp[3];
-};
+// LDS slot of one tile, filled by LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction) one tile ahead:
+//   Y: the conv-output rows 2k, 2k + 1 [2W][64] bf16 in the transposed-read swizzle (sb_swz, pre-applied on the
+//      source side), overwritten in place by dy0 in phase 1 (a thread reads and writes the same pixels and chunk);
+//   D / I: pooled gradient rows k, k + 1 [2][OW][64] bf16 and their argmax bytes [2][OW][64];
+//   P: the 9 input rows of the patch, [9][W + 4] super pixels (zeros outside the frame, from the DMA range check).
+constexpr int SB_YB = 2 * SB_MAXW * 128;                       // 28 KiB
+constexpr int SB_DB = 2 * (SB_MAXW / 2) * 128;                 // 14 KiB
+constexpr int SB_IB = 2 * (SB_MAXW / 2) * 64;                  // 7 KiB
+constexpr int SB_PI = (9 * (SB_MAXW + 4) * 16 + 1023) / 1024;  // patch DMA instructions (17)
+constexpr int SB_PB = SB_PI * 1024;
+constexpr int SB_SLOT = SB_YB + SB_DB + SB_IB + SB_PB;         // 66 KiB
 
 __global__ __launch_bounds__(SB_NTH) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_bwd_fused_kernel(StemBwdArgs a) {
-  constexpr int DYE = 2 * SB_MAXW * 64;        // dy0 tile elements
-  constexpr int PE = 9 * (SB_MAXW + 4) * 8;    // patch elements: 9 rows x (W + 4) super pixels
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (DYE + PE)];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SB_SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lg = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   const int wm = wave & 3, wn = wave >> 2;   // channels 16 wm .., n-tiles 7 wn .. 7 wn + 6
@@ -78,10 +104,19 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
   const int nitems = (W / 2) * 8;
   const int c8 = tid & 7, jj = tid >> 3;     // phase-1 item (fixed chunk per thread)
   const bool item = tid < nitems;
-  const int npch = 9 * SPW;                  // super-pixel chunks per patch
+  const int nY = 2 * W / 8, nD = OW / 4, nI = (OW + 7) / 8, nP = (9 * SPW + 63) / 64;
+  const int nDMA = nY + nD + nI + nP;
+
+  const uint32_t ybytes = (uint32_t)min((long long)a.N * H * W * 128, (long long)0xFFFFFF00LL);
+  const uint32_t dbytes = (uint32_t)((long long)a.N * OH * OW * 128);
+  const uint32_t ibytes = (uint32_t)((long long)a.N * OH * OW * 64);
+  const uint32_t xbytes = (uint32_t)((long long)a.N * HI * W * 16);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.y), 0, ybytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.dy), 0, dbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.idx), 0, ibytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.x), 0, xbytes, 0x00020000);
 
   // bn_bwd_apply's per-channel map (maxpool_bwd2_kernel MP_APPLY, same arithmetic) in LDS: [sc, sh, A, Bc, Cc][64]
-  // (read per item: registers go to the accumulators, fragments and the next tile's loads)
   __shared__ __attribute__((aligned(16))) float prm[5][64];
   if (tid < 64) {
     const int c = tid;
@@ -94,123 +129,145 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
     prm[3][c] = Bc;
     prm[4][c] = -A * a.sum_g[c] * a.inv_count - Bc * a.mean[c];
   }
-  __syncthreads();
+  const int ksteps = (2 * W + 31) / 32;  // k = the tile's 2W pixels, padded to 32 with zero dy0 rows
+  for (int i = 2 * W * 8 + tid; i < ksteps * 32 * 8; i += SB_NTH)  // (the pad rows of both slots, never DMA'd)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) *reinterpret_cast<uint4*>(smem + b * SB_SLOT + 16 * i) = uint4{0u, 0u, 0u, 0u};
 
-  SbRegs r;
-  auto load = [&](int lt) {
+  // tile lt's DMAs into slot lt & 1: instruction i = wave, wave + 8, ... of Y | D | I | P
+  auto issue = [&](int lt) {
     const int tg = t0 + lt, n = tg / TPI, k = tg - n * TPI;
-    if (item) {
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int oh = min(k + (qq >> 1), OH - 1), ow = min(jj + (qq & 1), OW - 1);
-        const long long o = (((long long)n * OH + oh) * OW + ow) * 64 + 8 * c8;
-        r.g[qq] = *reinterpret_cast<const uint4*>(a.dy + o);
-        r.w[qq] = *reinterpret_cast<const uint2*>(a.idx + o);
+    char* S = smem + (lt & 1) * SB_SLOT;
+    for (int i = wave; i < nDMA; i += SB_NTH / 64) {
+      if (i < nY) {
+        const int pix = 8 * i + (lane >> 3), aa = pix >= W, w = pix - aa * W;
+        const int c = sb_swz(pix, lane & 7);  // the chunk that lands at slot lane & 7 (XOR: its own inverse)
+        const uint32_t voff = (uint32_t)(((((long long)n * H + 2 * k + aa) * W + w) * 64 + 8 * c) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_void_t*)(S + 1024 * i), 16, voff, 0, 0, 0);
+      } else if (i < nY + nD) {
+        const int e = 8 * (i - nY) + (lane >> 3), pr = e / OW, pw = e - pr * OW;
+        const uint32_t voff = k + pr < OH ? (uint32_t)((((long long)n * OH + k + pr) * OW + pw) * 128 + 16 * (lane & 7))
+                                          : dbytes;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (lds_void_t*)(S + SB_YB + 1024 * (i - nY)), 16, voff, 0, 0, 0);
+      } else if (i < nY + nD + nI) {
+        const int b = 1024 * (i - nY - nD) + 16 * lane, e = b >> 6, pr = e / OW, pw = e - pr * OW;
+        const uint32_t voff = (pr < 2 && k + pr < OH)
+                                  ? (uint32_t)((((long long)n * OH + k + pr) * OW + pw) * 64 + (b & 63)) : ibytes;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ir, (lds_void_t*)(S + SB_YB + SB_DB + 1024 * (i - nY - nD)), 16, voff,
+                                                 0, 0, 0);
+      } else {
+        const int id = 64 * (i - nY - nD - nI) + lane, pr = id / SPW, sp = id - pr * SPW - 2, ih = 4 * k - 3 + pr;
+        const bool ok = id < 9 * SPW && (unsigned)ih < (unsigned)HI && (unsigned)sp < (unsigned)W;
+        const uint32_t voff = ok ? (uint32_t)((((long long)n * HI + ih) * W + sp) * 16) : xbytes;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(S + SB_YB + SB_DB + SB_IB + 1024 * (i - nY - nD - nI)),
+                                                 16, voff, 0, 0, 0);
       }
-#pragma unroll
-      for (int p4 = 0; p4 < 4; ++p4) {
-        const long long pix = ((long long)n * H + 2 * k + (p4 >> 1)) * W + 2 * jj + (p4 & 1);
-        r.yv[p4] = *reinterpret_cast<const uint4*>(a.y + pix * 64 + 8 * c8);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int id = tid + SB_NTH * u;
-      const int pr = id / SPW, sp = id - pr * SPW - 2;
-      const int ih = 4 * k - 3 + pr;
-      r.xp[u] = uint4{0u, 0u, 0u, 0u};
-      if (id < npch && (unsigned)ih < (unsigned)HI && (unsigned)sp < (unsigned)W)
-        r.xp[u] = *reinterpret_cast<const uint4*>(a.x + (((long long)n * HI + ih) * W + sp) * 8);
     }
   };
-  // phase 1: dy0 of the item's 4 pixels -> dyT, the patch chunks -> P
-  auto produce = [&](int lt, bf16_t* dyT, bf16_t* P) {
-    const int tg = t0 + lt, n = tg / TPI, k = tg - n * TPI;
-    (void)n;
-    if (item) {
-      float sc[8], sh[8], A[8], Bc[8], Cc[8];
-      {
-        float* dst[5] = {sc, sh, A, Bc, Cc};
+  // phase 1: dy0 of the item's 4 pixels, in place over their y chunks
+  auto produce = [&](int lt, char* S) {
+    const int tg = t0 + lt, k = tg - (tg / TPI) * TPI;
+    if (!item) return;
+    const bf16_t* Dg = reinterpret_cast<const bf16_t*>(S + SB_YB);
+    const uint8_t* Ib = reinterpret_cast<const uint8_t*>(S + SB_YB + SB_DB);
+    bf16_t* Y = reinterpret_cast<bf16_t*>(S);
+    float sc[8], sh[8], A[8], Bc[8], Cc[8];
+    uint4 g4[4], y4s[4];
+    uint2 w2[4];
+    bool use[4];
+    {
+      uint4 pr4[10];
 #pragma unroll
-        for (int v = 0; v < 5; ++v) {
-          const float4 lo = *reinterpret_cast<const float4*>(&prm[v][8 * c8]);
-          const float4 hi = *reinterpret_cast<const float4*>(&prm[v][8 * c8 + 4]);
-          dst[v][0] = lo.x; dst[v][1] = lo.y; dst[v][2] = lo.z; dst[v][3] = lo.w;
-          dst[v][4] = hi.x; dst[v][5] = hi.y; dst[v][6] = hi.z; dst[v][7] = hi.w;
-        }
+      for (int v = 0; v < 5; ++v) {
+        pr4[2 * v] = sb_ld16(&prm[v][8 * c8]);
+        pr4[2 * v + 1] = sb_ld16(&prm[v][8 * c8 + 4]);
       }
-      bool use[4];
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) use[qq] = k + (qq >> 1) < OH && jj + (qq & 1) < OW;
+      for (int qq = 0; qq < 4; ++qq) {
+        const int rr = qq >> 1, col = min(jj + (qq & 1), OW - 1);
+        use[qq] = k + rr < OH && jj + (qq & 1) < OW;
+        g4[qq] = sb_ld16(Dg + (rr * OW + col) * 64 + 8 * c8);
+        w2[qq] = sb_ld8(Ib + (rr * OW + col) * 64 + 8 * c8);
+      }
 #pragma unroll
       for (int p4 = 0; p4 < 4; ++p4) {
-        const int aa = p4 >> 1, cc = p4 & 1;
-        float acc[8], yv[8];
+        const int pix = (p4 >> 1) * W + 2 * jj + (p4 & 1);
+        y4s[p4] = sb_ld16(Y + pix * 64 + 8 * sb_swz(pix, c8));
+      }
+      sb_lgkm0();
+      float* dst[5] = {sc, sh, A, Bc, Cc};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int dr = qq >> 1, dc = qq & 1;
-          if ((dr && !aa) || (dc && !cc)) continue;  // the window's rows / columns miss this pixel
-          if (!use[qq]) continue;
-          const uint8_t want = (uint8_t)((aa + 1 - 2 * dr) * 3 + (cc + 1 - 2 * dc));
-          float gv[8];
-          const uint32_t gw[4] = {r.g[qq].x, r.g[qq].y, r.g[qq].z, r.g[qq].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            gv[2 * e] = __uint_as_float(gw[e] << 16);
-            gv[2 * e + 1] = __uint_as_float(gw[e] & 0xffff0000u);
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const uint32_t wd = e < 4 ? r.w[qq].x : r.w[qq].y;
-            if (((wd >> (8 * (e & 3))) & 0xFF) == want) acc[e] += gv[e];
-          }
-        }
-        const uint32_t yw[4] = {r.yv[p4].x, r.yv[p4].y, r.yv[p4].z, r.yv[p4].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          yv[2 * e] = __uint_as_float(yw[e] << 16);
-          yv[2 * e + 1] = __uint_as_float(yw[e] & 0xffff0000u);
-        }
-        uint32_t o[4];
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          float d[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            float v = fmaf(yv[e + h], sc[e + h], sh[e + h]) > 0.f ? acc[e + h] : 0.f;
-            const float gr = bf2f(f2bf(v));  // the gradient as maxpool_bwd2_kernel stores / recomputes it
-            d[h] = a.train ? fmaf(A[e + h], gr, fmaf(Bc[e + h], yv[e + h], Cc[e + h])) : A[e + h] * gr;
-          }
-          o[e >> 1] = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
-        }
-        const int pix = aa * W + 2 * jj + cc;
-        *reinterpret_cast<uint4*>(dyT + pix * 64 + 8 * sb_swz(pix, c8)) = uint4{o[0], o[1], o[2], o[3]};
+      for (int v = 0; v < 5; ++v) {
+        const uint4 lo = pr4[2 * v], hi = pr4[2 * v + 1];
+        dst[v][0] = __uint_as_float(lo.x); dst[v][1] = __uint_as_float(lo.y);
+        dst[v][2] = __uint_as_float(lo.z); dst[v][3] = __uint_as_float(lo.w);
+        dst[v][4] = __uint_as_float(hi.x); dst[v][5] = __uint_as_float(hi.y);
+        dst[v][6] = __uint_as_float(hi.z); dst[v][7] = __uint_as_float(hi.w);
       }
     }
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int id = tid + SB_NTH * u;
-      if (id < npch) *reinterpret_cast<uint4*>(P + id * 8) = r.xp[u];
+    for (int p4 = 0; p4 < 4; ++p4) {
+      const int aa = p4 >> 1, cc = p4 & 1;
+      const int pix = aa * W + 2 * jj + cc;
+      bf16_t* yp = Y + pix * 64 + 8 * sb_swz(pix, c8);
+      const uint4 y4 = y4s[p4];
+      float acc[8], yv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int dr = qq >> 1, dc = qq & 1;
+        if ((dr && !aa) || (dc && !cc)) continue;  // the window's rows / columns miss this pixel
+        if (!use[qq]) continue;
+        const uint8_t want = (uint8_t)((aa + 1 - 2 * dr) * 3 + (cc + 1 - 2 * dc));
+        const uint32_t gw[4] = {g4[qq].x, g4[qq].y, g4[qq].z, g4[qq].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gv = __uint_as_float((e & 1) ? (gw[e >> 1] & 0xffff0000u) : (gw[e >> 1] << 16));
+          const uint32_t wd = e < 4 ? w2[qq].x : w2[qq].y;
+          if (((wd >> (8 * (e & 3))) & 0xFF) == want) acc[e] += gv;
+        }
+      }
+      const uint32_t yw[4] = {y4.x, y4.y, y4.z, y4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        yv[2 * e] = __uint_as_float(yw[e] << 16);
+        yv[2 * e + 1] = __uint_as_float(yw[e] & 0xffff0000u);
+      }
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        float d[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v = fmaf(yv[e + h], sc[e + h], sh[e + h]) > 0.f ? acc[e + h] : 0.f;
+          const float gr = bf2f(f2bf(v));  // the gradient as maxpool_bwd2_kernel stores / recomputes it
+          d[h] = a.train ? fmaf(A[e + h], gr, fmaf(Bc[e + h], yv[e + h], Cc[e + h])) : A[e + h] * gr;
+        }
+        o[e >> 1] = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
+      }
+      sb_st16(yp, uint4{o[0], o[1], o[2], o[3]});
     }
   };
 
   f32x4 acc[7];
 #pragma unroll
   for (int u = 0; u < 7; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int ksteps = (2 * W + 31) / 32;  // k = the tile's 2W pixels, padded to 32 with zero dy0 rows
-  for (int i = 2 * W * 8 + tid; i < ksteps * 32 * 8; i += SB_NTH)  // (the pad rows of both buffers, written once)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) *reinterpret_cast<uint4*>(smem + b * (DYE + PE) + 8 * i) = uint4{0u, 0u, 0u, 0u};
   const int cl = 16 * wm + 4 * pp;  // this lane's channels in the dy0 transposed read
-  if (my > 0) load(0);
+  if (my > 0) issue(0);
   for (int lt = 0; lt < my; ++lt) {
-    bf16_t* dyT = smem + (lt & 1) * (DYE + PE);
-    bf16_t* P = dyT + DYE;
-    produce(lt, dyT, P);
-    if (lt + 1 < my) load(lt + 1);  // in flight under this tile's MFMAs
-    __syncthreads();
+    char* S = smem + (lt & 1) * SB_SLOT;
+    // this tile's DMAs have landed (every wave), and every wave is past tile lt - 1 (its slot is free). Raw
+    // barriers: __syncthreads' release fence would also drain the next tile's DMA.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    sb_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    if (lt + 1 < my) issue(lt + 1);      // in flight under this tile's two phases
+    produce(lt, S);
+    sb_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    const bf16_t* dyT = reinterpret_cast<const bf16_t*>(S);
+    const bf16_t* P = reinterpret_cast<const bf16_t*>(S + SB_YB + SB_DB + SB_IB);
     // phase 2: k = pixel; element j of lane 16g + i is pixel 32 s + 4g + 16 (j >> 2) + (j & 3) on both operands
     s16x4 al[2], ah[2], bl[2][7], bh[2][7];
     auto reads = [&](int s, int b) {

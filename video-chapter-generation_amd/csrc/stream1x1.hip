@@ -434,8 +434,10 @@ int rs_grid(int N) {
 
 // the fused 1x1 dgrad with mask bits and no y on the register-streaming kernel: eligible / partial-sum slots
 bool rs_dgrad_ok(const GemmParams& p) {
+  // opt-in (VCG_RS_DGRAD=1): at the l1 conv1 shape it ran no faster than the LDS-ring stream kernel (1189 vs 1147 us
+  // one-stream, profiles/r04_final_gemm_breakdown.txt), at 4.1-4.2 TB/s either way
   const char* v = getenv("VCG_RS_DGRAD");
-  if (v && v[0] == '0') return false;
+  if (!v || v[0] != '1') return false;
   const BwdEpi& e = p.bwd;
   const bool dense = p.a.KH == 0 && p.a.GH == 0;
   if (!dense || (p.K != 64 && p.K != 128) || p.N % RS_TN != 0 || p.N / RS_TN > 8 || p.batch_inner > 0 ||

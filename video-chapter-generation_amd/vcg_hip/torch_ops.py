@@ -16,7 +16,7 @@ tracing, and, where the reference op is differentiable, an autograd formula that
 The encoder engines (vcg_hip/trunk.py, bert.py) issue ~2000 launches per train step and call the C ABI through
 ctypes directly: a dispatcher round trip per launch (~5-10 us of host time) would make the step host-bound.
 """
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -107,6 +107,40 @@ def _(x, weight, bias, act):
     return x.new_empty((x.shape[0], weight.shape[0]))
 
 
+@torch.library.custom_op("vcg::linear_bwd", mutates_args=())
+def linear_bwd(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, out: Optional[torch.Tensor], act: int,
+               has_bias: bool) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """(dx, dW, db) of vcg::linear; db is [N] fp32 (empty without a bias). ReLU: the mask from the saved output."""
+    M, K = x.shape
+    N = weight.shape[0]
+    dy = dy.contiguous()
+    if act == ops.ACT_RELU:
+        if dy.dtype != torch.float32:
+            raise NotImplementedError("vcg::linear backward through ReLU: fp32 only (vcg_act_drop_bwd)")
+        dpre = torch.empty_like(dy)
+        ops._lib.call("vcg_act_drop_bwd", ops.P(dy), ops.P(out.contiguous()), ops.P(dpre), dy.numel(), ops.ACT_RELU,
+                      0.0, 0, ops.stream())
+        dy = dpre
+    elif act != ops.ACT_NONE:
+        raise NotImplementedError(f"vcg::linear backward: act {act} is forward-only (no pre-activation saved)")
+    dx = ops.gemm(dy, weight.contiguous(), M, K, N, N, K, transB=True)
+    # dW = dY^T X over the M rows: the split-K engine (fp32 slabs, any M), rounded to the weight's dtype
+    dw32 = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+    ops.gemm_splitk(dy, x.contiguous(), dw32, N, K, M, N, K, transA=True, transB=True, accumulate=False)
+    dw = dw32.to(weight.dtype)
+    db = torch.empty(N if has_bias else 0, dtype=torch.float32, device=dy.device)
+    if has_bias:
+        ops.colsum(dy, N, M, N, db, accumulate=False)
+    return dx, dw, db
+
+
+@linear_bwd.register_fake
+def _(dy, x, weight, out, act, has_bias):
+    N = weight.shape[0]
+    return (x.new_empty(x.shape), weight.new_empty(weight.shape),
+            dy.new_empty((N if has_bias else 0,), dtype=torch.float32))
+
+
 def _linear_setup(ctx, inputs, output):
     x, weight, bias, act = inputs
     ctx.act, ctx.has_bias = act, bias is not None
@@ -116,26 +150,8 @@ def _linear_setup(ctx, inputs, output):
 
 def _linear_backward(ctx, dy):
     x, weight, out = ctx.saved_tensors
-    M, K = x.shape
-    N = weight.shape[0]
-    dy = dy.contiguous()
-    if ctx.act == ops.ACT_RELU:
-        if dy.dtype != torch.float32:
-            raise NotImplementedError("vcg::linear backward through ReLU: fp32 only (vcg_act_drop_bwd)")
-        dpre = torch.empty_like(dy)
-        ops._lib.call("vcg_act_drop_bwd", ops.P(dy), ops.P(out.contiguous()), ops.P(dpre), dy.numel(), ops.ACT_RELU,
-                      0.0, 0, ops.stream())
-        dy = dpre
-    elif ctx.act != ops.ACT_NONE:
-        raise NotImplementedError(f"vcg::linear backward: act {ctx.act} is forward-only (no pre-activation saved)")
-    dx = ops.gemm(dy, weight.contiguous(), M, K, N, N, K, transB=True)
-    dw = ops.gemm(dy, x.contiguous(), N, K, M, N, K, transA=True, transB=True)
-    db = None
-    if ctx.has_bias:
-        db = torch.empty(N, dtype=torch.float32, device=dy.device)
-        ops.colsum(dy, N, M, N, db, accumulate=False)
-        db = db.to(ctx.bias_dtype)
-    return dx, dw, db, None
+    dx, dw, db = torch.ops.vcg.linear_bwd(dy, x, weight, out, ctx.act, ctx.has_bias)
+    return dx, dw, (db.to(ctx.bias_dtype) if ctx.has_bias else None), None
 
 
 linear.register_autograd(_linear_backward, setup_context=_linear_setup)
