@@ -15,17 +15,18 @@
 //            (igemm.hip pair_taps: K = 7 x 4 x 8 = 224), both operands read with ds_read_b64_tr_b16 (4
 //            consecutive pixels per lane); v_mfma_f32_16x16x32_bf16, 8 waves = 4 channel tiles x 2 halves of the
 //            14 n-tiles, fp32 accumulators for the whole range.
-// Every operand of a tile arrives by LDS-DMA into one of two slots, issued a whole tile ahead (both phases of the
-// current tile cover its latency; the first version loaded the next tile into registers under the MFMA phase only
-// and ran latency-bound at 1.43 ms). Each workgroup writes its [64][224] fp32 slab; stem_wgrad_reduce_kernel sums
+// Every operand of a tile arrives by LDS-DMA into the workgroup's slot; two workgroups per CU (256 threads, one
+// 66-KiB slot each) so one's DMA wait and VALU phase run under the other's MFMAs. (Measured at the bench shape: one
+// 512-thread workgroup per CU with the next tile's loads in registers under the MFMA phase 1.43 ms; with a 2-slot
+// LDS-DMA ring a tile ahead 1.63 ms -- phase 1 is VALU-bound and ran with only 2 waves per SIMD, none overlapping.) Each workgroup writes its [64][224] fp32 slab; stem_wgrad_reduce_kernel sums
 // the slabs in a fixed order (deterministic) into the OIHW weight gradient.
 #include "igemm.h"
 
 namespace vcg {
 namespace {
 
-constexpr int SB_NTH = 512;
-constexpr int SB_GRID = 256;   // workgroups = slabs (one per CU)
+constexpr int SB_NTH = 256;
+constexpr int SB_GRID = 512;   // workgroups = slabs (two per CU)
 constexpr int SB_N = 224;      // pair-packed 7x7 taps: 7 rows x 4 super pixels x 8 (2 pixels x RGB0)
 constexpr int SB_MAXW = 112;   // conv-output width (the tile's 2W pixels are the MFMA k)
 
@@ -90,10 +91,10 @@ constexpr int SB_SLOT = SB_YB + SB_DB + SB_IB + SB_PB;         // 66 KiB
 
 __global__ __launch_bounds__(SB_NTH) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_bwd_fused_kernel(StemBwdArgs a) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * SB_SLOT];
+  __shared__ __attribute__((aligned(1024))) char smem[SB_SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lg = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-  const int wm = wave & 3, wn = wave >> 2;   // channels 16 wm .., n-tiles 7 wn .. 7 wn + 6
+  const int wm = wave & 1, wn = wave >> 1;   // channels 32 wm .. + 31, n-tiles 7 wn .. 7 wn + 6
   const int W = a.W, H = a.H, OH = a.OH, OW = a.OW;
   const int SPW = W + 4;                     // super pixels per patch row (-2 .. W + 1)
   const int HI = 2 * H;
@@ -102,8 +103,7 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
   const int my = t1 - t0;
   const int TPI = H / 2;
   const int nitems = (W / 2) * 8;
-  const int c8 = tid & 7, jj = tid >> 3;     // phase-1 item (fixed chunk per thread)
-  const bool item = tid < nitems;
+  const int c8 = tid & 7;                    // phase-1 items tid, tid + 256 (fixed chunk per thread)
   const int nY = 2 * W / 8, nD = OW / 4, nI = (OW + 7) / 8, nP = (9 * SPW + 63) / 64;
   const int nDMA = nY + nD + nI + nP;
 
@@ -130,14 +130,13 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
     prm[4][c] = -A * a.sum_g[c] * a.inv_count - Bc * a.mean[c];
   }
   const int ksteps = (2 * W + 31) / 32;  // k = the tile's 2W pixels, padded to 32 with zero dy0 rows
-  for (int i = 2 * W * 8 + tid; i < ksteps * 32 * 8; i += SB_NTH)  // (the pad rows of both slots, never DMA'd)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) *reinterpret_cast<uint4*>(smem + b * SB_SLOT + 16 * i) = uint4{0u, 0u, 0u, 0u};
+  for (int i = 2 * W * 8 + tid; i < ksteps * 32 * 8; i += SB_NTH)  // (the pad rows, never DMA'd)
+    *reinterpret_cast<uint4*>(smem + 16 * i) = uint4{0u, 0u, 0u, 0u};
 
-  // tile lt's DMAs into slot lt & 1: instruction i = wave, wave + 8, ... of Y | D | I | P
+  // tile lt's DMAs into the slot: instruction i = wave, wave + 4, ... of Y | D | I | P
   auto issue = [&](int lt) {
     const int tg = t0 + lt, n = tg / TPI, k = tg - n * TPI;
-    char* S = smem + (lt & 1) * SB_SLOT;
+    char* S = smem;
     for (int i = wave; i < nDMA; i += SB_NTH / 64) {
       if (i < nY) {
         const int pix = 8 * i + (lane >> 3), aa = pix >= W, w = pix - aa * W;
@@ -165,9 +164,8 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
     }
   };
   // phase 1: dy0 of the item's 4 pixels, in place over their y chunks
-  auto produce = [&](int lt, char* S) {
+  auto produce = [&](int lt, char* S, int jj) {
     const int tg = t0 + lt, k = tg - (tg / TPI) * TPI;
-    if (!item) return;
     const bf16_t* Dg = reinterpret_cast<const bf16_t*>(S + SB_YB);
     const uint8_t* Ib = reinterpret_cast<const uint8_t*>(S + SB_YB + SB_DB);
     bf16_t* Y = reinterpret_cast<bf16_t*>(S);
@@ -250,30 +248,35 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
     }
   };
 
-  f32x4 acc[7];
+  f32x4 acc[2][7];
 #pragma unroll
-  for (int u = 0; u < 7; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int cl = 16 * wm + 4 * pp;  // this lane's channels in the dy0 transposed read
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int u = 0; u < 7; ++u) acc[mt][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (my > 0) issue(0);
   for (int lt = 0; lt < my; ++lt) {
-    char* S = smem + (lt & 1) * SB_SLOT;
-    // this tile's DMAs have landed (every wave), and every wave is past tile lt - 1 (its slot is free). Raw
-    // barriers: __syncthreads' release fence would also drain the next tile's DMA.
+    char* S = smem;
+    // this tile's DMAs have landed (every wave)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     sb_lgkm0();
     __builtin_amdgcn_s_barrier();
-    if (lt + 1 < my) issue(lt + 1);      // in flight under this tile's two phases
-    produce(lt, S);
+    if (tid < nitems) produce(lt, S, tid >> 3);
+    if (tid + SB_NTH < nitems) produce(lt, S, (tid + SB_NTH) >> 3);
     sb_lgkm0();
     __builtin_amdgcn_s_barrier();
     const bf16_t* dyT = reinterpret_cast<const bf16_t*>(S);
     const bf16_t* P = reinterpret_cast<const bf16_t*>(S + SB_YB + SB_DB + SB_IB);
     // phase 2: k = pixel; element j of lane 16g + i is pixel 32 s + 4g + 16 (j >> 2) + (j & 3) on both operands
-    s16x4 al[2], ah[2], bl[2][7], bh[2][7];
+    // (one fragment set: the other workgroup on the CU covers this wave's LDS latency)
+    s16x4 al[1][2], ah[1][2], bl[1][7], bh[1][7];
     auto reads = [&](int s, int b) {
       const int k0 = 32 * s + 4 * lg + q, k1 = k0 + 16;
-      sb_tr(al[b], dyT + k0 * 64 + 8 * sb_swz(k0, cl >> 3) + (cl & 7));
-      sb_tr(ah[b], dyT + k1 * 64 + 8 * sb_swz(k1, cl >> 3) + (cl & 7));
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int cl = 32 * wm + 16 * mt + 4 * pp;  // this lane's channels in the dy0 transposed read
+        sb_tr(al[b][mt], dyT + k0 * 64 + 8 * sb_swz(k0, cl >> 3) + (cl & 7));
+        sb_tr(ah[b][mt], dyT + k1 * 64 + 8 * sb_swz(k1, cl >> 3) + (cl & 7));
+      }
       const int a0 = k0 >= W, a1 = k1 >= W;
       const int ow0 = min(k0 - a0 * W, W - 1), ow1 = min(k1 - a1 * W, W - 1);  // (pad pixels: any in-bounds chunk)
 #pragma unroll
@@ -283,29 +286,33 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
         sb_tr(bh[b][u], P + ((2 * a1 + kh) * SPW + ow1 + kwp) * 8 + e0);
       }
     };
-    auto step = [&](int s, int b) {  // (b a compile-time constant at both call sites: register arrays, no scratch)
+    auto step = [&](int s, int b) {
+      reads(s, b);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < ksteps) reads(s + 1, b ^ 1);
-      const s16x8 af = sb_cat(al[b], ah[b]);
+      const s16x8 af0 = sb_cat(al[b][0], ah[b][0]), af1 = sb_cat(al[b][1], ah[b][1]);
 #pragma unroll
-      for (int u = 0; u < 7; ++u)
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sb_cat(bl[b][u], bh[b][u]), af, acc[u], 0, 0, 0);
+      for (int u = 0; u < 7; ++u) {
+        const s16x8 bf = sb_cat(bl[b][u], bh[b][u]);
+        acc[0][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af0, acc[0][u], 0, 0, 0);
+        acc[1][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af1, acc[1][u], 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     };
-    reads(0, 0);
-    for (int s = 0; s < ksteps; s += 2) {
-      step(s, 0);
-      if (s + 1 < ksteps) step(s + 1, 1);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int s = 0; s < ksteps; ++s) step(s, 0);
+    // every wave's reads of the slot have returned before the next tile's DMA refills it
+    sb_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    if (lt + 1 < my) issue(lt + 1);
   }
-  // acc[u][rr] = dW[co = 16 wm + li][n = 16 (7 wn + u) + 4 lg + rr]
+  // acc[mt][u][rr] = dW[co = 32 wm + 16 mt + li][n = 16 (7 wn + u) + 4 lg + rr]
   float* slab = a.ws + (long long)blockIdx.x * 64 * SB_N;
 #pragma unroll
-  for (int u = 0; u < 7; ++u)
-    *reinterpret_cast<float4*>(slab + (16 * wm + li) * SB_N + 16 * (7 * wn + u) + 4 * lg) =
-        make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+      *reinterpret_cast<float4*>(slab + (32 * wm + 16 * mt + li) * SB_N + 16 * (7 * wn + u) + 4 * lg) =
+          make_float4(acc[mt][u][0], acc[mt][u][1], acc[mt][u][2], acc[mt][u][3]);
 }
 
 // OIHW [64][3][7][7] (+)= sum of the slabs in slab order; n = (kh * 4 + kwp) * 8 + 4 j + ci, kw = 2 (kwp - 2) + j + 3
