@@ -295,21 +295,24 @@ def test_bn_bwd_apply_dual(K, dtype, P, C):
         assert ((o - r).abs() <= tol * r.abs() + 1e-6 * r.abs().max()).all()
 
 
-@pytest.mark.parametrize("case", [(8, 56, 56), (1, 56, 56), (6, 28, 28), (3, 20, 20), (2, 13, 9)])
+@pytest.mark.parametrize("case", [(8, 56, 56, 64, 64), (1, 56, 56, 64, 64), (6, 28, 28, 64, 64), (3, 20, 20, 64, 64),
+                                  (2, 13, 9, 64, 64), (4, 28, 28, 128, 128), (3, 14, 14, 256, 256),
+                                  (5, 14, 14, 512, 512), (2, 14, 14, 128, 256), (3, 16, 16, 64, 192)])
 def test_conv_wgrad_patch(K, case):
-    """The layer-1 3x3 weight gradient on the LDS patch (wgrad3x3_patch_kernel: C = Cout = 64, stride 1, pad 1; R rows
-    per tile = 2 / 2 / 4 / 5 / 13 here, ragged TM, workgroups with no tile) against float64 torch."""
+    """The stride-1 3x3 weight gradient on the LDS patch (wgrad3x3_patch_kernel: one workgroup per 64 x 64 channel
+    block and tile range, pad 1; R rows per tile = 2 / 2 / 4 / 5 / 13 / 4 / 7 / 7 here, ragged TM, 2- and 4-step
+    tiles, pitches 16 / 32 / 64, workgroups with no tile, Cin != Cout) against float64 torch."""
     dtype = torch.bfloat16
-    N, H, W = case
-    x = _rand((N, 64, H, W), dtype, 26).double()
-    w = _rand((64, 64, 3, 3), torch.float32, 27, 0.1).double().requires_grad_()
+    N, H, W, C, Co = case
+    x = _rand((N, C, H, W), dtype, 26).double()
+    w = _rand((Co, C, 3, 3), torch.float32, 27, 0.1).double().requires_grad_()
     y = F.conv2d(x, w, stride=1, padding=1)
     dy = _rand(y.shape, dtype, 28).double()
     (ref,) = torch.autograd.grad(y, w, dy)
     xs = x.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV)
     dys = dy.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV)
-    dw = torch.full((64, 64, 3, 3), 0.25, dtype=torch.float32, device=DEV)
-    K.conv_wgrad(xs, dys, dw, N, H, W, 64, 64, 64, 3, 3, 1, 1, 0, 0, accumulate=True)
+    dw = torch.full((Co, C, 3, 3), 0.25, dtype=torch.float32, device=DEV)
+    K.conv_wgrad(xs, dys, dw, N, H, W, C, C, Co, 3, 3, 1, 1, 0, 0, accumulate=True)
     err = (dw.double().cpu() - 0.25 - ref).abs().max().item()
     assert err <= 1e-4 * ref.abs().max().item() + 1e-6, f"max err {err}"
 

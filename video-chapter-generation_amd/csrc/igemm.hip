@@ -918,8 +918,8 @@ VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C,
   int M, Nn, K, splits, kps;
   bool fast;
   wgrad_geometry(dtype, N, H, W, C, Cout, KH, KW, stride, pad, &M, &Nn, &K, &splits, &kps, &fast);
-  if (wgrad_patch_rows(dtype, H, W, C, C, Cout, KH, KW, stride, pad, 0) > 0 && splits < wgrad_patch_splits())
-    splits = wgrad_patch_splits();  // the patch kernel's slabs
+  if (wgrad_patch_rows(dtype, H, W, C, C, Cout, KH, KW, stride, pad, 0) > 0 && splits < wgrad_patch_splits(C, Cout))
+    splits = wgrad_patch_splits(C, Cout);  // the patch kernel's slabs
   return (long long)splits * M * Nn * 4;
 }
 
@@ -971,12 +971,12 @@ static int conv_wgrad_impl(int dtype, const void* x, const float* in_sc, const f
   p.ws = ws;
   p.alpha = 1.f;
   const int wpr = wgrad_patch_rows(dtype, H, W, C, Cin, Cout, KH, KW, stride, pad, tsm_fold);
-  if (wpr > 0) {  // layer-1 3x3: im2col-free patch kernel (igemm_wgrad.hip), one slab per workgroup
-    const int wsp = wgrad_patch_splits();
+  if (wpr > 0) {  // stride-1 3x3: im2col-free patch kernel (igemm_wgrad.hip), one slab per tile range
+    const int wsp = wgrad_patch_splits(C, Cout);
     VCG_REQUIRE(ws_bytes >= (long long)wsp * M * Nn * 4, "workspace too small");
     if (FILE* f = gemm_log())
       fprintf(f, "a=3 b=4 epi=2 M=%d N=%d K=%d z=%d fast=3 conv=%dx%d/%d C=%d\n", M, Nn, K, wsp, KH, KW, stride, C);
-    int rc = run_wgrad_patch(x, dy, ws, N, H, W, wpr, stream);
+    int rc = run_wgrad_patch(x, dy, ws, N, H, W, C, Cout, wpr, stream);
     if (rc) return rc;
     const long long MN = (long long)M * Nn;
     splitk_reduce(stream, ws, wsp, MN,

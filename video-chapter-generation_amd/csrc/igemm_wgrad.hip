@@ -279,25 +279,27 @@ template <int BM, int BN, bool BG> int launch_wgrad(const GemmParams& p0, int sp
   return VCG_OK;
 }
 
-// ---- 3x3 / stride 1 / pad 1 weight gradient over C = Cout = 64 (layer 1) on an LDS-resident input patch ----------
+// ---- 3x3 / stride 1 / pad 1 weight gradient on an LDS-resident input patch (C, Cout multiples of 64) -------------
 // dW[co][(kh, kw, ci)] = sum_p dy[p][co] x[p + (kh - 1, kw - 1)][ci]. An M-tile is R whole output rows of one image
-// (TM = R W <= 128 pixels, the GEMM k of 4 steps of 32; pixels TM..127 are zero dy rows). Its dy rows ([128][64]) and
-// the (R + 2) x (W + 2) input pixels the 9 taps read (zero border from the descriptor range check) go to LDS ONCE by
+// (TM = R W <= 32 KS pixels, the GEMM k of KS steps of 32; pixels TM.. are zero dy rows). Its dy rows and the
+// (R + 2) x (W + 2) input pixels the 9 taps read (zero border from the descriptor range check) go to LDS ONCE by
 // LDS-DMA; the 9 taps read shifted transposed fragments of the patch, where the im2col gather of wgrad_fast_kernel
-// fetches x once per filter tap and dy once per 128-column tile through L2 (7.5x the operand bytes). A workgroup
-// (one per CU: the 64 x 576 fp32 accumulator is 144 registers per lane) walks a contiguous range of tiles (halo rows
-// shared in L2) and writes one fp32 slab [64][576] for splitk_reduce_kernel (fixed-order sum: deterministic).
-// Wave w owns input channels 16 w .. 16 w + 15 of every tap (acc[co tile][tap]); per k-step it reads 4 dy^T
-// fragments (shared by the 9 taps) and 9 patch fragments (shared by the 4 co tiles) with ds_read_b64_tr_b16 and runs
-// 36 MFMAs, the next k-step's reads in flight under them. Tiles are DMA'd two ahead into a 3-slot ring (counted
-// vmcnt, raw barriers: the pipeline of conv3x3_patch_kernel).
-constexpr int WP_SL = 32;      // 1-KiB (8-pixel) slices of a patch slot: (R + 2)(W + 2) <= 256 pixels
+// fetches x once per filter tap and dy once per 128-column tile through L2 (7.5x the operand bytes). A workgroup owns
+// one 64 x 64 (co, ci) channel block (the 64 x 576 fp32 accumulator is 144 registers per lane: one workgroup per CU)
+// and walks a contiguous range of tiles (halo rows shared in L2); the workgroups of one tile range (one per channel
+// block) sit on one XCD, so the x / dy rows they all read come from that L2. Each writes its block of the fp32 slab
+// [Cout][9 C] of its range for splitk_reduce_kernel (fixed-order sum: deterministic).
+// Wave w owns input channels 16 w .. 16 w + 15 of the block for every tap (acc[co tile][tap]); per k-step it reads 4
+// dy^T fragments (shared by the 9 taps) and 9 patch fragments (shared by the 4 co tiles) with ds_read_b64_tr_b16
+// and runs 36 MFMAs, the next k-step's reads in flight under them. Tiles are DMA'd two ahead into a 3-slot ring
+// (counted vmcnt, raw barriers: the pipeline of conv3x3_patch_kernel).
+constexpr int WP_SL = 32;      // 1-KiB (8-pixel) slices of a patch slot: (R + 2) PW <= 256 pixels
 constexpr int WP_RING = 3;
-constexpr int WP_GRID = 256;   // workgroups = fp32 slabs
-constexpr int WP_NIP = 12;     // LDS-DMA instructions per wave per tile (8 patch + 4 dy)
+constexpr int WP_GRID = 256;   // workgroups (at least; see wp_grid)
 
 struct WPatchGeom {
   int H, W, R, TM, PW, NP, NS, tiles, TPI;
+  int C, CO, nct, nch, nsplit;  // channels, output channels, C / 64, (C / 64)(CO / 64), tile ranges (slabs)
 };
 
 __device__ __forceinline__ int wp_swz(int row, int c) { return c ^ (2 * ((row >> 1) & 3)); }  // = wswz<64>
@@ -306,27 +308,32 @@ template <int OFF> __device__ __forceinline__ void tr_read_at(s16x4& v, uint32_t
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
 }
 
-// Patch rows at a fixed pitch PW (32 / 64 pixels >= W + 2, as conv3x3_patch_kernel): the swizzle depends on the
+// Patch rows at a fixed pitch PW (16 / 32 / 64 pixels >= W + 2, as conv3x3_patch_kernel): the swizzle depends on the
 // pixel row index mod 8, so a tap's row offset kh * PW is an immediate of the transposed read and the lane's
-// addresses (8 dy^T + 6 patch per k-step) are computed once per tile instead of per read.
-template <int PW>
+// addresses (8 dy^T + 6 patch per k-step) are computed once per k-step instead of per read. KS: k-steps per tile.
+template <int PW, int KS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, float* __restrict__ ws,
                            uint32_t xbytes, uint32_t dybytes, WPatchGeom g) {
-  constexpr int PE = WP_SL * 512, YE = 128 * 64;
+  constexpr int PE = WP_SL * 512, YE = 32 * KS * 64;
+  constexpr int NIP = 8 + KS;  // LDS-DMA instructions per wave per tile (8 patch + KS dy)
   __shared__ __attribute__((aligned(1024))) bf16_t smem[WP_RING * (PE + YE)];
   bf16_t* Ps = smem;
   bf16_t* Ys = smem + WP_RING * PE;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lg = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-  const int t0 = (int)(((long long)g.tiles * blockIdx.x) / gridDim.x);
-  const int t1 = (int)(((long long)g.tiles * (blockIdx.x + 1)) / gridDim.x);
+  // workgroup -> (tile range, channel block): the nch blocks of one range share blockIdx % 8 (one XCD)
+  const int b = blockIdx.x, rest = b >> 3;
+  const int chb = rest % g.nch, split = (rest / g.nch) * 8 + (b & 7);
+  const int ci_t = chb % g.nct, co_t = chb / g.nct;
+  const int t0 = (int)(((long long)g.tiles * split) / g.nsplit);
+  const int t1 = (int)(((long long)g.tiles * (split + 1)) / g.nsplit);
   const int my = t1 - t0;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x), 0, xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(dy), 0, dybytes, 0x00020000);
   const int HW = g.H * g.W;
 
-  // tile lt's DMAs: q8 < 8 patch slices wave + 4 q8 (slices >= NS repeat slice NS - 1), q8 >= 8 dy rows
+  // tile lt's DMAs: q8 < 8 patch slices wave + 4 q8 (slices >= NS repeat slice NS - 1), then KS dy slices
   auto issue_tile = [&](int lt) {
     const int tg = t0 + lt, img = tg / g.TPI, h0 = (tg - img * g.TPI) * g.R;
     bf16_t* P = Ps + (lt % WP_RING) * PE;
@@ -339,23 +346,25 @@ void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restric
       const int h = h0 - 1 + pr, w = pc - 1;
       const bool ok = pix < g.NP && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       const int c = wp_swz(pix, lane & 7);
-      const uint32_t voff = ok ? (uint32_t)((((img * HW + h * g.W + w) << 6) + 8 * c) * 2) : xbytes;
+      const uint32_t voff =
+          ok ? (uint32_t)((((long long)(img * HW + h * g.W + w)) * g.C + 64 * ci_t + 8 * c) * 2) : xbytes;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(P + slice * 512), 16, voff, 0, 0, 0);
     }
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
+    for (int q4 = 0; q4 < KS; ++q4) {
       const int slice = wave + 4 * q4;
       const int r = 8 * slice + (lane >> 3);
       const int c = wp_swz(r, lane & 7);
-      const uint32_t voff = r < g.TM ? (uint32_t)((((img * HW + h0 * g.W + r) << 6) + 8 * c) * 2) : dybytes;
+      const uint32_t voff =
+          r < g.TM ? (uint32_t)((((long long)(img * HW + h0 * g.W + r)) * g.CO + 64 * co_t + 8 * c) * 2) : dybytes;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_void_t*)(Y + slice * 512), 16, voff, 0, 0, 0);
     }
   };
 
   // this lane's patch pixel of tap (0, 0) for k = 32 s + 4 lg + q + 16 hh (pixels >= TM: any valid pixel, dy is 0)
-  int kpix[4][2];
+  int kpix[KS][2];
 #pragma unroll
-  for (int st = 0; st < 4; ++st)
+  for (int st = 0; st < KS; ++st)
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int k = 32 * st + 4 * lg + q + 16 * hh;
@@ -371,18 +380,18 @@ void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restric
 
   if (my > 0) issue_tile(0);
   if (my > 1) issue_tile(1);
-  const int cb = 16 * wave + 4 * pp;  // first input channel of this lane's 8-B transposed read
+  const int cb = 16 * wave + 4 * pp;  // first input channel (within the block) of this lane's 8-B transposed read
   for (int lt = 0; lt < my; ++lt) {
-    if (lt + 1 < my) __builtin_amdgcn_s_waitcnt(wvm(WP_NIP));
+    if (lt + 1 < my) __builtin_amdgcn_s_waitcnt(wvm(NIP));
     else __builtin_amdgcn_s_waitcnt(wvm(0));
     __builtin_amdgcn_s_barrier();
     if (lt + 2 < my) issue_tile(lt + 2);  // into the slot of tile lt - 1 (every wave is past its reads)
     const bf16_t* P = Ps + (lt % WP_RING) * PE;
     const bf16_t* Y = Ys + (lt % WP_RING) * YE;
     s16x4 al[2][4], ah[2][4], bl[2][9], bh[2][9];
-    auto reads = [&](int st, int b) {
+    auto reads = [&](int st, int b2) {
       const int k0 = 32 * st + 4 * lg + q, k1 = k0 + 16;
-      uint32_t ya[4][2], pa[3][2];  // (the same per tile: the compiler keeps them across the k-steps' reads)
+      uint32_t ya[4][2], pa[3][2];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         const int cl = 16 * ct + 4 * pp;
@@ -397,45 +406,48 @@ void wgrad3x3_patch_kernel(const bf16_t* __restrict__ x, const bf16_t* __restric
       }
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
-        tr_read_at<0>(al[b][ct], ya[ct][0]);
-        tr_read_at<0>(ah[b][ct], ya[ct][1]);
+        tr_read_at<0>(al[b2][ct], ya[ct][0]);
+        tr_read_at<0>(ah[b2][ct], ya[ct][1]);
       }
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {  // tap t = 3 kh + kw: + kh PW pixels = kh PW 128 bytes
-        tr_read_at<0>(bl[b][kw], pa[kw][0]);
-        tr_read_at<0>(bh[b][kw], pa[kw][1]);
-        tr_read_at<PW * 128>(bl[b][3 + kw], pa[kw][0]);
-        tr_read_at<PW * 128>(bh[b][3 + kw], pa[kw][1]);
-        tr_read_at<2 * PW * 128>(bl[b][6 + kw], pa[kw][0]);
-        tr_read_at<2 * PW * 128>(bh[b][6 + kw], pa[kw][1]);
+        tr_read_at<0>(bl[b2][kw], pa[kw][0]);
+        tr_read_at<0>(bh[b2][kw], pa[kw][1]);
+        tr_read_at<PW * 128>(bl[b2][3 + kw], pa[kw][0]);
+        tr_read_at<PW * 128>(bh[b2][3 + kw], pa[kw][1]);
+        tr_read_at<2 * PW * 128>(bl[b2][6 + kw], pa[kw][0]);
+        tr_read_at<2 * PW * 128>(bh[b2][6 + kw], pa[kw][1]);
       }
     };
     reads(0, 0);
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int b = st & 1;
+    for (int st = 0; st < KS; ++st) {
+      const int b2 = st & 1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      if (st + 1 < 4) reads(st + 1, b ^ 1);
+      if (st + 1 < KS) reads(st + 1, b2 ^ 1);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const s16x8 bf = cat8(bl[b][t], bh[b][t]);
+        const s16x8 bf = cat8(bl[b2][t], bh[b2][t]);
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
-          acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat8(al[b][ct], ah[b][ct]), bf, acc[ct][t], 0, 0, 0);
+          acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat8(al[b2][ct], ah[b2][ct]), bf, acc[ct][t], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (no reads outstanding: the ring slot may be refilled)
   }
-  // acc[ct][t][r] = dW[co = 16 ct + 4 lg + r][tap t][ci = 16 wave + li] -> this workgroup's slab [64][9 * 64]
-  float* slab = ws + (long long)blockIdx.x * 64 * 576;
+  // acc[ct][t][r] = dW[co = 64 co_t + 16 ct + 4 lg + r][tap t][ci = 64 ci_t + 16 wave + li] -> this range's slab
+  // [CO][9 C] (splitk_reduce's conv layout: n = tap C + ci)
+  const int NC = 9 * g.C;
+  float* slab = ws + (long long)split * g.CO * NC;
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) slab[(16 * ct + 4 * lg + r) * 576 + 64 * t + 16 * wave + li] = acc[ct][t][r];
+      for (int r = 0; r < 4; ++r)
+        slab[(long long)(64 * co_t + 16 * ct + 4 * lg + r) * NC + t * g.C + 64 * ci_t + 16 * wave + li] = acc[ct][t][r];
 }
 
 }  // namespace
@@ -459,43 +471,69 @@ int run_fast_wgrad(const GemmParams& p, int splits, hipStream_t s, bool dense_b)
   return launch_wgrad<64, 64, true>(p, splits, s);
 }
 
-// Rows per tile of wgrad3x3_patch_kernel (0: not eligible): bf16, x with C = 64 channels, Cout = 64, 3x3 / stride 1 /
-// pad 1, no TSM, R W <= 128, (R + 2)(W + 2) <= 256, H % R == 0. VCG_WGRAD_PATCH=0 disables it.
+// Rows per tile of wgrad3x3_patch_kernel (0: not eligible): bf16, x with C (= Cin, a multiple of 64, <= 512)
+// channels, Cout a multiple of 64 (<= 512), 3x3 / stride 1 / pad 1, no TSM, W + 2 <= 64, R W <= 128,
+// (R + 2) pitch <= 256, H % R == 0, W >= 14. VCG_WGRAD_PATCH=0 disables it; VCG_WGRAD_PATCH=1 keeps it to
+// C = Cout = 64 (layer 1, the round-3 scope).
 int wgrad_patch_rows(int dtype, int H, int W, int C, int Cin, int Cout, int KH, int KW, int stride, int pad,
                      int tsm_fold) {
   static int en = -1;
   if (en < 0) {
     const char* e = getenv("VCG_WGRAD_PATCH");
-    en = (e && e[0] == '0') ? 0 : 1;
+    en = (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : 2;
   }
-  if (!en || dtype != VCG_BF16 || C != 64 || Cin != 64 || Cout != 64 || KH != 3 || KW != 3 || stride != 1 ||
-      pad != 1 || tsm_fold != 0)
+  if (!en || dtype != VCG_BF16 || C != Cin || C % 64 != 0 || Cout % 64 != 0 || C > 512 || Cout > 512 || KH != 3 ||
+      KW != 3 || stride != 1 || pad != 1 || tsm_fold != 0)
     return 0;
-  if (W + 2 > 64) return 0;
-  const int pw = W + 2 <= 32 ? 32 : 64;
+  if (en == 1 && (C != 64 || Cout != 64)) return 0;
+  // (7 x 7 maps: 49-pixel tiles of 64-pixel k-steps, 64 channel blocks -- measured slower than the im2col engine,
+  // 442 vs 399 us at layer 4; layer 2 / 3: 320 vs 428, 328 vs 406 us, tools/bench_wgrad3x3.py)
+  if (W + 2 > 64 || W < 14) return 0;
+  const int pw = W + 2 <= 16 ? 16 : W + 2 <= 32 ? 32 : 64;
   for (int R = 128 / W; R >= 1; --R)
     if ((R + 2) * pw <= 8 * WP_SL && H % R == 0) return R;
   return 0;
 }
 
-int wgrad_patch_splits() { return WP_GRID; }
+// workgroups: at least WP_GRID, a multiple of 8 tile ranges per channel block
+static int wp_grid(int C, int Cout) {
+  const int nch = (C / 64) * (Cout / 64);
+  int nsplit = WP_GRID / nch;
+  nsplit = nsplit < 8 ? 8 : nsplit & ~7;
+  return nsplit * nch;
+}
 
-// x: NHWC [N][H][W][64] bf16, dy: [N][H][W][64] bf16 -> WP_GRID fp32 slabs [64][576] in ws
-int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int W, int R, hipStream_t s) {
+int wgrad_patch_splits(int C, int Cout) { return wp_grid(C, Cout) / ((C / 64) * (Cout / 64)); }
+
+template <int PW>
+static void launch_wgrad_patch(const void* x, const void* dy, float* ws, uint32_t xb, uint32_t yb, const WPatchGeom& g,
+                               int grid, hipStream_t s) {
+  if (g.TM <= 64)
+    hipLaunchKernelGGL((wgrad3x3_patch_kernel<PW, 2>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x,
+                       (const bf16_t*)dy, ws, xb, yb, g);
+  else
+    hipLaunchKernelGGL((wgrad3x3_patch_kernel<PW, 4>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x,
+                       (const bf16_t*)dy, ws, xb, yb, g);
+}
+
+// x: NHWC [N][H][W][C] bf16, dy: [N][H][W][Cout] bf16 -> wgrad_patch_splits(C, Cout) fp32 slabs [Cout][9 C] in ws
+int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int W, int C, int Cout, int R,
+                    hipStream_t s) {
   WPatchGeom g;
-  const int pw = W + 2 <= 32 ? 32 : 64;
+  const int pw = W + 2 <= 16 ? 16 : W + 2 <= 32 ? 32 : 64;
   g.H = H; g.W = W; g.R = R; g.TM = R * W; g.PW = pw; g.NP = (R + 2) * pw; g.NS = (g.NP + 7) / 8;
   g.TPI = H / R; g.tiles = N * g.TPI;
-  const long long xb = (long long)N * H * W * 64 * 2;
-  VCG_REQUIRE(xb < 0xFFFFFF00LL, "wgrad patch: x / dy must be below 4 GB");
+  g.C = C; g.CO = Cout; g.nct = C / 64; g.nch = (C / 64) * (Cout / 64);
+  const int grid = wp_grid(C, Cout);
+  g.nsplit = grid / g.nch;
+  const long long xb = (long long)N * H * W * C * 2, yb = (long long)N * H * W * Cout * 2;
+  VCG_REQUIRE(xb < 0xFFFFFF00LL && yb < 0xFFFFFF00LL, "wgrad patch: x / dy must be below 4 GB");
+  VCG_REQUIRE(g.TM <= 128, "wgrad patch: tile rows");
   const int tk = timing_begin(s);
-  if (pw == 64)
-    hipLaunchKernelGGL(wgrad3x3_patch_kernel<64>, dim3(WP_GRID), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dy,
-                       ws, (uint32_t)xb, (uint32_t)xb, g);
-  else
-    hipLaunchKernelGGL(wgrad3x3_patch_kernel<32>, dim3(WP_GRID), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dy,
-                       ws, (uint32_t)xb, (uint32_t)xb, g);
-  timing_end(tk, s, TIMING_WGRAD, 2.0 * 64 * 576 * (double)N * H * W, 2.0 * (double)xb + 4.0 * 64 * 576);
+  if (pw == 64) launch_wgrad_patch<64>(x, dy, ws, (uint32_t)xb, (uint32_t)yb, g, grid, s);
+  else if (pw == 32) launch_wgrad_patch<32>(x, dy, ws, (uint32_t)xb, (uint32_t)yb, g, grid, s);
+  else launch_wgrad_patch<16>(x, dy, ws, (uint32_t)xb, (uint32_t)yb, g, grid, s);
+  timing_end(tk, s, TIMING_WGRAD, 2.0 * Cout * 9 * C * (double)N * H * W, (double)xb + (double)yb + 4.0 * Cout * 9 * C);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
