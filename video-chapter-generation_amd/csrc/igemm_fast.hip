@@ -1584,7 +1584,13 @@ void conv3x3_patch_kernel(GemmParams p, PatchGeom g) {
     for (int u = 0; u < 18; ++u) {
       if (u + 2 < 18) unit_reads(af[(u + 2) % 3], u + 2);
       if (u < NIP && pre) issue_piece(lt + 2, tg2, img2, h02, u);
-      if ((u & 1) && (u >> 1) < KC && prev) process(u >> 1);
+      // the previous tile's stores / statistics in units after the DMA issues (both are expensive beside the MFMAs:
+      // the dgrad epilogue's ~60 VALU per chunk exceeds a unit's MFMA shadow)
+      if constexpr (NIP + 2 * KC <= 18) {
+        if (u >= NIP && ((u - NIP) & 1) == 0 && ((u - NIP) >> 1) < KC && prev) process((u - NIP) >> 1);
+      } else {
+        if (u >= 18 - KC && prev) process(u - (18 - KC));
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
