@@ -379,7 +379,7 @@ __device__ __forceinline__ void unpack8(const uint4& u, float (&v)[8]) {
 // residual is added per 16-B row chunk in the flush, so both the residual loads and the output stores are full rows.
 // ACT_GELU_BWD: the residual is the pre-activation and the output dh * GELU'(pre), dh rounded to bf16 first (as
 // torch autocast's bf16 matmul output feeding gelu_backward)
-template <int BM, int BN>
+template <int BM, int BN, bool GELU_BWD>
 __device__ __forceinline__ void epilogue_staged_res(f32x4 (&acc)[4][BN / 32], const GemmParams& p,
                                                     const float (&bv)[BN / 32][4], bf16_t* Cout, const bf16_t* Res,
                                                     bf16_t* stA, bf16_t* stB, int m0, int n0, int wm, int wn,
@@ -438,7 +438,7 @@ __device__ __forceinline__ void epilogue_staged_res(f32x4 (&acc)[4][BN / 32], co
       for (int e = 0; e < 8; ++e) r[e] = fmaf(r[e], rsc[e], rsh[e]);
     }
     uint32_t mb = 0;  // ReLU mask of the output (p.obits): bit e = out > 0, as vcg_bn_apply writes it
-    if (p.act == ACT_GELU_BWD) {  // BERT FFN2's input gradient: dh * GELU'(pre), dh rounded as stored
+    if constexpr (GELU_BWD) {  // BERT FFN2's input gradient: dh * GELU'(pre), dh rounded as stored
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] *= p.fast_act ? gelu_erf_grad_fast(r[e]) : gelu_erf_grad(r[e]);
     } else {
@@ -1052,7 +1052,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   }
 }
 
-template <int BM, int BN, int AM, int EPI, bool RES>
+template <int BM, int BN, int AM, int EPI, int RES>
 __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
   // Persistent-style grid: workgroup (bx, by) owns N-tile bx and M-tiles by, by + gy, by + 2gy, ...;
   // the (m-tile, k-tile) steps form one software pipeline, so the next tiles' loads are in flight while
@@ -1244,11 +1244,11 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
       } else if (BM == 256 || (staged && !RES && p.aux == nullptr && (p.ldc & 7) == 0 &&
                                ((uintptr_t)p.C & 15) == 0)) {
         epilogue_staged<BM, BN>(acc, p, bv, Cout, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
-      } else if (RES && (staged || p.obits) && p.aux == nullptr && !(p.act == ACT_GELU_BWD && p.res_sc) &&
-                 ((p.res_round && p.act == ACT_RELU) || (staged && p.act == ACT_GELU_BWD)) &&
+      } else if (RES && (staged || p.obits) && p.aux == nullptr &&
+                 (RES == 2 ? (staged && !p.res_sc) : (p.res_round && p.act == ACT_RELU)) &&
                  ((p.ldc | p.ldr | p.N) & 7) == 0 && (((uintptr_t)p.residual | (uintptr_t)p.C) & 15) == 0) {
         if constexpr (BM == 128 && RES)
-          epilogue_staged_res<BM, BN>(acc, p, bv, Cout, Res, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
+          epilogue_staged_res<BM, BN, RES == 2>(acc, p, bv, Cout, Res, stA, stB, mt * BM, n0, wm, wn, lane, p.M);
       } else {
         if constexpr (BM == 128)
           gemm_epilogue<bf16_t, BM, BN, EPI>(acc, p, red, bv, Cout, Res, mt * BM, n0, wm, wn, lane, mt, mtiles);
@@ -1272,7 +1272,7 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
 
 // The kernel: EPI_BWD_STREAM has its own tile schedule (bwd_stream_body; AM = K / 64, XF = its operand flags),
 // every other epilogue runs the persistent 2-stage pipeline above.
-template <int BM, int BN, int AM, int EPI, bool RES, int XF = 0>
+template <int BM, int BN, int AM, int EPI, int RES, int XF = 0>
 __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(EPI == EPI_BWD_AFF && BN == 64 ? 3 : 2)))
 void igemm_fast_kernel(GemmParams p) {
   if constexpr (EPI == EPI_BWD_STREAM)
@@ -1923,7 +1923,7 @@ int fast_bwd_slots(const GemmParams& p) {
 
 // Algorithmic HBM bytes of one launch (bench.py's per-launch roofline): every operand read once (a gathered A:
 // the source tensor once), the output written once, the epilogue's extra operands read once (bf16).
-template <int AM, int EPI, bool RES>
+template <int AM, int EPI, int RES>
 static double algorithmic_bytes(const GemmParams& p, int z) {
   const double mn = (double)p.M * p.N * z;
   double b = (AM == OP_DENSE_K || AM == OP_DENSE_K2 ? 2.0 * p.M * (double)p.K * z : (double)p.a.bytes) + 2.0 * p.N * (double)p.K * z;
@@ -1940,7 +1940,7 @@ static double algorithmic_bytes(const GemmParams& p, int z) {
   return b;
 }
 
-template <int BM, int BN, int AM, int EPI, bool RES>
+template <int BM, int BN, int AM, int EPI, int RES>
 static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   const int nx = (p.N + BN - 1) / BN;
   const int gy = grid_rows(p.M, p.N, z, BM, BN, EPI);
@@ -1969,7 +1969,7 @@ static int run_bwd_stream(const GemmParams& p, hipStream_t s) {
   return launch_bwd_stream<KC, XF_HASY | XF_Y2>(p, s);
 }
 
-template <int AM, int EPI, bool RES = false>
+template <int AM, int EPI, int RES = 0>
 static int fast_bn(const GemmParams& p, int z, hipStream_t s) {
   if constexpr (!RES) {
     if (fast_bm(p.M, p.N, z, p.aux != nullptr) == 256) return launch_fast<256, 128, AM, EPI, false>(p, z, s);
@@ -2073,7 +2073,11 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
     if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_STATS>(p, z, s);
     return fast_bn<OP_DENSE_K, EPI_STATS>(p, z, s);
   }
-  if (p.residual) return fast_bn<OP_DENSE_K, EPI_STORE, true>(p, z, s);  // dense layers only (BERT bwd)
+  // dense layers only; RES = 2: the GELU' x residual epilogue (BERT FFN2's input gradient) as its own kernel -- in
+  // the ReLU / add instantiation its erf code raised register use and slowed the scoring forward's folded conv3
+  // GEMMs by ~10 % (2.72-2.76 K vs 3.06 K windows/s, bisected to that change)
+  if (p.residual) return p.act == ACT_GELU_BWD ? fast_bn<OP_DENSE_K, EPI_STORE, 2>(p, z, s)
+                                               : fast_bn<OP_DENSE_K, EPI_STORE, 1>(p, z, s);
   if (p.aux && amode == OP_DENSE_K && (p.ldc & 7) == 0 && !getenv("VCG_NO_AUX_STAGE"))  // BERT FFN1 (GELU input)
     return fast_bn<OP_DENSE_K, EPI_STORE_AUX>(p, z, s);
   if (amode == OP_IM2COL_SMALLC) return fast_bn<OP_IM2COL_SMALLC, EPI_STORE>(p, z, s);
