@@ -497,8 +497,15 @@ def main():
             reducer.finish()
         opt.clip_and_step(1.0)
 
-    for _ in range(args.warmup):
+    from vcg_hip.trunk import ResNetTrunk
+    # the per-block path census (which bn3 fold / y3-drop / GEMM-pass variant every bottleneck ran) of the last
+    # warm-up step: the timed steps run the same path; the instrumented step below must too
+    timed_census = None
+    for i in range(args.warmup):
+        if i == args.warmup - 1 and args.mode == "train":
+            ResNetTrunk.census = []
         step()
+        timed_census, ResNetTrunk.census = ResNetTrunk.census, None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -536,13 +543,24 @@ def main():
     ms = max(ms, wall * 1000.0 / args.steps)
     # one extra (untimed) step with every fast-GEMM launch bracketed by HIP events; BERT runs on the trunk's
     # stream for this step, so a launch's duration is the kernel's own (not shared with a concurrent kernel)
-    from vcg_hip.trunk import ResNetTrunk
     sides = (model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream)
     # (and the weight gradients / downsample convs / weight re-layout on the trunk's stream)
     model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = False
     ops.timing_enable(True)
+    census = None
     if not args.no_roofline_step:
+        ResNetTrunk.census = [] if timed_census is not None else None
         step()
+        inst_census, ResNetTrunk.census = ResNetTrunk.census, None
+        if timed_census is not None:
+            # the one-stream instrumented step must run the timed step's kernels (bn3 folds, y3 drops, GEMM passes)
+            assert inst_census == timed_census, ("instrumented step ran another per-block path than the timed steps",
+                                                 timed_census, inst_census)
+            census = {"blocks_fwd": sum(e[0] == "fwd" for e in timed_census),
+                      "blocks_bwd": sum(e[0] == "bwd" for e in timed_census),
+                      "bn3_fold_bwd": sum(e[0] == "bwd" and e[3]["fold_dgrad"] for e in timed_census),
+                      "y3_drop": sum(e[0] == "fwd" and e[3]["y3_drop"] for e in timed_census),
+                      "identical_to_timed_step": True}
     torch.cuda.synchronize()
     # the dominant kernel: the bf16 fast engine, or the generic engine (exact fp32 MFMA) in the parity precision
     dom_id, dom_name = ((ops.TIMING_FAST_GEMM, "igemm_fast_kernel") if args.precision == "bf16"
@@ -605,6 +623,7 @@ def main():
                    # algorithmic bytes / HBM peak) per launch
                    "per_launch_roofline": _per_launch(rl[dom_id]),
                    "wgrad_fast_kernel": _per_launch(rl[ops.TIMING_WGRAD]),
+                   "path_census": census,
                    "timing": "HIP events around each launch on its stream, one instrumented step (no BERT side "
                              "stream in that step: unshared launch durations)"}
         out = {

@@ -116,14 +116,17 @@ VCG_API long long vcg_bn_apply_colsum_ws_bytes(long long P, int C);
 VCG_API int vcg_bn_apply_colsum(const void* y, const float* scale, const float* shift, int relu, void* out, float* colsum, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
 /* vcg_bn_apply_colsum (ReLU, bf16, C = 64 / 128 / 256) that also returns gram = out^T out (f32 [C][C], summed in a
    fixed order: deterministic): the bottleneck's bn2 -> relu -> a2 with the a2 statistics that bn3's batch statistics
-   (vcg_bn_stats_from_gram) and the a2 form of the bn3 backward fold need, so that neither reads a2 again. */
+   (vcg_bn_stats_from_gram) and the a2 form of the bn3 backward fold need, so that neither reads a2 again. g64
+   (optional, double [C * C + C]): the same Gram matrix then column sums in double, accumulated centred per workgroup
+   (the input of vcg_bn_stats_from_gram: no E[y^2] - E[y]^2 cancellation for large |mean| / std). */
 VCG_API long long vcg_bn_apply_gram_ws_bytes(long long P, int C);
-VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* shift, void* out, float* colsum, float* gram, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
-/* Batch statistics of y = x w^T (w bf16 [N][C], the conv's forward GEMM weights; M rows) from x's (gram, colsum):
+VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* shift, void* out, float* colsum, float* gram, double* g64, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
+/* Batch statistics of y = x w^T (w bf16 [N][C], the conv's forward GEMM weights; M rows) from x's double g64 =
+   (gram [C][C], colsum [C]) of vcg_bn_apply_gram:
    mean_n = w_n . colsum / M, var_n = w_n^T (gram / M - mu mu^T) w_n in double -- torchvision Bottleneck bn3 over
    conv3's output (model/vision/resnet50_tsm.py:15) without a statistics pass over a2. Writes the vcg_conv_fwd
    stats layout (one used slot) for vcg_bn_finalize. */
-VCG_API int vcg_bn_stats_from_gram(const float* gram, const float* colsum, const void* w, long long M, int N, int C, float* stats, int mtiles, hipStream_t s);
+VCG_API int vcg_bn_stats_from_gram(const double* g64, const void* w, long long M, int N, int C, float* stats, int mtiles, hipStream_t s);
 VCG_API int vcg_conv1x1_stats(const void* x, const void* w, float* stats, int M, int N, int K, hipStream_t stream);
 VCG_API int vcg_bn_bwd_sumgx_from_wgrad(const float* P, const void* w, int K, int C, const float* mean, const float* invstd, const float* sum_g, float* sum_gx, float* dgamma, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a, void* wfold, float* bias, hipStream_t stream);
@@ -165,7 +168,7 @@ VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* i
    output) instead of the pre-pool y: a window's gradient reaches its argmax pixel, whose ReLU output is mp, so the
    mask is mp > 0 and y - mean = (mp - mshift) / mscale - mean there (mscale != 0). The stem BN + ReLU + max-pool
    backward of Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15, torchvision bn1 -> relu -> maxpool). */
-VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void* mp, int N, int OH, int OW, int C, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t s);
+VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void* mp, const unsigned char* idx, const void* y, int N, int H, int W, int C, const float* mean, const float* invstd, const float* mscale, const float* mshift, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, hipStream_t s);
 /* the stem backward in two streaming passes (reference resnet50_tsm.py:19 torchvision stem: conv1 -> bn1 -> relu ->
    maxpool): dx = BN-backward-apply(g) with g = mask(maxpool_bwd(dy)) recomputed (rounded to dtype), sums from
    vcg_maxpool_bwd_bn(g = NULL) -- vcg_maxpool_bwd_bn + vcg_bn_bwd_apply without the g tensor */
@@ -175,8 +178,10 @@ VCG_API int vcg_maxpool_bwd_bn_apply(int dtype, const void* dy, const unsigned c
    conv-output row pair computed into LDS and contracted at once with the pair-packed frames x [N][2H][2W][4] into
    dW [64][3][7][7] (fp32, added to when accumulate) -- dy0 never reaches HBM. y [N][H][W][64], dy / idx
    [N][H/2][W/2][64]; H even, W % 8 == 0, W <= 112. Equals vcg_maxpool_bwd_bn_apply + vcg_conv_wgrad up to the
-   fp32 summation order (fixed: deterministic). */
+   fp32 summation order (fixed: deterministic). Returns VCG_ERR_UNSUPPORTED unless vcg_stem_bwd_fused_fits(N, H, W)
+   (every operand below 4 GB: 32-bit buffer offsets; the caller then runs the apply pass + weight gradient). */
 VCG_API long long vcg_stem_bwd_fused_ws_bytes(void);
+VCG_API int vcg_stem_bwd_fused_fits(int N, int H, int W);
 VCG_API int vcg_stem_bwd_fused(const void* dy, const unsigned char* idx, const void* y, const void* x, int N, int H, int W, const float* mean, const float* invstd, const float* mscale, const float* mshift, const float* gamma, const float* sum_g, const float* sum_gx, long long count, int train_stats, float* ws, long long ws_bytes, float* dw, int accumulate, hipStream_t s);
 /* the stem forward's BN + ReLU + maxpool 3x3/2 in one pass: out / idx = maxpool(relu(fma(y, scale, shift))) with the
    activation rounded to dtype (bit-identical to vcg_bn_apply then vcg_maxpool_fwd; no activation tensor) */

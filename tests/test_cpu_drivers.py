@@ -93,8 +93,10 @@ def test_synthetic_datasets_produce_reference_tuples():
 
 @pytest.mark.parametrize("ckpt", ["ck/", "ck/run", "ck/run.pth"])
 def test_ddp_checkpoint_search_matches_save_names(tmp_path, ckpt):
-    """find_latest_checkpoint looks where checkpoint_path writes, for a directory ("DIR/") and a name prefix
-    ("DIR/run", "DIR/run.pth") alike; other prefixes and non-checkpoint names are ignored."""
+    """find_latest_checkpoint: a directory ("DIR/") is searched as the reference does (every DIR/*.pth matched by
+    `_(\\d+)(?:_score_[\\d.]+)?\\.pth$`, whatever its prefix: other_9.pth wins); a name prefix ("DIR/run", "DIR/run.pth"),
+    where the reference finds nothing, is searched where checkpoint_path writes (other prefixes ignored). Names that
+    do not end in .pth are ignored either way."""
     import train_video_segment_ddp as drv
     path = str(tmp_path / ckpt)
     os.makedirs(tmp_path / "ck", exist_ok=True)
@@ -102,7 +104,29 @@ def test_ddp_checkpoint_search_matches_save_names(tmp_path, ckpt):
         p = drv.checkpoint_path(path, ep, best or 0.0, best is not None)
         open(p, "w").close()
     open(tmp_path / "ck" / "other_9.pth", "w").close()
-    open(tmp_path / "ck" / "run_7.pth.tmp", "w").close()
+    open(tmp_path / "ck" / "run_11.pth.tmp", "w").close()
     found, ep = drv.find_latest_checkpoint(path)
-    assert ep == 3 and found == drv.checkpoint_path(path, 3, 0.25, True)
+    if ckpt.endswith("/"):
+        assert ep == 9 and found == str(tmp_path / "ck" / "other_9.pth")
+        assert drv.find_latest_checkpoint(str(tmp_path / "ck"))[1] == 9  # (an existing directory without the "/")
+    else:
+        assert ep == 3 and found == drv.checkpoint_path(path, 3, 0.25, True)
     assert drv.find_latest_checkpoint(str(tmp_path / "none" / "x"))[0] is None
+
+
+@pytest.mark.parametrize("extra", [False, True])
+def test_ddp_fit_checkpoint_cadence(tmp_path, extra):
+    """The reference's cadence (train_video_segment_ddp.py:271-290): validation epochs write a best checkpoint when
+    the metric improves and never a regular one (`elif`); other epochs write a regular one every save_every epochs.
+    save_on_val_epochs adds the regular save on validation epochs without a new best."""
+    import train_video_segment_ddp as drv
+    tr = drv.DDPTrainer.__new__(drv.DDPTrainer)
+    results = iter([0.5, 0.4, float("nan")])  # epochs 2, 4, 6: best, worse, NaN
+    saved = []
+    tr.config = type("C", (), {"max_epochs": 7})()
+    tr.start_epoch, tr.best_result, tr.rank, tr.test_dataset = 0, float("-inf"), 1, object()
+    tr.run_epoch = lambda split, epoch: next(results) if split == "infer_test" else None
+    tr.save_checkpoint = lambda epoch, best, is_best=False: saved.append((epoch, is_best))
+    tr.fit(val_every=2, save_every=3, save_on_val_epochs=extra)
+    want = [(2, True), (3, False)] + ([(6, False)] if extra else [])
+    assert saved == want and tr.best_result == 0.5

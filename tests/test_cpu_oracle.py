@@ -131,6 +131,20 @@ def test_c_abi_library_exports_every_header_symbol():
     assert lib.vcg_version() == 1
 
 
+def test_stem_bwd_fused_size_guard():
+    """vcg_stem_bwd_fused addresses its operands with 32-bit buffer offsets: the host predicate admits the bench
+    shapes and refuses a conv output of 4 GB or more (y = N x 112 x 112 x 64 bf16: >= 2675 frames), where the trunk
+    runs the apply pass + weight gradient instead (host code only, no GPU)."""
+    from vcg_hip import ops
+    assert ops.stem_bwd_fused_fits(64 * 16, 112, 112)  # the C3 batch: 1024 frames, y 1.64 GB
+    lim = 0xFFFFFF00
+    n_max = (lim - 1) // (112 * 112 * 128)
+    assert ops.stem_bwd_fused_fits(n_max, 112, 112)
+    assert not ops.stem_bwd_fused_fits(n_max + 1, 112, 112)
+    assert not ops.stem_bwd_fused_fits(168 * 16, 112, 112)
+    assert not ops.stem_bwd_fused_fits(0, 112, 112)
+
+
 def test_no_cpu_fallback():
     """The product path refuses CPU tensors loudly."""
     from vcg_hip import ops

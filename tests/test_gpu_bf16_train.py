@@ -314,16 +314,24 @@ def test_full_res_train_step_vs_oracle():
     lo, lgo, vo, go = _oracle_step(T, HW, L, B, seed=11)
     la, lga, va, ga = _oracle_step(T, HW, L, B, seed=11, autocast=True)
     frames, ids, mask, labels = synth.clip_batch(B, T, HW, HW, L, seed=11, device=DEV)
+    from vcg_hip.trunk import ResNetTrunk
     res = {}
     for prec in ("fp32", "bf16"):
         m = _model(T, prec)
         from vcg_hip.functions import cross_entropy
         opt = m.configure_optimizers(_Cfg)
         opt.zero_grad()
-        lg, _, ve, _ = m(frames, ids, mask, return_emb=True)
-        loss = cross_entropy(lg, labels)
-        loss.backward()
-        torch.cuda.synchronize()
+        ResNetTrunk.census = [] if prec == "bf16" else None
+        try:
+            lg, _, ve, _ = m(frames, ids, mask, return_emb=True)
+            loss = cross_entropy(lg, labels)
+            loss.backward()
+            torch.cuda.synchronize()
+            census = ResNetTrunk.census
+        finally:
+            ResNetTrunk.census = None
+        if prec == "bf16":  # the oracle-anchored bf16 step ran the benchmarked per-block paths
+            _check_census(census)
         res[prec] = (loss.item(), lg.detach().double().cpu(), ve.detach().double().cpu(),
                      {n: p.grad.detach().double().cpu() for n, p in m.named_parameters()})
         del m, opt

@@ -830,12 +830,15 @@ def test_weight_prep_multi(K):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("hw", [(13, 12), (16, 10), (112, 112)])
-def test_maxpool_bwd_bn_sums_pooled(K, dtype, hw):
+@pytest.mark.parametrize("hw,degen", [((13, 12), False), ((16, 10), False), ((112, 112), False), ((16, 10), True),
+                                      ((112, 112), True)])
+def test_maxpool_bwd_bn_sums_pooled(K, dtype, hw, degen):
     """The stem BN-backward sums from the pooled activation (a window's gradient reaches its argmax pixel, whose
     activation is mp) == the per-pixel pass over y, up to rounding: the per-pixel pass sums g rounded to dtype per
     pixel (after adding the <= 4 windows' dy), and for g*xhat recovers nothing (y is read), while the pooled pass
-    recovers y as (mp - shift) / scale, exact up to mp's rounding to dtype (bf16: 2^-9 relative per term)."""
+    recovers y as (mp - shift) / scale, exact up to mp's rounding to dtype (bf16: 2^-9 relative per term).
+    degen: channels with a zero BN scale (either sign of the shift) and a tiny one, where mp says nothing about y:
+    the kernel reads y at the argmax pixel for them (finite sums equal to the per-pixel pass)."""
     N, C = 3, 64
     H, W = hw
     y = _rand((N, H, W, C), dtype, 88).to(DEV)
@@ -843,6 +846,11 @@ def test_maxpool_bwd_bn_sums_pooled(K, dtype, hw):
     sc = (torch.rand(C, generator=g0) * 2 - 0.5).to(DEV)
     sc = torch.where(sc.abs() < 0.05, torch.full_like(sc, 0.05), sc)
     sh = (torch.randn(C, generator=g0) * 0.3).to(DEV)
+    if degen:
+        sc[3], sh[3] = 0.0, 0.4
+        sc[9], sh[9] = 0.0, -0.2
+        sc[17], sh[17] = 0.0, 0.0
+        sc[40], sh[40] = 1e-4, 0.5
     mp, idx = K.bn_relu_maxpool(y, sc, sh, N, H, W, C)
     dys = _rand(mp.shape, dtype, 90).to(DEV)
     mean = (torch.randn(C, generator=g0) * 0.1).to(DEV)
@@ -850,7 +858,9 @@ def test_maxpool_bwd_bn_sums_pooled(K, dtype, hw):
     s_ref, s_new = torch.zeros((2, C), device=DEV), torch.zeros((2, C), device=DEV)
     dg, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), 0.25, device=DEV)
     K.maxpool_bwd_bn(dys, idx, N, H, W, C, y, mean, inv, sc, sh, s_ref, store_g=False)
-    K.maxpool_bwd_bn_sums_pooled(dys, mp, N, mp.shape[1], mp.shape[2], C, mean, inv, sc, sh, s_new, dg, db)
+    K.maxpool_bwd_bn_sums_pooled(dys, mp, idx, y, N, H, W, C, mean, inv, sc, sh, s_new, dg, db)
+    torch.cuda.synchronize()
+    assert torch.isfinite(s_new).all()
     tol = 1e-5 if dtype == torch.float32 else 4e-3
     for k in range(2):
         scale = s_ref[k].abs().max().item() + 1

@@ -16,9 +16,16 @@
 // with the 16-B chunk swizzle of the weight-gradient engine (igemm_wgrad.hip wswz), from which ds_read_b64_tr_b16
 // gives each lane 4 consecutive rows of one column. The C x C Gram block pairs (jb <= kb of 16 x 16, the upper
 // triangle: G is symmetric) are dealt round-robin to the 4 waves and accumulated with v_mfma_f32_16x16x32_bf16
-// over every row the workgroup sees (two LDS buffers, one barrier per iteration). Each workgroup writes a
-// [C * C + C] f32 slab (G mirrored to full, then colsum); gram_reduce sums the slabs in a fixed order in double
-// (deterministic).
+// over every row the workgroup sees (two LDS buffers, one barrier per iteration).
+//
+// Precision: y3's variance is w^T (G / M - mu mu^T) w, which cancels like E[y^2] - E[y]^2 when a y3 channel's |mean|
+// is much larger than its std. So the Gram is not formed from a but from a - c_b, with c_b the bf16-rounded column
+// means of the workgroup's FIRST iteration of rows (a per-workgroup centre close to the batch mean): the fp32 MFMA
+// accumulation then carries an error relative to the centred (variance-sized) entries, not to mean^2. Each
+// workgroup writes a [C * C + 2 C] f32 slab (centred G_b mirrored to full, centred colsum d_b = sum (a - c_b),
+// centre c_b); gram_reduce rebuilds the uncentred colsum = sum_b (d_b + n_b c_b) and
+// G = sum_b (G_b + d_b c_b^T + c_b d_b^T + n_b c_b c_b^T) in double in a fixed order (deterministic), and the
+// statistics kernel subtracts mu mu^T in double.
 #include "common.h"
 
 namespace vcg {
@@ -120,6 +127,35 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
     }
   };
   if (it < iters) load(it);
+  // the Gram centre c_b: bf16 column means of this workgroup's first iteration (every workgroup has one: grid <=
+  // iters), summed in a fixed order through LDS
+  float ctr[8];
+  {
+    float ps[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ps[e] = 0.f;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      if (it * R + r0 + u * RS < P) {
+        float a[8];
+        unpack8g(nx[u], a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ps[e] += bf2f(f2bf(fmaxf(fmaf(a[e], sc[e], sh[e]), 0.f)));
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[tid * 9 + e] = ps[e];
+    __syncthreads();
+    const long long left = P - it * R;
+    const float inv = 1.f / (float)(left < R ? left : R);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = 0.f;
+      for (int q = cc; q < 256; q += CPR) t += red[q * 9 + e];
+      ctr[e] = bf2f(f2bf(t * inv));
+    }
+    __syncthreads();  // (red is written again only after the main loop)
+  }
   int cur = 0;
   for (; it < iters; it += gridDim.x) {
     uint4 v[NV];
@@ -133,7 +169,7 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
       const long long row = it * R + lr;
       float a[8];
       unpack8g(v[u], a);
-      uint4 o = make_uint4(0u, 0u, 0u, 0u);
+      uint4 o = make_uint4(0u, 0u, 0u, 0u), d = make_uint4(0u, 0u, 0u, 0u);
       if (row < P) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) a[e] = fmaxf(fmaf(a[e], sc[e], sh[e]), 0.f);
@@ -145,12 +181,19 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
         float st[8];
         unpack8g(o, st);  // the stored (rounded) values
 #pragma unroll
-        for (int e = 0; e < 8; ++e) cs[e] += st[e];
+        for (int e = 0; e < 8; ++e) {
+          st[e] -= ctr[e];  // (exact in f32: both bf16 values)
+          cs[e] += st[e];   // the centred column sum (no cancellation against n c later)
+        }
+        d.x = (uint32_t)f2bf(st[0]) | ((uint32_t)f2bf(st[1]) << 16);
+        d.y = (uint32_t)f2bf(st[2]) | ((uint32_t)f2bf(st[3]) << 16);
+        d.z = (uint32_t)f2bf(st[4]) | ((uint32_t)f2bf(st[5]) << 16);
+        d.w = (uint32_t)f2bf(st[6]) | ((uint32_t)f2bf(st[7]) << 16);
       }
       // LDS: k-step lr / 64, k-row lr % 64, panel cc / (COLS / 8), swizzled slot of chunk cc % (COLS / 8)
       const int ks = lr >> 6, kr = lr & 63, pn = cc / (COLS / 8), pc = cc % (COLS / 8);
       bf16_t* dst = B + (ks * NP + pn) * 64 * COLS + kr * COLS + 8 * gswz<COLS>(kr, pc);
-      *reinterpret_cast<uint4*>(dst) = o;  // (rows past P: zeros, no contribution)
+      *reinterpret_cast<uint4*>(dst) = d;  // the centred row (rows past P: zeros, no contribution)
     }
     __syncthreads();  // the tile is in LDS; every wave's reads of the other buffer (two iterations ago) are done
 #pragma unroll
@@ -171,8 +214,8 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
     }
     cur ^= 1;
   }
-  // slab: G (mirrored to the full matrix) then colsum
-  float* sl = slab + (long long)blockIdx.x * (C * C + C);
+  // slab: the centred G (mirrored to the full matrix), centred colsum, centre
+  float* sl = slab + (long long)blockIdx.x * (C * C + 2 * C);
   const int g = lane >> 4, ci = lane & 15;
 #pragma unroll
   for (int t = 0; t < NF; ++t) {
@@ -194,6 +237,10 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
     for (int t = ch; t < 256; t += CPR) s += red[t * 9 + e];  // fixed order
     sl[C * C + o] = s;
   }
+  if (tid < CPR) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sl[C * C + C + 8 * tid + e] = ctr[e];
+  }
 }
 
 template <int C>
@@ -210,31 +257,56 @@ __global__ __launch_bounds__(256) void bn_apply_gram_kernel(const bf16_t* __rest
   }
 }
 
-// out[i] = sum over nb slabs of slab[b][i], in double (deterministic): a thread owns 4 consecutive entries (16-B
-// loads) and G threads split the slabs (thread t sums slabs t, t + G, ... in order, the G partials are combined in
-// t order through LDS). (One thread per entry over all 256-512 slabs ran latency-bound: 100 us per call at C = 64.)
+// Rows of `slab` b: the iterations b, b + nb, ... of R rows each, the last one possibly short.
+__device__ __forceinline__ double slab_rows(int b, int nb, long long P, int R) {
+  const long long iters = (P + R - 1) / R;
+  const long long nit = (iters - 1 - b) / nb + 1;
+  long long n = nit * R;
+  if ((iters - 1) % nb == b) n -= iters * R - P;
+  return (double)n;
+}
+
+// out[i] = the uncentred sum over nb slabs, in double (deterministic): for a Gram entry (j, k)
+// sum_b G_b[j][k] + d_b[j] c_b[k] + c_b[j] d_b[k] + n_b c_b[j] c_b[k], for a column sum sum_b d_b[k] + n_b c_b[k]
+// (G_b, d_b: centred at c_b). A thread owns 4
+// consecutive entries (16-B loads) and G threads split the slabs (thread t sums slabs t, t + G, ... in order, the G
+// partials are combined in t order through LDS). (One thread per entry over all 256-512 slabs ran latency-bound:
+// 100 us per call at C = 64.) Writes f32 gram / colsum and, when g64 != null, the double [C * C + C].
 __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ slab, int nb, int n, int G,
-                                                         float* __restrict__ gram, float* __restrict__ colsum, int C) {
+                                                         float* __restrict__ gram, float* __restrict__ colsum, int C,
+                                                         double* __restrict__ g64, long long P, int R) {
   __shared__ double red[4][256];
   const int QB = 256 / G;
   const int t = threadIdx.x / QB, ql = threadIdx.x - t * QB;
   const int quad = blockIdx.x * QB + ql, nq = n >> 2;
+  const int ns = C * C + 2 * C;  // slab stride (floats)
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   if (quad < nq) {
-    const float4* p = reinterpret_cast<const float4*>(slab) + quad;
-    int b = t;
-    for (; b + 3 * G < nb; b += 4 * G) {
-      float4 v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = p[(long long)(b + k * G) * nq];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        s0 += (double)v[k].x; s1 += (double)v[k].y; s2 += (double)v[k].z; s3 += (double)v[k].w;
+    const int i0 = 4 * quad;
+    if (i0 < C * C) {
+      const int j = i0 / C, k = i0 - j * C;
+      for (int b = t; b < nb; b += G) {
+        const float* sb = slab + (long long)b * ns;
+        const float4 g = *reinterpret_cast<const float4*>(sb + i0);
+        const float4 sk = *reinterpret_cast<const float4*>(sb + C * C + k);
+        const float4 ck = *reinterpret_cast<const float4*>(sb + C * C + C + k);
+        const double sj = (double)sb[C * C + j], cj = (double)sb[C * C + C + j];
+        const double nr = slab_rows(b, nb, P, R);
+        const double ncj = nr * cj;
+        s0 += (double)g.x + sj * (double)ck.x + cj * (double)sk.x + ncj * (double)ck.x;
+        s1 += (double)g.y + sj * (double)ck.y + cj * (double)sk.y + ncj * (double)ck.y;
+        s2 += (double)g.z + sj * (double)ck.z + cj * (double)sk.z + ncj * (double)ck.z;
+        s3 += (double)g.w + sj * (double)ck.w + cj * (double)sk.w + ncj * (double)ck.w;
       }
-    }
-    for (; b < nb; b += G) {
-      const float4 v = p[(long long)b * nq];
-      s0 += (double)v.x; s1 += (double)v.y; s2 += (double)v.z; s3 += (double)v.w;
+    } else {
+      for (int b = t; b < nb; b += G) {
+        const float* sb = slab + (long long)b * ns;
+        const float4 v = *reinterpret_cast<const float4*>(sb + i0);
+        const float4 c = *reinterpret_cast<const float4*>(sb + i0 + C);
+        const double nr = slab_rows(b, nb, P, R);
+        s0 += (double)v.x + nr * (double)c.x; s1 += (double)v.y + nr * (double)c.y;
+        s2 += (double)v.z + nr * (double)c.z; s3 += (double)v.w + nr * (double)c.w;
+      }
     }
   }
   if (G > 1) {
@@ -253,21 +325,24 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
     const int i = 4 * quad + e;
     if (i < C * C) gram[i] = (float)sv[e];
     else colsum[i - C * C] = (float)sv[e];
+    if (g64) g64[i] = sv[e];
   }
 }
 
-// bn3's batch statistics from (G, colsum) and conv3's bf16 weights w [N][C]: 8 output columns per workgroup,
-// thread t < C owns row t of the covariance; double throughout. Writes the vcg_conv_fwd stats layout with one
-// used slot: stats[n][0] = (mean, M2 = M var), count row slot 0 = (M, 1).
-__global__ __launch_bounds__(256) void gram_stats_kernel(const float* __restrict__ gram, const float* __restrict__ colsum,
-                                                        const bf16_t* __restrict__ w, long long M, int N, int C,
-                                                        float2* __restrict__ stats, int mtiles) {
+// bn3's batch statistics from the double (G, colsum) g64 [C * C + C] and conv3's bf16 weights w [N][C]: 8 output
+// columns per workgroup, thread t < C owns row t of the covariance; double throughout. Writes the vcg_conv_fwd stats
+// layout with one used slot: stats[n][0] = (mean, M2 = M var), count row slot 0 = (M, 1).
+__global__ __launch_bounds__(256) void gram_stats_kernel(const double* __restrict__ g64, const bf16_t* __restrict__ w,
+                                                        long long M, int N, int C, float2* __restrict__ stats,
+                                                        int mtiles) {
+  const double* __restrict__ gram = g64;
+  const double* __restrict__ colsum = g64 + (long long)C * C;
   __shared__ double mu[1024];
   __shared__ double wq[8][1024];
   __shared__ double pm[8][256], pv[8][256];
   const int n0 = blockIdx.x * 8, tid = threadIdx.x;
   const double invM = 1.0 / (double)M;
-  for (int k = tid; k < C; k += 256) mu[k] = (double)colsum[k] * invM;
+  for (int k = tid; k < C; k += 256) mu[k] = colsum[k] * invM;
   for (int i = tid; i < 8 * C; i += 256) {
     const int q = i / C, k = i - q * C;
     wq[q][k] = n0 + q < N ? (double)bf2f(w[(long long)(n0 + q) * C + k]) : 0.0;
@@ -280,9 +355,9 @@ __global__ __launch_bounds__(256) void gram_stats_kernel(const float* __restrict
     double u[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) u[q] = 0.0;
-    const float* gr = gram + (long long)t * C;
+    const double* gr = gram + (long long)t * C;
     for (int k = 0; k < C; ++k) {
-      const double cv = (double)gr[k] * invM - mu[t] * mu[k];
+      const double cv = gr[k] * invM - mu[t] * mu[k];
 #pragma unroll
       for (int q = 0; q < 8; ++q) u[q] = fma(cv, wq[q][k], u[q]);
     }
@@ -325,20 +400,23 @@ using namespace vcg;
 
 VCG_API long long vcg_bn_apply_gram_ws_bytes(long long P, int C) {
   if (C != 64 && C != 128 && C != 256) return 0;
-  return (long long)gram_grid(P, C) * ((long long)C * C + C) * 4;
+  return (long long)gram_grid(P, C) * ((long long)C * C + 2 * C) * 4;
 }
 
 // out = bf16(relu(fma(y, scale, shift))) (vcg_bn_apply's values), colsum[c] = sum of out's column c (as
-// vcg_bn_apply_colsum), gram[j][k] = sum_rows out[j] out[k] (f32 [C][C]). C = 64 / 128 / 256, bf16.
+// vcg_bn_apply_colsum), gram[j][k] = sum_rows out[j] out[k] (f32 [C][C]); g64 (optional): the same Gram matrix and
+// column sums in double, [C * C + C] (accumulated centred per workgroup, see the file comment: the input of
+// vcg_bn_stats_from_gram). C = 64 / 128 / 256, bf16.
 VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* shift, void* out, float* colsum,
-                              float* gram, float* ws, long long ws_bytes, long long P, int C, hipStream_t s) {
+                              float* gram, double* g64, float* ws, long long ws_bytes, long long P, int C,
+                              hipStream_t s) {
   VCG_REQUIRE(y && scale && shift && out && colsum && gram && ws, "null argument");
   VCG_REQUIRE(C == 64 || C == 128 || C == 256, "C must be 64, 128 or 256");
   VCG_REQUIRE(P > 0, "no rows");
   VCG_REQUIRE((((uintptr_t)y | (uintptr_t)out) & 15) == 0, "16-B alignment");
   const int g = gram_grid(P, C);
   const long long n = (long long)C * C + C;
-  VCG_REQUIRE(ws_bytes >= (long long)g * n * 4, "workspace too small");
+  VCG_REQUIRE(ws_bytes >= vcg_bn_apply_gram_ws_bytes(P, C), "workspace too small");
   if (C == 64)
     hipLaunchKernelGGL(bn_apply_gram_kernel<64>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
                        (bf16_t*)out, ws, P);
@@ -354,19 +432,19 @@ VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* sh
   while (G < 64 && G * 2 <= g && (long long)nq * G < 65536) G *= 2;
   const int QB = 256 / G;
   hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((nq + QB - 1) / QB)), dim3(256), 0, s, ws, g, (int)n, G, gram,
-                     colsum, C);
+                     colsum, C, g64, P, 16384 / C);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
 
-// conv3's batch statistics from vcg_bn_apply_gram's (gram, colsum) of its input and its bf16 weights w [N][C]
-// (the forward GEMM layout): stats in the vcg_conv_fwd layout ([N + 1][mtiles] float2, one used slot), for
-// vcg_bn_finalize.
-VCG_API int vcg_bn_stats_from_gram(const float* gram, const float* colsum, const void* w, long long M, int N, int C,
-                                   float* stats, int mtiles, hipStream_t s) {
-  VCG_REQUIRE(gram && colsum && w && stats, "null argument");
+// conv3's batch statistics from vcg_bn_apply_gram's double g64 (Gram matrix then column sums) of its input and its
+// bf16 weights w [N][C] (the forward GEMM layout): stats in the vcg_conv_fwd layout ([N + 1][mtiles] float2, one
+// used slot), for vcg_bn_finalize.
+VCG_API int vcg_bn_stats_from_gram(const double* g64, const void* w, long long M, int N, int C, float* stats,
+                                   int mtiles, hipStream_t s) {
+  VCG_REQUIRE(g64 && w && stats, "null argument");
   VCG_REQUIRE(C > 0 && C <= 1024 && N > 0 && M > 0 && mtiles > 0, "bad shape");
-  hipLaunchKernelGGL(gram_stats_kernel, dim3((N + 7) / 8), dim3(256), 0, s, gram, colsum, (const bf16_t*)w, M, N, C,
+  hipLaunchKernelGGL(gram_stats_kernel, dim3((N + 7) / 8), dim3(256), 0, s, g64, (const bf16_t*)w, M, N, C,
                      reinterpret_cast<float2*>(stats), mtiles);
   VCG_LAUNCH_CHECK();
   return VCG_OK;

@@ -362,6 +362,16 @@ using namespace vcg;
 
 VCG_API long long vcg_stem_bwd_fused_ws_bytes(void) { return (long long)SB_GRID * 64 * SB_N * 4; }
 
+// 1 when vcg_stem_bwd_fused takes this shape (conv output [N][H][W][64]): every operand's byte range fits the 32-bit
+// buffer offsets -- y [N][H][W][64] bf16, dy [N][OH][OW][64] bf16, idx [N][OH][OW][64] u8, x [N][2H][W][8] bf16
+VCG_API int vcg_stem_bwd_fused_fits(int N, int H, int W) {
+  const long long lim = 0xFFFFFF00LL;
+  const long long OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const long long yb = (long long)N * H * W * 128, db = (long long)N * OH * OW * 128;
+  const long long ib = (long long)N * OH * OW * 64, xb = (long long)N * 2 * H * W * 16;
+  return N > 0 && H > 0 && W > 0 && yb < lim && db < lim && ib < lim && xb < lim;
+}
+
 // The stem backward from the pooled-output gradient to the stem conv's weight gradient (bf16): max-pool backward
 // (argmax idx), BN1 + ReLU backward with the sums of vcg_maxpool_bwd_bn(_sums_pooled) (mask from y * mscale +
 // mshift > 0, batch statistics when train_stats), and dW of the 7x7 / stride 2 / pad 3 conv over the RGB0 frames
@@ -376,6 +386,11 @@ VCG_API int vcg_stem_bwd_fused(const void* dy, const unsigned char* idx, const v
               "arguments required");
   VCG_REQUIRE(N > 0 && H > 0 && H % 2 == 0 && W % 8 == 0 && W <= SB_MAXW, "H even, W a multiple of 8, W <= 112");
   VCG_REQUIRE(ws_bytes >= vcg_stem_bwd_fused_ws_bytes(), "workspace too small");
+  // every operand is addressed by a 32-bit buffer offset: y (the largest, 8x the frames) must stay below 4 GB
+  if (!vcg_stem_bwd_fused_fits(N, H, W)) {
+    vcg::set_error("vcg_stem_bwd_fused: y / dy / idx / x must each be below 4 GB (32-bit buffer offsets)");
+    return VCG_ERR_UNSUPPORTED;
+  }
   StemBwdArgs a{};
   a.dy = (const bf16_t*)dy; a.idx = idx; a.y = (const bf16_t*)y; a.x = (const bf16_t*)x;
   a.mean = mean; a.invstd = invstd; a.msc = mscale; a.msh = mshift; a.gamma = gamma; a.sum_g = sum_g;

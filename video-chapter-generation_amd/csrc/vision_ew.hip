@@ -780,22 +780,33 @@ __global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const T* __restrict__
 // sum_gx = invstd * sum [mp > 0] dy (y - mean). Reads dy and mp once (1/2 of the output rows' bytes each) instead
 // of dy, the argmax bytes and the whole pre-pool y (the stem's conv output, 4x the pooled size). mp is the bf16
 // max, so y - mean carries one bf16 rounding of the activation (the per-pixel path carries that of y).
+// Degenerate channels -- msc == 0 (a zero BN weight: mp says nothing about y) or |msh| > 32 |gamma| (the recovery
+// cancels: its error is ~2^-9 |msh| / |gamma| of a std) -- read y at the window's argmax pixel instead (idx byte
+// k: pixel (2 oh - 1 + k / 3, 2 ow - 1 + k % 3) of the [N][H][W][C] pre-pool y), for the windows that pass the mask.
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_bn_sums_pooled_kernel(const T* __restrict__ dy, const T* __restrict__ mp,
-                                                                     long long TV, int lcpr, MpBn bn) {
+                                                                     const uint8_t* __restrict__ idx,
+                                                                     const T* __restrict__ y, int H, int W, int OH,
+                                                                     int OW, long long TV, int lcpr, MpBn bn) {
   constexpr int VN = V<T>::N;
   __shared__ float red[2][256][VN];
   const int cpr = 1 << lcpr;
   const int chunk = threadIdx.x & (cpr - 1);
   const int c0 = chunk * VN;
-  float mu[VN], sc[VN], sh[VN], rsc[VN], off[VN], s1[VN], s2[VN];
+  const int C = cpr * VN;
+  float mu[VN], sc[VN], sh[VN], is[VN], rsc[VN], off[VN], s1[VN], s2[VN];
+  bool degen[VN];
+  bool any_degen = false;
   load_params<VN>(bn.mean, c0, mu);
   load_params<VN>(bn.msc, c0, sc);
   load_params<VN>(bn.msh, c0, sh);
+  load_params<VN>(bn.invstd, c0, is);
 #pragma unroll
   for (int e = 0; e < VN; ++e) {
-    rsc[e] = 1.f / sc[e];
-    off[e] = -sh[e] * rsc[e] - mu[e];  // y - mean = mp / msc + off
+    degen[e] = sc[e] == 0.f || !(fabsf(sh[e]) * is[e] <= 32.f * fabsf(sc[e]));
+    any_degen |= degen[e];
+    rsc[e] = degen[e] ? 0.f : 1.f / sc[e];
+    off[e] = degen[e] ? 0.f : -sh[e] * rsc[e] - mu[e];  // y - mean = mp / msc + off
     s1[e] = s2[e] = 0.f;
   }
   const long long stride = (long long)gridDim.x * SB;
@@ -816,6 +827,22 @@ __global__ __launch_bounds__(256) void maxpool_bn_sums_pooled_kernel(const T* __
         s1[e] += d;
         s2[e] = fmaf(d, fmaf(m[u][e], rsc[e], off[e]), s2[e]);
       }
+      if (any_degen) {  // (rare: a per-element gather of y at the argmax pixel)
+        const long long v = base + u * 256;
+        const long long pix = v >> lcpr;  // pooled pixel (n, oh, ow)
+        const int ow = (int)(pix % OW);
+        const long long t = pix / OW;
+        const int oh = (int)(t % OH);
+        const long long n = t / OH;
+#pragma unroll
+        for (int e = 0; e < VN; ++e) {
+          if (!degen[e] || !(m[u][e] > 0.f)) continue;
+          const int k = idx[v * VN + e];
+          const int ih = 2 * oh - 1 + k / 3, iw = 2 * ow - 1 + k % 3;
+          const float yv = to_f<T>(y[((n * H + ih) * W + iw) * C + c0 + e]);
+          s2[e] = fmaf(g[u][e], yv - mu[e], s2[e]);
+        }
+      }
     }
   }
 #pragma unroll
@@ -824,7 +851,6 @@ __global__ __launch_bounds__(256) void maxpool_bn_sums_pooled_kernel(const T* __
     red[1][threadIdx.x][e] = s2[e];
   }
   __syncthreads();
-  const int C = cpr * VN;
   for (int i = threadIdx.x; i < 2 * C; i += 256) {
     const int which = i >= C, c = i - which * C;
     const int ch = c / VN, e = c - ch * VN;
@@ -1170,16 +1196,18 @@ VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* i
 }
 
 // The sums of vcg_maxpool_bwd_bn (g == NULL) from the pooled activation mp [N][OH][OW][C] (the fused stem's
-// vcg_bn_relu_maxpool output) instead of the pre-pool y: see maxpool_bn_sums_pooled_kernel. mscale must be nonzero
-// (the BatchNorm weight times invstd).
-VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void* mp, int N, int OH, int OW, int C,
-                                           const float* mean, const float* invstd, const float* mscale,
-                                           const float* mshift, float* ws, long long ws_bytes, float* sum_g,
-                                           float* sum_gx, float* dgamma, float* dbeta, hipStream_t s) {
+// vcg_bn_relu_maxpool output) instead of the pre-pool y: see maxpool_bn_sums_pooled_kernel. idx (the forward's argmax
+// bytes) and the pre-pool y [N][H][W][C] are read only for degenerate channels (zero or tiny BN weight).
+VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void* mp, const unsigned char* idx,
+                                           const void* y, int N, int H, int W, int C, const float* mean,
+                                           const float* invstd, const float* mscale, const float* mshift, float* ws,
+                                           long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma,
+                                           float* dbeta, hipStream_t s) {
   const int VN = dtype == VCG_BF16 ? 8 : 4;
   VCG_REQUIRE(C % VN == 0 && (C & (C - 1)) == 0 && C / VN <= 256, "C must be a power of two multiple of the vector width");
-  VCG_REQUIRE(dy && mp && mean && invstd && mscale && mshift && sum_g && sum_gx, "BN arguments required");
+  VCG_REQUIRE(dy && mp && idx && y && mean && invstd && mscale && mshift && sum_g && sum_gx, "BN arguments required");
   VCG_REQUIRE(ws_bytes >= vcg_maxpool_bwd_bn_ws_bytes(C), "workspace too small");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
   const int lcpr = ilog2i(C / VN);
   const long long TV = (long long)N * OH * OW * (C / VN);
   if (TV == 0) return VCG_OK;
@@ -1188,10 +1216,10 @@ VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void
   bn.mean = mean; bn.invstd = invstd; bn.msc = mscale; bn.msh = mshift; bn.part = ws;
   if (dtype == VCG_BF16)
     hipLaunchKernelGGL(maxpool_bn_sums_pooled_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dy,
-                       (const bf16_t*)mp, TV, lcpr, bn);
+                       (const bf16_t*)mp, idx, (const bf16_t*)y, H, W, OH, OW, TV, lcpr, bn);
   else
     hipLaunchKernelGGL(maxpool_bn_sums_pooled_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dy,
-                       (const float*)mp, TV, lcpr, bn);
+                       (const float*)mp, idx, (const float*)y, H, W, OH, OW, TV, lcpr, bn);
   VCG_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
                      sum_g, sum_gx, dgamma, dbeta, 1);

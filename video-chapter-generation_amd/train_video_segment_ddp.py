@@ -36,19 +36,23 @@ CKPT_RE = re.compile(r"_(\d+)(?:_score_[\d.]+)?\.pth$")
 
 
 def find_latest_checkpoint(ckpt_path, rank=0):
-    """(path, epoch) of the newest `<base>_<epoch>[_score_<s>].pth` that `checkpoint_path(ckpt_path, ...)` would have
-    written, found on rank 0 and broadcast (`train_video_segment_ddp.py:176-207`); (None, 0) when there is none.
-    The search looks where the saves go: `<base>` = splitext(ckpt_path)[0], so "DIR/" finds DIR/_<e>.pth and "DIR/run"
-    finds DIR/run_<e>.pth (the reference globs ckpt_path as a directory, which only agrees with its own save names
-    for a trailing "/"). The epoch rule is the reference's `_(\\d+)(?:_score_[\\d.]+)?\\.pth$`."""
+    """(path, epoch) of the newest checkpoint, found on rank 0 and broadcast (`train_video_segment_ddp.py:176-207`);
+    (None, 0) when there is none. The epoch rule is the reference's `_(\\d+)(?:_score_[\\d.]+)?\\.pth$` (re.search).
+    A directory ckpt_path ("DIR/", or an existing directory) is searched exactly as the reference does: every
+    DIR/*.pth whose name matches, whatever its prefix. A name prefix ("DIR/run", "DIR/run.pth") -- where the
+    reference's directory glob finds nothing and so never resumes -- is searched where checkpoint_path() writes:
+    DIR/run_<epoch>[_score_<s>].pth only."""
     info = (None, 0)
     if rank == 0 and ckpt_path:
-        base = os.path.splitext(ckpt_path)[0]
-        folder, prefix = os.path.dirname(base) or ".", os.path.basename(base)
-        name_re = re.compile(re.escape(prefix) + CKPT_RE.pattern)
+        if ckpt_path.endswith(os.sep) or os.path.isdir(ckpt_path):
+            folder, name_re, match = ckpt_path, CKPT_RE, CKPT_RE.search
+        else:
+            base = os.path.splitext(ckpt_path)[0]
+            folder, prefix = os.path.dirname(base) or ".", os.path.basename(base)
+            match = re.compile(re.escape(prefix) + CKPT_RE.pattern).fullmatch
         best = (None, -1)
-        for f in glob.glob(os.path.join(glob.escape(folder), "*.pth")):
-            m = name_re.fullmatch(os.path.basename(f))
+        for f in sorted(glob.glob(os.path.join(glob.escape(folder), "*.pth"))):
+            m = match(os.path.basename(f))
             if m and int(m.group(1)) > best[1]:
                 best = (f, int(m.group(1)))
         if best[0] is not None:
@@ -111,16 +115,14 @@ class DDPTrainer:
                     "optimizer_state_dict": self.optimizer.state_dict()}, path)
         return path
 
-    def fit(self, val_every=30, save_every=10):
+    def fit(self, val_every=30, save_every=10, save_on_val_epochs=False):
         """The reference's epoch loop (`:265-290`): validation every `val_every` epochs (rank-averaged metric; a best
-        checkpoint when it improves) and a regular checkpoint every `save_every` epochs. The reference takes the
-        regular save only on non-validation epochs (an `elif`); here it is taken on every `save_every` epoch that did
-        not already write a best checkpoint, so a validation epoch with a NaN or non-improving metric does not lose
-        the epoch's progress for a resume."""
+        checkpoint when it improves), else a regular checkpoint every `save_every` epochs (the reference's `elif`: a
+        validation epoch never writes a regular checkpoint). save_on_val_epochs (not the reference's cadence): a
+        validation epoch that wrote no best checkpoint (NaN or no improvement) takes the regular save too."""
         best, result = self.best_result, None
         for epoch in range(self.start_epoch + 1, self.config.max_epochs + 1):
             self.run_epoch("train", epoch)
-            saved = False
             if self.test_dataset is not None and epoch % val_every == 0:
                 result = self.run_epoch("infer_test", epoch)
                 if self.rank == 0:
@@ -128,8 +130,9 @@ class DDPTrainer:
                 if result == result and result > best:
                     best = result
                     self.save_checkpoint(epoch, best, is_best=True)
-                    saved = True
-            if not saved and epoch % save_every == 0:
+                elif save_on_val_epochs and epoch % save_every == 0:
+                    self.save_checkpoint(epoch, best, is_best=False)
+            elif epoch % save_every == 0:
                 self.save_checkpoint(epoch, best, is_best=False)
         self.best_result = best
         return result
@@ -216,6 +219,8 @@ def main(argv=None):
                    help="checkpoint directory (+ name prefix); training resumes from its newest checkpoint")
     p.add_argument("--val_every", default=1, type=int, help="validate every N epochs (the reference: 30)")
     p.add_argument("--save_every", default=10, type=int, help="regular checkpoint every N epochs (the reference: 10)")
+    p.add_argument("--save_on_val_epochs", action="store_true",
+                   help="also take the regular checkpoint on validation epochs without a new best (not the reference)")
     args = p.parse_args(argv)
 
     from common_utils import set_random_seed
@@ -248,7 +253,7 @@ def _fit(tr, args, world):
     resumed = tr.resume()
     if resumed and tr.rank == 0:
         print(f"resumed from {resumed} (epoch {tr.start_epoch}, best {tr.best_result})")
-    result = tr.fit(args.val_every, args.save_every)
+    result = tr.fit(args.val_every, args.save_every, args.save_on_val_epochs)
     if world > 1:
         dist.destroy_process_group()
     return result

@@ -177,24 +177,28 @@ def bn_apply_colsum(y, scale, shift, C, relu=True):
 
 
 def bn_apply_gram(y, scale, shift, C):
-    """(relu(bn_apply(y)), its column sums f32 [C], its Gram matrix out^T out f32 [C, C]) in one pass
-    (vcg_bn_apply_gram, bf16, C in 64 / 128 / 256)."""
+    """(relu(bn_apply(y)), its column sums f32 [C], its Gram matrix out^T out f32 [C, C], the same Gram matrix and
+    column sums in double [C * C + C]) in one pass (vcg_bn_apply_gram, bf16, C in 64 / 128 / 256; the double copy,
+    accumulated centred per workgroup, is what bn_stats_from_gram reads)."""
     _chk(y, torch.bfloat16, "y")
     out = torch.empty_like(y)
     cs = torch.empty(C, dtype=torch.float32, device=y.device)
     gram = torch.empty((C, C), dtype=torch.float32, device=y.device)
+    g64 = torch.empty(C * C + C, dtype=torch.float64, device=y.device)
     P_ = y.numel() // C
     w = ws(_lib.query("vcg_bn_apply_gram_ws_bytes", P_, C), y.device)
-    _lib.call("vcg_bn_apply_gram", P(y), P(scale), P(shift), P(out), P(cs), P(gram), P(w), w.numel() * 4, P_, C,
-              stream())
-    return out, cs, gram
+    _lib.call("vcg_bn_apply_gram", P(y), P(scale), P(shift), P(out), P(cs), P(gram), P(g64), P(w), w.numel() * 4,
+              P_, C, stream())
+    return out, cs, gram, g64
 
 
-def bn_stats_from_gram(gram, colsum, w, M, N, C, stats):
-    """BN statistics of x w^T (w bf16 [N, C]) from x's Gram matrix and column sums into a stats_buffer(N, M)
-    (vcg_bn_stats_from_gram; one used slot, for bn_finalize)."""
+def bn_stats_from_gram(g64, w, M, N, C, stats):
+    """BN statistics of x w^T (w bf16 [N, C]) from x's double (Gram matrix, column sums) g64 [C * C + C]
+    (bn_apply_gram) into a stats_buffer(N, M) (vcg_bn_stats_from_gram; one used slot, for bn_finalize)."""
     _chk(w, torch.bfloat16, "w")
-    _lib.call("vcg_bn_stats_from_gram", P(gram), P(colsum), P(w), M, N, C, P(stats), stats.shape[1], stream())
+    _chk(g64, torch.float64, "g64")
+    assert g64.numel() == C * C + C
+    _lib.call("vcg_bn_stats_from_gram", P(g64), P(w), M, N, C, P(stats), stats.shape[1], stream())
     return stats
 
 
@@ -448,12 +452,17 @@ def maxpool_bwd_bn(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, sums, d
     return g
 
 
-def maxpool_bwd_bn_sums_pooled(dy, mp, N, OH, OW, C, mean, invstd, mscale, mshift, sums, dgamma=None, dbeta=None):
+def maxpool_bwd_bn_sums_pooled(dy, mp, idx, y, N, H, W, C, mean, invstd, mscale, mshift, sums, dgamma=None,
+                               dbeta=None):
     """The stem BN-backward sums of maxpool_bwd_bn(store_g=False) from the pooled activation mp (no pass over the
-    pre-pool y; vcg_maxpool_bwd_bn_sums_pooled)."""
+    pre-pool y [N, H, W, C], which -- with the argmax bytes idx -- is read only for channels with a zero or tiny BN
+    weight; vcg_maxpool_bwd_bn_sums_pooled)."""
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    assert tuple(mp.shape) == (N, OH, OW, C) and idx.shape == mp.shape and tuple(y.shape) == (N, H, W, C)
     w = ws(_lib.query("vcg_maxpool_bwd_bn_ws_bytes", C), dy.device)
-    _lib.call("vcg_maxpool_bwd_bn_sums_pooled", dt_code(dy.dtype), P(dy), P(mp), N, OH, OW, C, P(mean), P(invstd),
-              P(mscale), P(mshift), P(w), w.numel() * 4, P(sums[0]), P(sums[1]), P(dgamma), P(dbeta), stream())
+    _lib.call("vcg_maxpool_bwd_bn_sums_pooled", dt_code(dy.dtype), P(dy), P(mp), P(idx), P(y), N, H, W, C, P(mean),
+              P(invstd), P(mscale), P(mshift), P(w), w.numel() * 4, P(sums[0]), P(sums[1]), P(dgamma), P(dbeta),
+              stream())
 
 
 def maxpool_bwd_bn_apply(dy, idx, N, H, W, C, y, mean, invstd, mscale, mshift, gamma, sums, count, train_stats):
@@ -479,6 +488,12 @@ def stem_bwd_fused(dy, idx, y, x, N, H, W, mean, invstd, mscale, mshift, gamma, 
     _lib.call("vcg_stem_bwd_fused", P(dy), P(idx), P(y), P(x), N, H, W, P(mean), P(invstd), P(mscale), P(mshift),
               P(gamma), P(sums[0]), P(sums[1]), int(count), int(bool(train_stats)), P(w), w.numel() * 4, P(dw),
               int(bool(accumulate)), stream())
+
+
+def stem_bwd_fused_fits(N, H, W):
+    """stem_bwd_fused takes a [N][H][W][64] conv output: every operand below 4 GB (32-bit buffer offsets; host-side
+    predicate of the library, vcg_stem_bwd_fused_fits)."""
+    return bool(_lib.query("vcg_stem_bwd_fused_fits", int(N), int(H), int(W)))
 
 
 def bn_relu_maxpool(y, scale, shift, N, H, W, C):

@@ -220,13 +220,13 @@ class ResNetTrunk:
         ops.bn_finalize(stats, mt, M, Cout, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
                         bn.running_mean if upd else None, bn.running_var if upd else None, mom, bn.eps)
 
-    def _bn_from_gram(self, conv, bn, gram, colsum, M, C):
+    def _bn_from_gram(self, conv, bn, g64, M, C):
         """BN state of conv's (1x1) output from its input's Gram matrix and column sums (ops.bn_stats_from_gram:
         y = x w^T is linear, so its batch mean / variance follow from x^T x and colsum(x) -- no pass over x or y)."""
         Cout = conv.out_channels
-        st = BNState(Cout, gram.device, bn_mode(bn), M, bn)
-        stats = ops.stats_buffer(Cout, M, gram.device)
-        ops.bn_stats_from_gram(gram, colsum, self._wprep(conv, C).view(Cout, C), M, Cout, C, stats)
+        st = BNState(Cout, g64.device, bn_mode(bn), M, bn)
+        stats = ops.stats_buffer(Cout, M, g64.device)
+        ops.bn_stats_from_gram(g64, self._wprep(conv, C).view(Cout, C), M, Cout, C, stats)
         self._finalize(stats, stats.shape[1], M, Cout, bn, st)
         return st
 
@@ -297,14 +297,14 @@ class ResNetTrunk:
         y2, b2, H2, W2 = self._conv_bn(a1, blk.conv2, blk.bn2, N, H, W, planes)
         drop = self._drop_y3(blk, planes, need_grad)
         C3 = blk.conv3.out_channels
-        a2sum = a2gram = None
+        a2sum = a2gram = g64 = None
         fold_a2 = (need_grad and ResNetTrunk.bn_fold_bwd and ResNetTrunk.bn_fold_a2 and ResNetTrunk.fused_bwd
                    and self.dtype == torch.bfloat16 and bn_mode(blk.bn3) != "running"
                    and C3 <= ResNetTrunk.bn_fold_max_c3 and planes <= 2048)
         if (fold_a2 or drop) and ResNetTrunk.gram_stats and planes in (64, 128, 256) and bn_mode(blk.bn3) != "running":
             # a2 with colsum(a2) and a2^T a2 from the bn2 apply pass: bn3's statistics follow from them (no conv3
             # statistics pass over a2 when y3 is not stored), and so does the Gram term of the a2-form backward fold
-            a2, a2sum, a2gram = ops.bn_apply_gram(y2, b2.scale, b2.shift, planes)
+            a2, a2sum, a2gram, g64 = ops.bn_apply_gram(y2, b2.scale, b2.shift, planes)
         elif fold_a2:
             # (the a2 form of the bn3 backward fold needs colsum(a2): written by the bn2 apply pass itself. A
             # separate column-sum pass on the side stream contended with conv3's GEMMs -- ~4 ms of kernel time per
@@ -313,7 +313,7 @@ class ResNetTrunk:
         else:
             a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
         if drop and a2gram is not None:
-            y3, b3 = None, self._bn_from_gram(blk.conv3, blk.bn3, a2gram, a2sum, N * H2 * W2, planes)
+            y3, b3 = None, self._bn_from_gram(blk.conv3, blk.bn3, g64, N * H2 * W2, planes)
         else:
             y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
         if not fold_a2:  # (the backward's a2-form fold reads these only where it applies)
@@ -557,8 +557,8 @@ class ResNetTrunk:
         # activation mp (a window's gradient reaches its argmax pixel, whose activation is mp): dout and mp instead of
         # dout, idx and the 4x larger y0
         if ResNetTrunk.pooled_stem_sums:
-            ops.maxpool_bwd_bn_sums_pooled(dout, mp, N, mp.shape[1], mp.shape[2], 64, b0.mean, b0.invstd, b0.scale,
-                                           b0.shift, sums0, dg0, db0)
+            ops.maxpool_bwd_bn_sums_pooled(dout, mp, idx, y0, N, H1, W1, 64, b0.mean, b0.invstd, b0.scale, b0.shift,
+                                           sums0, dg0, db0)
         else:
             ops.maxpool_bwd_bn(dout, idx, N, H1, W1, 64, y0, b0.mean, b0.invstd, b0.scale, b0.shift, sums0, dg0, db0,
                                store_g=False)
@@ -578,12 +578,13 @@ class ResNetTrunk:
 
     def _stem_fused_ok(self, conv1, xs, N, H, W, cpad, H1, W1):
         """ops.stem_bwd_fused applies: bf16 pair-packed frames (C = 4), the 7x7 / 2 / pad 3 stem, even conv-output
-        height, width a multiple of 8 up to 112, a weight gradient to add to."""
+        height, width a multiple of 8 up to 112, a weight gradient to add to, every operand below 4 GB (32-bit buffer
+        offsets: beyond ~2600 frames per GPU the apply pass + weight-gradient GEMM run instead)."""
         w = conv1.weight
         return (ResNetTrunk.fused_stem_bwd and self.dtype == torch.bfloat16 and cpad == 4 and w.requires_grad
                 and w.grad is not None and tuple(w.shape) == (64, 3, 7, 7) and conv1.stride == (2, 2)
                 and conv1.padding == (3, 3) and H == 2 * H1 and W == 2 * W1 and H1 % 2 == 0 and W1 % 8 == 0
-                and W1 <= 112)
+                and W1 <= 112 and ops.stem_bwd_fused_fits(N, H1, W1))
 
     def _bn_grads(self, st):
         bn = st.bn
@@ -615,8 +616,9 @@ class ResNetTrunk:
 
     def _can_fold(self, r, ds):
         """bn3's backward folds into conv3's gradients here (bf16 fused engine, batch statistics, stored conv3 input,
-        layers up to bn_fold_max_c3 channels; a first bottleneck also needs the side stream, where its downsample
-        BN's apply pass then runs -- dyd feeds only side-stream work)."""
+        layers up to bn_fold_max_c3 channels). A first bottleneck runs its downsample BN's apply pass on the side
+        stream where there is one (dyd feeds only the downsample's gradients), inline otherwise: the same kernels
+        either way, so the one-stream instrumented / profiled step runs the timed step's path."""
         blk, b3, C3, planes = r["blk"], r["b3"], r["C3"], r["planes"]
         if not (ResNetTrunk.bn_fold_bwd and ResNetTrunk.fused_bwd and self.dtype == torch.bfloat16):
             return False
@@ -624,7 +626,7 @@ class ResNetTrunk:
             return False
         if blk.conv3.stride[0] != 1 or planes < 64 or (planes & (planes - 1)) != 0:
             return False
-        return not ds or (r["bd"].mode != "running" and self._ws is not None and ResNetTrunk.ds_stream)
+        return not ds or r["bd"].mode != "running"
 
     def _fold_conv3(self, r, g, sums3):
         """conv3's weight gradient with bn3's batch-statistics backward folded in (side stream): dW = A (g^T a2) +
