@@ -362,8 +362,9 @@ def test_bn_apply_colsum(rows, C):
 @pytest.mark.parametrize("rows,C", [(3211264 // 4 + 5, 64), (802816 // 2 + 13, 128), (200704, 256), (77, 64)])
 def test_bn_apply_gram(rows, C):
     """bn_apply + colsum + the Gram matrix a^T a of the stored output in one pass: a == bn_apply bit for bit, colsum
-    and gram against float64 sums of the same bf16 values (fixed-order fp32 / MFMA accumulation: ~1e-6 relative),
-    deterministic; ragged row counts (tail rows contribute nothing)."""
+    and gram against float64 sums of the same bf16 values, deterministic; ragged row counts (tail rows contribute
+    nothing). The Gram is accumulated from centred values a - c rounded stochastically to bf16 (bn_gram.hip): zero-mean
+    noise of ~2^-8 / sqrt(rows) of a diagonal entry (1e-5 - 3e-5 at the trunk's sizes, 1e-3 at 77 rows)."""
     gen = torch.Generator().manual_seed(rows % 89 + C)
     y = _bf(torch.randn(rows, C, generator=gen) + 0.2)
     sc = (0.5 + torch.rand(C, generator=gen)).to(DEV)
@@ -376,9 +377,12 @@ def test_bn_apply_gram(rows, C):
     csr = ad.sum(0)
     Gr = ad.t() @ ad
     assert ((cs.double() - csr).abs() / csr.abs().clamp_min(1.0)).max().item() < 1e-5
-    assert ((G.double() - Gr).abs().max() / Gr.abs().max()).item() < 1e-5
+    eg = ((G.double() - Gr).abs().max() / Gr.abs().max()).item()
+    print(f"gram max err {eg:.2e} of max |G|")
+    tol = 3e-5 + 0.02 / rows ** 0.5
+    assert eg < tol
     assert torch.equal(G, G.t())
-    assert ((g64[:C * C].view(C, C) - Gr).abs().max() / Gr.abs().max()).item() < 1e-5
+    assert ((g64[:C * C].view(C, C) - Gr).abs().max() / Gr.abs().max()).item() < tol
     assert torch.equal(g64[C * C:].float(), cs) and torch.equal(g64[:C * C].view(C, C).float(), G)
     a2, cs2, G2, g642 = ops.bn_apply_gram(y, sc, sh, C)
     assert torch.equal(cs, cs2) and torch.equal(G, G2) and torch.equal(g64, g642)

@@ -227,3 +227,49 @@ def test_score_windows_streams_identical():
     s4, l4 = lv.score_windows(model, frames, *args, batch_size=16, streams=4)
     torch.cuda.synchronize()
     assert torch.equal(s1, s4) and torch.equal(l1, l4)
+
+
+def test_c5_stride4_f1_vs_oracle_golden():
+    """BASELINE config 5's F1 end to end against the CPU oracle: the reference F1 pipeline's setting
+    (test_video_segment_point.py:244-377 -> eval_utils.py:3-92) -- stride 4 s (2 * max_offset,
+    flat_video2clip_for_quick_infer.py:66), batch-statistics BN over batches of 16 consecutive windows (:41,116-122),
+    fp32 -- over the 1 h synthetic video (896 windows). tests/golden/c5_stride4_batch16.npz holds the oracle's
+    prob[:, 1], labels and boundary metrics for every window (tools/oracle/make_golden_c5.py, the oracle run in the
+    build container) and the head's logit-1 bias shift it applied; the native fp32 path scores the same windows with
+    the same shift. prob within 1e-3; labels equal wherever the oracle's |p - 0.5| exceeds twice the largest
+    |dprob| measured (a label may differ only where the probability error can explain it: at random init every
+    probability lies within 1e-2 of 0.5, 126 of them within 1e-3); F / F@3 / F@5 (and every recall / precision)
+    equal when all labels agree."""
+    import long_video as lv
+    from data.synthetic_dataset import HashTokenizer
+    from test_video_segment_point import drop_bn_running_stats
+    from vcg_hip.build import build_two_stream
+    g = np.load(os.path.join(GOLD, "c5_stride4_batch16.npz"), allow_pickle=False)
+    F, T, HW, L, S, BS = (int(v) for v in g["config"])
+    frames, timestamps, subtitles = lv.synthetic_long_video(F, HW, HW, seed=123, device=DEV)
+    win, idx, ids, mask = lv.window_inputs(F, T, S, subtitles, HashTokenizer(), L)
+    assert np.array_equal(win, g["win"])
+    model = build_two_stream(clip_frame_num=T, seed=123, device=DEV, precision="fp32", dropout=0.0).eval()
+    assert drop_bn_running_stats(model) == 53
+    with torch.no_grad():
+        model.fusion_head.head.bias.data[1] += float(g["shift"])
+        model.native_flat().refresh_shadow(force=True)
+    idx_d, ids_d, mask_d = (torch.from_numpy(a).to(DEV) for a in (idx, ids, mask))
+    sc, lab = lv.score_windows(model, frames, idx_d, ids_d, mask_d, batch_size=BS)
+    torch.cuda.synchronize()
+    p32, l32 = sc.cpu().numpy().astype(np.float64), lab.cpu().numpy()
+    ref, ref_lab = g["prob1"], g["labels"]
+    d = np.abs(p32 - ref)
+    sure = np.abs(ref - 0.5) > 2 * d.max()
+    m32 = lv.boundary_metrics(l32.tolist(), timestamps, F, T, S)
+    print(f"C5 stride {S} batch-stat fp32 vs oracle: {len(win)} windows, max |dprob| {d.max():.2e}, "
+          f"{int((l32 != ref_lab).sum())} label differences ({int((~sure).sum())} windows within 2 max |dprob| of 0.5)")
+    print("native", {k: m32[k] for k in ("recall", "precision", "f", "f_3", "f_5")})
+    print("oracle", {k: float(g["metric_" + k]) for k in ("recall", "precision", "f", "f_3", "f_5")})
+    assert d.max() < 1e-3
+    assert np.array_equal(l32[sure], ref_lab[sure])
+    if np.array_equal(l32, ref_lab):
+        assert m32["gt_cut_points"] == g["gt_cut_points"].tolist()
+        assert m32["pred_cut_points"] == g["pred_cut_points"].tolist()
+        for k in ("recall", "recall_3", "recall_5", "precision", "precision_3", "precision_5", "f", "f_3", "f_5"):
+            assert m32[k] == float(g["metric_" + k]), k

@@ -21,7 +21,9 @@
 // Precision: y3's variance is w^T (G / M - mu mu^T) w, which cancels like E[y^2] - E[y]^2 when a y3 channel's |mean|
 // is much larger than its std. So the Gram is not formed from a but from a - c_b, with c_b the bf16-rounded column
 // means of the workgroup's FIRST iteration of rows (a per-workgroup centre close to the batch mean): the fp32 MFMA
-// accumulation then carries an error relative to the centred (variance-sized) entries, not to mean^2. Each
+// accumulation then carries an error relative to the centred (variance-sized) entries, not to mean^2. a - c is exact
+// in f32; it enters the MFMA rounded to bf16 stochastically (a counter hash of (row, channel): unbiased, so the Gram
+// is exact up to zero-mean noise of ~2^-9 / sqrt(rows) relative). Each
 // workgroup writes a [C * C + 2 C] f32 slab (centred G_b mirrored to full, centred colsum d_b = sum (a - c_b),
 // centre c_b); gram_reduce rebuilds the uncentred colsum = sum_b (d_b + n_b c_b) and
 // G = sum_b (G_b + d_b c_b^T + c_b d_b^T + n_b c_b c_b^T) in double in a fixed order (deterministic), and the
@@ -185,10 +187,20 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
           st[e] -= ctr[e];  // (exact in f32: both bf16 values)
           cs[e] += st[e];   // the centred column sum (no cancellation against n c later)
         }
-        d.x = (uint32_t)f2bf(st[0]) | ((uint32_t)f2bf(st[1]) << 16);
-        d.y = (uint32_t)f2bf(st[2]) | ((uint32_t)f2bf(st[3]) << 16);
-        d.z = (uint32_t)f2bf(st[4]) | ((uint32_t)f2bf(st[5]) << 16);
-        d.w = (uint32_t)f2bf(st[6]) | ((uint32_t)f2bf(st[7]) << 16);
+        // the centred values in bf16 with unbiased (stochastic) rounding: round-to-nearest of a - c is a fixed
+        // function of a, whose errors correlate with a - c and bias the diagonal of the Gram by ~2^-15 relative
+        const uint32_t hb = (uint32_t)row * 0x9E3779B1u + (uint32_t)cc * 0x85EBCA77u;
+        uint32_t dw[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t h = hb + (uint32_t)q * 0xC2B2AE3Du;
+          h ^= h >> 15;
+          h *= 0x2C1B3C6Du;
+          h ^= h >> 13;
+          dw[q] = ((__float_as_uint(st[2 * q]) + (h & 0xFFFFu)) >> 16) |
+                  ((__float_as_uint(st[2 * q + 1]) + (h >> 16)) & 0xFFFF0000u);
+        }
+        d = make_uint4(dw[0], dw[1], dw[2], dw[3]);
       }
       // LDS: k-step lr / 64, k-row lr % 64, panel cc / (COLS / 8), swizzled slot of chunk cc % (COLS / 8)
       const int ks = lr >> 6, kr = lr & 63, pn = cc / (COLS / 8), pc = cc % (COLS / 8);
