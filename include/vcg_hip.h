@@ -55,6 +55,8 @@ VCG_API int vcg_patch_stamps(unsigned long long* out, int n);
    k-step, after the last MFMAs, after the output staging, after the epilogue) -- only in a library built with
    -DVCG_FAST_STAMPS (make EXTRA=-DVCG_FAST_STAMPS); returns 1 otherwise. */
 VCG_API int vcg_fast_stamps(unsigned long long* out, int n);
+/* profiling aid: s_memtime phase stamps of the last 256-tile GEMM (a -DVCG_G256_STAMPS build; 1 otherwise) */
+VCG_API int vcg_g256_stamps(unsigned long long* out, int n);
 
 /* ---- MFMA implicit-GEMM engine (igemm.hip) ---------------------------------------------- */
 /* torchvision conv2d inside Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15,68-77), with
@@ -116,16 +118,16 @@ VCG_API long long vcg_bn_apply_colsum_ws_bytes(long long P, int C);
 VCG_API int vcg_bn_apply_colsum(const void* y, const float* scale, const float* shift, int relu, void* out, float* colsum, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
 /* vcg_bn_apply_colsum (ReLU, bf16, C = 64 / 128 / 256) that also returns gram = out^T out (f32 [C][C], summed in a
    fixed order: deterministic): the bottleneck's bn2 -> relu -> a2 with the a2 statistics that bn3's batch statistics
-   (vcg_bn_stats_from_gram) and the a2 form of the bn3 backward fold need, so that neither reads a2 again. g64
-   (optional, double [C * C + C]): the same Gram matrix then column sums in double, accumulated centred per workgroup
-   (the input of vcg_bn_stats_from_gram: no E[y^2] - E[y]^2 cancellation for large |mean| / std). */
+   (vcg_bn_stats_from_gram) and the a2 form of the bn3 backward fold need, so that neither reads a2 again.
+   mean / invstd: the statistics that scale / shift fold. g64 (double [C * C + 2 C]): the same Gram matrix and column
+   sums accumulated centred per channel, with the centres ([Gc | d | c]; c = bf16(beta) for channels whose BN shift
+   beta exceeds 6 |gamma|, else 0): the input of vcg_bn_stats_from_gram, free of E[y^2] - E[y]^2 cancellation. */
 VCG_API long long vcg_bn_apply_gram_ws_bytes(long long P, int C);
-VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* shift, void* out, float* colsum, float* gram, double* g64, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
-/* Batch statistics of y = x w^T (w bf16 [N][C], the conv's forward GEMM weights; M rows) from x's double g64 =
-   (gram [C][C], colsum [C]) of vcg_bn_apply_gram:
-   mean_n = w_n . colsum / M, var_n = w_n^T (gram / M - mu mu^T) w_n in double -- torchvision Bottleneck bn3 over
-   conv3's output (model/vision/resnet50_tsm.py:15) without a statistics pass over a2. Writes the vcg_conv_fwd
-   stats layout (one used slot) for vcg_bn_finalize. */
+VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* shift, const float* mean, const float* invstd, void* out, float* colsum, float* gram, double* g64, float* ws, long long ws_bytes, long long P, int C, hipStream_t s);
+/* Batch statistics of y = x w^T (w bf16 [N][C], the conv's forward GEMM weights; M rows) from x's g64 of
+   vcg_bn_apply_gram: mean_n = w_n . mu, var_n = w_n^T Cov w_n with Cov = Gc / M - (d / M)(d / M)^T, mu = c + d / M, in
+   double -- torchvision Bottleneck bn3 over conv3's output (model/vision/resnet50_tsm.py:15) without a statistics
+   pass over a2. Writes the vcg_conv_fwd stats layout (one used slot) for vcg_bn_finalize. */
 VCG_API int vcg_bn_stats_from_gram(const double* g64, const void* w, long long M, int N, int C, float* stats, int mtiles, hipStream_t s);
 VCG_API int vcg_conv1x1_stats(const void* x, const void* w, float* stats, int M, int N, int K, hipStream_t stream);
 VCG_API int vcg_bn_bwd_sumgx_from_wgrad(const float* P, const void* w, int K, int C, const float* mean, const float* invstd, const float* sum_g, float* sum_gx, float* dgamma, hipStream_t stream);

@@ -363,13 +363,15 @@ def test_bn_apply_colsum(rows, C):
 def test_bn_apply_gram(rows, C):
     """bn_apply + colsum + the Gram matrix a^T a of the stored output in one pass: a == bn_apply bit for bit, colsum
     and gram against float64 sums of the same bf16 values, deterministic; ragged row counts (tail rows contribute
-    nothing). The Gram is accumulated from centred values a - c rounded stochastically to bf16 (bn_gram.hip): zero-mean
-    noise of ~2^-8 / sqrt(rows) of a diagonal entry (1e-5 - 3e-5 at the trunk's sizes, 1e-3 at 77 rows)."""
+    nothing). The channels whose BN shift dominates (beta > 6 |gamma|) are accumulated centred (bn_gram.hip): the
+    rebuilt uncentred Gram is as exact as the plain one (fp32 MFMA accumulation: ~1e-6 relative)."""
     gen = torch.Generator().manual_seed(rows % 89 + C)
     y = _bf(torch.randn(rows, C, generator=gen) + 0.2)
     sc = (0.5 + torch.rand(C, generator=gen)).to(DEV)
     sh = (torch.randn(C, generator=gen) * 0.2).to(DEV)
-    a, cs, G, g64 = ops.bn_apply_gram(y, sc, sh, C)
+    sh[::5] += 12.0  # (every 5th channel centred: beta > 6 |gamma|)
+    mean, inv = torch.full((C,), 0.2, device=DEV), torch.ones(C, device=DEV)
+    a, cs, G, g64 = ops.bn_apply_gram(y, sc, sh, C, mean, inv)
     ref = ops.bn_apply(y, sc, sh, C, relu=True)
     torch.cuda.synchronize()
     assert torch.equal(a, ref)
@@ -379,12 +381,16 @@ def test_bn_apply_gram(rows, C):
     assert ((cs.double() - csr).abs() / csr.abs().clamp_min(1.0)).max().item() < 1e-5
     eg = ((G.double() - Gr).abs().max() / Gr.abs().max()).item()
     print(f"gram max err {eg:.2e} of max |G|")
-    tol = 3e-5 + 0.02 / rows ** 0.5
-    assert eg < tol
+    assert eg < 1e-5
     assert torch.equal(G, G.t())
-    assert ((g64[:C * C].view(C, C) - Gr).abs().max() / Gr.abs().max()).item() < tol
-    assert torch.equal(g64[C * C:].float(), cs) and torch.equal(g64[:C * C].view(C, C).float(), G)
-    a2, cs2, G2, g642 = ops.bn_apply_gram(y, sc, sh, C)
+    c = g64[C * C + C:]
+    assert (c[::5] > 0).all() and c.count_nonzero().item() <= (C + 4) // 5 + C // 4
+    d = g64[C * C:C * C + C]
+    Gc = g64[:C * C].view(C, C)
+    Gu = Gc + d[:, None] * c[None, :] + c[:, None] * d[None, :] + rows * c[:, None] * c[None, :]
+    assert ((Gu - Gr).abs().max() / Gr.abs().max()).item() < 1e-5
+    assert ((d + rows * c - csr).abs() / csr.abs().clamp_min(1.0)).max().item() < 1e-5
+    a2, cs2, G2, g642 = ops.bn_apply_gram(y, sc, sh, C, mean, inv)
     assert torch.equal(cs, cs2) and torch.equal(G, G2) and torch.equal(g64, g642)
 
 
@@ -398,7 +404,7 @@ def test_bn_stats_from_gram(M, C, N):
     y = _bf(torch.randn(M, C, generator=gen))
     sc = (0.5 + torch.rand(C, generator=gen)).to(DEV)
     sh = (torch.randn(C, generator=gen) * 0.3 + 0.2).to(DEV)
-    a, cs, G, g64 = ops.bn_apply_gram(y, sc, sh, C)
+    a, cs, G, g64 = ops.bn_apply_gram(y, sc, sh, C, torch.zeros(C, device=DEV), torch.ones(C, device=DEV))
     w = _bf(torch.randn(N, C, generator=gen) * (1.0 / C ** 0.5))
     stats = ops.stats_buffer(N, M, DEV)
     ops.bn_stats_from_gram(g64, w, M, N, C, stats)
@@ -443,15 +449,17 @@ def test_conv1x1_bn_res_relu_streaming_vs_persistent(monkeypatch, M, C, N):
 
 @pytest.mark.parametrize("M,C,N", [(200704, 64, 256), (50176 + 77, 256, 512)])
 def test_bn_stats_from_gram_large_mean(M, C, N):
-    """bn3's statistics from the Gram matrix where y3's |mean| is ~100-500x its std (a2 = relu(0.1 y + 3) > 0 with
-    all-positive conv3 weights): the E[y^2] - E[y]^2 form cancels there, so the Gram is accumulated centred per
-    workgroup and rebuilt in double (bn_gram.hip). mean within 1e-4 of std and invstd within 1e-4 relative of float64
-    statistics of the exact product (an uncentred fp32 Gram is off by ~1e-3 - 1e-2 here)."""
+    """bn3's statistics from the Gram matrix where the a2 channels' |mean| is 30x their std (a2 = relu(0.1 z + 3): the
+    BN shift dominates its scale, the ReLU always passes) and y3's 200-450x (all-positive conv3 weights): an uncentred
+    fp32 Gram cancels there (E[y^2] - E[y]^2 over channels whose mean^2 is 900x their variance), so such channels are
+    accumulated centred at bf16(beta) (bn_gram.hip) and the statistics subtract in double. mean within 1e-4 of std and
+    invstd within 1e-4 relative of float64 statistics of the exact product."""
     gen = torch.Generator().manual_seed(M % 97 + C)
     y = _bf(torch.randn(M, C, generator=gen))
     sc = torch.full((C,), 0.1).to(DEV)
     sh = torch.full((C,), 3.0).to(DEV)
-    a, cs, G, g64 = ops.bn_apply_gram(y, sc, sh, C)
+    a, cs, G, g64 = ops.bn_apply_gram(y, sc, sh, C, torch.zeros(C, device=DEV), torch.ones(C, device=DEV))
+    assert (g64[C * C + C:] == 3.0).all()
     w = _bf(torch.randn(N, C, generator=gen).abs() * (1.0 / C ** 0.5) + 0.05)
     stats = ops.stats_buffer(N, M, DEV)
     ops.bn_stats_from_gram(g64, w, M, N, C, stats)

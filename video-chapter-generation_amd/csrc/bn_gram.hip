@@ -16,18 +16,20 @@
 // with the 16-B chunk swizzle of the weight-gradient engine (igemm_wgrad.hip wswz), from which ds_read_b64_tr_b16
 // gives each lane 4 consecutive rows of one column. The C x C Gram block pairs (jb <= kb of 16 x 16, the upper
 // triangle: G is symmetric) are dealt round-robin to the 4 waves and accumulated with v_mfma_f32_16x16x32_bf16
-// over every row the workgroup sees (two LDS buffers, one barrier per iteration).
+// over every row the workgroup sees (two LDS buffers, one barrier per iteration). Each workgroup writes a
+// [C * C + C] f32 slab (G mirrored to full, then colsum); gram_reduce sums the slabs in a fixed order in double
+// (deterministic).
 //
-// Precision: y3's variance is w^T (G / M - mu mu^T) w, which cancels like E[y^2] - E[y]^2 when a y3 channel's |mean|
-// is much larger than its std. So the Gram is not formed from a but from a - c_b, with c_b the bf16-rounded column
-// means of the workgroup's FIRST iteration of rows (a per-workgroup centre close to the batch mean): the fp32 MFMA
-// accumulation then carries an error relative to the centred (variance-sized) entries, not to mean^2. a - c is exact
-// in f32; it enters the MFMA rounded to bf16 stochastically (a counter hash of (row, channel): unbiased, so the Gram
-// is exact up to zero-mean noise of ~2^-9 / sqrt(rows) relative). Each
-// workgroup writes a [C * C + 2 C] f32 slab (centred G_b mirrored to full, centred colsum d_b = sum (a - c_b),
-// centre c_b); gram_reduce rebuilds the uncentred colsum = sum_b (d_b + n_b c_b) and
-// G = sum_b (G_b + d_b c_b^T + c_b d_b^T + n_b c_b c_b^T) in double in a fixed order (deterministic), and the
-// statistics kernel subtracts mu mu^T in double.
+// Precision. y3's variance is w^T (G / M - mu mu^T) w. The fp32 accumulation errors of G are independent per entry,
+// so they are amplified only by the ratio |mean| / std of the a2 CHANNELS themselves (not of y3): ~1 for a ReLU of a
+// unit normal, but large for a channel whose BN shift dominates its scale (beta >> |gamma|: the ReLU almost always
+// passes and a2 ~ gamma z + beta). Such channels are centred: the Gram is accumulated over a - c with the per-channel
+// centre c = bf16(beta) where beta > 6 |gamma| (else 0, the exact uncentred Gram, whose relative error there is at most
+// ~40x the fp32 accumulation's). a - c is exact in bf16 whenever c / 2 <= a <= 2 c (Sterbenz): every row of a centred
+// channel but those 3 std below its mean, so the products stay exact (the rare others carry one rounding). The slabs
+// then hold the centred Gc and d = colsum(a - c); gram_reduce sums them in double into g64 = [Gc | d | c] and
+// gram_finish writes the uncentred f32 G = Gc + d c^T + c d^T + M c c^T and colsum = d + M c; the statistics read
+// g64 (Cov = Gc / M - (d / M)(d / M)^T, mu = c + d / M: no cancellation against the centre).
 #include "common.h"
 
 namespace vcg {
@@ -88,10 +90,19 @@ __host__ __device__ constexpr int pair_kb(int p, int nb) {
 
 // one wave's part: the pairs p = 4 t + W (compile-time indices, so the accumulators and the fragment addresses
 // are static); every wave runs the same loop and barriers
+// the Gram centre of channel k (see the file comment): bf16(beta) where beta > 6 |gamma|, else 0; gamma = scale /
+// invstd and beta = shift + scale mean recover the BN affine from the folded apply parameters
+__device__ __forceinline__ float gram_centre(float sc, float sh, float mean, float invstd) {
+  const float gamma = sc / invstd, beta = fmaf(sc, mean, sh);
+  return beta > 6.f * fabsf(gamma) ? bf2f(f2bf(beta)) : 0.f;
+}
+
 template <int C, int W>
 __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const float* __restrict__ scale,
-                                          const float* __restrict__ shift, bf16_t* __restrict__ out,
-                                          float* __restrict__ slab, long long P, bf16_t* buf, float* red) {
+                                          const float* __restrict__ shift, const float* __restrict__ mean,
+                                          const float* __restrict__ invstd, bf16_t* __restrict__ out,
+                                          float* __restrict__ slab, double* __restrict__ g64, long long P, bf16_t* buf,
+                                          float* red) {
   constexpr int COLS = C >= 128 ? 128 : 64;
   constexpr int NP = C / COLS;   // panels per 64-row k-step
   constexpr int KS = 256 / C;    // 64-row k-steps per iteration
@@ -107,12 +118,17 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int cc = tid % CPR, r0 = tid / CPR;  // this thread's chunk and first row of an iteration
-  float sc[8], sh[8], cs[8];
+  float sc[8], sh[8], cs[8], ctr[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     sc[e] = scale[8 * cc + e];
     sh[e] = shift[8 * cc + e];
+    ctr[e] = gram_centre(sc[e], sh[e], mean[8 * cc + e], invstd[8 * cc + e]);
     cs[e] = 0.f;
+  }
+  if (blockIdx.x == 0 && W == 0 && tid < CPR) {  // (wave 0 holds every chunk once: CPR <= 32 threads)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g64[C * C + C + 8 * cc + e] = (double)ctr[e];
   }
   f32x4 acc[NF > 0 ? NF : 1];
 #pragma unroll
@@ -129,35 +145,6 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
     }
   };
   if (it < iters) load(it);
-  // the Gram centre c_b: bf16 column means of this workgroup's first iteration (every workgroup has one: grid <=
-  // iters), summed in a fixed order through LDS
-  float ctr[8];
-  {
-    float ps[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ps[e] = 0.f;
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      if (it * R + r0 + u * RS < P) {
-        float a[8];
-        unpack8g(nx[u], a);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ps[e] += bf2f(f2bf(fmaxf(fmaf(a[e], sc[e], sh[e]), 0.f)));
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[tid * 9 + e] = ps[e];
-    __syncthreads();
-    const long long left = P - it * R;
-    const float inv = 1.f / (float)(left < R ? left : R);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float t = 0.f;
-      for (int q = cc; q < 256; q += CPR) t += red[q * 9 + e];
-      ctr[e] = bf2f(f2bf(t * inv));
-    }
-    __syncthreads();  // (red is written again only after the main loop)
-  }
   int cur = 0;
   for (; it < iters; it += gridDim.x) {
     uint4 v[NV];
@@ -184,23 +171,13 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
         unpack8g(o, st);  // the stored (rounded) values
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          st[e] -= ctr[e];  // (exact in f32: both bf16 values)
-          cs[e] += st[e];   // the centred column sum (no cancellation against n c later)
+          st[e] -= ctr[e];  // (exact in f32; exact in bf16 for a 0 centre and, by Sterbenz, for c / 2 <= a <= 2 c)
+          cs[e] += st[e];
         }
-        // the centred values in bf16 with unbiased (stochastic) rounding: round-to-nearest of a - c is a fixed
-        // function of a, whose errors correlate with a - c and bias the diagonal of the Gram by ~2^-15 relative
-        const uint32_t hb = (uint32_t)row * 0x9E3779B1u + (uint32_t)cc * 0x85EBCA77u;
-        uint32_t dw[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint32_t h = hb + (uint32_t)q * 0xC2B2AE3Du;
-          h ^= h >> 15;
-          h *= 0x2C1B3C6Du;
-          h ^= h >> 13;
-          dw[q] = ((__float_as_uint(st[2 * q]) + (h & 0xFFFFu)) >> 16) |
-                  ((__float_as_uint(st[2 * q + 1]) + (h >> 16)) & 0xFFFF0000u);
-        }
-        d = make_uint4(dw[0], dw[1], dw[2], dw[3]);
+        d.x = (uint32_t)f2bf(st[0]) | ((uint32_t)f2bf(st[1]) << 16);
+        d.y = (uint32_t)f2bf(st[2]) | ((uint32_t)f2bf(st[3]) << 16);
+        d.z = (uint32_t)f2bf(st[4]) | ((uint32_t)f2bf(st[5]) << 16);
+        d.w = (uint32_t)f2bf(st[6]) | ((uint32_t)f2bf(st[7]) << 16);
       }
       // LDS: k-step lr / 64, k-row lr % 64, panel cc / (COLS / 8), swizzled slot of chunk cc % (COLS / 8)
       const int ks = lr >> 6, kr = lr & 63, pn = cc / (COLS / 8), pc = cc % (COLS / 8);
@@ -226,8 +203,8 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
     }
     cur ^= 1;
   }
-  // slab: the centred G (mirrored to the full matrix), centred colsum, centre
-  float* sl = slab + (long long)blockIdx.x * (C * C + 2 * C);
+  // slab: the centred G (mirrored to the full matrix) then the centred colsum d
+  float* sl = slab + (long long)blockIdx.x * (C * C + C);
   const int g = lane >> 4, ci = lane & 15;
 #pragma unroll
   for (int t = 0; t < NF; ++t) {
@@ -249,76 +226,50 @@ __device__ __forceinline__ void gram_body(const bf16_t* __restrict__ y, const fl
     for (int t = ch; t < 256; t += CPR) s += red[t * 9 + e];  // fixed order
     sl[C * C + o] = s;
   }
-  if (tid < CPR) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sl[C * C + C + 8 * tid + e] = ctr[e];
-  }
 }
 
 template <int C>
 __global__ __launch_bounds__(256) void bn_apply_gram_kernel(const bf16_t* __restrict__ y, const float* __restrict__ scale,
-                                                           const float* __restrict__ shift, bf16_t* __restrict__ out,
-                                                           float* __restrict__ slab, long long P) {
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd, bf16_t* __restrict__ out,
+                                                           float* __restrict__ slab, double* __restrict__ g64,
+                                                           long long P) {
   __shared__ __attribute__((aligned(1024))) bf16_t buf[2 * 16384];
   __shared__ float red[256 * 9];
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: gram_body<C, 0>(y, scale, shift, out, slab, P, buf, red); break;
-    case 1: gram_body<C, 1>(y, scale, shift, out, slab, P, buf, red); break;
-    case 2: gram_body<C, 2>(y, scale, shift, out, slab, P, buf, red); break;
-    default: gram_body<C, 3>(y, scale, shift, out, slab, P, buf, red); break;
+    case 0: gram_body<C, 0>(y, scale, shift, mean, invstd, out, slab, g64, P, buf, red); break;
+    case 1: gram_body<C, 1>(y, scale, shift, mean, invstd, out, slab, g64, P, buf, red); break;
+    case 2: gram_body<C, 2>(y, scale, shift, mean, invstd, out, slab, g64, P, buf, red); break;
+    default: gram_body<C, 3>(y, scale, shift, mean, invstd, out, slab, g64, P, buf, red); break;
   }
 }
 
-// Rows of `slab` b: the iterations b, b + nb, ... of R rows each, the last one possibly short.
-__device__ __forceinline__ double slab_rows(int b, int nb, long long P, int R) {
-  const long long iters = (P + R - 1) / R;
-  const long long nit = (iters - 1 - b) / nb + 1;
-  long long n = nit * R;
-  if ((iters - 1) % nb == b) n -= iters * R - P;
-  return (double)n;
-}
-
-// out[i] = the uncentred sum over nb slabs, in double (deterministic): for a Gram entry (j, k)
-// sum_b G_b[j][k] + d_b[j] c_b[k] + c_b[j] d_b[k] + n_b c_b[j] c_b[k], for a column sum sum_b d_b[k] + n_b c_b[k]
-// (G_b, d_b: centred at c_b). A thread owns 4
-// consecutive entries (16-B loads) and G threads split the slabs (thread t sums slabs t, t + G, ... in order, the G
-// partials are combined in t order through LDS). (One thread per entry over all 256-512 slabs ran latency-bound:
-// 100 us per call at C = 64.) Writes f32 gram / colsum and, when g64 != null, the double [C * C + C].
+// out[i] = sum over nb slabs of slab[b][i], in double (deterministic): a thread owns 4 consecutive entries (16-B
+// loads) and G threads split the slabs (thread t sums slabs t, t + G, ... in order, the G partials are combined in
+// t order through LDS). (One thread per entry over all 256-512 slabs ran latency-bound: 100 us per call at C = 64.)
 __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ slab, int nb, int n, int G,
-                                                         float* __restrict__ gram, float* __restrict__ colsum, int C,
-                                                         double* __restrict__ g64, long long P, int R) {
+                                                         double* __restrict__ g64) {
   __shared__ double red[4][256];
   const int QB = 256 / G;
   const int t = threadIdx.x / QB, ql = threadIdx.x - t * QB;
   const int quad = blockIdx.x * QB + ql, nq = n >> 2;
-  const int ns = C * C + 2 * C;  // slab stride (floats)
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   if (quad < nq) {
-    const int i0 = 4 * quad;
-    if (i0 < C * C) {
-      const int j = i0 / C, k = i0 - j * C;
-      for (int b = t; b < nb; b += G) {
-        const float* sb = slab + (long long)b * ns;
-        const float4 g = *reinterpret_cast<const float4*>(sb + i0);
-        const float4 sk = *reinterpret_cast<const float4*>(sb + C * C + k);
-        const float4 ck = *reinterpret_cast<const float4*>(sb + C * C + C + k);
-        const double sj = (double)sb[C * C + j], cj = (double)sb[C * C + C + j];
-        const double nr = slab_rows(b, nb, P, R);
-        const double ncj = nr * cj;
-        s0 += (double)g.x + sj * (double)ck.x + cj * (double)sk.x + ncj * (double)ck.x;
-        s1 += (double)g.y + sj * (double)ck.y + cj * (double)sk.y + ncj * (double)ck.y;
-        s2 += (double)g.z + sj * (double)ck.z + cj * (double)sk.z + ncj * (double)ck.z;
-        s3 += (double)g.w + sj * (double)ck.w + cj * (double)sk.w + ncj * (double)ck.w;
+    const float4* p = reinterpret_cast<const float4*>(slab) + quad;
+    int b = t;
+    for (; b + 3 * G < nb; b += 4 * G) {
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = p[(long long)(b + k * G) * nq];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s0 += (double)v[k].x; s1 += (double)v[k].y; s2 += (double)v[k].z; s3 += (double)v[k].w;
       }
-    } else {
-      for (int b = t; b < nb; b += G) {
-        const float* sb = slab + (long long)b * ns;
-        const float4 v = *reinterpret_cast<const float4*>(sb + i0);
-        const float4 c = *reinterpret_cast<const float4*>(sb + i0 + C);
-        const double nr = slab_rows(b, nb, P, R);
-        s0 += (double)v.x + nr * (double)c.x; s1 += (double)v.y + nr * (double)c.y;
-        s2 += (double)v.z + nr * (double)c.z; s3 += (double)v.w + nr * (double)c.w;
-      }
+    }
+    for (; b < nb; b += G) {
+      const float4 v = p[(long long)b * nq];
+      s0 += (double)v.x; s1 += (double)v.y; s2 += (double)v.z; s3 += (double)v.w;
     }
   }
   if (G > 1) {
@@ -331,30 +282,48 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
     }
   }
   if (quad >= nq) return;
-  const double sv[4] = {s0, s1, s2, s3};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int i = 4 * quad + e;
-    if (i < C * C) gram[i] = (float)sv[e];
-    else colsum[i - C * C] = (float)sv[e];
-    if (g64) g64[i] = sv[e];
+  double* o = g64 + 4 * quad;
+  o[0] = s0; o[1] = s1; o[2] = s2; o[3] = s3;
+}
+
+// the uncentred f32 Gram matrix and column sums from g64 = [Gc | d | c] (M rows): G = Gc + d c^T + c d^T + M c c^T,
+// colsum = d + M c, in double
+__global__ __launch_bounds__(256) void gram_finish_kernel(const double* __restrict__ g64, long long M, int C,
+                                                         float* __restrict__ gram, float* __restrict__ colsum) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const double* d = g64 + (long long)C * C;
+  const double* c = d + C;
+  const double m = (double)M;
+  if (i < C * C) {
+    const int j = i / C, k = i - j * C;
+    gram[i] = (float)(g64[i] + d[j] * c[k] + c[j] * d[k] + m * c[j] * c[k]);
+  } else if (i < C * C + C) {
+    const int k = i - C * C;
+    colsum[k] = (float)(d[k] + m * c[k]);
   }
 }
 
-// bn3's batch statistics from the double (G, colsum) g64 [C * C + C] and conv3's bf16 weights w [N][C]: 8 output
-// columns per workgroup, thread t < C owns row t of the covariance; double throughout. Writes the vcg_conv_fwd stats
-// layout with one used slot: stats[n][0] = (mean, M2 = M var), count row slot 0 = (M, 1).
+// bn3's batch statistics from g64 = [Gc | d | c] (the centred Gram matrix and column sums of conv3's input, and the
+// centre: bn_gram's file comment) and conv3's bf16 weights w [N][C]: Cov = Gc / M - (d / M)(d / M)^T and
+// mu = c + d / M; 8 output columns per workgroup, thread t < C owns row t of the covariance; double throughout.
+// Writes the vcg_conv_fwd stats layout with one used slot: stats[n][0] = (mean, M2 = M var), count row slot 0 =
+// (M, 1).
 __global__ __launch_bounds__(256) void gram_stats_kernel(const double* __restrict__ g64, const bf16_t* __restrict__ w,
                                                         long long M, int N, int C, float2* __restrict__ stats,
                                                         int mtiles) {
   const double* __restrict__ gram = g64;
-  const double* __restrict__ colsum = g64 + (long long)C * C;
+  const double* __restrict__ dsum = g64 + (long long)C * C;
+  const double* __restrict__ ctr = dsum + C;
+  __shared__ double dm[1024];
   __shared__ double mu[1024];
   __shared__ double wq[8][1024];
   __shared__ double pm[8][256], pv[8][256];
   const int n0 = blockIdx.x * 8, tid = threadIdx.x;
   const double invM = 1.0 / (double)M;
-  for (int k = tid; k < C; k += 256) mu[k] = colsum[k] * invM;
+  for (int k = tid; k < C; k += 256) {
+    dm[k] = dsum[k] * invM;
+    mu[k] = ctr[k] + dm[k];
+  }
   for (int i = tid; i < 8 * C; i += 256) {
     const int q = i / C, k = i - q * C;
     wq[q][k] = n0 + q < N ? (double)bf2f(w[(long long)(n0 + q) * C + k]) : 0.0;
@@ -369,7 +338,7 @@ __global__ __launch_bounds__(256) void gram_stats_kernel(const double* __restric
     for (int q = 0; q < 8; ++q) u[q] = 0.0;
     const double* gr = gram + (long long)t * C;
     for (int k = 0; k < C; ++k) {
-      const double cv = gr[k] * invM - mu[t] * mu[k];
+      const double cv = gr[k] * invM - dm[t] * dm[k];
 #pragma unroll
       for (int q = 0; q < 8; ++q) u[q] = fma(cv, wq[q][k], u[q]);
     }
@@ -412,45 +381,45 @@ using namespace vcg;
 
 VCG_API long long vcg_bn_apply_gram_ws_bytes(long long P, int C) {
   if (C != 64 && C != 128 && C != 256) return 0;
-  return (long long)gram_grid(P, C) * ((long long)C * C + 2 * C) * 4;
+  return (long long)gram_grid(P, C) * ((long long)C * C + C) * 4;
 }
 
 // out = bf16(relu(fma(y, scale, shift))) (vcg_bn_apply's values), colsum[c] = sum of out's column c (as
-// vcg_bn_apply_colsum), gram[j][k] = sum_rows out[j] out[k] (f32 [C][C]); g64 (optional): the same Gram matrix and
-// column sums in double, [C * C + C] (accumulated centred per workgroup, see the file comment: the input of
-// vcg_bn_stats_from_gram). C = 64 / 128 / 256, bf16.
-VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* shift, void* out, float* colsum,
-                              float* gram, double* g64, float* ws, long long ws_bytes, long long P, int C,
-                              hipStream_t s) {
-  VCG_REQUIRE(y && scale && shift && out && colsum && gram && ws, "null argument");
+// vcg_bn_apply_colsum, up to the summation order), gram[j][k] = sum_rows out[j] out[k] (f32 [C][C]); g64 (double
+// [C * C + 2 C]) = [Gc | d | c], the Gram matrix and column sums centred at c (the file comment), which
+// vcg_bn_stats_from_gram reads. mean / invstd: the BatchNorm statistics that scale / shift fold (for the centre).
+// C = 64 / 128 / 256, bf16.
+VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* shift, const float* mean,
+                              const float* invstd, void* out, float* colsum, float* gram, double* g64, float* ws,
+                              long long ws_bytes, long long P, int C, hipStream_t s) {
+  VCG_REQUIRE(y && scale && shift && mean && invstd && out && colsum && gram && g64 && ws, "null argument");
   VCG_REQUIRE(C == 64 || C == 128 || C == 256, "C must be 64, 128 or 256");
   VCG_REQUIRE(P > 0, "no rows");
   VCG_REQUIRE((((uintptr_t)y | (uintptr_t)out) & 15) == 0, "16-B alignment");
   const int g = gram_grid(P, C);
   const long long n = (long long)C * C + C;
-  VCG_REQUIRE(ws_bytes >= vcg_bn_apply_gram_ws_bytes(P, C), "workspace too small");
-  if (C == 64)
-    hipLaunchKernelGGL(bn_apply_gram_kernel<64>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
-                       (bf16_t*)out, ws, P);
-  else if (C == 128)
-    hipLaunchKernelGGL(bn_apply_gram_kernel<128>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
-                       (bf16_t*)out, ws, P);
-  else
-    hipLaunchKernelGGL(bn_apply_gram_kernel<256>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift,
-                       (bf16_t*)out, ws, P);
+  VCG_REQUIRE(ws_bytes >= (long long)g * n * 4, "workspace too small");
+#define VCG_GRAM(CC)                                                                                            \
+  hipLaunchKernelGGL(bn_apply_gram_kernel<CC>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift, mean, \
+                     invstd, (bf16_t*)out, ws, g64, P)
+  if (C == 64) VCG_GRAM(64);
+  else if (C == 128) VCG_GRAM(128);
+  else VCG_GRAM(256);
+#undef VCG_GRAM
   VCG_LAUNCH_CHECK();
   const int nq = (int)(n / 4);  // (n = C (C + 1), C a power of two >= 64: a multiple of 4)
   int G = 1;
   while (G < 64 && G * 2 <= g && (long long)nq * G < 65536) G *= 2;
   const int QB = 256 / G;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((nq + QB - 1) / QB)), dim3(256), 0, s, ws, g, (int)n, G, gram,
-                     colsum, C, g64, P, 16384 / C);
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((nq + QB - 1) / QB)), dim3(256), 0, s, ws, g, (int)n, G, g64);
+  VCG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(gram_finish_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g64, P, C, gram, colsum);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
 
-// conv3's batch statistics from vcg_bn_apply_gram's double g64 (Gram matrix then column sums) of its input and its
-// bf16 weights w [N][C] (the forward GEMM layout): stats in the vcg_conv_fwd layout ([N + 1][mtiles] float2, one
+// conv3's batch statistics from vcg_bn_apply_gram's g64 (its input's centred Gram matrix, column sums and centre) and
+// its bf16 weights w [N][C] (the forward GEMM layout): stats in the vcg_conv_fwd layout ([N + 1][mtiles] float2, one
 // used slot), for vcg_bn_finalize.
 VCG_API int vcg_bn_stats_from_gram(const double* g64, const void* w, long long M, int N, int C, float* stats,
                                    int mtiles, hipStream_t s) {

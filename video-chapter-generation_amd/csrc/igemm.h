@@ -309,4 +309,8 @@ int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int 
 int wgrad_fast_tile_m(int M);
 int wgrad_fast_tile_n(int N);
 
+// the 256 x 256-tile engine (igemm256.hip): whether it takes a GEMM, and its launch
+bool gemm256_ok(const GemmParams& p, int amode, int epi, int z);
+int run_gemm256(const GemmParams& p, int amode, int epi, hipStream_t s);
+
 }  // namespace vcg

@@ -176,28 +176,29 @@ def bn_apply_colsum(y, scale, shift, C, relu=True):
     return out, cs
 
 
-def bn_apply_gram(y, scale, shift, C):
-    """(relu(bn_apply(y)), its column sums f32 [C], its Gram matrix out^T out f32 [C, C], the same Gram matrix and
-    column sums in double [C * C + C]) in one pass (vcg_bn_apply_gram, bf16, C in 64 / 128 / 256; the double copy,
-    accumulated centred per workgroup, is what bn_stats_from_gram reads)."""
+def bn_apply_gram(y, scale, shift, C, mean, invstd):
+    """(relu(bn_apply(y)), its column sums f32 [C], its Gram matrix out^T out f32 [C, C], and g64: the same Gram
+    matrix and column sums accumulated centred per channel, with the centres, double [C * C + 2 C]) in one pass
+    (vcg_bn_apply_gram, bf16, C in 64 / 128 / 256; mean / invstd: the BN statistics scale / shift fold; g64 is what
+    bn_stats_from_gram reads)."""
     _chk(y, torch.bfloat16, "y")
     out = torch.empty_like(y)
     cs = torch.empty(C, dtype=torch.float32, device=y.device)
     gram = torch.empty((C, C), dtype=torch.float32, device=y.device)
-    g64 = torch.empty(C * C + C, dtype=torch.float64, device=y.device)
+    g64 = torch.empty(C * C + 2 * C, dtype=torch.float64, device=y.device)
     P_ = y.numel() // C
     w = ws(_lib.query("vcg_bn_apply_gram_ws_bytes", P_, C), y.device)
-    _lib.call("vcg_bn_apply_gram", P(y), P(scale), P(shift), P(out), P(cs), P(gram), P(g64), P(w), w.numel() * 4,
-              P_, C, stream())
+    _lib.call("vcg_bn_apply_gram", P(y), P(scale), P(shift), P(mean), P(invstd), P(out), P(cs), P(gram), P(g64),
+              P(w), w.numel() * 4, P_, C, stream())
     return out, cs, gram, g64
 
 
 def bn_stats_from_gram(g64, w, M, N, C, stats):
-    """BN statistics of x w^T (w bf16 [N, C]) from x's double (Gram matrix, column sums) g64 [C * C + C]
-    (bn_apply_gram) into a stats_buffer(N, M) (vcg_bn_stats_from_gram; one used slot, for bn_finalize)."""
+    """BN statistics of x w^T (w bf16 [N, C]) from x's centred (Gram matrix, column sums, centres) g64 [C * C + 2 C]
+    of bn_apply_gram into a stats_buffer(N, M) (vcg_bn_stats_from_gram; one used slot, for bn_finalize)."""
     _chk(w, torch.bfloat16, "w")
     _chk(g64, torch.float64, "g64")
-    assert g64.numel() == C * C + C
+    assert g64.numel() == C * C + 2 * C
     _lib.call("vcg_bn_stats_from_gram", P(g64), P(w), M, N, C, P(stats), stats.shape[1], stream())
     return stats
 

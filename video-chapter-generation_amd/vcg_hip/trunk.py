@@ -304,7 +304,7 @@ class ResNetTrunk:
         if (fold_a2 or drop) and ResNetTrunk.gram_stats and planes in (64, 128, 256) and bn_mode(blk.bn3) != "running":
             # a2 with colsum(a2) and a2^T a2 from the bn2 apply pass: bn3's statistics follow from them (no conv3
             # statistics pass over a2 when y3 is not stored), and so does the Gram term of the a2-form backward fold
-            a2, a2sum, a2gram, g64 = ops.bn_apply_gram(y2, b2.scale, b2.shift, planes)
+            a2, a2sum, a2gram, g64 = ops.bn_apply_gram(y2, b2.scale, b2.shift, planes, b2.mean, b2.invstd)
         elif fold_a2:
             # (the a2 form of the bn3 backward fold needs colsum(a2): written by the bn2 apply pass itself. A
             # separate column-sum pass on the side stream contended with conv3's GEMMs -- ~4 ms of kernel time per
