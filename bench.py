@@ -117,9 +117,8 @@ def cpu_model():
 def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=None, bn="running"):
     """The oracle (oracle/model.py: fp32 CPU restatement of the reference path, test infrastructure) timed on this
     host: train = one reference train step (fwd BN-train with BERT dropout 0.1 as the GPU step runs it + CE + bwd +
-    clip_grad_norm_ + AdamW), fwd = the eval forward. Median of `reps` timed runs after 1 warm-up. B is a bounded
-    sample (train: 4 windows x 2 timed runs, fwd: 4 windows x 3; 15-30 s of CPU work in all) so the default bench
-    finishes in minutes. The per-window CPU rate barely depends on B (the CPU path has no batch-level parallelism
+    clip_grad_norm_ + AdamW), fwd = the eval forward. Median of `reps` (3) timed runs after 1 warm-up. B is a bounded
+    sample (4 windows per run; 30-60 s of CPU work in all) so the default bench finishes in minutes. The per-window CPU rate barely depends on B (the CPU path has no batch-level parallelism
     beyond the threads; the round-3 sweep, profiles/r03_cpu_sweep_*.jsonl: the forward at B 64 is ~20 % SLOWER per
     window than at B 4), so a small B does not understate the CPU."""
     import torch
@@ -127,7 +126,7 @@ def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=None, bn="running
     from vcg_hip.build import build_two_stream
     from vcg_hip import synth
     B = B or 4
-    reps = reps or (2 if mode == "train" else 3)
+    reps = reps or 3
     torch.set_num_threads(threads)
     m = build_two_stream(clip_frame_num=T, dropout=0.1)
     sd = m.state_dict()
@@ -154,7 +153,12 @@ def cpu_baseline(T, HW, L, threads, mode="train", B=None, reps=None, bn="running
     return {"value": round(B / med, 4), "unit": "clip-windows/sec", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"oracle/ CPU {what} on B={B} windows of {T}x{HW}^2 + {L} tokens; median of {reps} timed runs "
-                      f"({', '.join(f'{t:.2f}' for t in times)} s) after 1 warm-up; torch.set_num_threads({threads})"}
+                      f"({', '.join(f'{t:.2f}' for t in times)} s) after 1 warm-up; torch.set_num_threads({threads})",
+            "why_this_sample": "B=4, not the GPU's 64: a bounded 30-60 s sample, and the CPU's per-window rate does not "
+                               "grow with B (round-3 sweep, profiles/r03_cpu_sweep_*.jsonl: the forward at B=64 is ~20 % "
+                               "slower per window than at B=4); 16 threads: the one-GPU box's CPU share (os.cpu_count() "
+                               "reports the whole host), within 10 % of the best thread count in every sweep (4-32 "
+                               "threads; 64+ ran slower)"}
 
 
 # ----------------------------------------------------------------------------- config 5

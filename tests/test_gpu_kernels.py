@@ -120,7 +120,7 @@ def test_conv_fwd_and_stats(K, dtype, case):
 
 @pytest.mark.parametrize("case", [(16, 56, 56, 64, 256, 1, 1, 0, 0, 2.0), (8, 28, 28, 128, 128, 3, 1, 1, 0, 0.0),
                                   (8, 29, 27, 64, 64, 3, 1, 1, 4, 3.0),
-                                  # >= 64 Ki rows (the 256-row kernel's shapes when VCG_BIG_TILE=1)
+                                  # >= 64 Ki rows
                                   (24, 56, 56, 64, 256, 1, 1, 0, 0, 2.0), (16, 65, 71, 64, 128, 3, 1, 1, 4, 1.0)])
 def test_conv_stats_multitile(K, case):
     """BN statistics when persistent workgroups walk several M-tiles (one stats slot per workgroup
@@ -519,7 +519,7 @@ def test_transpose_multi(K):
 
 # (N, H, W, C = dgrad output channels, Cout, k, stride, pad, T) of the fused trunk-backward dgrad
 DGRAD_BWD_CASES = [
-    (16, 65, 71, 128, 64, 3, 1, 1, 4),  # >= 64 Ki rows, 128 columns (256-row kernel with VCG_BIG_TILE=1)
+    (16, 65, 71, 128, 64, 3, 1, 1, 4),  # >= 64 Ki rows, 128 columns
     (16, 64, 70, 256, 64, 1, 1, 0, 8),  # same, dense 1x1
     (8, 9, 9, 64, 64, 3, 1, 1, 4),     # conv2 3x3
     (8, 10, 10, 64, 128, 3, 2, 1, 4),  # conv2 3x3 / 2 (block 0 of a stage): four sub-pixel class GEMMs
@@ -639,36 +639,6 @@ def test_conv_dgrad_bwd_stream_vs_persistent(K, case, y2, monkeypatch):
     assert torch.equal(ga, gb), f"g differs: max {(ga.float() - gb.float()).abs().max().item():.3e}"
     for a, b in ((sa, sb), (xa, xb)):
         assert (a.double() - b.double()).abs().max().item() <= 1e-4 * (b.abs().max().item() + 1.0)
-
-
-@pytest.mark.parametrize("case", [(16, 56, 56, 256, 64, 8, 1), (16, 28, 28, 512, 128, 8, 1), (5, 7, 7, 256, 64, 5, 1),
-                                  (4, 14, 14, 1024, 128, 4, 1), (16, 56, 56, 256, 128, 8, 2), (5, 7, 7, 256, 64, 5, 2)])
-def test_conv_dgrad_bwd_register_stream(K, case, monkeypatch):
-    """The register-streaming fused 1x1 dgrad with mask bits and no y (stream1x1.hip, the trunk's conv1 input
-    gradients after a block whose y3 is not stored) against the LDS-ring / persistent engines (VCG_RS_DGRAD=0):
-    g bit for bit (TSM adjoint with clip edges, tiles straddling frames, ragged rows, 1-3 shift variants per column
-    block, the compact stride-2 residual of a layer's first block), sum_g to float rounding."""
-    N, H, W, C, Cout, T, rs = case
-    dtype = torch.bfloat16
-    fold = C // 8
-    dy = _rand((N, H, W, Cout), dtype, 81).to(DEV)
-    wt = K.weight_prep(_rand((Cout, C, 1, 1), torch.float32, 82, 0.1).to(DEV), C, dtype, transposed=True)
-    res = _rand((N, (H + 1) // 2, (W + 1) // 2, C) if rs == 2 else (N, H, W, C), dtype, 85).to(DEV)
-    _, bits = K.bn_apply(_rand((N, H, W, C), dtype, 86).to(DEV), torch.ones(C, device=DEV),
-                         torch.zeros(C, device=DEV), C, relu=True, bits=True)
-    outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("VCG_RS_DGRAD", flag)
-        sums = torch.zeros((2, C), device=DEV)
-        g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, 1, 1, 1, 0, tsm_T=T, tsm_fold=fold, res=res, res_stride=rs,
-                             bits=bits, sums=sums)
-        assert g is not None
-        torch.cuda.synchronize()
-        outs.append((g.clone(), sums.clone()))
-    (ga, sa), (gb, sb) = outs
-    assert torch.equal(ga, gb), f"g differs: max {(ga.float() - gb.float()).abs().max().item():.3e}"
-    assert (sa[0].double() - sb[0].double()).abs().max().item() <= 1e-4 * (sb[0].abs().max().item() + 1.0)
-    assert torch.equal(sa[1], sb[1])  # (no y: no sum against it)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -897,7 +867,7 @@ def test_attention_softmax_dropout(K):
 @pytest.mark.parametrize("case", [(16, 65, 71, 128, 64, 3, 1, 1), (16, 64, 70, 256, 64, 1, 1, 0),
                                   (8, 130, 66, 128, 64, 3, 2, 1)])
 def test_conv_dgrad_big(K, case):
-    """Input gradients with >= 64 Ki rows (the 256-row kernel's shapes with VCG_BIG_TILE=1) against torch in float64."""
+    """Input gradients with >= 64 Ki rows against torch in float64."""
     dtype = torch.bfloat16
     N, H, W, Cin, Cout, KH, s, p = case
     x = torch.zeros((N, Cin, H, W), dtype=torch.float64, requires_grad=True)

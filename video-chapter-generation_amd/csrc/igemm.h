@@ -299,9 +299,6 @@ int wgrad_patch_rows(int dtype, int H, int W, int C, int Cin, int Cout, int KH, 
                      int tsm_fold);
 int wgrad_patch_splits(int C, int Cout);
 // stream1x1.hip: relu(bf16(x wfold^T + bias) + res) + mask bits on the register-streaming kernel (-1: not eligible)
-bool rs_dgrad_ok(const GemmParams& p);      // stream1x1.hip: the fused 1x1 dgrad (mask bits, no y) there
-int rs_dgrad_slots(const GemmParams& p);
-int run_rs1x1_dgrad(const GemmParams& p, hipStream_t s);
 int run_rs1x1_bnres(const void* x, const void* wfold, const float* bias, const void* res, void* out, uint8_t* bits,
                     long long M, int N, int K, hipStream_t s);
 int run_wgrad_patch(const void* x, const void* dy, float* ws, int N, int H, int W, int C, int Cout, int R,

@@ -1063,22 +1063,9 @@ static int grid_rows(int M, int N, int z, int BM, int BN, int epi) {
 
 static int fast_bn_cols(int N) { return (N % 128 == 0 || N > 64 * 3) ? 128 : 64; }
 
-// 256-row tiles (8 waves, 3-stage ring, 1 workgroup per CU) for the big conv GEMMs (>= 64 Ki rows,
-// 128-column tiles, no residual / aux epilogue, not batched): opt-in with VCG_BIG_TILE=1. Measured
-// slower than two 4-wave 128-row workgroups per CU on every conv shape (l3 conv2 3x3: 367 vs 295 us;
-// train step 565 vs 620 windows/s): with one barrier-synchronised workgroup per CU nothing overlaps
-// the barrier stalls. Kept as the base of an 8-phase schedule.
-static bool big_tile_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("VCG_BIG_TILE");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
-static int fast_bm(int M, int N, int z, bool res_or_aux) {
-  return (big_tile_enabled() && M >= 65536 && fast_bn_cols(N) == 128 && z == 1 && !res_or_aux) ? 256 : 128;
-}
+// (The 256-row 3-stage variant of this engine, opt-in VCG_BIG_TILE in rounds 2-4, measured slower than two 4-wave
+// 128-row workgroups per CU on every conv shape and was removed; the 256 x 256 8-wave engine is igemm256.hip.)
+static int fast_bm(int, int, int, bool) { return 128; }
 
 int fast_grid_rows(int M, int N, int z, int epi) {
   return grid_rows(M, N, z, fast_bm(M, N, z, false), fast_bn_cols(N), epi);
@@ -1681,7 +1668,6 @@ static int bwd_stream_rows(const GemmParams& p) {
 }
 
 int fast_bwd_slots(const GemmParams& p) {
-  if (rs_dgrad_ok(p)) return rs_dgrad_slots(p);
   if (bwd_stream_ok(p)) return bwd_stream_rows(p);
   const int R = patch_rows(p, OP_DGRAD);
   if (R > 0) return patch_grid_rows(p, patch_geom(p, R));
@@ -1738,9 +1724,6 @@ static int run_bwd_stream(const GemmParams& p, hipStream_t s) {
 
 template <int AM, int EPI, int RES = 0>
 static int fast_bn(const GemmParams& p, int z, hipStream_t s) {
-  if constexpr (!RES) {
-    if (fast_bm(p.M, p.N, z, p.aux != nullptr) == 256) return launch_fast<256, 128, AM, EPI, false>(p, z, s);
-  }
   if (fast_bn_cols(p.N) == 128) return launch_fast<128, 128, AM, EPI, RES>(p, z, s);
   return launch_fast<128, 64, AM, EPI, RES>(p, z, s);
 }
@@ -1816,12 +1799,6 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
     }
   }
   if (amode != OP_IM2COL_SMALLC && gemm256_ok(p, amode, epi, z)) return run_gemm256(p, amode, epi, s);
-  if (epi == EPI_BWD && amode == OP_DENSE_K && z == 1 && rs_dgrad_ok(p)) {  // the register-streaming kernel
-    const int tk = timing_begin(s);
-    const int rc = run_rs1x1_dgrad(p, s);
-    timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_DENSE_K, EPI_BWD, false>(p, 1));
-    return rc;
-  }
   if (epi == EPI_BWD && amode == OP_DENSE_K && z == 1 && bwd_stream_ok(p))
     return p.K == 64 ? run_bwd_stream<1>(p, s) : run_bwd_stream<2>(p, s);
   if (epi == EPI_BWD && bwd_light(p)) {

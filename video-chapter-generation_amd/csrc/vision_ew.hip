@@ -781,13 +781,16 @@ __global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const T* __restrict__
 // of dy, the argmax bytes and the whole pre-pool y (the stem's conv output, 4x the pooled size). mp is the bf16
 // max, so y - mean carries one bf16 rounding of the activation (the per-pixel path carries that of y).
 // Degenerate channels -- msc == 0 (a zero BN weight: mp says nothing about y) or |msh| > 32 |gamma| (the recovery
-// cancels: its error is ~2^-9 |msh| / |gamma| of a std) -- read y at the window's argmax pixel instead (idx byte
-// k: pixel (2 oh - 1 + k / 3, 2 ow - 1 + k % 3) of the [N][H][W][C] pre-pool y), for the windows that pass the mask.
+// cancels: its error is ~2^-9 |msh| / |gamma| of a std) -- contribute no sum_gx here; maxpool_bn_sums_degen_kernel
+// adds theirs from y at the windows' argmax pixels in a slot of its own. (A per-element gather branch inside this
+// loop, never taken on the bench, cost the train step ~1 % on the same box: profiles/r05_degen_branch_ab.txt.)
+__device__ __forceinline__ bool pooled_degen(float sc, float sh, float is) {
+  return sc == 0.f || !(fabsf(sh) * is <= 32.f * fabsf(sc));
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_bn_sums_pooled_kernel(const T* __restrict__ dy, const T* __restrict__ mp,
-                                                                     const uint8_t* __restrict__ idx,
-                                                                     const T* __restrict__ y, int H, int W, int OH,
-                                                                     int OW, long long TV, int lcpr, MpBn bn) {
+                                                                     long long TV, int lcpr, MpBn bn) {
   constexpr int VN = V<T>::N;
   __shared__ float red[2][256][VN];
   const int cpr = 1 << lcpr;
@@ -795,18 +798,15 @@ __global__ __launch_bounds__(256) void maxpool_bn_sums_pooled_kernel(const T* __
   const int c0 = chunk * VN;
   const int C = cpr * VN;
   float mu[VN], sc[VN], sh[VN], is[VN], rsc[VN], off[VN], s1[VN], s2[VN];
-  bool degen[VN];
-  bool any_degen = false;
   load_params<VN>(bn.mean, c0, mu);
   load_params<VN>(bn.msc, c0, sc);
   load_params<VN>(bn.msh, c0, sh);
   load_params<VN>(bn.invstd, c0, is);
 #pragma unroll
   for (int e = 0; e < VN; ++e) {
-    degen[e] = sc[e] == 0.f || !(fabsf(sh[e]) * is[e] <= 32.f * fabsf(sc[e]));
-    any_degen |= degen[e];
-    rsc[e] = degen[e] ? 0.f : 1.f / sc[e];
-    off[e] = degen[e] ? 0.f : -sh[e] * rsc[e] - mu[e];  // y - mean = mp / msc + off
+    const bool dg = pooled_degen(sc[e], sh[e], is[e]);
+    rsc[e] = dg ? 0.f : 1.f / sc[e];
+    off[e] = dg ? 0.f : -sh[e] * rsc[e] - mu[e];  // y - mean = mp / msc + off
     s1[e] = s2[e] = 0.f;
   }
   const long long stride = (long long)gridDim.x * SB;
@@ -827,22 +827,6 @@ __global__ __launch_bounds__(256) void maxpool_bn_sums_pooled_kernel(const T* __
         s1[e] += d;
         s2[e] = fmaf(d, fmaf(m[u][e], rsc[e], off[e]), s2[e]);
       }
-      if (any_degen) {  // (rare: a per-element gather of y at the argmax pixel)
-        const long long v = base + u * 256;
-        const long long pix = v >> lcpr;  // pooled pixel (n, oh, ow)
-        const int ow = (int)(pix % OW);
-        const long long t = pix / OW;
-        const int oh = (int)(t % OH);
-        const long long n = t / OH;
-#pragma unroll
-        for (int e = 0; e < VN; ++e) {
-          if (!degen[e] || !(m[u][e] > 0.f)) continue;
-          const int k = idx[v * VN + e];
-          const int ih = 2 * oh - 1 + k / 3, iw = 2 * ow - 1 + k % 3;
-          const float yv = to_f<T>(y[((n * H + ih) * W + iw) * C + c0 + e]);
-          s2[e] = fmaf(g[u][e], yv - mu[e], s2[e]);
-        }
-      }
     }
   }
 #pragma unroll
@@ -858,6 +842,45 @@ __global__ __launch_bounds__(256) void maxpool_bn_sums_pooled_kernel(const T* __
     for (int kk = ch; kk < 256; kk += cpr) a += red[which][kk][e];
     if (which) a *= bn.invstd[c];
     bn.part[(long long)blockIdx.x * 2 * C + i] = a;
+  }
+}
+
+// sum_gx of the degenerate channels (pooled_degen) of maxpool_bn_sums_pooled_kernel, into the partial slot `slot`:
+// one workgroup per channel; a regular channel writes zeros and returns at once (the bench's case: no channel is
+// degenerate), a degenerate one sums dy (y - mean) over the windows that pass the mask, y read at the argmax pixel
+// (idx byte k: pixel (2 oh - 1 + k / 3, 2 ow - 1 + k % 3) of the [N][H][W][C] pre-pool y), in a fixed order.
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bn_sums_degen_kernel(const T* __restrict__ dy, const T* __restrict__ mp,
+                                                                    const uint8_t* __restrict__ idx,
+                                                                    const T* __restrict__ y, int H, int W, int OH,
+                                                                    int OW, long long npix, int C, MpBn bn, int slot) {
+  __shared__ float red[256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const float sc = bn.msc[c], sh = bn.msh[c], is = bn.invstd[c], mu = bn.mean[c];
+  float* out = bn.part + (long long)slot * 2 * C;
+  if (!pooled_degen(sc, sh, is)) {
+    if (tid == 0) out[c] = out[C + c] = 0.f;
+    return;
+  }
+  float s2 = 0.f;
+  for (long long v = tid; v < npix; v += 256) {
+    const float m = to_f<T>(mp[v * C + c]);
+    if (!(m > 0.f)) continue;
+    const int ow = (int)(v % OW);
+    const long long t = v / OW;
+    const int oh = (int)(t % OH);
+    const long long n = t / OH;
+    const int k = idx[v * C + c];
+    const int ih = 2 * oh - 1 + k / 3, iw = 2 * ow - 1 + k % 3;
+    s2 = fmaf(to_f<T>(dy[v * C + c]), to_f<T>(y[((n * H + ih) * W + iw) * C + c]) - mu, s2);
+  }
+  red[tid] = s2;
+  __syncthreads();
+  if (tid == 0) {
+    float a = 0.f;
+    for (int t = 0; t < 256; ++t) a += red[t];
+    out[c] = 0.f;  // (sum_g: the main pass counts every channel)
+    out[C + c] = a * is;
   }
 }
 
@@ -1154,7 +1177,7 @@ VCG_API int vcg_maxpool_bwd(int dtype, const void* dy, const unsigned char* idx,
   return VCG_OK;
 }
 
-VCG_API long long vcg_maxpool_bwd_bn_ws_bytes(int C) { return GRID_MAX * 2 * C * 4 + 64; }
+VCG_API long long vcg_maxpool_bwd_bn_ws_bytes(int C) { return (GRID_MAX + 1) * 2 * C * 4 + 64; }
 
 // max-pool backward fused with the stem BatchNorm-backward reduction: g = maxpool_bwd(dy) masked by the
 // forward ReLU (fma(y, mscale, mshift) > 0); sum_g / sum_gx finalized, dgamma / dbeta accumulated. g == NULL:
@@ -1214,14 +1237,20 @@ VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void
   const unsigned nb = stream_grid(TV);
   MpBn bn{};
   bn.mean = mean; bn.invstd = invstd; bn.msc = mscale; bn.msh = mshift; bn.part = ws;
-  if (dtype == VCG_BF16)
+  const long long npix = (long long)N * OH * OW;
+  if (dtype == VCG_BF16) {
     hipLaunchKernelGGL(maxpool_bn_sums_pooled_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dy,
-                       (const bf16_t*)mp, idx, (const bf16_t*)y, H, W, OH, OW, TV, lcpr, bn);
-  else
+                       (const bf16_t*)mp, TV, lcpr, bn);
+    hipLaunchKernelGGL(maxpool_bn_sums_degen_kernel<bf16_t>, dim3(C), dim3(256), 0, s, (const bf16_t*)dy,
+                       (const bf16_t*)mp, idx, (const bf16_t*)y, H, W, OH, OW, npix, C, bn, (int)nb);
+  } else {
     hipLaunchKernelGGL(maxpool_bn_sums_pooled_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)dy,
-                       (const float*)mp, idx, (const float*)y, H, W, OH, OW, TV, lcpr, bn);
+                       (const float*)mp, TV, lcpr, bn);
+    hipLaunchKernelGGL(maxpool_bn_sums_degen_kernel<float>, dim3(C), dim3(256), 0, s, (const float*)dy,
+                       (const float*)mp, idx, (const float*)y, H, W, OH, OW, npix, C, bn, (int)nb);
+  }
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb + 1, C, 2LL * C, C,
                      sum_g, sum_gx, dgamma, dbeta, 1);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
