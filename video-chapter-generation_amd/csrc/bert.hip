@@ -708,14 +708,15 @@ __global__ __launch_bounds__(256) void colsum_tall_kernel(const T* __restrict__ 
   }
 }
 
-// Column sums of partial rows, 64 columns x 16 row-stripes per block (1024 threads), fixed order:
-//   out_k[c] (+)= sum_i part[i * stride + k * N + c], k < nout
-__global__ __launch_bounds__(1024) void colred16_kernel(const float* __restrict__ part, int nblocks, long long stride,
-                                                        int N, int nout, float* out0, float* out1, float* out2,
-                                                        int accumulate) {
-  __shared__ double sa[3][16][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+// Column sums of partial rows, 16 columns x 16 row-stripes per 256-thread block, fixed order (thread ty sums rows ty,
+// ty + 16, ... in double, then the 16 stripes in order): out_k[c] (+)= sum_i part[i * stride + k * N + c], k < nout.
+// (1024-thread blocks waited tens of us for a free CU beside the trunk's kernels.)
+__global__ __launch_bounds__(256) void colred16_kernel(const float* __restrict__ part, int nblocks, long long stride,
+                                                       int N, int nout, float* out0, float* out1, float* out2,
+                                                       int accumulate) {
+  __shared__ double sa[3][16][16];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + tx;
   double a[3] = {0, 0, 0};
   if (c < N) {
     for (int i = ty; i < nblocks; i += 16)
@@ -876,7 +877,7 @@ VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* r
 #undef VCG_LNB_Q
 #undef VCG_LNB
     VCG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(colred16_kernel, dim3((H + 63) / 64), dim3(1024), 0, s, ws, nbr, (long long)nred * H, H, nred,
+    hipLaunchKernelGGL(colred16_kernel, dim3((H + 15) / 16), dim3(256), 0, s, ws, nbr, (long long)nred * H, H, nred,
                        gamma_grad, beta_grad, bias_grad, 1);
     VCG_LAUNCH_CHECK();
     return VCG_OK;
@@ -934,7 +935,7 @@ VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, 
     hipLaunchKernelGGL((colsum_tall_kernel<bf16_t, 4>), dim3(nbx), dim3(256), 0, s, (const bf16_t*)x, ld, rows, N, cpr,
                        ws);
     VCG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(colred16_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, ws, nbx, (long long)N, N, 1, out,
+    hipLaunchKernelGGL(colred16_kernel, dim3((N + 15) / 16), dim3(256), 0, s, ws, nbx, (long long)N, N, 1, out,
                        (float*)nullptr, (float*)nullptr, accumulate);
     VCG_LAUNCH_CHECK();
     return VCG_OK;
@@ -949,7 +950,7 @@ VCG_API int vcg_colsum(int dtype, const void* x, long long ld, int rows, int N, 
     else
       hipLaunchKernelGGL(colsum_rw_kernel<float>, g, dim3(256), 0, s, (const float*)x, ld, rows, N, ws);
     VCG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(colred16_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, ws, nbx, (long long)N, N, 1, out,
+    hipLaunchKernelGGL(colred16_kernel, dim3((N + 15) / 16), dim3(256), 0, s, ws, nbx, (long long)N, N, 1, out,
                        (float*)nullptr, (float*)nullptr, accumulate);
     VCG_LAUNCH_CHECK();
     return VCG_OK;

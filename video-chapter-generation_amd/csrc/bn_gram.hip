@@ -368,6 +368,65 @@ __global__ __launch_bounds__(256) void gram_stats_kernel(const double* __restric
   }
 }
 
+// The same statistics for C <= 256 with the covariance walked by rows: thread k owns column k (the Gram loads of a row
+// are coalesced; the old form read one strided row per thread), 16 output columns per workgroup share each load,
+// and the per-column sums over k are combined by a fixed-order tree (deterministic).
+constexpr int GS_Q = 16;
+__global__ __launch_bounds__(256) void gram_stats_rows_kernel(const double* __restrict__ g64, const bf16_t* __restrict__ w,
+                                                             long long M, int N, int C, float2* __restrict__ stats,
+                                                             int mtiles) {
+  const double* __restrict__ gram = g64;
+  const double* __restrict__ dsum = g64 + (long long)C * C;
+  const double* __restrict__ ctr = dsum + C;
+  __shared__ double dm[256], mu[256];
+  __shared__ double wq[GS_Q][256];
+  __shared__ double red[2][GS_Q][256];
+  const int n0 = blockIdx.x * GS_Q, k = threadIdx.x;
+  const double invM = 1.0 / (double)M;
+  if (k < C) {
+    dm[k] = dsum[k] * invM;
+    mu[k] = ctr[k] + dm[k];
+  }
+  for (int i = k; i < GS_Q * C; i += 256) {
+    const int q = i / C, kk = i - q * C;
+    wq[q][kk] = n0 + q < N ? (double)bf2f(w[(long long)(n0 + q) * C + kk]) : 0.0;
+  }
+  __syncthreads();
+  double acc[GS_Q];
+#pragma unroll
+  for (int q = 0; q < GS_Q; ++q) acc[q] = 0.0;
+  if (k < C) {
+    const double dk = dm[k];
+    for (int t = 0; t < C; ++t) {
+      const double cv = gram[(long long)t * C + k] * invM - dm[t] * dk;
+#pragma unroll
+      for (int q = 0; q < GS_Q; ++q) acc[q] = fma(wq[q][t], cv, acc[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < GS_Q; ++q) {
+    red[0][q][k] = k < C ? wq[q][k] * mu[k] : 0.0;
+    red[1][q][k] = k < C ? wq[q][k] * acc[q] : 0.0;
+  }
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {  // fixed-order tree over the 256 columns
+    if (k < h) {
+#pragma unroll
+      for (int q = 0; q < GS_Q; ++q) {
+        red[0][q][k] += red[0][q][k + h];
+        red[1][q][k] += red[1][q][k + h];
+      }
+    }
+    __syncthreads();
+  }
+  if (k < GS_Q && n0 + k < N)
+    stats[(long long)(n0 + k) * mtiles] = make_float2((float)red[0][k][0], (float)(fmax(red[1][k][0], 0.0) * (double)M));
+  if (blockIdx.x == 0 && k == 0) {
+    float2* cnt = stats + (long long)N * mtiles;
+    cnt[0] = make_float2((float)M, 1.f);  // one used slot (bn_finalize reads cnt[0].y slots)
+  }
+}
+
 int gram_grid(long long P, int C) {
   const long long iters = (P + 16384 / C - 1) / (16384 / C);
   const long long cap = C >= 256 ? 256 : 512;
@@ -425,8 +484,12 @@ VCG_API int vcg_bn_stats_from_gram(const double* g64, const void* w, long long M
                                    int mtiles, hipStream_t s) {
   VCG_REQUIRE(g64 && w && stats, "null argument");
   VCG_REQUIRE(C > 0 && C <= 1024 && N > 0 && M > 0 && mtiles > 0, "bad shape");
-  hipLaunchKernelGGL(gram_stats_kernel, dim3((N + 7) / 8), dim3(256), 0, s, g64, (const bf16_t*)w, M, N, C,
-                     reinterpret_cast<float2*>(stats), mtiles);
+  if (C <= 256)
+    hipLaunchKernelGGL(gram_stats_rows_kernel, dim3((N + GS_Q - 1) / GS_Q), dim3(256), 0, s, g64, (const bf16_t*)w, M,
+                       N, C, reinterpret_cast<float2*>(stats), mtiles);
+  else
+    hipLaunchKernelGGL(gram_stats_kernel, dim3((N + 7) / 8), dim3(256), 0, s, g64, (const bf16_t*)w, M, N, C,
+                       reinterpret_cast<float2*>(stats), mtiles);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

@@ -145,12 +145,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ y, 
   }
 }
 
-// out[c] = sum_b part[b][c] (fixed order: 16 row stripes per channel in double, then the stripes in order)
-__global__ __launch_bounds__(1024) void colpart_reduce_kernel(const float* __restrict__ part, int nb, int C,
-                                                              float* __restrict__ out) {
-  __shared__ double sa[16][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+// out[c] = sum_b part[b][c] (fixed order: 16 row stripes per channel in double, then the stripes in order; 16 channels
+// per 256-thread block)
+__global__ __launch_bounds__(256) void colpart_reduce_kernel(const float* __restrict__ part, int nb, int C,
+                                                             float* __restrict__ out) {
+  __shared__ double sa[16][16];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + tx;
   double a = 0;
   if (c < C)
     for (int b = ty; b < nb; b += 16) a += part[(long long)b * C + c];
@@ -242,17 +243,19 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   }
 }
 
-// Column sums of partial[nb][2C] -> sum_g, sum_gx (+ dgamma/dbeta): 64 channels x 16 row-stripes per
-// block (1024 threads), loads coalesced across channels and unrolled across rows; fixed summation
-// order (deterministic).
+// Column sums of partial[nb][2C] -> sum_g, sum_gx (+ dgamma/dbeta): 16 channels x 16 row-stripes per 256-thread
+// block, loads coalesced across channels and unrolled across rows; fixed summation order (deterministic: thread ty sums
+// rows ty, ty + 16, ... in double, then the 16 stripes in order). (It ran with 64 channels x 16 stripes per 1024-thread
+// block: on a GPU busy with the side streams' kernels a 16-wave workgroup waited ~30 us for a CU to take it -- 53
+// of these per train step sit on the trunk's critical path, tools/queue_busy.py.)
 // (row i of partial: sum_g at [i * ld + c], sum_gx at [i * ld + gx_off + c]; ld = 2C / gx_off = C for
 // bn_bwd_reduce's partials)
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nb, int C,
-                                                               long long ld, int gx_off, float* sum_g, float* sum_gx,
-                                                               float* dgamma, float* dbeta, int accumulate) {
-  __shared__ double sa[16][64], sb[16][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nb, int C,
+                                                              long long ld, int gx_off, float* sum_g, float* sum_gx,
+                                                              float* dgamma, float* dbeta, int accumulate) {
+  __shared__ double sa[16][16], sb[16][16];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + tx;
   double a = 0, b = 0;
   if (c < C) {
     const float* p = partial + c;
@@ -943,7 +946,7 @@ namespace vcg {
 // column sums of EPI_BWD partials (igemm_fast.hip) -> sum_g / sum_gx (+ dgamma / dbeta, accumulated)
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
                            float* dgamma, float* dbeta, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, partial, nb, C, ld, gx_off, sum_g,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, partial, nb, C, ld, gx_off, sum_g,
                      sum_gx, dgamma, dbeta, accumulate);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -970,7 +973,7 @@ VCG_API int vcg_bn_apply_colsum(const void* y, const float* scale, const float* 
                      (const bf16_t*)nullptr, (const float*)nullptr, (const float*)nullptr, relu, (bf16_t*)out,
                      (uint8_t*)nullptr, TV, C / 8, ws);
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colpart_reduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)g, C, colsum);
+  hipLaunchKernelGGL(colpart_reduce_kernel, dim3((C + 15) / 16), dim3(256), 0, s, ws, (int)g, C, colsum);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
@@ -1075,7 +1078,7 @@ VCG_API int vcg_bn_bwd_reduce(int dtype, const void* dout, int mask_mode, const 
 #undef VCG_BN_RED_T
 #undef VCG_BN_RED
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, ws, (int)nb, C, 2LL * C, C,
                      sum_g, sum_gx, dgamma, dbeta, accumulate);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -1212,7 +1215,7 @@ VCG_API int vcg_maxpool_bwd_bn(int dtype, const void* dy, const unsigned char* i
     if (g) VCG_MPB(float, MP_RED, g); else VCG_MPB(float, MP_RED_ONLY, g);
   }
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb, C, 2LL * C, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, ws, (int)nb, C, 2LL * C, C,
                      sum_g, sum_gx, dgamma, dbeta, 1);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -1250,7 +1253,7 @@ VCG_API int vcg_maxpool_bwd_bn_sums_pooled(int dtype, const void* dy, const void
                        (const float*)mp, idx, (const float*)y, H, W, OH, OW, npix, C, bn, (int)nb);
   }
   VCG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ws, (int)nb + 1, C, 2LL * C, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, ws, (int)nb + 1, C, 2LL * C, C,
                      sum_g, sum_gx, dgamma, dbeta, 1);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
