@@ -601,18 +601,21 @@ def test_conv_dgrad_bwd(K, case, mode):
         assert (dbet2.double() - 0.25 - sg).abs().max().item() <= tol(sg)
 
 
-# the trunk's conv1 input gradients that the streaming EPI_BWD kernel takes (layers 1-2 at 16 frames):
-# (N, H, W, C, Cout, T, res_stride)
-STREAM_CASES = [(16, 56, 56, 256, 64, 8, 1), (16, 28, 28, 512, 128, 8, 1), (16, 56, 56, 256, 128, 8, 2)]
+# the trunk's conv1 input gradients that the streaming EPI_BWD kernel takes (layers 1-3 at 16 frames; K = 256: layer 3,
+# one A tile per ring slot and the weights in registers): (N, H, W, C, Cout, T, res_stride)
+STREAM_CASES = [(16, 56, 56, 256, 64, 8, 1), (16, 28, 28, 512, 128, 8, 1), (16, 56, 56, 256, 128, 8, 2),
+                (16, 14, 14, 1024, 256, 8, 1), (16, 28, 28, 512, 256, 8, 2), (5, 14, 14, 1024, 256, 5, 1)]
 
 
 @pytest.mark.parametrize("case", STREAM_CASES)
-@pytest.mark.parametrize("y2", [False, True])
-def test_conv_dgrad_bwd_stream_vs_persistent(K, case, y2, monkeypatch):
+@pytest.mark.parametrize("ops_", ["y", "y2", "bits"])
+def test_conv_dgrad_bwd_stream_vs_persistent(K, case, ops_, monkeypatch):
     """The streaming fused 1x1 dgrad (EPI_BWD_STREAM: A rows and residual / y / mask operands DMA'd into an LDS ring
     tiles ahead) against the persistent engine's EPI_BWD (VCG_BWD_STREAM=0) at the trunk's shapes: g bit for bit,
-    the BN sums to float rounding (different tilings sum in different orders)."""
+    the BN sums to float rounding (different tilings sum in different orders). ops_: the epilogue operands (y + mask
+    bits, + the downsample's y2, or the mask bits alone: the trunk's blocks whose previous y3 is not stored)."""
     N, H, W, C, Cout, T, rs = case
+    y2 = ops_ == "y2"
     dtype = torch.bfloat16
     fold = C // 8
     dy = _rand((N, H, W, Cout), dtype, 71).to(DEV)
@@ -626,19 +629,20 @@ def test_conv_dgrad_bwd_stream_vs_persistent(K, case, y2, monkeypatch):
     mean, inv = (torch.randn(C, generator=g0) * 0.1).to(DEV), (torch.rand(C, generator=g0) + 0.5).to(DEV)
     mean2, inv2 = (torch.randn(C, generator=g0) * 0.1).to(DEV), (torch.rand(C, generator=g0) + 0.5).to(DEV)
     outs = []
-    for flag in ("1", "0"):
+    for flag in ("1", "64", "0"):  # streaming (64 x 128 tiles where they apply), streaming 64 x 64, persistent
         monkeypatch.setenv("VCG_BWD_STREAM", flag)
         sums, sgx2 = torch.zeros((2, C), device=DEV), torch.zeros(C, device=DEV)
         kw = dict(y2=y2t, mean2=mean2, invstd2=inv2, sum_gx2=sgx2) if y2 else {}
         g = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, 1, 1, 1, 0, tsm_T=T, tsm_fold=fold, res=res, res_stride=rs,
-                             bits=bits, y=y, mean=mean, invstd=inv, sums=sums, **kw)
+                             bits=bits, y=None if ops_ == "bits" else y, mean=mean, invstd=inv, sums=sums, **kw)
         assert g is not None
         torch.cuda.synchronize()
         outs.append((g.clone(), sums.clone(), sgx2.clone()))
-    (ga, sa, xa), (gb, sb, xb) = outs
-    assert torch.equal(ga, gb), f"g differs: max {(ga.float() - gb.float()).abs().max().item():.3e}"
-    for a, b in ((sa, sb), (xa, xb)):
-        assert (a.double() - b.double()).abs().max().item() <= 1e-4 * (b.abs().max().item() + 1.0)
+    gb, sb, xb = outs[-1]
+    for ga, sa, xa in outs[:-1]:
+        assert torch.equal(ga, gb), f"g differs: max {(ga.float() - gb.float()).abs().max().item():.3e}"
+        for a, b in ((sa, sb), (xa, xb)):
+            assert (a.double() - b.double()).abs().max().item() <= 1e-4 * (b.abs().max().item() + 1.0)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)

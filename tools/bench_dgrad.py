@@ -20,6 +20,7 @@ SHAPES = [  # (name, N, H, W, C (dx channels), Cout (dy channels), T, residual s
     ("l2 b0 conv1 dgrad", 1024, 56, 56, 256, 128, 16, 2),
     ("l2 conv1 dgrad", 1024, 28, 28, 512, 128, 16, 1),
     ("l3 conv1 dgrad", 1024, 14, 14, 1024, 256, 16, 1),
+    ("l3 b0 conv1 dgrad", 1024, 28, 28, 512, 256, 16, 2),
 ]
 
 
@@ -67,9 +68,9 @@ def run(name, N, H, W, C, Co, T, rs=1):
     print(line, flush=True)
 
 
-# argv: [name prefix] [flags "10" / "1" / "0"]; VCG_BENCH_NOTSM=1: no TSM adjoint (A/B of the access pattern)
+# argv: [name prefix] [comma-separated VCG_BWD_STREAM values: 1 (streaming), 64 (streaming, 64-column tiles), 0]; VCG_BENCH_NOTSM=1: no TSM adjoint (A/B of the access pattern)
 sel = sys.argv[1] if len(sys.argv) > 1 else ""
-flags = sys.argv[2] if len(sys.argv) > 2 else "10"
+flags = sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "0"]  # VCG_BWD_STREAM values, e.g. 1,64,0
 for s in SHAPES:  # the streaming kernel (EPI_BWD_STREAM, K <= 128) and the persistent engine, same process
     if not s[0].startswith(sel):
         continue

@@ -397,10 +397,16 @@ __global__ __launch_bounds__(256) void gram_stats_rows_kernel(const double* __re
   for (int q = 0; q < GS_Q; ++q) acc[q] = 0.0;
   if (k < C) {
     const double dk = dm[k];
-    for (int t = 0; t < C; ++t) {
-      const double cv = gram[(long long)t * C + k] * invM - dm[t] * dk;
+    for (int t0 = 0; t0 < C; t0 += 16) {  // (C % 16 == 0: 16 row loads in flight per batch)
+      double gv[16];
 #pragma unroll
-      for (int q = 0; q < GS_Q; ++q) acc[q] = fma(wq[q][t], cv, acc[q]);
+      for (int u = 0; u < 16; ++u) gv[u] = gram[(long long)(t0 + u) * C + k];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const double cv = gv[u] * invM - dm[t0 + u] * dk;
+#pragma unroll
+        for (int q = 0; q < GS_Q; ++q) acc[q] = fma(wq[q][t0 + u], cv, acc[q]);
+      }
     }
   }
 #pragma unroll
@@ -484,7 +490,7 @@ VCG_API int vcg_bn_stats_from_gram(const double* g64, const void* w, long long M
                                    int mtiles, hipStream_t s) {
   VCG_REQUIRE(g64 && w && stats, "null argument");
   VCG_REQUIRE(C > 0 && C <= 1024 && N > 0 && M > 0 && mtiles > 0, "bad shape");
-  if (C <= 256)
+  if (C <= 256 && C % 16 == 0)
     hipLaunchKernelGGL(gram_stats_rows_kernel, dim3((N + GS_Q - 1) / GS_Q), dim3(256), 0, s, g64, (const bf16_t*)w, M,
                        N, C, reinterpret_cast<float2*>(stats), mtiles);
   else

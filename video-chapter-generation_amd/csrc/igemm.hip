@@ -1116,13 +1116,28 @@ __global__ __launch_bounds__(256) void bn_fold_weights_a2_kernel(const bf16_t* _
     acc += (-A * sum_g[k] * ic) * w;
   }
   __syncthreads();
-  for (int j = t; j < C; j += 256) {  // Q[j][n] = sum_k wt[j][k] B_k wt[n][k]
+  // Q[j][n] = sum_k wt[j][k] B_k wt[n][k]: one wave per row j (16-B coalesced row reads, K % 8 == 0), lane partials
+  // combined by a fixed butterfly (deterministic)
+  const int wv = t >> 6, ln = t & 63;
+  for (int j = wv; j < C; j += 4) {
     const bf16_t* row = wt + (long long)j * K;
     float q = 0.f;
-    for (int k = 0; k < K; ++k) q = fmaf(bf2f(row[k]), bw[k], q);
-    const bf16_t qb = f2bf(q);
-    wf[(long long)n * (K + C) + K + j] = qb;
-    acc -= colsum_a[j] * ic * bf2f(qb);
+    for (int k = 8 * ln; k < K; k += 512) {
+      const uint4 u = *reinterpret_cast<const uint4*>(row + k);
+      const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        q = fmaf(__uint_as_float(w4[i] << 16), bw[k + 2 * i], q);
+        q = fmaf(__uint_as_float(w4[i] & 0xffff0000u), bw[k + 2 * i + 1], q);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    if (ln == 0) {
+      const bf16_t qb = f2bf(q);
+      wf[(long long)n * (K + C) + K + j] = qb;
+      acc -= colsum_a[j] * ic * bf2f(qb);
+    }
   }
   red[t] = acc;
   __syncthreads();
@@ -1152,7 +1167,13 @@ __global__ __launch_bounds__(256) void bn_fold_wgrad_a2_kernel(const float* __re
   const float Cc = -A * sum_g[k] * ic - B * mean[k];
   for (int j = threadIdx.x; j < C; j += 256) {
     float wg = 0.f;
-    for (int i = 0; i < C; ++i) wg = fmaf(wr[i], G[(long long)i * C + j], wg);
+    for (int i0 = 0; i0 < C; i0 += 16) {  // (C % 16 == 0: 16 row loads in flight per batch)
+      float gv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) gv[u] = G[(long long)(i0 + u) * C + j];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) wg = fmaf(wr[i0 + u], gv[u], wg);
+    }
     const float v = fmaf(A, P[(long long)k * C + j], fmaf(B, wg, Cc * cs[j]));
     float* o = dw + (long long)k * C + j;
     *o = accumulate ? *o + v : v;
@@ -1196,7 +1217,8 @@ VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float
                                        const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a,
                                        void* wfold, float* bias, hipStream_t stream) {
   VCG_REQUIRE(wt && wfold && bias && invstd && sum_g && sum_gx && colsum_a, "null argument");
-  VCG_REQUIRE(C > 0 && K > 0 && K <= 2048, "K must be <= 2048");
+  VCG_REQUIRE(C > 0 && K > 0 && K <= 2048 && K % 8 == 0, "K must be a multiple of 8, <= 2048");
+  VCG_REQUIRE(((uintptr_t)wt & 15) == 0, "wt must be 16-B aligned");
   hipLaunchKernelGGL(bn_fold_weights_a2_kernel, dim3(C), dim3(256), 0, stream, (const bf16_t*)wt, C, K, invstd, gamma,
                      sum_g, sum_gx, inv_count, colsum_a, (bf16_t*)wfold, bias);
   VCG_LAUNCH_CHECK();
@@ -1208,7 +1230,7 @@ VCG_API int vcg_bn_bwd_fold_wgrad_a2(const float* P, const float* G, const float
                                      float inv_count, const float* colsum_a, float* dw, int accumulate,
                                      hipStream_t stream) {
   VCG_REQUIRE(P && G && w3 && mean && invstd && sum_g && sum_gx && colsum_a && dw, "null argument");
-  VCG_REQUIRE(C > 0 && C <= 512 && K > 0, "C must be <= 512");
+  VCG_REQUIRE(C > 0 && C <= 512 && C % 16 == 0 && K > 0, "C must be a multiple of 16, <= 512");
   hipLaunchKernelGGL(bn_fold_wgrad_a2_kernel, dim3(K), dim3(256), 0, stream, P, G, w3, K, C, mean, invstd, gamma,
                      sum_g, sum_gx, inv_count, colsum_a, dw, accumulate);
   VCG_LAUNCH_CHECK();

@@ -545,17 +545,24 @@ __device__ __forceinline__ int bwd_tsm_shift(const BwdEpi& e, int n) {
   return n < e.tsm_fold ? 1 : (n < 2 * e.tsm_fold ? -1 : 0);
 }
 
+// K = 256 (KC = 4, layer 3): one A tile per slot (the host admits it only when no workgroup's 64 columns straddle two
+// TSM shifts) and the weight fragments of a wave's 32 columns in registers (64 VGPRs) instead of LDS, so the ring
+// keeps 3 slots (with the weights in LDS and one A tile per slot it had 2, measured step-neutral in round 4).
+__host__ __device__ constexpr bool bwd_stream_wide(int KC) { return KC > 2; }
 // LDS bytes of one ring slot / of the fixed part (weights, stage, column parameters) and the ring depth
 __host__ __device__ constexpr int bwd_stream_buf(int KC, int XF) {
-  return 2 * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 : 0) + ((XF & (XF_HASY | XF_BITS)) ? 8 * 256 : 0) +
-         ((XF & XF_Y2) ? 8192 : 0);
+  return (bwd_stream_wide(KC) ? 1 : 2) * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 : 0) +
+         ((XF & (XF_HASY | XF_BITS)) ? 8 * 256 : 0) + ((XF & XF_Y2) ? 8192 : 0);
 }
 #ifndef VCG_STREAM_NBUF
 #define VCG_STREAM_NBUF 4  // ring slots at most (build knob for A/B builds)
 #endif
+__host__ __device__ constexpr int bwd_stream_fixed(int KC) {
+  return (bwd_stream_wide(KC) ? 0 : KC * 8192) + 8192 + 1024;
+}
 __host__ __device__ constexpr int bwd_stream_nbuf(int KC, int XF) {
-  return (160 * 1024 - (KC * 8192 + 8192 + 1024)) / bwd_stream_buf(KC, XF) >= VCG_STREAM_NBUF ? VCG_STREAM_NBUF
-         : (160 * 1024 - (KC * 8192 + 8192 + 1024)) / bwd_stream_buf(KC, XF);
+  return (160 * 1024 - bwd_stream_fixed(KC)) / bwd_stream_buf(KC, XF) >= VCG_STREAM_NBUF ? VCG_STREAM_NBUF
+         : (160 * 1024 - bwd_stream_fixed(KC)) / bwd_stream_buf(KC, XF);
 }
 
 template <int KC, int XF>
@@ -564,15 +571,16 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   constexpr bool HASB = HASY || (XF & XF_BITS) != 0;  // mask bits + sum g
   static_assert(!Y2 || HASY, "y2 comes with y");
   constexpr int TM = 64, TN = 64, NTH = 512, NW = 8;
+  constexpr bool WIDE = bwd_stream_wide(KC);
   constexpr int NBUF = bwd_stream_nbuf(KC, XF);
-  static_assert(NBUF >= 2, "LDS ring");
+  static_assert(NBUF >= 2, "LDS ring");  // (WIDE: 3 without y2; the host keeps WIDE + y2 on the persistent engine)
   constexpr int AT = KC * TM * 64 * 2;  // one A tile ([64][64] swizzled sub-tiles, fast_frag layout); two per slot
   constexpr int OB = TM * TN * 2;       // one row-major [64][64] bf16 epilogue operand (res / y / y2)
-  constexpr int OFF_R = 2 * AT, OFF_Y = OFF_R + OB, OFF_BITS = OFF_Y + (HASY ? OB : 0);
+  constexpr int OFF_R = (WIDE ? 1 : 2) * AT, OFF_Y = OFF_R + OB, OFF_BITS = OFF_Y + (HASY ? OB : 0);
   constexpr int OFF_Y2 = OFF_BITS + (HASB ? NW * 256 : 0);  // mask bytes [64][8]: 16 lanes x 4 B per wave (+ pad)
   constexpr int BUF = OFF_Y2 + (Y2 ? OB : 0);
   static_assert(BUF == bwd_stream_buf(KC, XF), "slot layout");
-  constexpr int BB = KC * TN * 64 * 2;
+  constexpr int BB = WIDE ? 0 : KC * TN * 64 * 2;
   constexpr int SB = TM * TN * 2;
   constexpr int TOTAL = NBUF * BUF + BB + SB + 4 * TN * 4;
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
@@ -623,9 +631,9 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
     mu[i] = cpar[8 * cc + i];
     mu2[i] = cpar[TN + 8 * cc + i];
   }
-  // TSM shifts of the workgroup's two 32-column halves; two A tiles when they differ
+  // TSM shifts of the workgroup's two 32-column halves; two A tiles when they differ (never for WIDE: host check)
   const int sh0 = bwd_tsm_shift(e, n0), sh1 = bwd_tsm_shift(e, n0 + 32);
-  const bool two = sh0 != sh1;
+  const bool two = !WIDE && sh0 != sh1;
 
   // buffer descriptors of the epilogue operands (offset beyond num_records -> zeros)
   const long long ld = p.ldc;
@@ -643,9 +651,32 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   if constexpr (Y2) rs_y2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.y2), 0, nb_full, 0x00020000);
 
   FastLoader<64, OP_DENSE_K, NW> la, lb;
-  lb.init(p.b, 0, n0, wave, lane);
+  const int g = lane >> 4, ci = lane & 15;
+  const int wr = wave & 3, wc = wave >> 2;  // MFMA block: rows 16 wr .. + 15, columns 32 wc .. + 31 of the tile
+  // WIDE: this wave's weight fragments (columns 32 wc + 16 j + ci, k = 64 kc + 32 s + 8 g .. + 7: fast_frag's
+  // lane map) straight into registers, retired before the ring's first DMA (so no wait inside the loop counts them)
+  s16x8 bfr[WIDE ? KC : 1][2][2];
+  if constexpr (WIDE) {
+    const bf16_t* bp = reinterpret_cast<const bf16_t*>(p.b.ptr);
 #pragma unroll
-  for (int kc = 0; kc < KC; ++kc) lb.issue(p.b, kc * 64, p.K, Bs + kc * 4096, wave);
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfr[kc][s][j] = *reinterpret_cast<const s16x8*>(bp + (long long)(n0 + 32 * wc + 16 * j + ci) * p.b.ld +
+                                                          64 * kc + 32 * s + 8 * g);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(bfr[kc][s][j]));
+  } else {
+    lb.init(p.b, 0, n0, wave, lane);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) lb.issue(p.b, kc * 64, p.K, Bs + kc * 4096, wave);
+  }
 
   auto issue_tile = [&](int t) {
     const int d0 = (by + t * gy) * TM;
@@ -706,8 +737,6 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = s3[i] = 0.f;
   bf16_t* Cout = reinterpret_cast<bf16_t*>(p.C);
-  const int g = lane >> 4, ci = lane & 15;
-  const int wr = wave & 3, wc = wave >> 2;  // MFMA block: rows 16 wr .. + 15, columns 32 wc .. + 31 of the tile
 
   for (int t = 0; t < my_tiles; ++t) {
     FAST_STAMP(t, 0);
@@ -734,9 +763,12 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
       for (int s = 0; s < 2; ++s) {
         const s16x8 af = fast_frag(At + kc * 4096, 16 * wr, lane, s);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fast_frag(Bs + kc * 4096, 32 * wc + 16 * j, lane, s), af,
-                                                           acc[j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          s16x8 bf;
+          if constexpr (WIDE) bf = bfr[kc][s][j];
+          else bf = fast_frag(Bs + kc * 4096, 32 * wc + 16 * j, lane, s);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af, acc[j], 0, 0, 0);
+        }
       }
     // stage the bf16 GEMM value: row 16 wr + ci, columns 32 wc + 16 j + 4 g .. + 3
 #pragma unroll
@@ -816,6 +848,271 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
   if constexpr (HASB) {
     if (e.nred > 0) bwd_finish<256, 64>(p, reinterpret_cast<float*>(smem), cpar + 2 * TN, s1, s2, s3, n0, by);
+  }
+}
+
+// K = 256 with 64 x 128 tiles (the layer-3 conv1 input gradients: every 128-column tile inside one TSM shift, fold
+// % 128 == 0, and the mask bits without y -- the previous block's y3 is not stored). Per-tile stamps of the 64 x 64
+// form (tools/bench_dgrad.py, -DVCG_FAST_STAMPS) put ~2/3 of a tile in the phase that issues the next tile's LDS-DMA
+// (6 1-KB pieces per wave) next to the MFMAs; here one A tile (32 KB) serves 128 columns (LDS-DMA per output byte
+// 50 / 16 instead of 40.5 / 8), the next tile's A pieces are issued between the k-steps' MFMAs, and the epilogue runs
+// in the MFMA lanes on the residual rows in LDS: g = mask(bf16(acc) + res) is written back over the residual (same
+// lane, same bytes: no barrier, no separate stage), and the flush threads only copy 16-B chunks out and sum them.
+// The residual rows land pre-swizzled (16-B chunk c of row r at slot c ^ (r & 15)), so the MFMA lanes' 8-B accesses
+// (16 rows, one column group) and the flush's 16-B row reads are both conflict-free. The weight fragments of a wave's
+// 32 columns stay in registers; 3 slots of 50 KB.
+template <int XF>
+__device__ __forceinline__ void bwd_stream128_body(const GemmParams& p) {
+  constexpr bool HASB = (XF & XF_BITS) != 0;
+  static_assert((XF & (XF_HASY | XF_Y2)) == 0, "the mask bits without y only");
+  constexpr int KC = 4, TM = 64, TN = 128, NTH = 512, NW = 8;
+  constexpr int AT = KC * TM * 64 * 2;               // A tile [4][64][64] swizzled (fast_frag layout), 32 KB
+  constexpr int OB = TM * TN * 2;                    // residual rows -> g, [64][128] bf16 swizzled, 16 KB
+  constexpr int OFF_R = AT, OFF_BITS = OFF_R + OB;  // mask bytes [8 waves][256 B]: rows 8 w .. + 7 x 16 B (+ pad)
+  constexpr int BUF = OFF_BITS + (HASB ? NW * 256 : 0);
+  constexpr int CP = 4 * TN * 4;
+  constexpr int NBUF = (160 * 1024 - CP) / BUF;
+  static_assert(NBUF >= 3 && NBUF * BUF + CP <= 160 * 1024, "LDS ring");
+  static_assert(NBUF * BUF >= 3 * NTH * 8 * 4, "bwd_finish scratch");
+  // VMEM instructions per wave: one tile's DMA (A 4, residual 2, bits 1), one flush's stores (2)
+  constexpr int OPS = KC + 2 + (HASB ? 1 : 0), STO = 2;
+  constexpr int VMW = (NBUF - 2) * OPS + (NBUF - 1) * STO;
+  static_assert(VMW < 64, "vmcnt field");
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUF + CP];  // the ONLY LDS object
+  char* ring = smem;
+  float* cpar = reinterpret_cast<float*>(smem + NBUF * BUF);  // mean | mean2 | invstd | invstd2 [TN]
+
+  const BwdEpi& e = p.bwd;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nx = p.N / TN, gy = gridDim.x / nx;
+  int bx, by;
+  if ((gy & 7) == 0) {  // every column tile of an M-tile row on one XCD (the A rows come from HBM once)
+    const int sidx = blockIdx.x >> 3;
+    bx = sidx % nx;
+    by = (sidx / nx) * 8 + (blockIdx.x & 7);
+  } else {
+    bx = blockIdx.x % nx;
+    by = blockIdx.x / nx;
+  }
+  const int n0 = bx * TN;
+  const int mtiles = (p.M + TM - 1) / TM;
+  const int my_tiles = by < mtiles ? (mtiles - 1 - by) / gy + 1 : 0;
+  if (my_tiles == 0) {  // no rows: an all-zero partial slot
+    if (e.nred > 0 && tid < TN)
+      for (int r = 0; r < e.nred; ++r) e.part[((long long)by * e.nred + r) * p.N + n0 + tid] = 0.f;
+    return;
+  }
+  if (tid < TN) {
+    const int n = n0 + tid;
+    cpar[tid] = e.mean ? e.mean[n] : 0.f;
+    cpar[TN + tid] = e.mean2 ? e.mean2[n] : 0.f;
+    cpar[2 * TN + tid] = e.invstd ? e.invstd[n] : 0.f;
+    cpar[3 * TN + tid] = e.invstd2 ? e.invstd2[n] : 0.f;
+  }
+  __syncthreads();  // (no LDS-DMA issued yet)
+  const int cc = tid & 15;  // the flush's 16-B column chunk of this thread (fixed for the whole kernel)
+  const int sh = bwd_tsm_shift(e, n0);  // one shift for the tile's 128 columns (host check)
+
+  const long long ld = p.ldc;
+  const long long rrows = e.res_s > 1 ? (long long)(p.M / e.hw) * e.rH * e.rW : (long long)p.M;
+  const uint32_t nb_res = (uint32_t)min(rrows * ld * 2, (long long)0xFFFFFF00LL);
+  const __amdgpu_buffer_rsrc_t rs_res = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.res), 0, nb_res, 0x00020000);
+  __amdgpu_buffer_rsrc_t rs_bits = rs_res;
+  uint32_t nb_bits = 0;
+  if constexpr (HASB) {
+    nb_bits = (uint32_t)(((long long)p.M * ld) >> 3);
+    rs_bits = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(e.bits), 0, nb_bits, 0x00020000);
+  }
+
+  FastLoader<64, OP_DENSE_K, NW> la;
+  const int g = lane >> 4, ci = lane & 15;
+  const int wr = wave & 1, wc = wave >> 1;  // MFMA block: rows 32 wr .. + 31, columns 32 wc .. + 31 of the tile
+  // this wave's weight fragments (columns 32 wc + 16 j + ci, k = 64 kc + 32 s + 8 g .. + 7: fast_frag's lane map),
+  // retired before the ring's first DMA (no wait inside the loop counts them)
+  s16x8 bfr[KC][2][2];
+  {
+    const bf16_t* bp = reinterpret_cast<const bf16_t*>(p.b.ptr);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfr[kc][s][j] = *reinterpret_cast<const s16x8*>(bp + (long long)(n0 + 32 * wc + 16 * j + ci) * p.b.ld +
+                                                          64 * kc + 32 * s + 8 * g);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(bfr[kc][s][j]));
+  }
+
+  // tile t's A rows (piece kc) / residual rows + mask bytes into its ring slot
+  auto a_init = [&](int t) {
+    const int d0 = (by + t * gy) * TM;
+    la.init(p.a, 0, d0, wave, lane);
+    const int d = d0 + wave * 8 + (lane >> 3);  // FastLoader<64, dense, 8 waves>: one row per lane
+    int tt = 0;
+    if (e.tsm_T > 0 && sh != 0) {  // destination row d reads GEMM row d - s hw, zero outside the clip
+      const int f = (int)fdiv((uint32_t)min(d, p.M - 1), e.fd_hw);
+      tt = f - (int)fdiv((uint32_t)f, e.fd_T) * e.tsm_T;
+    }
+    const bool ok = d < p.M && (unsigned)(tt - sh) < (unsigned)max(e.tsm_T, 1);
+    la.off[0] = ok ? (int)((long long)(d - sh * e.hw) * p.a.ld) : -1;
+  };
+  auto a_piece = [&](int t, int kc) {
+    la.issue(p.a, kc * 64, p.K, reinterpret_cast<bf16_t*>(ring + (t % NBUF) * BUF) + kc * 4096, wave);
+  };
+  // residual rows: instruction h of this wave covers tile rows 32 h + 4 wave .. + 3; the lane at LDS slot q of row
+  // r loads chunk q ^ (r & 15)
+  auto res_piece = [&](int t, int h) {
+    const int d0 = (by + t * gy) * TM;
+    char* buf = ring + (t % NBUF) * BUF;
+    {
+      const int r = 32 * h + 4 * wave + (lane >> 4);
+      const int dr = d0 + r, n = n0 + 8 * ((lane & 15) ^ (r & 15));
+      uint32_t roff = (uint32_t)((long long)dr * ld + n) * 2u;
+      if (e.res_s > 1) {  // compact residual of a 1x1 / stride-2 conv: only even (h, w) rows carry one
+        const uint32_t f2 = fdiv((uint32_t)dr, e.fd_hw), rr = (uint32_t)dr - f2 * (uint32_t)e.hw;
+        const uint32_t hh = fdiv(rr, e.fd_w), w = rr - hh * e.fd_w.d;
+        roff = ((hh | w) & 1u) ? nb_res : (uint32_t)((((long long)(f2 * e.rH + (hh >> 1)) * e.rW + (w >> 1)) * ld + n) * 2);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_res, (lds_void_t*)(buf + OFF_R + (8 * h + wave) * 1024), 16,
+                                               dr < p.M ? roff : nb_res, 0, 0, 0);
+    }
+  };
+  auto bits_piece = [&](int t) {
+    const int d0 = (by + t * gy) * TM;
+    char* buf = ring + (t % NBUF) * BUF;
+    if constexpr (HASB) {  // mask bytes: lane < 32 -> row 8 wave + lane / 4, 32 columns (dword lane & 3)
+      const int dr = d0 + 8 * wave + ((lane & 31) >> 2), n = n0 + 32 * (lane & 3);
+      const bool okb = lane < 32 && dr < p.M;
+      const uint32_t boff = (uint32_t)(((long long)dr * ld + n) >> 3);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_bits, (lds_void_t*)(buf + OFF_BITS + wave * 256), 4,
+                                               okb ? boff : nb_bits, 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < my_tiles) {
+      a_init(i);
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) a_piece(i, kc);
+      res_piece(i, 0);
+      res_piece(i, 1);
+      bits_piece(i);
+    }
+
+  float s1[8], s0[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s1[i] = s0[i] = 0.f;
+  bf16_t* Cout = reinterpret_cast<bf16_t*>(p.C);
+
+  for (int t = 0; t < my_tiles; ++t) {
+    FAST_STAMP(t, 0);
+    if (t >= NBUF - 1 && t + NBUF - 2 < my_tiles) __builtin_amdgcn_s_waitcnt(waitcnt_vm(VMW));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    // tile t visible to every wave; every wave's reads of the slot refilled below (tile t - 1's) retired
+    __builtin_amdgcn_s_barrier();
+    FAST_STAMP(t, 1);
+    const bool nxt = t + NBUF - 1 < my_tiles;
+    if (nxt) a_init(t + NBUF - 1);
+    const int d0 = (by + t * gy) * TM;
+    char* buf = ring + (t % NBUF) * BUF;
+    const bf16_t* At = reinterpret_cast<const bf16_t*>(buf);
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      if (nxt) {  // the next tile's DMA pieces spread over the k-steps' MFMAs (7 per wave, as the prologue's)
+        a_piece(t + NBUF - 1, kc);
+        if (kc < 2) res_piece(t + NBUF - 1, kc);
+        if (kc == 2) bits_piece(t + NBUF - 1);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 a0 = fast_frag(At + kc * 4096, 32 * wr, lane, s);
+        const s16x8 a1 = fast_frag(At + kc * 4096, 32 * wr + 16, lane, s);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kc][s][j], a0, acc[0][j], 0, 0, 0);
+          acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kc][s][j], a1, acc[1][j], 0, 0, 0);
+        }
+      }
+    }
+    FAST_STAMP(t, 2);
+    // epilogue in the MFMA lanes: row 32 wr + 16 i + ci, columns 32 wc + 16 j + 4 g .. + 3 of the residual / g rows
+    bf16_t* Rg = reinterpret_cast<bf16_t*>(buf + OFF_R);
+    const uint8_t* Bt = reinterpret_cast<const uint8_t*>(buf + OFF_BITS);
+    uint2 rv[2][2];
+    uint32_t bw[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = 32 * wr + 16 * i + ci, col = 32 * wc + 16 * j + 4 * g;
+        // (LDS reads / writes as inline asm: hipcc would wait vmcnt(0) for the ring's in-flight DMA first)
+        asm volatile("ds_read_b64 %0, %1"
+                     : "=v"(rv[i][j])
+                     : "v"(lds_u32(Rg + row * TN + 8 * st_slot<TN>(row, col >> 3) + (col & 7)))
+                     : "memory");
+        bw[i][j] = 0xFFu;
+        if constexpr (HASB)
+          asm volatile("ds_read_u8 %0, %1" : "=v"(bw[i][j]) : "v"(lds_u32(Bt + (row >> 3) * 256 + (row & 7) * 16 + (col >> 3)))
+                       : "memory");
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = 32 * wr + 16 * i + ci, col = 32 * wc + 16 * j + 4 * g;
+        const uint32_t rw[2] = {rv[i][j].x, rv[i][j].y};
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float r = __uint_as_float((q & 1) ? (rw[q >> 1] & 0xffff0000u) : (rw[q >> 1] << 16));
+          v[q] = bf2f(f2bf(acc[i][j][q])) + r;  // the staged bf16 GEMM value + residual (stage_flush_bwd order)
+          if constexpr (HASB) v[q] = ((bw[i][j] >> ((col & 7) + q)) & 1u) ? v[q] : 0.f;
+        }
+        uint2 o;
+        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        asm volatile("ds_write_b64 %0, %1" ::"v"(lds_u32(Rg + row * TN + 8 * st_slot<TN>(row, col >> 3) + (col & 7))),
+                     "v"(o) : "memory");
+      }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    FAST_STAMP(t, 3);
+    // flush: each thread copies row chunks (r, cc) of g out and sums them
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = (tid >> 4) + 32 * h;
+      const int d = d0 + r, n = n0 + 8 * cc;
+      uint4 o;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(o) : "v"(lds_u32(Rg + r * TN + 8 * st_slot<TN>(r, cc))) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (d < p.M) {
+        *reinterpret_cast<uint4*>(Cout + (long long)d * ld + n) = o;
+        if constexpr (HASB) {
+          float v[8];
+          unpack8(o, v);  // sum of the stored (rounded) gradient
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s1[i] += v[i];
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  if constexpr (HASB) {
+    if (e.nred > 0) bwd_finish<256, 128>(p, reinterpret_cast<float*>(smem), cpar + 2 * TN, s1, s0, s0, n0, by);
   }
 }
 
@@ -1042,7 +1339,9 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
 template <int BM, int BN, int AM, int EPI, int RES, int XF = 0>
 __global__ __launch_bounds__(BM * 2) __attribute__((amdgpu_waves_per_eu(EPI == EPI_BWD_AFF && BN == 64 ? 3 : 2)))
 void igemm_fast_kernel(GemmParams p) {
-  if constexpr (EPI == EPI_BWD_STREAM)
+  if constexpr (EPI == EPI_BWD_STREAM && BN == 128)
+    bwd_stream128_body<XF>(p);
+  else if constexpr (EPI == EPI_BWD_STREAM)
     bwd_stream_body<AM, XF>(p);
   else
     igemm_fast_body<BM, BN, AM, EPI, RES>(p);
@@ -1642,25 +1941,39 @@ static int patch_grid_rows(const GemmParams& p, const PatchGeom& g) {
 }
 
 // EPI_BWD_STREAM applies to a full EPI_BWD (residual; mask bits with y, or neither) of a dense 1x1 dgrad with
-// K = 64 or 128; VCG_BWD_STREAM=0 keeps it on the persistent engine (read per call: tests compare both paths)
+// K = 64, 128 or 256 (256: every 64-column tile inside one TSM shift); VCG_BWD_STREAM=0 keeps it on the persistent
+// engine (read per call: tests compare both paths)
 static bool bwd_stream_ok(const GemmParams& p) {
   const char* v = getenv("VCG_BWD_STREAM");
   if (v && v[0] == '0') return false;
   const BwdEpi& e = p.bwd;
   const bool dense = p.a.KH == 0 && p.a.GH == 0;  // dense_op(): no conv geometry
-  if (!dense || (p.K != 64 && p.K != 128) || p.N % 64 != 0 || p.batch_inner > 0 || p.ldc != p.N || p.a.ld != p.K ||
+  if (!dense || (p.K != 64 && p.K != 128 && p.K != 256) || p.N % 64 != 0 || p.batch_inner > 0 || p.ldc != p.N || p.a.ld != p.K ||
       !e.res || e.msc || e.sub || bwd_light(p))
     return false;
   if ((e.y && !e.bits) || (e.y2 && !e.y)) return false;
   if ((e.y || e.bits) && e.nred < 2) return false;
   if (e.tsm_T > 0 && e.tsm_fold % 32 != 0) return false;  // one TSM shift per wave's 32 columns
+  // K = 256: one A tile per slot and 3 slots; with y the 64 x 64 form measured slower than the persistent engine
+  // (tools/bench_dgrad.py: 400.6 vs 385.1 us at layer 3), so only the mask-bits-only epilogues stream
+  if (p.K == 256 && ((e.tsm_T > 0 && e.tsm_fold % 64 != 0) || e.y)) return false;
+  if (p.K == 256 && ((uintptr_t)p.b.ptr & 15 || p.b.ld % 8 != 0)) return false;  // 16-B weight fragment loads
   if (((uintptr_t)p.C | (uintptr_t)e.res | (uintptr_t)e.y | (uintptr_t)e.y2 | (uintptr_t)p.a.ptr) & 15) return false;
   if (e.res_s > 1 && (p.M % e.hw) != 0) return false;
   return true;
 }
 
+// column tile of the streaming kernel: 128 for K = 256 with the mask bits alone and one TSM shift per 128 columns
+// (bwd_stream128_body), else 64; VCG_BWD_STREAM=64 keeps 64 (read per call: tests compare the tilings)
+static int bwd_stream_tn(const GemmParams& p) {
+  const BwdEpi& e = p.bwd;
+  const char* v = getenv("VCG_BWD_STREAM");
+  if (v && v[0] == '6') return 64;
+  return p.K == 256 && p.N % 128 == 0 && !e.y && (e.tsm_T <= 0 || e.tsm_fold % 128 == 0) ? 128 : 64;
+}
+
 static int bwd_stream_rows(const GemmParams& p) {
-  const int nx = p.N / 64, mtiles = (p.M + 63) / 64;
+  const int nx = p.N / bwd_stream_tn(p), mtiles = (p.M + 63) / 64;
   int gy = 256 / nx;  // one workgroup per CU (~100-147 KB of LDS)
   if (gy >= 8) gy &= ~7;
   if (gy > mtiles) gy = mtiles >= 8 ? (mtiles & ~7) : mtiles;
@@ -1705,11 +2018,11 @@ static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   return VCG_OK;
 }
 
-template <int KC, int XF>
+template <int KC, int XF, int TN = 64>
 static int launch_bwd_stream(const GemmParams& p, hipStream_t s) {
-  const int nx = p.N / 64, gy = bwd_stream_rows(p);
+  const int nx = p.N / TN, gy = bwd_stream_rows(p);
   const int tk = timing_begin(s);
-  hipLaunchKernelGGL((igemm_fast_kernel<256, 64, KC, EPI_BWD_STREAM, false, XF>), dim3(nx * gy), dim3(512), 0, s, p);
+  hipLaunchKernelGGL((igemm_fast_kernel<256, TN, KC, EPI_BWD_STREAM, false, XF>), dim3(nx * gy), dim3(512), 0, s, p);
   timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_DENSE_K, EPI_BWD, false>(p, 1));
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -1717,6 +2030,10 @@ static int launch_bwd_stream(const GemmParams& p, hipStream_t s) {
 
 template <int KC>
 static int run_bwd_stream(const GemmParams& p, hipStream_t s) {
+  if constexpr (KC == 4) {
+    if (bwd_stream_tn(p) == 128)
+      return p.bwd.bits ? launch_bwd_stream<4, XF_BITS, 128>(p, s) : launch_bwd_stream<4, 0, 128>(p, s);
+  }
   if (!p.bwd.y) return p.bwd.bits ? launch_bwd_stream<KC, XF_BITS>(p, s) : launch_bwd_stream<KC, 0>(p, s);
   if (!p.bwd.y2) return launch_bwd_stream<KC, XF_HASY>(p, s);
   return launch_bwd_stream<KC, XF_HASY | XF_Y2>(p, s);
@@ -1800,7 +2117,7 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   }
   if (amode != OP_IM2COL_SMALLC && gemm256_ok(p, amode, epi, z)) return run_gemm256(p, amode, epi, s);
   if (epi == EPI_BWD && amode == OP_DENSE_K && z == 1 && bwd_stream_ok(p))
-    return p.K == 64 ? run_bwd_stream<1>(p, s) : run_bwd_stream<2>(p, s);
+    return p.K == 64 ? run_bwd_stream<1>(p, s) : p.K == 128 ? run_bwd_stream<2>(p, s) : run_bwd_stream<4>(p, s);
   if (epi == EPI_BWD && bwd_light(p)) {
     if (amode == OP_DGRAD) return fast_bn<OP_DGRAD, EPI_BWD_AFF>(p, z, s);
     if (amode == OP_DENSE_K) return fast_bn<OP_DENSE_K, EPI_BWD_AFF>(p, z, s);
