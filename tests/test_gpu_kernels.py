@@ -883,3 +883,49 @@ def test_conv_dgrad_big(K, case):
     wt = K.weight_prep(w.to(DEV), Cin, dtype, transposed=True)
     dx = K.conv_dgrad(dys, wt, N, H, W, Cin, Cout, KH, KH, s, p)
     _close(dx.permute(0, 3, 1, 2), ref, dtype, "conv dgrad (>= 64 Ki rows)")
+
+
+# the 256 x 256-tile engine (igemm256.hip) against the 128 x 128 engine: (kind, shape). Dense GEMMs (M, N, K) with
+# ragged M / N, 3x3 im2col convs and TSM 1x1 convs (N frames, H, W, C, Cout), each large enough for >= 128 tiles
+G256_CASES = [("dense", (8192 + 77, 2048 + 8, 320)), ("dense", (8192, 3072, 768)),
+              ("conv3x3", (64, 28, 28, 128, 512)), ("conv3x3", (1024, 7, 7, 512, 512)),
+              ("conv1x1_tsm", (64, 14, 14, 1024, 1024))]
+
+
+@pytest.mark.parametrize("case", G256_CASES)
+def test_gemm256_vs_128(K, case, monkeypatch):
+    """VCG_G256=1 / 2 (four / two MFMA phases per k-step) against VCG_G256=0 (the 128 x 128 engine): outputs bit for
+    bit (same products, same k order, fp32 accumulation, one rounding); for the convs also the BN statistics
+    through bn_finalize (different row partials: to float rounding). The unset default routes the layer-4 3x3
+    forward with statistics (the 1024-frame case) to the 256 engine."""
+    kind, shp = case
+    dt = torch.bfloat16
+    outs = {}
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("VCG_G256", mode)
+        if kind == "dense":
+            M, N, Kd = shp
+            A = _rand((M, Kd), dt, 81).to(DEV)
+            B = _rand((N, Kd), dt, 82, 0.05).to(DEV)
+            outs[mode] = (K.gemm(A, B, M, N, Kd, Kd, Kd), None)
+        else:
+            Nf, H, W, C, Co = shp
+            k, pad = (3, 1) if kind == "conv3x3" else (1, 0)
+            T, fold = (16, C // 8) if kind == "conv1x1_tsm" else (0, 0)
+            x = _rand((Nf, H, W, C), dt, 83).to(DEV)
+            w = K.weight_prep(_rand((Co, C, k, k), torch.float32, 84, 0.05).to(DEV), C, dt)
+            M = Nf * H * W
+            st = K.stats_buffer(Co, M, DEV)
+            y = K.conv_fwd(x, w, Nf, H, W, C, Co, k, k, 1, pad, T, fold, stats=st)
+            fin = [torch.empty(Co, device=DEV) for _ in range(4)]
+            K.bn_finalize(st, st.shape[1], M, Co, None, None, *fin, None, None, 0.1, 1e-5)
+            outs[mode] = (y, (fin[0].double(), fin[1].double()))
+        torch.cuda.synchronize()
+    ref, rst = outs["0"]
+    for mode in ("1", "2"):
+        y, st = outs[mode]
+        assert torch.equal(y.view(torch.int16), ref.view(torch.int16)), \
+            f"VCG_G256={mode}: max {(y.float() - ref.float()).abs().max().item():.3e}"
+        if st is not None:
+            assert ((st[0] - rst[0]).abs() * rst[1]).max().item() < 1e-5
+            assert ((st[1] - rst[1]).abs() / rst[1]).max().item() < 1e-5

@@ -413,16 +413,23 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p) {
 
 }  // namespace
 
-// 1 when the 256-tile engine takes this GEMM: bf16 K-contiguous operands below 4 GB, EPI_STORE without residual /
-// aux, unbatched, N a multiple of 8 (16-B output chunks), opt-in VCG_G256=1 (measured per shape before it becomes a
-// default)
+// 1 when the 256-tile engine takes this GEMM: bf16 K-contiguous operands below 4 GB, EPI_STORE / EPI_STATS without
+// residual / aux, unbatched, N a multiple of 8 (16-B output chunks). VCG_G256=1 / 2 routes every such GEMM here (4 /
+// 2 phases per k-step), 0 none; unset, the one class measured faster goes here: the 3x3 forward convs with their BN
+// statistics at N >= 512, K >= 4096 (layer 4: 215.5 vs 256.4 us, tools/bench_g256.py, profiles/r05_g256.txt)
 static int g256_mode() {
   const char* e = getenv("VCG_G256");  // (read per call: tests and benches switch it inside one process)
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : -1;
+}
+
+static bool g256_default(const GemmParams& p, int amode, int epi) {
+  return amode == OP_IM2COL && epi == EPI_STATS && p.N >= 512 && p.K >= 4096;
 }
 
 bool gemm256_ok(const GemmParams& p, int amode, int epi, int z) {
-  if (!g256_mode() || z != 1 || p.batch_inner > 0 || (epi != EPI_STORE && epi != EPI_STATS) || p.residual ||
+  const int mode = g256_mode();
+  if (mode == 0 || (mode < 0 && !g256_default(p, amode, epi))) return false;
+  if (z != 1 || p.batch_inner > 0 || (epi != EPI_STORE && epi != EPI_STATS) || p.residual ||
       p.aux)
     return false;
   if (epi == EPI_STATS && (p.bias || !p.stats)) return false;
@@ -453,7 +460,7 @@ static void launch256(const GemmParams& p, int amode, int tiles, hipStream_t s) 
 int run_gemm256(const GemmParams& p, int amode, int epi, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   const int tk = timing_begin(s);
-  const bool two = g256_mode() == 2;  // (VCG_G256=2: two 32-MFMA phases per k-step)
+  const bool two = g256_mode() != 1;  // (two 32-MFMA phases per k-step unless VCG_G256=1: four of 16)
   if (epi == EPI_STATS) two ? launch256<EPI_STATS, 2>(p, amode, tiles, s) : launch256<EPI_STATS, 4>(p, amode, tiles, s);
   else two ? launch256<EPI_STORE, 2>(p, amode, tiles, s) : launch256<EPI_STORE, 4>(p, amode, tiles, s);
   timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K, g256_bytes(p, amode));
