@@ -277,8 +277,10 @@ def test_conv1x1_stats_matches_stored():
 
 @pytest.mark.parametrize("shape", [(4, 28, 28, 256, 64, 4), (4, 14, 14, 512, 128, 4), (8, 14, 14, 1024, 256, 4)])
 def test_dgrad_bits_only_sums_and_sumgx(shape):
-    """The conv1 dgrad epilogue with the mask bits and no y (the previous block's y3 not stored): the same g and
-    sum g as with y, sum_gx written 0; sum_gx from g^T a2 (bn_bwd_sumgx_from_wgrad) matches the y3 reduction."""
+    """The conv1 dgrad epilogue with the mask bits and no y (the previous block's y3 not stored): the same g as with
+    y, sum g to float rounding (at K = 256 the bits-only epilogue streams in 64 x 128 tiles while the y form stays on
+    the persistent engine: other partial sums), sum_gx written 0; sum_gx from g^T a2 (bn_bwd_sumgx_from_wgrad)
+    matches the y3 reduction."""
     N, H, W, C, Co, T = shape
     M = N * H * W
     gen = torch.Generator().manual_seed(11)
@@ -303,7 +305,8 @@ def test_dgrad_bits_only_sums_and_sumgx(shape):
     torch.cuda.synchronize()
     (g1, s1), (g2, s2) = outs
     assert torch.equal(g1, g2)
-    assert torch.equal(s1[0], s2[0]) and (s2[1] == 0).all()
+    assert (s1[0].double() - s2[0].double()).abs().max().item() <= 1e-4 * (s1[0].abs().max().item() + 1.0)
+    assert (s2[1] == 0).all()
     Pg = torch.empty(C, planes, 1, 1, device=DEV)
     ops.conv_wgrad(a2.view(N, H, W, planes), g2.view(M, C), Pg, N, H, W, planes, planes, C, 1, 1, 1, 0,
                    accumulate=False)
