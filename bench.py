@@ -629,7 +629,8 @@ def main():
                    "wgrad_fast_kernel": _per_launch(rl[ops.TIMING_WGRAD]),
                    "path_census": census,
                    "timing": "HIP events around each launch on its stream, one instrumented step (no BERT side "
-                             "stream in that step: unshared launch durations)"}
+                             "stream in that step: unshared launch durations); the category also holds the 256-tile "
+                             "engine's launches (rocprof name gemm256_kernel: the layer-4 3x3 forward convs)"}
         out = {
             "metric": METRIC if args.mode == "train" else METRIC_FWD, "value": round(value, 3), "unit": "clip-windows/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,

@@ -5,7 +5,7 @@ import csv
 import sys
 
 log = [l.strip() for l in open(sys.argv[1]) if l.strip()]
-rows = [r for r in csv.DictReader(open(sys.argv[2])) if any(k in r["Kernel_Name"] for k in ("igemm", "wgrad_fast", "wgrad3x3_patch", "conv3x3_patch", "stem_patch", "rs1x1"))]
+rows = [r for r in csv.DictReader(open(sys.argv[2])) if any(k in r["Kernel_Name"] for k in ("igemm", "gemm256", "wgrad_fast", "wgrad3x3_patch", "conv3x3_patch", "stem_patch", "rs1x1"))]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 steps = float(sys.argv[3]) if len(sys.argv) > 3 else 3.0
 if len(log) != len(rows):
