@@ -106,7 +106,7 @@ VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* m
    vcg_bn_bwd_fold_weights_a2: wfold [C][K + C] = [A_k wt | w3^T diag(B) w3] and the bias, colsum_a = column sums of
    a2 (f32 [C]); the dgrad then runs vcg_conv_dgrad_bwd_bnfold with yg = a2, Ky = C; vcg_bn_bwd_fold_wgrad_a2:
    dw[K][C] (+)= A P + B (w3 G) + Cc colsum_a from P = g^T a2 and G = a2^T a2 (f32, vcg_conv_wgrad products) and
-   the f32 conv3 weight w3 [K][C]. Shapes: fold_weights_a2 needs K % 8 == 0 and a 16-B aligned wt, fold_wgrad_a2
+   the f32 conv3 weight w3 [K][C]. Shapes: fold_weights_a2 needs K % 64 == 0 and a 16-B aligned wt, fold_wgrad_a2
    C % 16 == 0 (VCG_ERR_INVALID otherwise). */
 /* bn3 with y3 never stored (the forward keeps only its statistics, vcg_conv1x1_stats, and applies it by
    vcg_conv1x1_bn_res_relu): sum_gx of its backward from P = g^T a2 (vcg_conv_wgrad) and the forward's bf16 conv weight

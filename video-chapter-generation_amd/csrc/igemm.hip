@@ -1096,6 +1096,10 @@ VCG_API int vcg_bn_bwd_fold_weights(const void* wt, int N, int K, const float* m
 // bf16(Q[j][n]) with abar = colsum(a2) / M: GEMM + bias = sum g (A w) + sum_j (a2 - abar)_j Q - sum A gbar w, centred
 // like the y3 form (B (y3 - mean) with mean = abar w3^T).
 namespace {
+// FW_NB output columns n per workgroup: the A_k wt[n][k] rows and the bias partials, then thread j streams row j of
+// wt once (16-B loads) for all FW_NB columns of Q; every sum keeps the sequential k order and the bias its fixed tree
+// (the values of one column per workgroup, with half the row reads)
+constexpr int FW_NB = 2;
 __global__ __launch_bounds__(256) void bn_fold_weights_a2_kernel(const bf16_t* __restrict__ wt, int C, int K,
                                                                  const float* __restrict__ invstd,
                                                                  const float* __restrict__ gamma,
@@ -1103,49 +1107,68 @@ __global__ __launch_bounds__(256) void bn_fold_weights_a2_kernel(const bf16_t* _
                                                                  const float* __restrict__ sum_gx, float ic,
                                                                  const float* __restrict__ colsum_a,
                                                                  bf16_t* __restrict__ wf, float* __restrict__ bias) {
-  __shared__ float bw[2048];  // B_k wt[n][k]
-  __shared__ float red[256];
-  const int n = blockIdx.x, t = threadIdx.x;
-  float acc = 0.f;
+  __shared__ float bw[FW_NB][2048];  // B_k wt[n][k]
+  __shared__ float red[FW_NB][256];
+  const int n0 = blockIdx.x * FW_NB, t = threadIdx.x;
+  float acc[FW_NB];
+#pragma unroll
+  for (int q = 0; q < FW_NB; ++q) acc[q] = 0.f;
   for (int k = t; k < K; k += 256) {
     const float is = invstd[k], A = (gamma ? gamma[k] : 1.f) * is;
     const float B = -A * is * sum_gx[k] * ic;
-    const float w = bf2f(wt[(long long)n * K + k]);
-    bw[k] = B * w;
-    wf[(long long)n * (K + C) + k] = f2bf(A * w);
-    acc += (-A * sum_g[k] * ic) * w;
+#pragma unroll
+    for (int q = 0; q < FW_NB; ++q) {
+      const int n = n0 + q;
+      if (n < C) {
+        const float w = bf2f(wt[(long long)n * K + k]);
+        bw[q][k] = B * w;
+        wf[(long long)n * (K + C) + k] = f2bf(A * w);
+        acc[q] += (-A * sum_g[k] * ic) * w;
+      }
+    }
   }
   __syncthreads();
-  // Q[j][n] = sum_k wt[j][k] B_k wt[n][k]: one wave per row j (16-B coalesced row reads, K % 8 == 0), lane partials
-  // combined by a fixed butterfly (deterministic)
-  const int wv = t >> 6, ln = t & 63;
-  for (int j = wv; j < C; j += 4) {
+  for (int j = t; j < C; j += 256) {  // Q[j][n] = sum_k wt[j][k] B_k wt[n][k]
     const bf16_t* row = wt + (long long)j * K;
-    float q = 0.f;
-    for (int k = 8 * ln; k < K; k += 512) {
-      const uint4 u = *reinterpret_cast<const uint4*>(row + k);
-      const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+    float qv[FW_NB];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        q = fmaf(__uint_as_float(w4[i] << 16), bw[k + 2 * i], q);
-        q = fmaf(__uint_as_float(w4[i] & 0xffff0000u), bw[k + 2 * i + 1], q);
+    for (int q = 0; q < FW_NB; ++q) qv[q] = 0.f;
+    for (int k0 = 0; k0 < K; k0 += 64) {  // (K % 64 == 0: 8 row loads in flight per batch)
+      uint4 u8[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) u8[b] = *reinterpret_cast<const uint4*>(row + k0 + 8 * b);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint32_t w4[4] = {u8[b].x, u8[b].y, u8[b].z, u8[b].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float w = __uint_as_float((e & 1) ? (w4[e >> 1] & 0xffff0000u) : (w4[e >> 1] << 16));
+#pragma unroll
+          for (int q = 0; q < FW_NB; ++q) qv[q] = fmaf(w, bw[q][k0 + 8 * b + e], qv[q]);
+        }
       }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
-    if (ln == 0) {
-      const bf16_t qb = f2bf(q);
-      wf[(long long)n * (K + C) + K + j] = qb;
-      acc -= colsum_a[j] * ic * bf2f(qb);
+    for (int q = 0; q < FW_NB; ++q) {
+      const int n = n0 + q;
+      if (n < C) {
+        const bf16_t qb = f2bf(qv[q]);
+        wf[(long long)n * (K + C) + K + j] = qb;
+        acc[q] -= colsum_a[j] * ic * bf2f(qb);
+      }
     }
   }
-  red[t] = acc;
+#pragma unroll
+  for (int q = 0; q < FW_NB; ++q) red[q][t] = acc[q];
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if (t < o) red[t] += red[t + o];
+    if (t < o) {
+#pragma unroll
+      for (int q = 0; q < FW_NB; ++q) red[q][t] += red[q][t + o];
+    }
     __syncthreads();
   }
-  if (t == 0) bias[n] = red[0];
+  if (t < FW_NB && n0 + t < C) bias[n0 + t] = red[t][0];
 }
 
 // dw[k][j] (+)= A_k P[k][j] + B_k (w3 G)[k][j] + Cc_k cs[j]: P = g^T a2 [K][C], G = a2^T a2 [C][C], w3 [K][C] f32
@@ -1217,9 +1240,9 @@ VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float
                                        const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a,
                                        void* wfold, float* bias, hipStream_t stream) {
   VCG_REQUIRE(wt && wfold && bias && invstd && sum_g && sum_gx && colsum_a, "null argument");
-  VCG_REQUIRE(C > 0 && K > 0 && K <= 2048 && K % 8 == 0, "K must be a multiple of 8, <= 2048");
+  VCG_REQUIRE(C > 0 && K > 0 && K <= 2048 && K % 64 == 0, "K must be a multiple of 64, <= 2048");
   VCG_REQUIRE(((uintptr_t)wt & 15) == 0, "wt must be 16-B aligned");
-  hipLaunchKernelGGL(bn_fold_weights_a2_kernel, dim3(C), dim3(256), 0, stream, (const bf16_t*)wt, C, K, invstd, gamma,
+  hipLaunchKernelGGL(bn_fold_weights_a2_kernel, dim3((C + FW_NB - 1) / FW_NB), dim3(256), 0, stream, (const bf16_t*)wt, C, K, invstd, gamma,
                      sum_g, sum_gx, inv_count, colsum_a, (bf16_t*)wfold, bias);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
