@@ -81,7 +81,12 @@ VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
    dgrad runs as four sub-pixel classes (dx pixels of one (h, w) parity) over only the taps reaching each.
    bf16 fast engine only; VCG_ERR_UNSUPPORTED elsewhere. */
 VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C, int Cout, int KH, int KW);
-VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, const void* res, int res_stride, const unsigned char* bits, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, const void* y2, const float* mean2, const float* invstd2, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, float* sum_gx2, float* dgamma2, float* dbeta2, hipStream_t s);
+/* a2 (optional, with bits and no y): the previous block's conv3 input [N*H*W][a2_c] bf16 (a2_c 64 / 128); the kernel then
+   also accumulates pg [C][a2_c] f32 = g^T a2 (the conv3 weight-gradient product that gives bn3's sum_gx) from the g
+   tiles it stores, with the partial slabs in pws (vcg_conv_dgrad_bwd_p_ws_bytes). VCG_ERR_UNSUPPORTED when that
+   product does not apply to the shape (the streaming 1x1 kernel only): the caller runs the plain call and the GEMM. */
+VCG_API long long vcg_conv_dgrad_bwd_p_ws_bytes(int C, int a2_c);
+VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold, const void* res, int res_stride, const unsigned char* bits, const void* y, const float* mean, const float* invstd, const float* mscale, const float* mshift, const void* y2, const float* mean2, const float* invstd2, float* ws, long long ws_bytes, float* sum_g, float* sum_gx, float* dgamma, float* dbeta, float* sum_gx2, float* dgamma2, float* dbeta2, const void* a2, int a2_c, float* pg, float* pws, long long pws_bytes, hipStream_t s);
 /* autograd of conv2d: weight gradient, split-K over pixels, written in OIHW (state-dict layout); bf16 C = 4:
    the pair-packed stem gather (as vcg_conv_fwd) */
 VCG_API long long vcg_conv_wgrad_ws_bytes(int dtype, int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad);

@@ -373,11 +373,12 @@ def _check_census(census):
     fwd = [c for c in census if c[0] == "fwd"]
     bwd = [c for c in census if c[0] == "bwd"][::-1]  # (the backward walks the blocks in reverse)
     assert len(fwd) == 16 and len(bwd) == 16, (len(fwd), len(bwd))
-    for (_, c3, ds, f), (_, c3b, dsb, b) in zip(fwd, bwd):
+    for i, ((_, c3, ds, f), (_, c3b, dsb, b)) in enumerate(zip(fwd, bwd)):
         assert (c3, ds) == (c3b, dsb)
         small = c3 <= 1024
         want_f = {"a2sum": small, "y3_drop": small and not ds, "bn3_gemm": small and not ds}
-        want_b = {"fold_wgrad": small, "fold_dgrad": small, "a2_form": small}
+        # P = g^T a2 from the next block's streaming conv1 dgrad (K <= 128): layer-1 blocks 1-2, layer-2 blocks 1-2
+        want_b = {"fold_wgrad": small, "fold_dgrad": small, "p_dgrad": i in (1, 2, 4, 5), "a2_form": small}
         assert f == want_f, (c3, ds, f)
         assert b == want_b, (c3, ds, b)
 

@@ -929,3 +929,42 @@ def test_gemm256_vs_128(K, case, monkeypatch):
         if st is not None:
             assert ((st[0] - rst[0]).abs() * rst[1]).max().item() < 1e-5
             assert ((st[1] - rst[1]).abs() / rst[1]).max().item() < 1e-5
+
+
+# conv1 input gradients whose epilogue also forms the previous block's P = g^T a2 (mask bits, no y):
+# (N, H, W, C, Cout, T, res_stride, a2 columns)
+P_CASES = [(16, 56, 56, 256, 64, 8, 1, 64), (16, 56, 56, 256, 128, 8, 2, 64), (16, 28, 28, 512, 128, 8, 1, 128),
+           (5, 28, 28, 512, 128, 5, 1, 128)]
+
+
+@pytest.mark.parametrize("case", P_CASES)
+def test_conv_dgrad_bwd_p_product(K, case):
+    """vcg_conv_dgrad_bwd with a2: g and sum g exactly those of the call without it, and pg = g^T a2 against float64
+    as close as the weight-gradient GEMM it replaces (trunk.py: bn3's sum_gx of a block whose y3 is not stored)."""
+    N, H, W, C, Cout, T, rs, PJ = case
+    dt = torch.bfloat16
+    dy = _rand((N, H, W, Cout), dt, 91).to(DEV)
+    wt = K.weight_prep(_rand((Cout, C, 1, 1), torch.float32, 92, 0.1).to(DEV), C, dt, transposed=True)
+    res = _rand((N, (H + 1) // 2, (W + 1) // 2, C) if rs == 2 else (N, H, W, C), dt, 93).to(DEV)
+    _, bits = K.bn_apply(_rand((N, H, W, C), dt, 94).to(DEV), torch.ones(C, device=DEV), torch.zeros(C, device=DEV),
+                         C, relu=True, bits=True)
+    a2 = torch.relu(_rand((N, H, W, PJ), torch.float32, 95)).to(dt).to(DEV)
+    mean, inv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    kw = dict(tsm_T=T, tsm_fold=C // 8, res=res, res_stride=rs, bits=bits, mean=mean, invstd=inv)
+    s0 = torch.zeros((2, C), device=DEV)
+    g0 = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, 1, 1, 1, 0, sums=s0, **kw)
+    s1 = torch.zeros((2, C), device=DEV)
+    pg = torch.empty((C, PJ), device=DEV)
+    g1, done = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, 1, 1, 1, 0, sums=s1, a2=a2, pg=pg, **kw)
+    assert done, "the streaming kernel must take the P product at this shape"
+    M = N * H * W
+    ref_gemm = torch.empty((C, PJ, 1, 1), device=DEV)
+    K.conv_wgrad(a2, g1, ref_gemm, N, H, W, PJ, PJ, C, 1, 1, 1, 0, accumulate=False)
+    torch.cuda.synchronize()
+    assert torch.equal(g0, g1)
+    assert (s0[0].double() - s1[0].double()).abs().max().item() <= 1e-4 * (s0[0].abs().max().item() + 1.0)
+    ref = g1.view(M, C).double().t() @ a2.view(M, PJ).double()
+    sc = ref.abs().max().item() + 1e-6
+    e_p = (pg.double() - ref).abs().max().item() / sc
+    e_g = (ref_gemm.view(C, PJ).double() - ref).abs().max().item() / sc
+    assert e_p <= max(2.0 * e_g, 1e-5), (e_p, e_g)

@@ -82,6 +82,11 @@ struct BwdEpi {
   const float *mean2, *invstd2;
   float* part;  // [slots][nred][N]
   int nred;     // 0 (no reduction), 2 or 3
+  // the previous block's conv3 weight-gradient product P = g^T a2 accumulated from the stored g (streaming kernel,
+  // mask bits without y): a2 [M][pj] bf16 (pj 64 / 128, 0: off), ppart [slots][N][pj] f32 partials
+  const void* a2;
+  int pj;
+  float* ppart;
   // sub-pixel class rows (sub != 0): GEMM row m = (f, i, j) of the cH x cW class grid is dx row
   // f * fH * fW + (2i + ry) * fW + (2j + rx)
   int sub, cW, ry, rx, fH, fW;
@@ -291,6 +296,7 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
 
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
 int fast_grid_rows(int M, int N, int z, int epi);
+bool fast_bwd_streams(const GemmParams& p);  // a dense EPI_BWD GEMM runs on the streaming kernel (P product: only there)
 int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an EPI_BWD launch of run_fast_gemm
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
                            float* dgamma, float* dbeta, int accumulate, hipStream_t s);  // grid rows (slots of EPI_BWD partials) of a fast-kernel launch

@@ -751,13 +751,35 @@ __global__ void pack_class_taps_kernel(const bf16_t* __restrict__ wt, bf16_t* __
 // are finalized into sum_g / sum_gx (/ sum_gx2) with dgamma / dbeta (dgamma2 / dbeta2) accumulated: the
 // input of vcg_bn_bwd_apply with mask_mode 0. y == NULL: no reduction. Fast bf16 engine only:
 // returns VCG_ERR_UNSUPPORTED where it does not apply (the caller then runs the unfused ops).
+namespace {
+// P = sum of the streaming dgrad's per-workgroup-row slabs, in slot order (deterministic)
+__global__ __launch_bounds__(256) void p_slab_reduce_kernel(const float4* __restrict__ slabs, int nslab, long long n4,
+                                                            float4* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 a = slabs[i];
+  for (int k = 1; k < nslab; ++k) {
+    const float4 b = slabs[(long long)k * n4 + i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  out[i] = a;
+}
+}  // namespace
+
+// P partial slabs of vcg_conv_dgrad_bwd with a2: at most 256 x 64 (workgroup rows x columns) [C][a2_c] f32 entries
+VCG_API long long vcg_conv_dgrad_bwd_p_ws_bytes(int C, int a2_c) {
+  (void)C;
+  return 256LL * 64 * (a2_c > 0 ? a2_c : 0) * 4;
+}
+
 VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C,
                                int Cout, int KH, int KW, int stride, int pad, int tsm_T, int tsm_fold,
                                const void* res, int res_stride, const unsigned char* bits, const void* y, const float* mean,
                                const float* invstd, const float* mscale, const float* mshift, const void* y2,
                                const float* mean2, const float* invstd2, float* ws, long long ws_bytes,
                                float* sum_g, float* sum_gx, float* dgamma, float* dbeta, float* sum_gx2,
-                               float* dgamma2, float* dbeta2, hipStream_t stream) {
+                               float* dgamma2, float* dbeta2, const void* a2, int a2_c, float* pg, float* pws,
+                               long long pws_bytes, hipStream_t stream) {
   const int logCo = ilog2_exact(Cout);
   VCG_REQUIRE(logCo >= 0 && Cout >= 8, "Cout must be a power of two >= 8");
   VCG_REQUIRE(C % 64 == 0, "C must be a multiple of 64");
@@ -770,6 +792,8 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
               "bad TSM geometry");
   VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C, Cout, KH, KW), "workspace too small");
   VCG_REQUIRE(res_stride == 1 || (res_stride == 2 && res), "res_stride must be 1, or 2 with a residual");
+  VCG_REQUIRE(!a2 || (pg && pws && (a2_c == 64 || a2_c == 128) && pws_bytes >= vcg_conv_dgrad_bwd_p_ws_bytes(C, a2_c)),
+              "a2 needs a2_c 64 / 128, pg and the P workspace");
   const long long nelem = (long long)N * H * W * C;
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   if (dtype != VCG_BF16 || !fast_gemm_enabled() || nelem * 2 >= 0xFFFFFF00LL ||
@@ -813,6 +837,10 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   e.part = ws;
   // (bits without y: the sums row of g only -- sum_gx comes from elsewhere, the previous block's y3 not stored)
   e.nred = y ? (y2 ? 3 : 2) : ((bits && sum_g && sum_gx) ? 2 : 0);
+  if (a2) {  // P = g^T a2 from the stored g tiles: the streaming kernel only (else the caller runs the GEMM)
+    e.a2 = a2; e.pj = a2_c; e.ppart = pws;
+    if (!dense || !fast_bwd_streams(p)) return VCG_ERR_UNSUPPORTED;
+  }
   if (subpix) {
     bf16_t* wpk = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(ws) + dgrad_bwd_part_bytes(C));
     const int cH = H / 2, cW = W / 2;
@@ -865,6 +893,12 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   }
   int rc = run_fast_gemm(p, dense ? OP_DENSE_K : OP_DGRAD, EPI_BWD, 1, stream);
   if (rc) return rc;
+  if (a2) {  // the P slabs [slots][C][a2_c] in slot order
+    const long long n = (long long)C * a2_c;
+    hipLaunchKernelGGL(p_slab_reduce_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, stream,
+                       (const float4*)pws, fast_bwd_slots(p), n / 4, (float4*)pg);
+    VCG_LAUNCH_CHECK();
+  }
   if (e.nred > 0) {
     const int slots = fast_bwd_slots(p);
     rc = bn_bwd_finalize_launch(ws, slots, C, (long long)e.nred * C, C, sum_g, sum_gx, dgamma, dbeta, 1, stream);

@@ -539,6 +539,15 @@ __device__ unsigned long long g_fast_stamps[64 * 4];
 constexpr int XF_HASY = 1;  // y + mask bits present (the BN sums of the previous block's bn3)
 constexpr int XF_BITS = 4;  // mask bits without y: sum g only (the previous block's y3 is not stored, trunk.py)
 constexpr int XF_Y2 = 2;    // y2 present (the previous block's downsample BN)
+// with XF_BITS: P = g^T a2 of the previous block (a2 of 64 / 128 columns) accumulated from the stored g tile, so the
+// separate weight-gradient GEMM that re-read g and a2 for bn3's sum_gx (trunk.py) is gone; the weight fragments then
+// sit in registers and, for 128 columns (TSM fold % 64 == 0), one A tile per slot, to keep the ring at 3-4 slots
+constexpr int XF_P64 = 8, XF_P128 = 16;
+typedef unsigned int pk_u32x4 __attribute__((ext_vector_type(4)));
+// transposed LDS read (4 bf16 per lane) as inline asm: a plain LDS read makes hipcc wait vmcnt(0) for the ring's DMA
+__device__ __forceinline__ void lds_tr_b16(s16x4& v, const bf16_t* p) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_u32(p)) : "memory");
+}
 
 __device__ __forceinline__ int bwd_tsm_shift(const BwdEpi& e, int n) {
   if (e.tsm_T <= 0) return 0;
@@ -549,20 +558,23 @@ __device__ __forceinline__ int bwd_tsm_shift(const BwdEpi& e, int n) {
 // TSM shifts) and the weight fragments of a wave's 32 columns in registers (64 VGPRs) instead of LDS, so the ring
 // keeps 3 slots (with the weights in LDS and one A tile per slot it had 2, measured step-neutral in round 4).
 __host__ __device__ constexpr bool bwd_stream_wide(int KC) { return KC > 2; }
+__host__ __device__ constexpr int bwd_stream_pj(int XF) { return (XF & XF_P64) ? 64 : ((XF & XF_P128) ? 128 : 0); }
+__host__ __device__ constexpr bool bwd_stream_breg(int KC, int XF) { return KC > 2 || bwd_stream_pj(XF) > 0; }
+__host__ __device__ constexpr int bwd_stream_na(int KC, int XF) { return (KC > 2 || (XF & XF_P128)) ? 1 : 2; }
 // LDS bytes of one ring slot / of the fixed part (weights, stage, column parameters) and the ring depth
 __host__ __device__ constexpr int bwd_stream_buf(int KC, int XF) {
-  return (bwd_stream_wide(KC) ? 1 : 2) * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 : 0) +
-         ((XF & (XF_HASY | XF_BITS)) ? 8 * 256 : 0) + ((XF & XF_Y2) ? 8192 : 0);
+  return bwd_stream_na(KC, XF) * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 : 0) +
+         ((XF & (XF_HASY | XF_BITS)) ? 8 * 256 : 0) + ((XF & XF_Y2) ? 8192 : 0) + bwd_stream_pj(XF) * 128;
 }
 #ifndef VCG_STREAM_NBUF
 #define VCG_STREAM_NBUF 4  // ring slots at most (build knob for A/B builds)
 #endif
-__host__ __device__ constexpr int bwd_stream_fixed(int KC) {
-  return (bwd_stream_wide(KC) ? 0 : KC * 8192) + 8192 + 1024;
+__host__ __device__ constexpr int bwd_stream_fixed(int KC, int XF) {
+  return (bwd_stream_breg(KC, XF) ? 0 : KC * 8192) + 8192 + 1024;
 }
 __host__ __device__ constexpr int bwd_stream_nbuf(int KC, int XF) {
-  return (160 * 1024 - bwd_stream_fixed(KC)) / bwd_stream_buf(KC, XF) >= VCG_STREAM_NBUF ? VCG_STREAM_NBUF
-         : (160 * 1024 - bwd_stream_fixed(KC)) / bwd_stream_buf(KC, XF);
+  return (160 * 1024 - bwd_stream_fixed(KC, XF)) / bwd_stream_buf(KC, XF) >= VCG_STREAM_NBUF ? VCG_STREAM_NBUF
+         : (160 * 1024 - bwd_stream_fixed(KC, XF)) / bwd_stream_buf(KC, XF);
 }
 
 template <int KC, int XF>
@@ -571,23 +583,27 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   constexpr bool HASB = HASY || (XF & XF_BITS) != 0;  // mask bits + sum g
   static_assert(!Y2 || HASY, "y2 comes with y");
   constexpr int TM = 64, TN = 64, NTH = 512, NW = 8;
-  constexpr bool WIDE = bwd_stream_wide(KC);
+  constexpr int PJ = bwd_stream_pj(XF);
+  static_assert(PJ == 0 || ((XF & XF_BITS) && !HASY), "P = g^T a2 with the mask bits alone");
+  constexpr bool BREG = bwd_stream_breg(KC, XF);  // weight fragments in registers
+  constexpr int NA = bwd_stream_na(KC, XF);       // A tiles per slot
   constexpr int NBUF = bwd_stream_nbuf(KC, XF);
   static_assert(NBUF >= 2, "LDS ring");  // (WIDE: 3 without y2; the host keeps WIDE + y2 on the persistent engine)
   constexpr int AT = KC * TM * 64 * 2;  // one A tile ([64][64] swizzled sub-tiles, fast_frag layout); two per slot
   constexpr int OB = TM * TN * 2;       // one row-major [64][64] bf16 epilogue operand (res / y / y2)
-  constexpr int OFF_R = (WIDE ? 1 : 2) * AT, OFF_Y = OFF_R + OB, OFF_BITS = OFF_Y + (HASY ? OB : 0);
+  constexpr int OFF_R = NA * AT, OFF_Y = OFF_R + OB, OFF_BITS = OFF_Y + (HASY ? OB : 0);
   constexpr int OFF_Y2 = OFF_BITS + (HASB ? NW * 256 : 0);  // mask bytes [64][8]: 16 lanes x 4 B per wave (+ pad)
-  constexpr int BUF = OFF_Y2 + (Y2 ? OB : 0);
+  constexpr int OFF_A2 = OFF_Y2 + (Y2 ? OB : 0);             // a2 rows [64][PJ], 16-B chunks swizzled (stem_bwd)
+  constexpr int BUF = OFF_A2 + PJ * 128;
   static_assert(BUF == bwd_stream_buf(KC, XF), "slot layout");
-  constexpr int BB = WIDE ? 0 : KC * TN * 64 * 2;
+  constexpr int BB = BREG ? 0 : KC * TN * 64 * 2;
   constexpr int SB = TM * TN * 2;
   constexpr int TOTAL = NBUF * BUF + BB + SB + 4 * TN * 4;
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
   static_assert(NBUF * BUF >= 3 * NTH * 8 * 4, "bwd_finish scratch");
   // VMEM instructions per wave: one tile's DMA (A 1 per k tile and A tile, res 1, y 1 + bits 1, y2 1), one flush's
   // stores (1)
-  constexpr int OPS1 = KC + 1 + (HASY ? 1 : 0) + (HASB ? 1 : 0) + (Y2 ? 1 : 0), OPS2 = OPS1 + KC;
+  constexpr int OPS1 = KC + 1 + (HASY ? 1 : 0) + (HASB ? 1 : 0) + (Y2 ? 1 : 0) + PJ / 64, OPS2 = OPS1 + KC;
   constexpr int VMW1 = (NBUF - 2) * OPS1 + (NBUF - 1), VMW2 = (NBUF - 2) * OPS2 + (NBUF - 1);
   static_assert(VMW2 < 64, "vmcnt field");
   __shared__ __attribute__((aligned(1024))) char smem[TOTAL];  // the ONLY LDS object (see FastLoader)
@@ -614,6 +630,8 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   if (my_tiles == 0) {  // no rows: an all-zero partial slot
     if (e.nred > 0 && tid < TN)
       for (int r = 0; r < e.nred; ++r) e.part[((long long)by * e.nred + r) * p.N + n0 + tid] = 0.f;
+    if constexpr (PJ > 0)
+      for (int i = tid; i < TN * PJ; i += NTH) e.ppart[((long long)by * p.N + n0) * PJ + i] = 0.f;
     return;
   }
   if (tid < TN) {
@@ -633,7 +651,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   }
   // TSM shifts of the workgroup's two 32-column halves; two A tiles when they differ (never for WIDE: host check)
   const int sh0 = bwd_tsm_shift(e, n0), sh1 = bwd_tsm_shift(e, n0 + 32);
-  const bool two = !WIDE && sh0 != sh1;
+  const bool two = NA == 2 && sh0 != sh1;
 
   // buffer descriptors of the epilogue operands (offset beyond num_records -> zeros)
   const long long ld = p.ldc;
@@ -649,14 +667,20 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
     rs_bits = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(e.bits), 0, nb_bits, 0x00020000);
   }
   if constexpr (Y2) rs_y2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.y2), 0, nb_full, 0x00020000);
+  uint32_t nb_a2 = 0;
+  __amdgpu_buffer_rsrc_t rs_a2 = rs_res;
+  if constexpr (PJ > 0) {
+    nb_a2 = (uint32_t)min((long long)p.M * PJ * 2, (long long)0xFFFFFF00LL);
+    rs_a2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(e.a2), 0, nb_a2, 0x00020000);
+  }
 
   FastLoader<64, OP_DENSE_K, NW> la, lb;
   const int g = lane >> 4, ci = lane & 15;
   const int wr = wave & 3, wc = wave >> 2;  // MFMA block: rows 16 wr .. + 15, columns 32 wc .. + 31 of the tile
   // WIDE: this wave's weight fragments (columns 32 wc + 16 j + ci, k = 64 kc + 32 s + 8 g .. + 7: fast_frag's
   // lane map) straight into registers, retired before the ring's first DMA (so no wait inside the loop counts them)
-  s16x8 bfr[WIDE ? KC : 1][2][2];
-  if constexpr (WIDE) {
+  s16x8 bfr[BREG ? KC : 1][2][2];
+  if constexpr (BREG) {
     const bf16_t* bp = reinterpret_cast<const bf16_t*>(p.b.ptr);
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
@@ -727,6 +751,17 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_bits, (lds_void_t*)(buf + OFF_BITS + wave * 256), 4,
                                                ok ? boff : nb_bits, 0, 0, 0);
     }
+    if constexpr (PJ > 0) {  // a2 rows [64][PJ]: 1 KB per instruction, the lane at slot q of row r loads chunk
+#pragma unroll                // q ^ 2 ((r >> 1) & 3) (the transposed reads' swizzle, stem_bwd.hip sb_swz)
+      for (int h = 0; h < PJ / 64; ++h) {
+        constexpr int CPRA = PJ / 8;  // 16-B chunks per a2 row
+        const int r = (8 * h + wave) * (1024 / (PJ * 2)) + lane / CPRA, q = lane % CPRA;
+        const int dr = d0 + r, c = q ^ (2 * ((r >> 1) & 3));
+        const uint32_t aoff = dr < p.M ? (uint32_t)(((long long)dr * PJ + 8 * c) * 2) : nb_a2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_a2, (lds_void_t*)(buf + OFF_A2 + (8 * h + wave) * 1024), 16,
+                                                 aoff, 0, 0, 0);
+      }
+    }
   };
 
 #pragma unroll
@@ -736,6 +771,9 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
   float s1[8], s2[8], s3[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = s3[i] = 0.f;
+  f32x4 accp[PJ > 0 ? PJ / 32 : 1];
+#pragma unroll
+  for (int i = 0; i < (PJ > 0 ? PJ / 32 : 1); ++i) accp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16_t* Cout = reinterpret_cast<bf16_t*>(p.C);
 
   for (int t = 0; t < my_tiles; ++t) {
@@ -765,7 +803,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           s16x8 bf;
-          if constexpr (WIDE) bf = bfr[kc][s][j];
+          if constexpr (BREG) bf = bfr[kc][s][j];
           else bf = fast_frag(Bs + kc * 4096, 32 * wc + 16 * j, lane, s);
           acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af, acc[j], 0, 0, 0);
         }
@@ -804,6 +842,7 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
         asm volatile("ds_read_b128 %0, %1" : "=v"(y2v) : "v"(lds_u32(Y2p + r * 64 + 8 * cc)) : "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      uint4 o = make_uint4(0u, 0u, 0u, 0u);  // (rows past M: zeros for the P product)
       if (d < p.M) {
         float v[8], rr[8];
         unpack8(sv, v);
@@ -814,7 +853,6 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) v[i] = ((bits >> i) & 1u) ? v[i] : 0.f;
         }
-        uint4 o;
         o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
         o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
         o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
@@ -842,10 +880,51 @@ __device__ __forceinline__ void bwd_stream_body(const GemmParams& p) {
           }
         }
       }
+      if constexpr (PJ > 0) {  // the stored g over its own stage chunk, for the P product below
+        const pk_u32x4 ov = {o.x, o.y, o.z, o.w};
+        asm volatile("ds_write_b128 %0, %1" ::"v"(lds_u32(St + r * 64 + 8 * st_slot<64>(r, cc))), "v"(ov) : "memory");
+      }
+    }
+    if constexpr (PJ > 0) {
+      // P[n][j] += sum_r g[r][n] a2[r][j] over the tile's 64 rows: both operands by transposed LDS reads
+      // (ds_read_b64_tr_b16, stem_bwd.hip's lane map: lanes 4q + pp of group g address row 4 g + q, columns 4 pp ..)
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's g chunks are in St
+      __builtin_amdgcn_s_barrier();        // ... and every wave's
+      const bf16_t* A2 = reinterpret_cast<const bf16_t*>(buf + OFF_A2);
+      const int nb = wave & 3, q = ci >> 2, pp = ci & 3;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int k0 = 32 * ks + 4 * g + q, k1 = k0 + 16;
+        const int cl = 16 * nb + 4 * pp;
+        s16x4 gl, gh, al[PJ / 32], ah[PJ / 32];
+        lds_tr_b16(gl, St + k0 * 64 + 8 * st_slot<64>(k0, cl >> 3) + (cl & 7));
+        lds_tr_b16(gh, St + k1 * 64 + 8 * st_slot<64>(k1, cl >> 3) + (cl & 7));
+#pragma unroll
+        for (int i = 0; i < PJ / 32; ++i) {
+          const int cj = 16 * ((wave >> 2) + 2 * i) + 4 * pp;
+          lds_tr_b16(al[i], A2 + k0 * PJ + 8 * ((cj >> 3) ^ (2 * ((k0 >> 1) & 3))) + (cj & 7));
+          lds_tr_b16(ah[i], A2 + k1 * PJ + 8 * ((cj >> 3) ^ (2 * ((k1 >> 1) & 3))) + (cj & 7));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const s16x8 gf = s16x8{gl[0], gl[1], gl[2], gl[3], gh[0], gh[1], gh[2], gh[3]};
+#pragma unroll
+        for (int i = 0; i < PJ / 32; ++i)
+          accp[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              s16x8{al[i][0], al[i][1], al[i][2], al[i][3], ah[i][0], ah[i][1], ah[i][2], ah[i][3]}, gf, accp[i], 0, 0,
+              0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     FAST_STAMP(t, 3);
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  if constexpr (PJ > 0) {  // accp[i][rr] = P[n0 + 16 nb + ci][16 ((wave >> 2) + 2 i) + 4 g + rr] -> slab `by`
+    float* pp = e.ppart + ((long long)by * p.N + n0 + 16 * (wave & 3) + ci) * PJ;
+#pragma unroll
+    for (int i = 0; i < PJ / 32; ++i)
+      *reinterpret_cast<f32x4*>(pp + 16 * ((wave >> 2) + 2 * i) + 4 * g) = accp[i];
+  }
   if constexpr (HASB) {
     if (e.nred > 0) bwd_finish<256, 64>(p, reinterpret_cast<float*>(smem), cpar + 2 * TN, s1, s2, s3, n0, by);
   }
@@ -1960,6 +2039,11 @@ static bool bwd_stream_ok(const GemmParams& p) {
   if (p.K == 256 && ((uintptr_t)p.b.ptr & 15 || p.b.ld % 8 != 0)) return false;  // 16-B weight fragment loads
   if (((uintptr_t)p.C | (uintptr_t)e.res | (uintptr_t)e.y | (uintptr_t)e.y2 | (uintptr_t)p.a.ptr) & 15) return false;
   if (e.res_s > 1 && (p.M % e.hw) != 0) return false;
+  if (e.pj > 0) {  // P = g^T a2: the mask bits alone, K 64 / 128, a2 of 64 / 128 columns (128: one A tile per slot)
+    if (e.y || !e.bits || p.K > 128 || (e.pj != 64 && e.pj != 128) || ((uintptr_t)e.a2 & 15) || !e.ppart) return false;
+    if (e.pj == 128 && e.tsm_T > 0 && e.tsm_fold % 64 != 0) return false;
+    if (((uintptr_t)p.b.ptr & 15) || p.b.ld % 8 != 0) return false;  // weight fragments in registers
+  }
   return true;
 }
 
@@ -1979,6 +2063,8 @@ static int bwd_stream_rows(const GemmParams& p) {
   if (gy > mtiles) gy = mtiles >= 8 ? (mtiles & ~7) : mtiles;
   return gy < 1 ? 1 : gy;
 }
+
+bool fast_bwd_streams(const GemmParams& p) { return bwd_stream_ok(p); }
 
 int fast_bwd_slots(const GemmParams& p) {
   if (bwd_stream_ok(p)) return bwd_stream_rows(p);
@@ -2033,6 +2119,10 @@ static int run_bwd_stream(const GemmParams& p, hipStream_t s) {
   if constexpr (KC == 4) {
     if (bwd_stream_tn(p) == 128)
       return p.bwd.bits ? launch_bwd_stream<4, XF_BITS, 128>(p, s) : launch_bwd_stream<4, 0, 128>(p, s);
+  }
+  if constexpr (KC <= 2) {
+    if (p.bwd.pj == 64) return launch_bwd_stream<KC, XF_BITS | XF_P64>(p, s);
+    if (p.bwd.pj == 128) return launch_bwd_stream<KC, XF_BITS | XF_P128>(p, s);
   }
   if (!p.bwd.y) return p.bwd.bits ? launch_bwd_stream<KC, XF_BITS>(p, s) : launch_bwd_stream<KC, 0>(p, s);
   if (!p.bwd.y2) return launch_bwd_stream<KC, XF_HASY>(p, s);

@@ -135,11 +135,14 @@ def conv_dgrad(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, out=None):
 
 def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_fold=0, res=None, res_stride=1,
                    bits=None, y=None, mean=None, invstd=None, mscale=None, mshift=None, y2=None, mean2=None, invstd2=None, sums=None,
-                   sum_gx2=None, dgamma=None, dbeta=None, dgamma2=None, dbeta2=None, out=None, workspace=None):
+                   sum_gx2=None, dgamma=None, dbeta=None, dgamma2=None, dbeta2=None, out=None, workspace=None, a2=None,
+                   pg=None):
     """Conv input gradient fused with the trunk backward's next steps (vcg_conv_dgrad_bwd, igemm.h BwdEpi):
     g = mask(tsm_adjoint(dgrad) + res) and the BN-backward sums of g against y (sums [2, C] = sum_g,
     sum_gx) and y2 (res_stride 2: res is the compact [N, H/2, W/2, C] gradient of a 1x1 / stride-2 conv) (sum_gx2 [C]); dgamma/dbeta (dgamma2/dbeta2) accumulate. Returns g, or None where the
-    fused engine does not apply (fp32 / unsupported shape): the caller then runs the unfused ops."""
+    fused engine does not apply (fp32 / unsupported shape): the caller then runs the unfused ops.
+    a2 (bf16 [N, H, W, a2_c], a2_c 64 / 128) with pg (f32 [C, a2_c]): also pg = g^T a2 from the stored g tiles; then
+    the return value is (g, done) -- done False where that product does not apply (g computed without it)."""
     OH, OW = conv_out_hw(H, W, KH, KW, stride, pad)
     _chk(dy, None, "dy")
     assert dy.numel() == N * OH * OW * Cout and wt.numel() == C * KH * KW * Cout
@@ -152,16 +155,30 @@ def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_f
             _chk(t, dy.dtype)
             assert t.numel() == (N * ((H + 1) // 2) * ((W + 1) // 2) * C if t is res and res_stride == 2
                                  else N * H * W * C)
-    rc = _lib.query("vcg_conv_dgrad_bwd", dt_code(dy.dtype), P(dy), P(wt), P(g), N, H, W, C, Cout, KH, KW, stride,
-                    pad, tsm_T, tsm_fold, P(res), int(res_stride), P(bits), P(y), P(mean), P(invstd), P(mscale),
-                    P(mshift), P(y2), P(mean2), P(invstd2), P(workspace), workspace.numel() * 4,
-                    P(sums[0]) if sums is not None else None, P(sums[1]) if sums is not None else None, P(dgamma),
-                    P(dbeta), P(sum_gx2), P(dgamma2), P(dbeta2), stream())
-    if rc == -2:  # VCG_ERR_UNSUPPORTED
-        return None
+    def call(a2_, pg_, pws_):
+        return _lib.query("vcg_conv_dgrad_bwd", dt_code(dy.dtype), P(dy), P(wt), P(g), N, H, W, C, Cout, KH, KW,
+                          stride, pad, tsm_T, tsm_fold, P(res), int(res_stride), P(bits), P(y), P(mean), P(invstd),
+                          P(mscale), P(mshift), P(y2), P(mean2), P(invstd2), P(workspace), workspace.numel() * 4,
+                          P(sums[0]) if sums is not None else None, P(sums[1]) if sums is not None else None,
+                          P(dgamma), P(dbeta), P(sum_gx2), P(dgamma2), P(dbeta2), P(a2_),
+                          a2_.shape[-1] if a2_ is not None else 0, P(pg_), P(pws_),
+                          pws_.numel() * 4 if pws_ is not None else 0, stream())
+    done = False
+    rc = -2
+    if a2 is not None:
+        _chk(a2, torch.bfloat16, "a2")
+        _chk(pg, torch.float32, "pg")
+        assert a2.numel() == N * H * W * a2.shape[-1] and pg.numel() == C * a2.shape[-1]
+        pws = ws(_lib.query("vcg_conv_dgrad_bwd_p_ws_bytes", C, a2.shape[-1]), dy.device)
+        rc = call(a2, pg, pws)
+        done = rc == 0
+    if rc == -2:  # VCG_ERR_UNSUPPORTED (with a2: retried without the P product)
+        rc = call(None, None, None)
+    if rc == -2:
+        return (None, False) if a2 is not None else None
     if rc != 0:
         raise _lib.VcgError(f"vcg_conv_dgrad_bwd failed ({rc}): {_lib.last_error()}")
-    return g
+    return (g, done) if a2 is not None else g
 
 
 def bn_apply_colsum(y, scale, shift, C, relu=True):

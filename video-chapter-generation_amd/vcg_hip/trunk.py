@@ -146,6 +146,9 @@ class ResNetTrunk:
     # the stem's BN-backward apply and conv1 weight gradient as one pass (ops.stem_bwd_fused); False: the apply pass
     # writes dy0 and the im2col weight-gradient GEMM reads it (tests compare both)
     fused_stem_bwd = os.environ.get("VCG_FUSED_STEM_BWD", "1") != "0"
+    # a y3-drop block's P = g^T a2 formed by the next block's streaming conv1 dgrad (layers 1-2); False: the weight-
+    # gradient GEMM (tests compare both)
+    dgrad_p = os.environ.get("VCG_DGRAD_P", "1") != "0"
 
     def __init__(self, net, dtype):
         self.net = net
@@ -705,8 +708,10 @@ class ResNetTrunk:
             g, sums3, sumsd = gin
             b3, bd = r["b3"], r.get("bd")
             if r["y3"] is None and not ds:  # bn3's sum_gx from g^T a2 (the conv1 dgrad reduced only sum g)
-                Pg = torch.empty((C3, planes, 1, 1), dtype=torch.float32, device=g.device)
-                ops.conv_wgrad(r["a2"], g, Pg, N, H2, W2, planes, planes, C3, 1, 1, 1, 0, accumulate=False)
+                Pg = r.get("Pg")  # (formed by the next block's conv1 dgrad from its stored g tiles where it could)
+                if Pg is None:
+                    Pg = torch.empty((C3, planes, 1, 1), dtype=torch.float32, device=g.device)
+                    ops.conv_wgrad(r["a2"], g, Pg, N, H2, W2, planes, planes, C3, 1, 1, 1, 0, accumulate=False)
                 ops.bn_bwd_sumgx_from_wgrad(Pg.view(C3, planes), self._wprep(blk.conv3, planes), C3, planes, b3.mean,
                                             b3.invstd, sums3[0], sums3[1], self._bn_grads(b3)[0])
                 r["Pg"] = Pg
@@ -743,6 +748,7 @@ class ResNetTrunk:
                 dy3 = self._bn_apply_bwd(bnf[0], self._y3(r), r["b3"], C3, bnf[1])
         if ResNetTrunk.census is not None:
             ResNetTrunk.census.append(("bwd", C3, ds, {"fold_wgrad": bnf is not None, "fold_dgrad": dy2 is not None,
+                                                       "p_dgrad": bool(r.get("Pg_dgrad")),
                                                        "a2_form": bnf is not None and r.get("a2sum") is not None}))
         if dy2 is None:
             dy2 = self._dgrad_bn(blk.conv3, dy3, N, H2, W2, r["y2"], r["b2"], planes)
@@ -790,7 +796,20 @@ class ResNetTrunk:
                 dg2, db2 = self._bn_grads(prev["bd"])
                 kw.update(y2=prev["yd"], mean2=prev["bd"].mean, invstd2=prev["bd"].invstd, sum_gx2=s3[2],
                           dgamma2=dg2, dbeta2=db2)
-        out = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, **kw) if ResNetTrunk.fused_bwd else None
+        pg = None
+        if (ResNetTrunk.fused_bwd and ResNetTrunk.dgrad_p and prev is not None and prev["y3"] is None
+                and prev["blk"].downsample is None and prev["a2"] is not None and prev["planes"] in (64, 128)
+                and prev["a2"].numel() == N * H * W * prev["planes"]):
+            # the previous block's P = g^T a2 (its bn3 sum_gx and conv3 weight gradient) from this dgrad's stored g
+            # tiles instead of a weight-gradient GEMM that re-reads g and a2
+            pg = torch.empty((Cin1, prev["planes"], 1, 1), dtype=torch.float32, device=dy1.device)
+            out, done = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, a2=prev["a2"],
+                                           pg=pg.view(Cin1, prev["planes"]), **kw)
+            if done:
+                prev["Pg"] = pg
+                prev["Pg_dgrad"] = True
+        else:
+            out = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, **kw) if ResNetTrunk.fused_bwd else None
         ResNetTrunk.path_counts["unfused" if out is None else "fused"] += 1
         if ds:
             if out is None and res_stride == 2:  # unfused fallback: the full-grid downsample input gradient
