@@ -934,7 +934,7 @@ def test_gemm256_vs_128(K, case, monkeypatch):
 # conv1 input gradients whose epilogue also forms the previous block's P = g^T a2 (mask bits, no y):
 # (N, H, W, C, Cout, T, res_stride, a2 columns)
 P_CASES = [(16, 56, 56, 256, 64, 8, 1, 64), (16, 56, 56, 256, 128, 8, 2, 64), (16, 28, 28, 512, 128, 8, 1, 128),
-           (5, 28, 28, 512, 128, 5, 1, 128)]
+           (5, 28, 28, 512, 128, 5, 1, 128), (16, 28, 28, 512, 256, 8, 2, 128)]
 
 
 @pytest.mark.parametrize("case", P_CASES)

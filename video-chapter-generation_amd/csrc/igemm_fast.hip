@@ -2039,8 +2039,10 @@ static bool bwd_stream_ok(const GemmParams& p) {
   if (p.K == 256 && ((uintptr_t)p.b.ptr & 15 || p.b.ld % 8 != 0)) return false;  // 16-B weight fragment loads
   if (((uintptr_t)p.C | (uintptr_t)e.res | (uintptr_t)e.y | (uintptr_t)e.y2 | (uintptr_t)p.a.ptr) & 15) return false;
   if (e.res_s > 1 && (p.M % e.hw) != 0) return false;
-  if (e.pj > 0) {  // P = g^T a2: the mask bits alone, K 64 / 128, a2 of 64 / 128 columns (128: one A tile per slot)
-    if (e.y || !e.bits || p.K > 128 || (e.pj != 64 && e.pj != 128) || ((uintptr_t)e.a2 & 15) || !e.ppart) return false;
+  if (e.pj > 0) {  // P = g^T a2: the mask bits alone, K 64 / 128 (a2 of 64 / 128 columns; 128: one A tile per slot)
+    // or K = 256 on the 64-column tiles (a2 of 128 columns, 2 slots: the layer-3 first block's dgrad)
+    if (e.y || !e.bits || (e.pj != 64 && e.pj != 128) || ((uintptr_t)e.a2 & 15) || !e.ppart) return false;
+    if (p.K == 256 && e.pj != 128) return false;
     if (e.pj == 128 && e.tsm_T > 0 && e.tsm_fold % 64 != 0) return false;
     if (((uintptr_t)p.b.ptr & 15) || p.b.ld % 8 != 0) return false;  // weight fragments in registers
   }
@@ -2052,7 +2054,7 @@ static bool bwd_stream_ok(const GemmParams& p) {
 static int bwd_stream_tn(const GemmParams& p) {
   const BwdEpi& e = p.bwd;
   const char* v = getenv("VCG_BWD_STREAM");
-  if (v && v[0] == '6') return 64;
+  if ((v && v[0] == '6') || p.bwd.pj > 0) return 64;  // (the P product lives in the 64-column kernel)
   return p.K == 256 && p.N % 128 == 0 && !e.y && (e.tsm_T <= 0 || e.tsm_fold % 128 == 0) ? 128 : 64;
 }
 
@@ -2122,8 +2124,8 @@ static int run_bwd_stream(const GemmParams& p, hipStream_t s) {
   }
   if constexpr (KC <= 2) {
     if (p.bwd.pj == 64) return launch_bwd_stream<KC, XF_BITS | XF_P64>(p, s);
-    if (p.bwd.pj == 128) return launch_bwd_stream<KC, XF_BITS | XF_P128>(p, s);
   }
+  if (p.bwd.pj == 128) return launch_bwd_stream<KC, XF_BITS | XF_P128>(p, s);
   if (!p.bwd.y) return p.bwd.bits ? launch_bwd_stream<KC, XF_BITS>(p, s) : launch_bwd_stream<KC, 0>(p, s);
   if (!p.bwd.y2) return launch_bwd_stream<KC, XF_HASY>(p, s);
   return launch_bwd_stream<KC, XF_HASY | XF_Y2>(p, s);
