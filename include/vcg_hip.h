@@ -81,7 +81,7 @@ VCG_API int vcg_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, 
    dgrad runs as four sub-pixel classes (dx pixels of one (h, w) parity) over only the taps reaching each.
    bf16 fast engine only; VCG_ERR_UNSUPPORTED elsewhere. */
 VCG_API long long vcg_conv_dgrad_bwd_ws_bytes(int C, int Cout, int KH, int KW);
-/* a2 (optional, with bits and no y): the previous block's conv3 input [N*H*W][a2_c] bf16 (a2_c 64 / 128); the kernel then
+/* a2 (optional, with bits and no y): the previous block's conv3 input [N*H*W][a2_c] bf16 (a2_c 64; K <= 128); the kernel then
    also accumulates pg [C][a2_c] f32 = g^T a2 (the conv3 weight-gradient product that gives bn3's sum_gx) from the g
    tiles it stores, with the partial slabs in pws (vcg_conv_dgrad_bwd_p_ws_bytes). VCG_ERR_UNSUPPORTED when that
    product does not apply to the shape (the streaming 1x1 kernel only): the caller runs the plain call and the GEMM. */

@@ -377,8 +377,8 @@ def _check_census(census):
         assert (c3, ds) == (c3b, dsb)
         small = c3 <= 1024
         want_f = {"a2sum": small, "y3_drop": small and not ds, "bn3_gemm": small and not ds}
-        # P = g^T a2 from the next block's streaming conv1 dgrad: layer-1 blocks 1-2, layer-2 blocks 1-3
-        want_b = {"fold_wgrad": small, "fold_dgrad": small, "p_dgrad": i in (1, 2, 4, 5, 6), "a2_form": small}
+        # P = g^T a2 from the next block's streaming conv1 dgrad: layer-1 blocks 1-2
+        want_b = {"fold_wgrad": small, "fold_dgrad": small, "p_dgrad": i in (1, 2), "a2_form": small}
         assert f == want_f, (c3, ds, f)
         assert b == want_b, (c3, ds, b)
 

@@ -933,14 +933,15 @@ def test_gemm256_vs_128(K, case, monkeypatch):
 
 # conv1 input gradients whose epilogue also forms the previous block's P = g^T a2 (mask bits, no y):
 # (N, H, W, C, Cout, T, res_stride, a2 columns)
-P_CASES = [(16, 56, 56, 256, 64, 8, 1, 64), (16, 56, 56, 256, 128, 8, 2, 64), (16, 28, 28, 512, 128, 8, 1, 128),
-           (5, 28, 28, 512, 128, 5, 1, 128), (16, 28, 28, 512, 256, 8, 2, 128)]
+P_CASES = [(16, 56, 56, 256, 64, 8, 1, 64), (16, 56, 56, 256, 128, 8, 2, 64), (5, 56, 56, 256, 64, 5, 1, 64),
+           (3, 28, 28, 256, 128, 3, 2, 64)]
 
 
 @pytest.mark.parametrize("case", P_CASES)
 def test_conv_dgrad_bwd_p_product(K, case):
     """vcg_conv_dgrad_bwd with a2: g and sum g exactly those of the call without it, and pg = g^T a2 against float64
-    as close as the weight-gradient GEMM it replaces (trunk.py: bn3's sum_gx of a block whose y3 is not stored)."""
+    as close as the weight-gradient GEMM it replaces (trunk.py: bn3's sum_gx of a layer-1 block whose y3 is not
+    stored); a2 of 128 columns is refused (VCG_ERR_UNSUPPORTED -> done False, g still computed)."""
     N, H, W, C, Cout, T, rs, PJ = case
     dt = torch.bfloat16
     dy = _rand((N, H, W, Cout), dt, 91).to(DEV)
@@ -968,3 +969,7 @@ def test_conv_dgrad_bwd_p_product(K, case):
     e_p = (pg.double() - ref).abs().max().item() / sc
     e_g = (ref_gemm.view(C, PJ).double() - ref).abs().max().item() / sc
     assert e_p <= max(2.0 * e_g, 1e-5), (e_p, e_g)
+    a2w = torch.relu(_rand((N, H, W, 128), torch.float32, 96)).to(dt).to(DEV)
+    g2, done2 = K.conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, 1, 1, 1, 0, sums=torch.zeros((2, C), device=DEV), a2=a2w,
+                                 pg=torch.empty((C, 128), device=DEV), **kw)
+    assert not done2 and torch.equal(g2, g0)

@@ -792,8 +792,8 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
               "bad TSM geometry");
   VCG_REQUIRE(ws_bytes >= vcg_conv_dgrad_bwd_ws_bytes(C, Cout, KH, KW), "workspace too small");
   VCG_REQUIRE(res_stride == 1 || (res_stride == 2 && res), "res_stride must be 1, or 2 with a residual");
-  VCG_REQUIRE(!a2 || (pg && pws && (a2_c == 64 || a2_c == 128) && pws_bytes >= vcg_conv_dgrad_bwd_p_ws_bytes(C, a2_c)),
-              "a2 needs a2_c 64 / 128, pg and the P workspace");
+  VCG_REQUIRE(!a2 || (pg && pws && a2_c > 0 && a2_c % 64 == 0 && pws_bytes >= vcg_conv_dgrad_bwd_p_ws_bytes(C, a2_c)),
+              "a2 needs a2_c a multiple of 64, pg and the P workspace");
   const long long nelem = (long long)N * H * W * C;
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   if (dtype != VCG_BF16 || !fast_gemm_enabled() || nelem * 2 >= 0xFFFFFF00LL ||

@@ -539,10 +539,11 @@ __device__ unsigned long long g_fast_stamps[64 * 4];
 constexpr int XF_HASY = 1;  // y + mask bits present (the BN sums of the previous block's bn3)
 constexpr int XF_BITS = 4;  // mask bits without y: sum g only (the previous block's y3 is not stored, trunk.py)
 constexpr int XF_Y2 = 2;    // y2 present (the previous block's downsample BN)
-// with XF_BITS: P = g^T a2 of the previous block (a2 of 64 / 128 columns) accumulated from the stored g tile, so the
-// separate weight-gradient GEMM that re-read g and a2 for bn3's sum_gx (trunk.py) is gone; the weight fragments then
-// sit in registers and, for 128 columns (TSM fold % 64 == 0), one A tile per slot, to keep the ring at 3-4 slots
-constexpr int XF_P64 = 8, XF_P128 = 16;
+// with XF_BITS: P = g^T a2 of the previous block (a2 of 64 columns: layer 1) accumulated from the stored g tile, so
+// the separate weight-gradient GEMM that re-read g and a2 for bn3's sum_gx (trunk.py) is gone; the weight fragments
+// then sit in registers to keep the ring at 3-4 slots. (128 a2 columns -- layer 2 -- cost the dgrad as much as the
+// GEMM they replace: tools/bench_dgrad_p.py, +212 us vs 225 us; not built.)
+constexpr int XF_P64 = 8;
 typedef unsigned int pk_u32x4 __attribute__((ext_vector_type(4)));
 // transposed LDS read (4 bf16 per lane) as inline asm: a plain LDS read makes hipcc wait vmcnt(0) for the ring's DMA
 __device__ __forceinline__ void lds_tr_b16(s16x4& v, const bf16_t* p) {
@@ -558,9 +559,9 @@ __device__ __forceinline__ int bwd_tsm_shift(const BwdEpi& e, int n) {
 // TSM shifts) and the weight fragments of a wave's 32 columns in registers (64 VGPRs) instead of LDS, so the ring
 // keeps 3 slots (with the weights in LDS and one A tile per slot it had 2, measured step-neutral in round 4).
 __host__ __device__ constexpr bool bwd_stream_wide(int KC) { return KC > 2; }
-__host__ __device__ constexpr int bwd_stream_pj(int XF) { return (XF & XF_P64) ? 64 : ((XF & XF_P128) ? 128 : 0); }
+__host__ __device__ constexpr int bwd_stream_pj(int XF) { return (XF & XF_P64) ? 64 : 0; }
 __host__ __device__ constexpr bool bwd_stream_breg(int KC, int XF) { return KC > 2 || bwd_stream_pj(XF) > 0; }
-__host__ __device__ constexpr int bwd_stream_na(int KC, int XF) { return (KC > 2 || (XF & XF_P128)) ? 1 : 2; }
+__host__ __device__ constexpr int bwd_stream_na(int KC, int XF) { return KC > 2 ? 1 : 2; }
 // LDS bytes of one ring slot / of the fixed part (weights, stage, column parameters) and the ring depth
 __host__ __device__ constexpr int bwd_stream_buf(int KC, int XF) {
   return bwd_stream_na(KC, XF) * KC * 8192 + 8192 + ((XF & XF_HASY) ? 8192 : 0) +
@@ -2041,9 +2042,7 @@ static bool bwd_stream_ok(const GemmParams& p) {
   if (e.res_s > 1 && (p.M % e.hw) != 0) return false;
   if (e.pj > 0) {  // P = g^T a2: the mask bits alone, K 64 / 128 (a2 of 64 / 128 columns; 128: one A tile per slot)
     // or K = 256 on the 64-column tiles (a2 of 128 columns, 2 slots: the layer-3 first block's dgrad)
-    if (e.y || !e.bits || (e.pj != 64 && e.pj != 128) || ((uintptr_t)e.a2 & 15) || !e.ppart) return false;
-    if (p.K == 256 && e.pj != 128) return false;
-    if (e.pj == 128 && e.tsm_T > 0 && e.tsm_fold % 64 != 0) return false;
+    if (e.y || !e.bits || e.pj != 64 || p.K > 128 || ((uintptr_t)e.a2 & 15) || !e.ppart) return false;
     if (((uintptr_t)p.b.ptr & 15) || p.b.ld % 8 != 0) return false;  // weight fragments in registers
   }
   return true;
@@ -2125,7 +2124,6 @@ static int run_bwd_stream(const GemmParams& p, hipStream_t s) {
   if constexpr (KC <= 2) {
     if (p.bwd.pj == 64) return launch_bwd_stream<KC, XF_BITS | XF_P64>(p, s);
   }
-  if (p.bwd.pj == 128) return launch_bwd_stream<KC, XF_BITS | XF_P128>(p, s);
   if (!p.bwd.y) return p.bwd.bits ? launch_bwd_stream<KC, XF_BITS>(p, s) : launch_bwd_stream<KC, 0>(p, s);
   if (!p.bwd.y2) return launch_bwd_stream<KC, XF_HASY>(p, s);
   return launch_bwd_stream<KC, XF_HASY | XF_Y2>(p, s);

@@ -141,7 +141,7 @@ def conv_dgrad_bwd(dy, wt, N, H, W, C, Cout, KH, KW, stride, pad, tsm_T=0, tsm_f
     g = mask(tsm_adjoint(dgrad) + res) and the BN-backward sums of g against y (sums [2, C] = sum_g,
     sum_gx) and y2 (res_stride 2: res is the compact [N, H/2, W/2, C] gradient of a 1x1 / stride-2 conv) (sum_gx2 [C]); dgamma/dbeta (dgamma2/dbeta2) accumulate. Returns g, or None where the
     fused engine does not apply (fp32 / unsupported shape): the caller then runs the unfused ops.
-    a2 (bf16 [N, H, W, a2_c], a2_c 64 / 128) with pg (f32 [C, a2_c]): also pg = g^T a2 from the stored g tiles; then
+    a2 (bf16 [N, H, W, a2_c], a2_c 64) with pg (f32 [C, a2_c]): also pg = g^T a2 from the stored g tiles; then
     the return value is (g, done) -- done False where that product does not apply (g computed without it)."""
     OH, OW = conv_out_hw(H, W, KH, KW, stride, pad)
     _chk(dy, None, "dy")

@@ -798,10 +798,11 @@ class ResNetTrunk:
                           dgamma2=dg2, dbeta2=db2)
         pg = None
         if (ResNetTrunk.fused_bwd and ResNetTrunk.dgrad_p and prev is not None and prev["y3"] is None
-                and prev["blk"].downsample is None and prev["a2"] is not None and prev["planes"] in (64, 128)
+                and prev["blk"].downsample is None and prev["a2"] is not None and prev["planes"] == 64
                 and prev["a2"].numel() == N * H * W * prev["planes"]):
             # the previous block's P = g^T a2 (its bn3 sum_gx and conv3 weight gradient) from this dgrad's stored g
-            # tiles instead of a weight-gradient GEMM that re-reads g and a2
+            # tiles instead of a weight-gradient GEMM that re-reads g and a2 (layer 1: the dgrad pays 110-245 us for
+            # a 405 us GEMM; with layer 2's 128 columns it pays as much as it saves, tools/bench_dgrad_p.py)
             pg = torch.empty((Cin1, prev["planes"], 1, 1), dtype=torch.float32, device=dy1.device)
             out, done = ops.conv_dgrad_bwd(dy1, wt, N, H, W, Cin1, Cout1, KH, KW, s, p, a2=prev["a2"],
                                            pg=pg.view(Cin1, prev["planes"]), **kw)
