@@ -2110,7 +2110,10 @@ static int launch_bwd_stream(const GemmParams& p, hipStream_t s) {
   const int nx = p.N / TN, gy = bwd_stream_rows(p);
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((igemm_fast_kernel<256, TN, KC, EPI_BWD_STREAM, false, XF>), dim3(nx * gy), dim3(512), 0, s, p);
-  timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_DENSE_K, EPI_BWD, false>(p, 1));
+  // (with the g^T a2 product: + its flops, the a2 read and the P slabs written and reduced)
+  const double pj = bwd_stream_pj(XF);
+  timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K + 2.0 * p.M * p.N * pj,
+             algorithmic_bytes<OP_DENSE_K, EPI_BWD, false>(p, 1) + 2.0 * p.M * pj + 4.0 * p.N * pj);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }
