@@ -752,17 +752,30 @@ __global__ void pack_class_taps_kernel(const bf16_t* __restrict__ wt, bf16_t* __
 // input of vcg_bn_bwd_apply with mask_mode 0. y == NULL: no reduction. Fast bf16 engine only:
 // returns VCG_ERR_UNSUPPORTED where it does not apply (the caller then runs the unfused ops).
 namespace {
-// P = sum of the streaming dgrad's per-workgroup-row slabs, in slot order (deterministic)
+// P = sum of the streaming dgrad's per-workgroup-row slabs: 32 float4 entries per workgroup, 8 slot groups (group g
+// sums slots g, g + 8, ... in order), the groups combined in order through LDS (deterministic; one thread walking
+// all 64 slots serially took 41 us)
 __global__ __launch_bounds__(256) void p_slab_reduce_kernel(const float4* __restrict__ slabs, int nslab, long long n4,
                                                             float4* __restrict__ out) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n4) return;
-  float4 a = slabs[i];
-  for (int k = 1; k < nslab; ++k) {
-    const float4 b = slabs[(long long)k * n4 + i];
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  __shared__ float4 part[8][32];
+  const int e = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const long long i = (long long)blockIdx.x * 32 + e;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4)
+    for (int k = g; k < nslab; k += 8) {
+      const float4 b = slabs[(long long)k * n4 + i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+  part[g][e] = a;
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 s = part[0][e];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) {
+      s.x += part[q][e].x; s.y += part[q][e].y; s.z += part[q][e].z; s.w += part[q][e].w;
+    }
+    out[i] = s;
   }
-  out[i] = a;
 }
 }  // namespace
 
@@ -895,7 +908,7 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   if (rc) return rc;
   if (a2) {  // the P slabs [slots][C][a2_c] in slot order
     const long long n = (long long)C * a2_c;
-    hipLaunchKernelGGL(p_slab_reduce_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, stream,
+    hipLaunchKernelGGL(p_slab_reduce_kernel, dim3((unsigned)((n / 4 + 31) / 32)), dim3(256), 0, stream,
                        (const float4*)pws, fast_bwd_slots(p), n / 4, (float4*)pg);
     VCG_LAUNCH_CHECK();
   }
