@@ -135,6 +135,15 @@ VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* sh
    double -- torchvision Bottleneck bn3 over conv3's output (model/vision/resnet50_tsm.py:15) without a statistics
    pass over a2. Writes the vcg_conv_fwd stats layout (one used slot) for vcg_bn_finalize. */
 VCG_API int vcg_bn_stats_from_gram(const double* g64, const void* w, long long M, int N, int C, float* stats, int mtiles, hipStream_t s);
+/* vcg_bn_stats_from_gram + vcg_bn_finalize for its one slot of M rows (running_mean / running_var updated with
+   momentum when given, both or neither) + vcg_weight_fold of the f32 master weight w32 [N][C] by the new scale into
+   wfold (bf16 [N][C]; both or neither) in one launch, with the same values as the three calls: bn3's state and the
+   folded weight of the y3-drop block's GEMM pass (model/two_stream.py:VideoEncoder -> torchvision Bottleneck.bn3).
+   C <= 256, C % 16 == 0 (VCG_ERR_INVALID otherwise). */
+VCG_API int vcg_bn_finalize_from_gram(const double* g64, const void* w, long long M, int N, int C, const float* gamma,
+                                      const float* beta, float* mean, float* invstd, float* scale, float* shift,
+                                      float* running_mean, float* running_var, float momentum, float eps,
+                                      const float* w32, void* wfold, hipStream_t s);
 VCG_API int vcg_conv1x1_stats(const void* x, const void* w, float* stats, int M, int N, int K, hipStream_t stream);
 VCG_API int vcg_bn_bwd_sumgx_from_wgrad(const float* P, const void* w, int K, int C, const float* mean, const float* invstd, const float* sum_g, float* sum_gx, float* dgamma, hipStream_t stream);
 VCG_API int vcg_bn_bwd_fold_weights_a2(const void* wt, int C, int K, const float* invstd, const float* gamma, const float* sum_g, const float* sum_gx, float inv_count, const float* colsum_a, void* wfold, float* bias, hipStream_t stream);

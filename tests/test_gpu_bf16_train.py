@@ -156,6 +156,30 @@ def test_c1_bf16_bn_fold_vs_apply():
     assert np.median(errs) <= 2e-2 and errs.max() <= 8e-2 and coss.min() >= 0.998
 
 
+def test_gram_fin_model_identical():
+    """The fused bn3 statistics + finalize + weight fold launch (ResNetTrunk.gram_fin) against the three-call chain in
+    a whole bf16 train step: bit-identical loss, gradients and BN running statistics."""
+    from vcg_hip import synth
+    from vcg_hip.trunk import ResNetTrunk
+    st = dict(_gold("bn_running_stats.npz"))
+    frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=78, device=DEV)
+    res = {}
+    saved = ResNetTrunk.gram_fin
+    try:
+        for fin in (True, False):
+            ResNetTrunk.gram_fin = fin
+            m = _model(4, "bf16", st)
+            loss, _, g, _ = _step(m, frames, ids, mask, labels)
+            run = {n: b.detach().clone() for n, b in m.named_buffers() if "running" in n}
+            res[fin] = (loss, g, run)
+    finally:
+        ResNetTrunk.gram_fin = saved
+    (l1, g1, r1), (l2, g2, r2) = res[True], res[False]
+    assert l1 == l2
+    assert g1.keys() == g2.keys() and all(torch.equal(g1[n], g2[n]) for n in g1)
+    assert r1.keys() == r2.keys() and len(r1) > 0 and all(torch.equal(r1[n], r2[n]) for n in r1)
+
+
 def test_gram_stats_forward():
     """bn3's batch statistics from the bn2 apply pass's (a2^T a2, colsum(a2)) (ResNetTrunk.gram_stats, the exact y3
     statistics) against the conv3 statistics GEMM (of the bf16-rounded y3), C1 shapes, BN in training mode: the

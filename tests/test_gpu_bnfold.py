@@ -479,3 +479,48 @@ def test_bn_stats_from_gram_large_mean(M, C, N):
           f"{e_inv:.2e}")
     assert ratio > 30
     assert e_mean < 1e-4 and e_inv < 1e-4
+
+
+@pytest.mark.parametrize("M,C,N,fold,upd", [(3211264 // 8, 64, 256, True, True), (802816 // 4 + 3, 128, 512, True, False),
+                                            (50176, 256, 1024, False, True), (7, 64, 256, True, True),
+                                            (100352, 48, 200, True, True)])
+def test_bn_finalize_from_gram_vs_three_calls(M, C, N, fold, upd):
+    """bn_finalize_from_gram (statistics + finalize + weight fold in one launch) against bn_stats_from_gram ->
+    bn_finalize -> weight_fold: bit-identical mean / invstd / scale / shift, running statistics and folded weights
+    (the same float roundings of the same double arithmetic); ragged M, N not a multiple of 16 included."""
+    gen = torch.Generator().manual_seed(M % 89 + C + N)
+    y = _bf(torch.randn(M, C, generator=gen))
+    sc = (0.5 + torch.rand(C, generator=gen)).to(DEV)
+    sh = (torch.randn(C, generator=gen) * 0.3 + 0.2).to(DEV)
+    if C in (64, 128, 256):
+        _, _, _, g64 = ops.bn_apply_gram(y, sc, sh, C, torch.zeros(C, device=DEV), torch.ones(C, device=DEV))
+    else:  # (C = 48: a synthetic centred Gram record -- the row kernel's C % 16 shapes beyond bn_apply_gram's)
+        a = torch.relu(y.float() * sc + sh).double()
+        c = torch.zeros(C, dtype=torch.float64, device=DEV)
+        g64 = torch.cat([(a.t() @ a).flatten(), a.sum(0), c])
+    w32 = (torch.randn(N, C, generator=gen) * (1.0 / C ** 0.5)).to(DEV)
+    w = w32.to(torch.bfloat16)
+    gamma = (1.0 + 0.2 * torch.randn(N, generator=gen)).to(DEV)
+    beta = (0.1 * torch.randn(N, generator=gen)).to(DEV)
+    rm0 = torch.randn(N, generator=gen).to(DEV)
+    rv0 = (0.5 + torch.rand(N, generator=gen)).to(DEV)
+    stats = ops.stats_buffer(N, M, DEV)
+    ops.bn_stats_from_gram(g64, w, M, N, C, stats)
+    ref = [torch.empty(N, device=DEV) for _ in range(4)]
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    ops.bn_finalize(stats, stats.shape[1], M, N, gamma, beta, *ref, rm1 if upd else None, rv1 if upd else None,
+                    0.1, 1e-5)
+    wf_ref = ops.weight_fold(w32, ref[2], torch.bfloat16) if fold else None
+    out = [torch.full((N,), float("nan"), device=DEV) for _ in range(4)]
+    rm2, rv2 = rm0.clone(), rv0.clone()
+    wf = torch.empty((N, C), dtype=torch.bfloat16, device=DEV) if fold else None
+    ops.bn_finalize_from_gram(g64, w, M, N, C, gamma, beta, *out, rm2 if upd else None, rv2 if upd else None, 0.1,
+                              1e-5, w32 if fold else None, wf)
+    torch.cuda.synchronize()
+    for r, o in zip(ref, out):
+        assert torch.equal(r, o)
+    assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
+    if not upd:
+        assert torch.equal(rm2, rm0) and torch.equal(rv2, rv0)
+    if fold:
+        assert torch.equal(wf_ref, wf)

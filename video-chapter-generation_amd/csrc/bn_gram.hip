@@ -372,9 +372,21 @@ __global__ __launch_bounds__(256) void gram_stats_kernel(const double* __restric
 // are coalesced; the old form read one strided row per thread), 16 output columns per workgroup share each load,
 // and the per-column sums over k are combined by a fixed-order tree (deterministic).
 constexpr int GS_Q = 16;
+// With fin (vcg_bn_finalize_from_gram): also bn_finalize's outputs for the one-slot statistics (the same float
+// rounding of (mean, M2) and the same double arithmetic, so the values equal the separate finalize's) and the bn3 GEMM
+// pass's folded weights bf16(w32 row n x scale n) (vcg_weight_fold's values) -- two launches fewer on the forward's
+// critical path.
+struct GramFin {
+  const float *gamma, *beta;
+  float *mean, *invstd, *scale, *shift, *rmean, *rvar;
+  float momentum, eps;
+  const float* w32;  // master conv weight [N][C] f32 (nullptr: no fold)
+  bf16_t* wfold;     // [N][C]
+};
+
 __global__ __launch_bounds__(256) void gram_stats_rows_kernel(const double* __restrict__ g64, const bf16_t* __restrict__ w,
                                                              long long M, int N, int C, float2* __restrict__ stats,
-                                                             int mtiles) {
+                                                             int mtiles, GramFin fin, int has_fin) {
   const double* __restrict__ gram = g64;
   const double* __restrict__ dsum = g64 + (long long)C * C;
   const double* __restrict__ ctr = dsum + C;
@@ -425,11 +437,40 @@ __global__ __launch_bounds__(256) void gram_stats_rows_kernel(const double* __re
     }
     __syncthreads();
   }
-  if (k < GS_Q && n0 + k < N)
-    stats[(long long)(n0 + k) * mtiles] = make_float2((float)red[0][k][0], (float)(fmax(red[1][k][0], 0.0) * (double)M));
-  if (blockIdx.x == 0 && k == 0) {
+  __shared__ float fscale[GS_Q];
+  if (k < GS_Q && n0 + k < N) {
+    const float mf = (float)red[0][k][0], m2f = (float)(fmax(red[1][k][0], 0.0) * (double)M);
+    if (stats) stats[(long long)(n0 + k) * mtiles] = make_float2(mf, m2f);
+    if (has_fin) {  // bn_finalize_kernel's arithmetic for one slot of (float) M rows
+      const int c = n0 + k;
+      const double Nn = (double)(float)M, mu = (double)mf;
+      const double var = (double)m2f / Nn;
+      const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
+      const float g = fin.gamma ? fin.gamma[c] : 1.f, b = fin.beta ? fin.beta[c] : 0.f;
+      if (fin.mean) fin.mean[c] = (float)mu;
+      if (fin.invstd) fin.invstd[c] = invstd;
+      fin.scale[c] = g * invstd;
+      fin.shift[c] = b - (float)mu * g * invstd;
+      fscale[k] = g * invstd;
+      if (fin.rmean) {
+        const double unbiased = Nn > 1 ? (double)m2f / (Nn - 1) : var;
+        fin.rmean[c] = (float)((1.0 - fin.momentum) * fin.rmean[c] + fin.momentum * mu);
+        fin.rvar[c] = (float)((1.0 - fin.momentum) * fin.rvar[c] + fin.momentum * unbiased);
+      }
+    }
+  }
+  if (stats && blockIdx.x == 0 && k == 0) {
     float2* cnt = stats + (long long)N * mtiles;
     cnt[0] = make_float2((float)M, 1.f);  // one used slot (bn_finalize reads cnt[0].y slots)
+  }
+  if (has_fin && fin.w32) {  // the folded rows of this workgroup's columns
+    __syncthreads();
+    const int rows = min(GS_Q, N - n0);
+    for (int i = k; i < rows * C; i += 256) {
+      const int q = i / C;
+      const long long o = (long long)(n0 + q) * C + (i - q * C);
+      fin.wfold[o] = f2bf(fin.w32[o] * fscale[q]);
+    }
   }
 }
 
@@ -492,10 +533,29 @@ VCG_API int vcg_bn_stats_from_gram(const double* g64, const void* w, long long M
   VCG_REQUIRE(C > 0 && C <= 1024 && N > 0 && M > 0 && mtiles > 0, "bad shape");
   if (C <= 256 && C % 16 == 0)
     hipLaunchKernelGGL(gram_stats_rows_kernel, dim3((N + GS_Q - 1) / GS_Q), dim3(256), 0, s, g64, (const bf16_t*)w, M,
-                       N, C, reinterpret_cast<float2*>(stats), mtiles);
+                       N, C, reinterpret_cast<float2*>(stats), mtiles, GramFin{}, 0);
   else
     hipLaunchKernelGGL(gram_stats_kernel, dim3((N + 7) / 8), dim3(256), 0, s, g64, (const bf16_t*)w, M, N, C,
                        reinterpret_cast<float2*>(stats), mtiles);
+  VCG_LAUNCH_CHECK();
+  return VCG_OK;
+}
+
+// vcg_bn_stats_from_gram + vcg_bn_finalize (one slot of M rows; running statistics updated when rmean / rvar are
+// given) + vcg_weight_fold of the conv's f32 master weight w32 [N][C] by the new scale into wfold (bf16; both
+// optional) in one launch: the same values as the three calls. C <= 256, C % 16 == 0.
+VCG_API int vcg_bn_finalize_from_gram(const double* g64, const void* w, long long M, int N, int C, const float* gamma,
+                                      const float* beta, float* mean, float* invstd, float* scale, float* shift,
+                                      float* running_mean, float* running_var, float momentum, float eps,
+                                      const float* w32, void* wfold, hipStream_t s) {
+  VCG_REQUIRE(g64 && w && scale && shift, "null argument");
+  VCG_REQUIRE(C > 0 && C <= 256 && C % 16 == 0 && N > 0 && M > 0, "C must be a multiple of 16, <= 256");
+  VCG_REQUIRE(!running_mean == !running_var, "running_mean and running_var together");
+  VCG_REQUIRE(!w32 == !wfold, "w32 and wfold together");
+  GramFin f{gamma, beta, mean, invstd, scale, shift, running_mean, running_var, momentum, eps, w32,
+            (bf16_t*)wfold};
+  hipLaunchKernelGGL(gram_stats_rows_kernel, dim3((N + GS_Q - 1) / GS_Q), dim3(256), 0, s, g64, (const bf16_t*)w, M,
+                     N, C, (float2*)nullptr, 1, f, 1);
   VCG_LAUNCH_CHECK();
   return VCG_OK;
 }

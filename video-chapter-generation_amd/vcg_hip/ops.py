@@ -220,6 +220,21 @@ def bn_stats_from_gram(g64, w, M, N, C, stats):
     return stats
 
 
+def bn_finalize_from_gram(g64, w, M, N, C, gamma, beta, mean, invstd, scale, shift, running_mean=None,
+                          running_var=None, momentum=0.1, eps=1e-5, w32=None, wfold=None):
+    """bn_stats_from_gram + bn_finalize (+ weight_fold of the f32 master weight w32 [N, C] by the new scale into wfold,
+    bf16) in one launch (vcg_bn_finalize_from_gram; the same values as the three calls). C <= 256, C % 16 == 0."""
+    _chk(w, torch.bfloat16, "w")
+    _chk(g64, torch.float64, "g64")
+    assert g64.numel() == C * C + 2 * C and C <= 256 and C % 16 == 0
+    if w32 is not None:
+        _chk(w32, torch.float32, "w32")
+        _chk(wfold, torch.bfloat16, "wfold")
+        assert w32.numel() == N * C and wfold.numel() == N * C
+    _lib.call("vcg_bn_finalize_from_gram", P(g64), P(w), M, N, C, P(gamma), P(beta), P(mean), P(invstd), P(scale),
+              P(shift), P(running_mean), P(running_var), float(momentum), float(eps), P(w32), P(wfold), stream())
+
+
 def conv1x1_stats(x, w, stats, M, N, K):
     """BatchNorm statistics of x [M, K] @ w [N, K]^T without storing the product (vcg_conv1x1_stats). False where
     the fused engine does not apply."""

@@ -149,6 +149,9 @@ class ResNetTrunk:
     # a y3-drop block's P = g^T a2 formed by the next block's streaming conv1 dgrad (layers 1-2); False: the weight-
     # gradient GEMM (tests compare both)
     dgrad_p = os.environ.get("VCG_DGRAD_P", "1") != "0"
+    # bn3's statistics, finalize and the GEMM pass's folded weight as one launch (ops.bn_finalize_from_gram) where the
+    # Gram statistics apply; False: bn_stats_from_gram + bn_finalize + weight_fold (tests compare both)
+    gram_fin = os.environ.get("VCG_GRAM_FIN", "1") != "0"
 
     def __init__(self, net, dtype):
         self.net = net
@@ -223,15 +226,25 @@ class ResNetTrunk:
         ops.bn_finalize(stats, mt, M, Cout, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
                         bn.running_mean if upd else None, bn.running_var if upd else None, mom, bn.eps)
 
-    def _bn_from_gram(self, conv, bn, g64, M, C):
+    def _bn_from_gram(self, conv, bn, g64, M, C, fold=False):
         """BN state of conv's (1x1) output from its input's Gram matrix and column sums (ops.bn_stats_from_gram:
-        y = x w^T is linear, so its batch mean / variance follow from x^T x and colsum(x) -- no pass over x or y)."""
+        y = x w^T is linear, so its batch mean / variance follow from x^T x and colsum(x) -- no pass over x or y).
+        fold: also the conv weight folded by the new scale (bf16 [Cout, C], for conv1x1_bn_res_relu), else None."""
         Cout = conv.out_channels
         st = BNState(Cout, g64.device, bn_mode(bn), M, bn)
+        w = self._wprep(conv, C).view(Cout, C)
+        if ResNetTrunk.gram_fin and C <= 256 and C % 16 == 0:
+            upd = st.mode == "train"
+            w32 = conv.weight.data.view(Cout, C) if fold else None
+            wf = torch.empty((Cout, C), dtype=torch.bfloat16, device=g64.device) if fold else None
+            ops.bn_finalize_from_gram(g64, w, M, Cout, C, bn.weight, bn.bias, st.mean, st.invstd, st.scale, st.shift,
+                                      bn.running_mean if upd else None, bn.running_var if upd else None,
+                                      bn.momentum if bn.momentum is not None else 0.1, bn.eps, w32, wf)
+            return st, wf
         stats = ops.stats_buffer(Cout, M, g64.device)
-        ops.bn_stats_from_gram(g64, self._wprep(conv, C).view(Cout, C), M, Cout, C, stats)
+        ops.bn_stats_from_gram(g64, w, M, Cout, C, stats)
         self._finalize(stats, stats.shape[1], M, Cout, bn, st)
-        return st
+        return st, None
 
     # ---------------------------------------------------------------- forward
     def forward(self, x, need_grad):
@@ -315,8 +328,12 @@ class ResNetTrunk:
             a2, a2sum = ops.bn_apply_colsum(y2, b2.scale, b2.shift, planes)
         else:
             a2 = ops.bn_apply(y2, b2.scale, b2.shift, planes, relu=True)
+        wf = None
         if drop and a2gram is not None:
-            y3, b3 = None, self._bn_from_gram(blk.conv3, blk.bn3, g64, N * H2 * W2, planes)
+            # (a y3-drop block always takes the GEMM pass below: downsample-free, stride 1, batch statistics)
+            b3, wf = self._bn_from_gram(blk.conv3, blk.bn3, g64, N * H2 * W2, planes,
+                                        fold=self.dtype == torch.bfloat16 and C3 <= ResNetTrunk.bn3_gemm_max_c3)
+            y3 = None
         else:
             y3, b3, _, _ = self._conv_bn(a2, blk.conv3, blk.bn3, N, H2, W2, planes, store=not drop)
         if not fold_a2:  # (the backward's a2-form fold reads these only where it applies)
@@ -335,7 +352,8 @@ class ResNetTrunk:
             if (self.dtype == torch.bfloat16 and C3 <= ResNetTrunk.bn3_gemm_max_c3
                     and b3.mode != "running" and blk.conv3.stride[0] == 1):
                 M = N * H2 * W2
-                wf = ops.weight_fold(blk.conv3.weight.data.view(C3, planes), b3.scale, self.dtype)
+                if wf is None:
+                    wf = ops.weight_fold(blk.conv3.weight.data.view(C3, planes), b3.scale, self.dtype)
                 r2 = ops.conv1x1_bn_res_relu(a2.view(M, planes), wf, b3.shift, x, M, C3, planes)
             if r2 is not None:
                 out, obits = r2
