@@ -26,6 +26,7 @@ def timeit(fn, iters=20):
 
 def main():
     dt, dev = torch.bfloat16, "cuda"
+    print("torch blas:", torch.backends.cuda.preferred_blas_library(), flush=True)
     R, H, I = 8192, 768, 3072
     x = torch.randn(R, H, device=dev).to(dt)
     xi = torch.randn(R, I, device=dev).to(dt)
@@ -36,6 +37,9 @@ def main():
         fl = 2.0 * R * N * K
         t = timeit(lambda: ops.gemm(A, W, R, N, K, K, K, bias=b))
         line = [f"{name:9s} fwd {t:7.1f}us {fl / t / 1e6:6.0f}TF/s"]
+        # (the vendor library on the same shape, for the headroom estimate only -- never on the product path)
+        t = timeit(lambda: torch.matmul(A, W.t()))
+        line.append(f"[hipBLASLt {t:7.1f}us {fl / t / 1e6:6.0f}TF/s]")
         if name == "ffn1":
             pre = torch.empty(R, N, dtype=dt, device=dev)
             t = timeit(lambda: ops.gemm(A, W, R, N, K, K, K, bias=b, act=ops.ACT_GELU, aux=pre))
@@ -59,6 +63,10 @@ def main():
             line.append(f"dX (W^T resident)+gelu' {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
         t = timeit(lambda: ops.gemm(dY, ops.transpose(W), R, K, N, N, N))
         line.append(f"dX W^T {t:7.1f}us {fl / t / 1e6:6.0f}TF/s")
+        t = timeit(lambda: torch.matmul(dY, W))
+        line.append(f"[lib dX {t:7.1f}us {fl / t / 1e6:6.0f}TF/s]")
+        t = timeit(lambda: torch.matmul(dY.t(), A))
+        line.append(f"[lib dW {t:7.1f}us {fl / t / 1e6:6.0f}TF/s]")
         t = timeit(lambda: ops.transpose(W))
         line.append(f"(transpose {t:5.1f}us)")
         gW = torch.zeros(N, K, device=dev)

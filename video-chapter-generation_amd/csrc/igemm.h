@@ -297,6 +297,13 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
 int fast_grid_rows(int M, int N, int z, int epi);
 bool fast_bwd_streams(const GemmParams& p);  // a dense EPI_BWD GEMM runs on the streaming kernel (P product: only there)
+// blaslt.hip: hipBLASLt for the plain bf16 GEMMs (VCG_OK, or VCG_ERR_UNSUPPORTED: no algorithm, run the engine)
+bool lt_gemm_enabled();
+int lt_gemm(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B, long long ldb,
+            const void* C, long long ldc, void* D, long long ldd, int d_f32, const float* bias, float beta,
+            hipStream_t stream);
+int lt_gemm_gelu(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
+                 long long ldb, const float* bias, void* pre, void* out, long long ld, int fast, hipStream_t stream);
 int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an EPI_BWD launch of run_fast_gemm
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
                            float* dgamma, float* dbeta, int accumulate, hipStream_t s);  // grid rows (slots of EPI_BWD partials) of a fast-kernel launch

@@ -1505,6 +1505,31 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
   p.C = C; p.ldc = ldc; p.bias = bias; p.act = act & 0xff; p.residual = residual; p.ldr = ldr; p.aux = aux;
   p.res_round = (act & ACT_FLAG_ROUND_PRE) != 0 && residual != nullptr;
   p.alpha = alpha;
+  // BERT's FFN1 (GELU with the pre-activation kept): the library GEMM into the pre-activation + a GELU pass
+  // (88 -> 44 + ~20 us at B = 64, tools/bench_bert_gemm.py; VCG_LT_GELU_OFF=1: the fused engine epilogue)
+  if (dtype == VCG_BF16 && act == ACT_GELU && aux != nullptr && residual == nullptr && alpha == 1.f &&
+      lt_gemm_enabled() && !getenv_flag("VCG_LT_GELU_OFF") && (long long)M * N * K >= (1LL << 31)) {
+    const int rc = lt_gemm_gelu(transA, transB, M, N, K, A, lda, B, ldb, bias, aux, C, ldc, fast_gelu_enabled() ? 1 : 0,
+                                stream);
+    if (rc == VCG_OK)
+      if (FILE* f = gemm_log()) {
+        fprintf(f, "lt M=%d N=%d K=%d gelu\n", M, N, K);
+        fflush(f);
+      }
+    if (rc != VCG_ERR_UNSUPPORTED) return rc;
+  }
+  // BERT's bias-only / addend-only GEMMs: the vendor library where it has an algorithm (blaslt.hip)
+  if (dtype == VCG_BF16 && act == 0 && aux == nullptr && alpha == 1.f && lt_gemm_enabled() &&
+      (long long)M * N * K >= (1LL << 31) && (residual == nullptr || residual != C)) {
+    const int rc = lt_gemm(transA, transB, M, N, K, A, lda, B, ldb, residual, ldr, C, ldc, 0, bias,
+                           residual ? 1.f : 0.f, stream);
+    if (rc == VCG_OK)
+      if (FILE* f = gemm_log()) {
+        fprintf(f, "lt M=%d N=%d K=%d\n", M, N, K);
+        fflush(f);
+      }
+    if (rc != VCG_ERR_UNSUPPORTED) return rc;
+  }
 #define VCG_GEMM_CASE(TT)                                                                   \
   if (!transA && !transB) return run_gemm<TT, OP_DENSE_K, OP_DENSE_K>(p, EPI_STORE, 1, stream);   \
   if (!transA && transB) return run_gemm<TT, OP_DENSE_K, OP_DENSE_MN>(p, EPI_STORE, 1, stream);   \
@@ -1530,6 +1555,18 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
   int kps = (K + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
   splits = (K + kps - 1) / kps;
+  // (the library's weight gradients measured slower than the wgrad engine on 3 of BERT's 4 shapes, 50 vs 33 us at
+  // 768 x 768: opt-in only, VCG_LT_DW=1)
+  if (dtype == VCG_BF16 && transA && transB && lt_gemm_enabled() && getenv_flag("VCG_LT_DW") &&
+      (long long)M * N * K >= (1LL << 31)) {
+    const int rc = lt_gemm(1, 1, M, N, K, A, lda, B, ldb, out, N, out, N, 1, nullptr, accumulate ? 1.f : 0.f, stream);
+    if (rc == VCG_OK)
+      if (FILE* f = gemm_log()) {
+        fprintf(f, "lt M=%d N=%d K=%d dW\n", M, N, K);
+        fflush(f);
+      }
+    if (rc != VCG_ERR_UNSUPPORTED) return rc;
+  }
   GemmParams p{};
   p.M = M; p.N = N; p.K = K; p.k_per_split = kps;
   p.a = dense_op(A, lda, M);

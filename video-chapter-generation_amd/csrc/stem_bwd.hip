@@ -89,6 +89,7 @@ constexpr int SB_PI = (9 * (SB_MAXW + 4) * 16 + 1023) / 1024;  // patch DMA inst
 constexpr int SB_PB = SB_PI * 1024;
 constexpr int SB_SLOT = SB_YB + SB_DB + SB_IB + SB_PB;         // 66 KiB
 
+template <int DBG>
 __global__ __launch_bounds__(SB_NTH) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void stem_bwd_fused_kernel(StemBwdArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[SB_SLOT];
@@ -260,8 +261,10 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     sb_lgkm0();
     __builtin_amdgcn_s_barrier();
-    if (tid < nitems) produce(lt, S, tid >> 3);
-    if (tid + SB_NTH < nitems) produce(lt, S, (tid + SB_NTH) >> 3);
+    if (DBG != 2) {
+      if (tid < nitems) produce(lt, S, tid >> 3);
+      if (tid + SB_NTH < nitems) produce(lt, S, (tid + SB_NTH) >> 3);
+    }
     sb_lgkm0();
     __builtin_amdgcn_s_barrier();
     const bf16_t* dyT = reinterpret_cast<const bf16_t*>(S);
@@ -299,7 +302,8 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
       }
       __builtin_amdgcn_sched_barrier(0);
     };
-    for (int s = 0; s < ksteps; ++s) step(s, 0);
+    if (DBG != 1)
+      for (int s = 0; s < ksteps; ++s) step(s, 0);
     // every wave's reads of the slot have returned before the next tile's DMA refills it
     sb_lgkm0();
     __builtin_amdgcn_s_barrier();
@@ -397,7 +401,10 @@ VCG_API int vcg_stem_bwd_fused(const void* dy, const unsigned char* idx, const v
   a.sum_gx = sum_gx; a.inv_count = 1.f / (float)count; a.train = train_stats; a.ws = ws;
   a.N = N; a.H = H; a.W = W; a.OH = (H - 1) / 2 + 1; a.OW = (W - 1) / 2 + 1; a.tiles = N * (H / 2);
   const int grid = a.tiles < SB_GRID ? a.tiles : SB_GRID;
-  hipLaunchKernelGGL(stem_bwd_fused_kernel, dim3(grid), dim3(SB_NTH), 0, s, a);
+  static const int dbg = getenv("VCG_STEM_BWD_DBG") ? atoi(getenv("VCG_STEM_BWD_DBG")) : 0;  // timing breakdown only
+  if (dbg == 1) hipLaunchKernelGGL(stem_bwd_fused_kernel<1>, dim3(grid), dim3(SB_NTH), 0, s, a);
+  else if (dbg == 2) hipLaunchKernelGGL(stem_bwd_fused_kernel<2>, dim3(grid), dim3(SB_NTH), 0, s, a);
+  else hipLaunchKernelGGL(stem_bwd_fused_kernel<0>, dim3(grid), dim3(SB_NTH), 0, s, a);
   VCG_LAUNCH_CHECK();
   hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(64 * SB_N / 4 / SR_Q), dim3(256), 0, s, ws, grid, dw, accumulate);
   VCG_LAUNCH_CHECK();
