@@ -30,6 +30,13 @@ enum { VCG_ACT_NONE = 0, VCG_ACT_RELU = 1, VCG_ACT_GELU = 2, VCG_ACT_TANH = 3, V
    unfolded conv3 -> bn3 path stores y3 in bf16; the scoring forward's folded conv3 sets it to match). Without it the
    residual is added to the f32 accumulator value. */
 enum { VCG_ACT_FLAG_ROUND_PRE = 0x100 };
+/* vcg_gemm act flag: the caller allows the vendor library (hipBLASLt) for this GEMM -- BERT's Linear layers and the
+   trunk's stride-2 downsample input gradient (a plain GEMM over the output pixels) set it.
+   Taken for bf16 GEMMs of >= 2^31 MACs with alpha = 1 that carry only a bias (act NONE), a residual addend (act
+   NONE, residual != C), or a bias + GELU with the pre-activation (aux: the library writes the rounded pre-activation,
+   a GELU pass the output); every other GEMM, and every GEMM without the flag, runs on the hand-written engine.
+   VCG_LT_GEMM=0 in the environment turns the library off. */
+enum { VCG_ACT_FLAG_LIB = 0x200 };
 
 /* ---- library ---------------------------------------------------------------------------- */
 VCG_API const char* vcg_last_error(void);

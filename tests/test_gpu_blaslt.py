@@ -14,6 +14,7 @@ from vcg_hip import _lib, ops
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 R, H, I = 8192, 768, 3072
+LIB = ops.ACT_FLAG_LIB
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -44,12 +45,12 @@ def test_forward_bias(monkeypatch, N, K):
     gen = torch.Generator().manual_seed(N + K)
     A, W = _bf((R, K), gen), _bf((N, K), gen, 0.02)
     b = (torch.randn(N, generator=gen) * 0.1).to(DEV)
-    lt, eng = _both(monkeypatch, lambda: ops.gemm(A, W, R, N, K, K, K, bias=b))
+    lt, eng = _both(monkeypatch, lambda: ops.gemm(A, W, R, N, K, K, K, bias=b, act=LIB))
     ref = A.double() @ W.double().t() + b.double()
     e_lt, e_eng = _rel(lt, ref), _rel(eng, ref)
     print(f"fwd N={N} K={K}: lib {e_lt:.2e} engine {e_eng:.2e}")
     assert e_lt < 1.5 * e_eng + 4e-3
-    again = ops.gemm(A, W, R, N, K, K, K, bias=b)
+    again = ops.gemm(A, W, R, N, K, K, K, bias=b, act=LIB)
     torch.cuda.synchronize()
     assert torch.equal(lt, again)
 
@@ -64,9 +65,9 @@ def test_input_gradient(monkeypatch, N, K, res, wt):
     r = _bf((R, N), gen, 0.01) if res else None
     Wt = W.t().contiguous()
     if wt:
-        fn = lambda: ops.gemm(dY, Wt, R, N, K, K, K, residual=r, ldr=N)  # noqa: E731
+        fn = lambda: ops.gemm(dY, Wt, R, N, K, K, K, residual=r, ldr=N, act=LIB)  # noqa: E731
     else:
-        fn = lambda: ops.gemm(dY, W, R, N, K, K, N, transB=True, residual=r, ldr=N)  # noqa: E731
+        fn = lambda: ops.gemm(dY, W, R, N, K, K, N, transB=True, residual=r, ldr=N, act=LIB)  # noqa: E731
     lt, eng = _both(monkeypatch, fn)
     ref = dY.double() @ W.double() + (r.double() if res else 0.0)
     e_lt, e_eng = _rel(lt, ref), _rel(eng, ref)
@@ -77,7 +78,6 @@ def test_input_gradient(monkeypatch, N, K, res, wt):
 @pytest.mark.parametrize("M,N,acc", [(H, I, True), (I, H, False), (3 * H, H, True), (H, H, True)])
 def test_weight_gradient(monkeypatch, M, N, acc):
     """gW [M, N] (+)= dY^T [M, R] @ X [R, N] into fp32 (gemm_splitk, transA / transB)."""
-    monkeypatch.setenv("VCG_LT_DW", "1")  # (opt-in: slower than the wgrad engine on 3 of the 4 shapes)
     gen = torch.Generator().manual_seed(M + 7 * N)
     dY, X = _bf((R, M), gen, 0.05), _bf((R, N), gen)
     g0 = torch.randn(M, N, generator=gen).to(DEV) * 0.1
@@ -100,14 +100,14 @@ def test_small_and_fused_stay_on_engine(monkeypatch):
     gen = torch.Generator().manual_seed(5)
     A, W = _bf((64, H), gen), _bf((H, H), gen, 0.02)
     b = torch.randn(H, generator=gen).to(DEV) * 0.1
-    lt, eng = _both(monkeypatch, lambda: ops.gemm(A, W, 64, H, H, H, H, bias=b, act=ops.ACT_TANH))
+    lt, eng = _both(monkeypatch, lambda: ops.gemm(A, W, 64, H, H, H, H, bias=b, act=ops.ACT_TANH | LIB))
     assert torch.equal(lt, eng)
     A2, W2 = _bf((R, H), gen), _bf((I, H), gen, 0.02)
     b2 = torch.randn(I, generator=gen).to(DEV) * 0.1
 
     def ffn1():
         p = torch.empty((R, I), dtype=torch.bfloat16, device=DEV)
-        o = ops.gemm(A2, W2, R, I, H, H, H, bias=b2, act=ops.ACT_GELU, aux=p)
+        o = ops.gemm(A2, W2, R, I, H, H, H, bias=b2, act=ops.ACT_GELU | LIB, aux=p)
         return torch.cat([o, p])
     monkeypatch.setenv("VCG_LT_GELU_OFF", "1")
     lt, eng = _both(monkeypatch, ffn1)
@@ -125,7 +125,7 @@ def test_ffn1_gelu_library_plus_pass(monkeypatch):
 
     def ffn1():
         p = torch.empty((R, I), dtype=torch.bfloat16, device=DEV)
-        o = ops.gemm(A, W, R, I, H, H, H, bias=b, act=ops.ACT_GELU, aux=p)
+        o = ops.gemm(A, W, R, I, H, H, H, bias=b, act=ops.ACT_GELU | LIB, aux=p)
         return o, p
     (o_lt, p_lt), (o_en, p_en) = _both(monkeypatch, ffn1)
     ref = A.double() @ W.double().t() + b.double()
@@ -138,3 +138,13 @@ def test_ffn1_gelu_library_plus_pass(monkeypatch):
     o2, p2 = ffn1()
     torch.cuda.synchronize()
     assert torch.equal(o2, o_lt) and torch.equal(p2, p_lt)
+
+
+def test_without_flag_stays_on_engine(monkeypatch):
+    """A GEMM without ops.ACT_FLAG_LIB (every trunk GEMM) runs on the engine whatever its shape: bit-identical with
+    the library on and off."""
+    gen = torch.Generator().manual_seed(7)
+    A, W = _bf((R, H), gen), _bf((I, H), gen, 0.02)
+    b = torch.randn(I, generator=gen).to(DEV) * 0.1
+    lt, eng = _both(monkeypatch, lambda: ops.gemm(A, W, R, I, H, H, H, bias=b))
+    assert torch.equal(lt, eng)

@@ -1,11 +1,12 @@
 """Join a VCG_GEMM_LOG dispatch log with a rocprofv3 kernel_trace.csv (igemm launches pair up in
-order) and print time per GEMM shape. usage: gemm_breakdown.py LOG TRACE_CSV [n_steps]"""
+order; "lt ..." lines are the hipBLASLt GEMMs, one Cijk_* kernel each) and print time per GEMM shape.
+usage: gemm_breakdown.py LOG TRACE_CSV [n_steps]"""
 import collections
 import csv
 import sys
 
 log = [l.strip() for l in open(sys.argv[1]) if l.strip()]
-rows = [r for r in csv.DictReader(open(sys.argv[2])) if any(k in r["Kernel_Name"] for k in ("igemm", "gemm256", "wgrad_fast", "wgrad3x3_patch", "conv3x3_patch", "stem_patch", "rs1x1"))]
+rows = [r for r in csv.DictReader(open(sys.argv[2])) if any(k in r["Kernel_Name"] for k in ("igemm", "gemm256", "wgrad_fast", "wgrad3x3_patch", "conv3x3_patch", "stem_patch", "rs1x1", "Cijk_"))]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 steps = float(sys.argv[3]) if len(sys.argv) > 3 else 3.0
 if len(log) != len(rows):
@@ -19,8 +20,8 @@ for l, r in zip(log, rows):
 tot = sum(v[1] for v in agg.values())
 print(f"igemm total {tot / steps / 1e3:.2f} ms/step")
 for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: int(sys.argv[4]) if len(sys.argv) > 4 else 40]:
-    f = dict(x.split("=") for x in k.split())
+    f = dict(x.split("=") for x in k.split() if "=" in x)
     M, N, K = int(f["M"]), int(f["N"]), int(f["K"])
-    z = int(f["z"])
+    z = int(f.get("z", 1))
     fl = 2.0 * M * N * K * (z if f.get("epi") != "2" else 1)
     print(f"{us / steps / 1e3:7.2f} ms/step  n={n / steps:4.1f} avg={us / n:8.1f}us  {fl / (us / n) / 1e6:6.1f}TF/s  {k}")

@@ -16,6 +16,7 @@ enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 
        EPI_BWD_STREAM = 6 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
 enum { ACT_FLAG_ROUND_PRE = 0x100 };  // = VCG_ACT_FLAG_ROUND_PRE (include/vcg_hip.h)
+enum { ACT_FLAG_LIB = 0x200 };        // = VCG_ACT_FLAG_LIB: the vendor library may run this GEMM (blaslt.hip)
 
 template <typename T> struct Cfg;
 template <> struct Cfg<float> { static constexpr int VEC = 4, BK = 16, LDK = 20; };   // 80-B rows

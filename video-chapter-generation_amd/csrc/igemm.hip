@@ -1501,14 +1501,16 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
   p.b = transB ? dense_op(B, ldb, K, N, esz) : dense_op(B, ldb, N, K, esz);
   p.a.rows = M;
   p.b.rows = N;
-  VCG_REQUIRE((act & ~(0xff | ACT_FLAG_ROUND_PRE)) == 0, "unknown act flags");
+  VCG_REQUIRE((act & ~(0xff | ACT_FLAG_ROUND_PRE | ACT_FLAG_LIB)) == 0, "unknown act flags");
+  const bool lib = (act & ACT_FLAG_LIB) != 0 && dtype == VCG_BF16 && alpha == 1.f && lt_gemm_enabled() &&
+                   (long long)M * N * K >= (1LL << 31);
+  act &= ~ACT_FLAG_LIB;
   p.C = C; p.ldc = ldc; p.bias = bias; p.act = act & 0xff; p.residual = residual; p.ldr = ldr; p.aux = aux;
   p.res_round = (act & ACT_FLAG_ROUND_PRE) != 0 && residual != nullptr;
   p.alpha = alpha;
   // BERT's FFN1 (GELU with the pre-activation kept): the library GEMM into the pre-activation + a GELU pass
   // (88 -> 44 + ~20 us at B = 64, tools/bench_bert_gemm.py; VCG_LT_GELU_OFF=1: the fused engine epilogue)
-  if (dtype == VCG_BF16 && act == ACT_GELU && aux != nullptr && residual == nullptr && alpha == 1.f &&
-      lt_gemm_enabled() && !getenv_flag("VCG_LT_GELU_OFF") && (long long)M * N * K >= (1LL << 31)) {
+  if (lib && act == ACT_GELU && aux != nullptr && residual == nullptr && !getenv_flag("VCG_LT_GELU_OFF")) {
     const int rc = lt_gemm_gelu(transA, transB, M, N, K, A, lda, B, ldb, bias, aux, C, ldc, fast_gelu_enabled() ? 1 : 0,
                                 stream);
     if (rc == VCG_OK)
@@ -1519,8 +1521,7 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
     if (rc != VCG_ERR_UNSUPPORTED) return rc;
   }
   // BERT's bias-only / addend-only GEMMs: the vendor library where it has an algorithm (blaslt.hip)
-  if (dtype == VCG_BF16 && act == 0 && aux == nullptr && alpha == 1.f && lt_gemm_enabled() &&
-      (long long)M * N * K >= (1LL << 31) && (residual == nullptr || residual != C)) {
+  if (lib && act == 0 && aux == nullptr && (residual == nullptr || residual != C)) {
     const int rc = lt_gemm(transA, transB, M, N, K, A, lda, B, ldb, residual, ldr, C, ldc, 0, bias,
                            residual ? 1.f : 0.f, stream);
     if (rc == VCG_OK)
@@ -1540,6 +1541,11 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
 #undef VCG_GEMM_CASE
 }
 
+static bool lt_dw_off() {
+  const char* e = getenv("VCG_LT_DW");
+  return e != nullptr && e[0] == '0';
+}
+
 VCG_API long long vcg_gemm_splitk_ws_bytes(int dtype, int M, int N, int K) {
   const int splits = choose_splits(M, N, K, dtype == VCG_BF16 ? 32 : 16);
   return (long long)splits * M * N * 4;
@@ -1555,9 +1561,10 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
   int kps = (K + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
   splits = (K + kps - 1) / kps;
-  // (the library's weight gradients measured slower than the wgrad engine on 3 of BERT's 4 shapes, 50 vs 33 us at
-  // 768 x 768: opt-in only, VCG_LT_DW=1)
-  if (dtype == VCG_BF16 && transA && transB && lt_gemm_enabled() && getenv_flag("VCG_LT_DW") &&
+  // (isolated, the library's weight gradients are slower than the wgrad engine on 3 of BERT's 4 shapes -- 50 vs 33
+  // us at 768 x 768 -- but they write no split-K slabs and leave the splitk_reduce pass out: the train step runs
+  // +0.7 % with them, profiles/r05_bert_lt_ab.txt; VCG_LT_DW=0: the engine)
+  if (dtype == VCG_BF16 && transA && transB && lt_gemm_enabled() && !lt_dw_off() &&
       (long long)M * N * K >= (1LL << 31)) {
     const int rc = lt_gemm(1, 1, M, N, K, A, lda, B, ldb, out, N, out, N, 1, nullptr, accumulate ? 1.f : 0.f, stream);
     if (rc == VCG_OK)

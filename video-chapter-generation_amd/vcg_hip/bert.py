@@ -16,6 +16,10 @@ import torch
 from . import ops
 
 
+# BERT's Linear GEMMs may run on the vendor library (ops.ACT_FLAG_LIB: bias-only / addend-only bf16 GEMMs and FFN1's
+# GELU, csrc/blaslt.hip); the flag is ignored in fp32 and for GEMMs with a fused epilogue
+LIB = ops.ACT_FLAG_LIB
+
 def _seed(base, layer, site):
     return (base * 0x9E3779B1 + layer * 7919 + site * 104729) & ((1 << 63) - 1)
 
@@ -97,6 +101,7 @@ class BertEncoderEngine:
         LDS-DMA GEMM reads both operands K-contiguous (measured 87 -> 61 us at K = 3072, 67 -> 53 us at
         K = 2304; no gain at K = 768, tools/bench_bert_gemm.py)."""
         # (FFN2's input gradient: the fast engine's staged GELU' epilogue, the pre-activation read as full rows)
+        kw["act"] = kw.get("act", ops.ACT_NONE) | LIB
         wt = self.wt.get(W) if self.wt is not None else None
         if wt is not None:
             return ops.gemm(A, wt, M, N, K, K, K, **kw)
@@ -140,17 +145,17 @@ class BertEncoderEngine:
             bqkv = flat.contiguous_view([sq.bias, sk.bias, sv.bias], (3 * H,), "data")
             qkv_buf = torch.empty((rows + 8, 3 * H), dtype=dt, device=dev)  # +8 rows: padded key reads
             qkv = qkv_buf[:rows]
-            ops.gemm(h, Wqkv, rows, 3 * H, H, H, H, out=qkv, ldc=3 * H, bias=bqkv)
+            ops.gemm(h, Wqkv, rows, 3 * H, H, H, H, out=qkv, ldc=3 * H, bias=bqkv, act=LIB)
             sa = _seed(seed, i + 1, 1)
             ctx, att = attention_fwd(qkv_buf, mask, B, nh, L, Lp, dh, scale, p_a, sa, self._fused_attn(L, dh))
-            ao = ops.gemm(ctx, self._w(at.output.dense.weight), rows, H, H, H, H, bias=at.output.dense.bias)
+            ao = ops.gemm(ctx, self._w(at.output.dense.weight), rows, H, H, H, H, bias=at.output.dense.bias, act=LIB)
             s1 = _seed(seed, i + 1, 2)
             h1, m1, r1 = ops.ln_fwd(ao, h, at.output.LayerNorm.weight, at.output.LayerNorm.bias, rows, H, eps, p_h, s1)
             inter, out = layer.intermediate.dense, layer.output.dense
             I = inter.out_features
             pre = torch.empty((rows, I), dtype=dt, device=dev) if need_grad else None
-            ff = ops.gemm(h1, self._w(inter.weight), rows, I, H, H, H, bias=inter.bias, act=ops.ACT_GELU, aux=pre)
-            fo = ops.gemm(ff, self._w(out.weight), rows, H, I, I, I, bias=out.bias)
+            ff = ops.gemm(h1, self._w(inter.weight), rows, I, H, H, H, bias=inter.bias, act=ops.ACT_GELU | LIB, aux=pre)
+            fo = ops.gemm(ff, self._w(out.weight), rows, H, I, I, I, bias=out.bias, act=LIB)
             s2 = _seed(seed, i + 1, 3)
             h2, m2, r2 = ops.ln_fwd(fo, h1, layer.output.LayerNorm.weight, layer.output.LayerNorm.bias, rows, H, eps,
                                     p_h, s2)

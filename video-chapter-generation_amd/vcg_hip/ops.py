@@ -13,6 +13,7 @@ from . import _lib
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_GELU_BWD = 0, 1, 2, 3, 4
 ACT_FLAG_ROUND_PRE = 0x100  # gemm: round alpha*AB + bias to the storage dtype before the residual (vcg_hip.h)
+ACT_FLAG_LIB = 0x200  # gemm: the vendor library may run it (BERT's Linear layers; vcg_hip.h VCG_ACT_FLAG_LIB)
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 

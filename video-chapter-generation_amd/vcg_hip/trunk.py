@@ -528,7 +528,9 @@ class ResNetTrunk:
             if cds.stride[0] == 2:
                 wt_ds = self._wprep_t(cds, Cin)
                 Mo = dyd.numel() // C3
-                res, res_stride = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3), 2
+                # (a plain GEMM: the vendor library may run it, ops.ACT_FLAG_LIB)
+                res, res_stride = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3,
+                                           act=ops.ACT_FLAG_LIB), 2
             else:
                 res, res_stride = self._dgrad(cds, dyd, N, H, W), 1
             ev = torch.cuda.Event()
@@ -788,7 +790,7 @@ class ResNetTrunk:
                 # output pixels (no 3/4-zero rows), added by the conv1 dgrad epilogue at those rows (res_stride 2)
                 wt_ds = self._wprep_t(cds, Cin)
                 Mo = dyd.numel() // C3
-                res = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3)
+                res = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3, act=ops.ACT_FLAG_LIB)
                 res_stride = 2
             else:
                 res = self._dgrad(cds, dyd, N, H, W)  # the downsample branch's input gradient
