@@ -148,3 +148,30 @@ def test_without_flag_stays_on_engine(monkeypatch):
     b = torch.randn(I, generator=gen).to(DEV) * 0.1
     lt, eng = _both(monkeypatch, lambda: ops.gemm(A, W, R, I, H, H, H, bias=b))
     assert torch.equal(lt, eng)
+
+
+@pytest.mark.parametrize("M,N,K,pad", [(8255, 2304, 768, 64), (9000, 768, 3072, 0), (6400, 3072, 768, 8)])
+def test_ragged_rows_and_pitch(monkeypatch, M, N, K, pad):
+    """Row counts that are not a multiple of any tile (B x L of other batch / sequence sizes) and an output row pitch
+    wider than N (a view into a wider buffer): the library writes exactly the M x N block -- the padding columns keep
+    their sentinel -- within bf16 rounding of float64, with the bias and with a residual of the same pitch."""
+    gen = torch.Generator().manual_seed(M + N + K)
+    A, W = _bf((M, K), gen), _bf((N, K), gen, 0.02)
+    b = (torch.randn(N, generator=gen) * 0.1).to(DEV)
+    ld = N + pad
+    r = _bf((M, ld), gen, 0.01)
+
+    def run(res):
+        buf = torch.full((M, ld), 7.0, dtype=torch.bfloat16, device=DEV)
+        out = buf[:, :N]
+        if res:
+            ops.gemm(A, W, M, N, K, K, K, out=out, ldc=ld, residual=r, ldr=ld, act=LIB)
+        else:
+            ops.gemm(A, W, M, N, K, K, K, out=out, ldc=ld, bias=b, act=LIB)
+        return buf
+    for res in (False, True):
+        lt, eng = _both(monkeypatch, lambda: run(res))
+        ref = A.double() @ W.double().t() + (r[:, :N].double() if res else b.double())
+        assert _rel(lt[:, :N], ref) < 1.5 * _rel(eng[:, :N], ref) + 4e-3
+        if pad:
+            assert (lt[:, N:] == 7.0).all()
