@@ -37,6 +37,14 @@ enum { VCG_ACT_FLAG_ROUND_PRE = 0x100 };
    a GELU pass the output); every other GEMM, and every GEMM without the flag, runs on the hand-written engine.
    VCG_LT_GEMM=0 in the environment turns the library off. */
 enum { VCG_ACT_FLAG_LIB = 0x200 };
+/* Library algorithm check (csrc/blaslt.hip; tools/lt_tune.py, not on the product path): times the hipBLASLt
+   heuristic's candidates (up to 16, its order) for one library GEMM of vcg_gemm's form on the given operands (D
+   written, C read when beta != 0: scratch buffers); us[i] = average microseconds of candidate i, -1 if it failed.
+   Returns the number of candidates. The product path always runs candidate 0 (profiles/r05_lt_tune.txt: the fastest
+   of 16 on 10 of BERT's 11 shapes). */
+VCG_API int vcg_lt_tune(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
+                        long long ldb, const void* C, long long ldc, void* D, long long ldd, int d_f32,
+                        const float* bias, float beta, int reps, float* us, int max_out, hipStream_t stream);
 
 /* ---- library ---------------------------------------------------------------------------- */
 VCG_API const char* vcg_last_error(void);

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <vector>
 
 #include "igemm.h"
 
@@ -30,7 +31,9 @@ struct LtPlan {
   hipblasLtMatmulDesc_t desc = nullptr;
   hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr, ld = nullptr;
   hipblasLtMatmulAlgo_t algo{};
+  std::vector<hipblasLtMatmulAlgo_t> cands;  // the heuristic's candidates in its order; algo = cands[0]
 };
+constexpr int LT_CANDS = 16;
 
 struct LtState {
   std::mutex mu;
@@ -101,16 +104,19 @@ int lt_gemm(int transA, int transB, int M, int N, int K, const void* A, long lon
     if (good) {
       hipblasLtMatmulPreference_t pref = nullptr;
       uint64_t wsb = LT_WS;
-      hipblasLtMatmulHeuristicResult_t res[1];
+      hipblasLtMatmulHeuristicResult_t res[LT_CANDS];
       int n = 0;
       if (hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS &&
           hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)) ==
               HIPBLAS_STATUS_SUCCESS &&
-          hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.la, p.lb, p.lc, p.ld, pref, 1, res, &n) ==
-              HIPBLAS_STATUS_SUCCESS &&
-          n > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS && res[0].workspaceSize <= LT_WS) {
-        p.algo = res[0].algo;
-        p.ok = true;
+          hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.la, p.lb, p.lc, p.ld, pref, LT_CANDS, res, &n) ==
+              HIPBLAS_STATUS_SUCCESS) {
+        for (int i = 0; i < n; ++i)
+          if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= LT_WS) p.cands.push_back(res[i].algo);
+        if (!p.cands.empty()) {
+          p.algo = p.cands[0];
+          p.ok = true;
+        }
       }
       if (pref) hipblasLtMatmulPreferenceDestroy(pref);
     }
@@ -175,3 +181,45 @@ int lt_gemm_gelu(int transA, int transB, int M, int N, int K, const void* A, lon
 }
 
 }  // namespace vcg
+
+using namespace vcg;
+
+// Tuning aid (tools/lt_tune.py; not on the product path): time the heuristic's candidates for one vcg_gemm-shaped
+// library GEMM on the caller's operands, each `reps` times on `stream` (D written, C read when beta != 0: pass scratch
+// buffers). us[i] = average microseconds of candidate i (-1: the candidate failed). Returns the number of candidates.
+VCG_API int vcg_lt_tune(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
+                        long long ldb, const void* C, long long ldc, void* D, long long ldd, int d_f32,
+                        const float* bias, float beta, int reps, float* us, int max_out, hipStream_t stream) {
+  // build (or find) the plan with one real call
+  int rc = lt_gemm(transA, transB, M, N, K, A, lda, B, ldb, C, ldc, D, ldd, d_f32, bias, beta, stream);
+  if (rc != VCG_OK) return rc;
+  LtState& st = lt_state();
+  int dev = 0;
+  VCG_CHECK_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(st.mu);
+  const bool has_c = C != nullptr && beta != 0.f;
+  LtPlan& p = st.plans[std::make_tuple(dev, transA, transB, M, N, K, lda, ldb, has_c ? ldc : 0LL, ldd, d_f32,
+                                       bias != nullptr ? 1 : 0, has_c ? 1 : 0)];
+  void* w = st.ws[{dev, stream}];
+  hipEvent_t e0, e1;
+  VCG_CHECK_HIP(hipEventCreate(&e0));
+  VCG_CHECK_HIP(hipEventCreate(&e1));
+  const int n = (int)p.cands.size() < max_out ? (int)p.cands.size() : max_out;
+  const float alpha = 1.f, b = has_c ? beta : 0.f;
+  for (int i = 0; i < n; ++i) {
+    bool ok = hipblasLtMatmul(st.handle[dev], p.desc, &alpha, B, p.la, A, p.lb, &b, has_c ? C : D, p.lc, D, p.ld,
+                              &p.cands[i], w, LT_WS, stream) == HIPBLAS_STATUS_SUCCESS;  // warm-up
+    VCG_CHECK_HIP(hipEventRecord(e0, stream));
+    for (int r = 0; ok && r < reps; ++r)
+      ok = hipblasLtMatmul(st.handle[dev], p.desc, &alpha, B, p.la, A, p.lb, &b, has_c ? C : D, p.lc, D, p.ld,
+                           &p.cands[i], w, LT_WS, stream) == HIPBLAS_STATUS_SUCCESS;
+    VCG_CHECK_HIP(hipEventRecord(e1, stream));
+    VCG_CHECK_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    VCG_CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
+    us[i] = ok ? ms * 1000.f / reps : -1.f;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return n;
+}
