@@ -1541,6 +1541,14 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
 #undef VCG_GEMM_CASE
 }
 
+// Weight gradients with fewer than this many outputs stay on the split-K engine: at 768 x 768 (BERT's attention
+// output projection) the library took 48 vs 33 us and the step ran +0.5 % with the engine there
+// (profiles/r05_bert_lt_ab.txt; VCG_LT_DW_MIN_MN overrides)
+static long long lt_dw_min_mn() {
+  const char* e = getenv("VCG_LT_DW_MIN_MN");
+  return e ? atoll(e) : (1LL << 20);
+}
+
 static bool lt_dw_off() {
   const char* e = getenv("VCG_LT_DW");
   return e != nullptr && e[0] == '0';
@@ -1565,6 +1573,7 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
   // us at 768 x 768 -- but they write no split-K slabs and leave the splitk_reduce pass out: the train step runs
   // +0.7 % with them, profiles/r05_bert_lt_ab.txt; VCG_LT_DW=0: the engine)
   if (dtype == VCG_BF16 && transA && transB && lt_gemm_enabled() && !lt_dw_off() &&
+      (long long)M * N >= lt_dw_min_mn() &&
       (long long)M * N * K >= (1LL << 31)) {
     const int rc = lt_gemm(1, 1, M, N, K, A, lda, B, ldb, out, N, out, N, 1, nullptr, accumulate ? 1.f : 0.f, stream);
     if (rc == VCG_OK)
