@@ -646,11 +646,11 @@ def test_conv_dgrad_bwd_stream_vs_persistent(K, case, ops_, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("H", [768, 200])
-def test_layernorm_fwd_bwd(K, dtype, H):
+@pytest.mark.parametrize("H,rows", [(768, 37), (200, 37), (768, 2085)])
+def test_layernorm_fwd_bwd(K, dtype, H, rows):
     """LN(x + res) forward / backward (row-wise wave kernels at H = 768, block kernels at H = 200) against
-    torch autograd in float64; the fused bias gradient = column sums of dx."""
-    rows = 37
+    torch autograd in float64; the fused bias gradient = column sums of dx. 2085 rows: every wave of the row-wise
+    backward walks several rows (the next row's operands prefetched under this row's arithmetic)."""
     x = _rand((rows, H), dtype, 71)
     r = _rand((rows, H), dtype, 72)
     g0 = torch.Generator().manual_seed(73)

@@ -563,17 +563,36 @@ __global__ __launch_bounds__(256) void ln_bwd_rw_kernel(const T* __restrict__ do
 #pragma unroll
     for (int i = 0; i < 4; ++i) pg[q][i] = pb[q][i] = pd[q][i] = 0.f;
   }
-  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+  // a wave walks rows row0, row0 + stride, ...; the next row's operands are loaded before this row's arithmetic
+  // (one wave per SIMD walks up to 8 rows: without the prefetch each row paid a full HBM round trip)
+  const int stride = gridDim.x * 4;
+  float nx[NQ][4] = {}, nr[NQ][4] = {}, nd[NQ][4] = {}, nmean = 0.f, nrstd = 0.f;
+  auto load_row = [&](int row) {
     const long long rb = (long long)row * H;
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xv[NQ][4], rv[NQ][4], dv[NQ][4];
+    nmean = mean_in[row];
+    nrstd = rstd_in[row];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int c = 4 * (lane + 64 * q);
-      ld4<T>(x + rb + c, xv[q]);
-      if (res) ld4<T>(res + rb + c, rv[q]);
-      ld4<T>(dout + rb + c, dv[q]);
+      ld4<T>(x + rb + c, nx[q]);
+      if (res) ld4<T>(res + rb + c, nr[q]);
+      ld4<T>(dout + rb + c, nd[q]);
     }
+  };
+  if (blockIdx.x * 4 + wave < rows) load_row(blockIdx.x * 4 + wave);
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += stride) {
+    const long long rb = (long long)row * H;
+    const float mean = nmean, rstd = nrstd;
+    float xv[NQ][4], rv[NQ][4], dv[NQ][4];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xv[q][i] = nx[q][i];
+        rv[q][i] = nr[q][i];
+        dv[q][i] = nd[q][i];
+      }
+    if (row + stride < rows) load_row(row + stride);
     float a = 0.f, b = 0.f;
     uint32_t kb = 0xFFFFFFFFu;  // dropout keep bits of this lane's elements (hashed once)
 #pragma unroll
