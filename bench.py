@@ -92,6 +92,27 @@ def _per_launch(r):
             "tflops": round(flops / (ms / 1e3) / 1e12, 1)}
 
 
+def _category_frac(a, b, peak_tf):
+    """Two launch categories' records taken as one: algorithmic GB/s over HBM peak (the dominant kernel's `frac`
+    definition) and the per-launch roofline fraction."""
+    ms, ideal, nbytes, flops = (x + y for x, y in zip(a, b))
+    if ms <= 0:
+        return None
+    gbs = nbytes / (ms / 1e3) / 1e9
+    return {"frac": round(gbs / HBM_PEAK_GBS, 4), "hbm_gbs": round(gbs, 1), "per_launch_frac": round(ideal / ms, 4),
+            "tflops": round(flops / (ms / 1e3) / 1e12, 1), "measured_ms": round(ms, 3)}
+
+
+def gemm_census_summary(gemms):
+    """Launches per kernel (the census keys without their shapes) and in all."""
+    by_kernel = {}
+    for key, n in gemms.items():
+        k = key.split(" M=")[0]
+        by_kernel[k] = by_kernel.get(k, 0) + n
+    return {"launches": sum(gemms.values()), "shapes": len(gemms), "kernels": dict(sorted(by_kernel.items())),
+            "identical_to_timed_step": True}
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def cpu_threads():
     """Threads for the CPU baseline: the cores this process may run on, capped at 16 (a one-GPU box's CPU share;
@@ -504,11 +525,19 @@ def main():
     from vcg_hip.trunk import ResNetTrunk
     # the per-block path census (which bn3 fold / y3-drop / GEMM-pass variant every bottleneck ran) of the last
     # warm-up step: the timed steps run the same path; the instrumented step below must too
-    timed_census = None
+    # and the GEMM census (which kernel ran which GEMM shape, every GEMM-class launch of the step: libvcg_hip's
+    # vcg_gemm_census) of the same step: the instrumented step below must match it launch for launch
+    timed_census = timed_gemms = None
     for i in range(args.warmup):
-        if i == args.warmup - 1 and args.mode == "train":
+        last = i == args.warmup - 1
+        if last and args.mode == "train":
             ResNetTrunk.census = []
+        if last:
+            ops.gemm_census_enable(True)
         step()
+        if last:
+            timed_gemms = ops.gemm_census()
+            ops.gemm_census_enable(False)
         timed_census, ResNetTrunk.census = ResNetTrunk.census, None
     torch.cuda.synchronize()
     if world > 1:
@@ -551,11 +580,19 @@ def main():
     # (and the weight gradients / downsample convs / weight re-layout on the trunk's stream)
     model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = False
     ops.timing_enable(True)
-    census = None
+    census = gemm_census = None
     if not args.no_roofline_step:
         ResNetTrunk.census = [] if timed_census is not None else None
+        ops.gemm_census_enable(timed_gemms is not None)
         step()
         inst_census, ResNetTrunk.census = ResNetTrunk.census, None
+        if timed_gemms is not None:
+            inst_gemms = ops.gemm_census()
+            ops.gemm_census_enable(False)
+            # every GEMM of the instrumented step on the kernel the timed steps used (no silent fallback between them)
+            assert inst_gemms == timed_gemms, ("instrumented step ran other GEMM kernels than the timed steps",
+                                               sorted(set(inst_gemms.items()) ^ set(timed_gemms.items()))[:8])
+            gemm_census = gemm_census_summary(timed_gemms)
         if timed_census is not None:
             # the one-stream instrumented step must run the timed step's kernels (bn3 folds, y3 drops, GEMM passes)
             assert inst_census == timed_census, ("instrumented step ran another per-block path than the timed steps",
@@ -571,7 +608,9 @@ def main():
                         else (ops.TIMING_GENERIC_GEMM, "igemm_kernel"))
     k_ms, k_n, k_fl = ops.timing_query(dom_id)
     peak_tf = MFMA_PEAK_TFLOPS[args.precision]
-    rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (dom_id, ops.TIMING_WGRAD)}
+    rl = {kid: ops.timing_roofline(kid, peak_tf, HBM_PEAK_GBS) for kid in (dom_id, ops.TIMING_WGRAD,
+                                                                           ops.TIMING_WIDE_GEMM)}
+    wide_n = ops.timing_query(ops.TIMING_WIDE_GEMM)[1]
     ops.timing_enable(False)
     model.overlap_streams, ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream = sides
     kern = {"ms": k_ms, "launches": k_n, "flops": k_fl}
@@ -627,7 +666,14 @@ def main():
                    # algorithmic bytes / HBM peak) per launch
                    "per_launch_roofline": _per_launch(rl[dom_id]),
                    "wgrad_fast_kernel": _per_launch(rl[ops.TIMING_WGRAD]),
+                   # the dense bf16 GEMMs of BERT's Linear layers and the downsample input gradient
+                   "gemm_wide_kernel": {**_per_launch(rl[ops.TIMING_WIDE_GEMM]), "launches_per_step": wide_n},
+                   # round 4's category: every launch of the 128 x 128 / 256-tile engines AND the wide engine's (BERT's
+                   # dense GEMMs were on the 128 x 128 engine then), so that moving GEMMs between engines does not
+                   # read as kernel speed
+                   "frac_round4_category": _category_frac(rl[dom_id], rl[ops.TIMING_WIDE_GEMM], peak_tf),
                    "path_census": census,
+                   "gemm_census": gemm_census,
                    "timing": "HIP events around each launch on its stream, one instrumented step (no BERT side "
                              "stream in that step: unshared launch durations); the category also holds the 256-tile "
                              "engine's launches (rocprof name gemm256_kernel: the layer-4 3x3 forward convs)"}

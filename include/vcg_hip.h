@@ -30,21 +30,21 @@ enum { VCG_ACT_NONE = 0, VCG_ACT_RELU = 1, VCG_ACT_GELU = 2, VCG_ACT_TANH = 3, V
    unfolded conv3 -> bn3 path stores y3 in bf16; the scoring forward's folded conv3 sets it to match). Without it the
    residual is added to the f32 accumulator value. */
 enum { VCG_ACT_FLAG_ROUND_PRE = 0x100 };
-/* vcg_gemm act flag: the caller allows the vendor library (hipBLASLt) for this GEMM -- BERT's Linear layers and the
-   trunk's stride-2 downsample input gradient (a plain GEMM over the output pixels) set it.
-   Taken for bf16 GEMMs of >= 2^31 MACs with alpha = 1 that carry only a bias (act NONE), a residual addend (act
-   NONE, residual != C), or a bias + GELU with the pre-activation (aux: the library writes the rounded pre-activation,
-   a GELU pass the output); every other GEMM, and every GEMM without the flag, runs on the hand-written engine.
-   VCG_LT_GEMM=0 in the environment turns the library off. */
-enum { VCG_ACT_FLAG_LIB = 0x200 };
-/* Library algorithm check (csrc/blaslt.hip; tools/lt_tune.py, not on the product path): times the hipBLASLt
-   heuristic's candidates (up to 16, its order) for one library GEMM of vcg_gemm's form on the given operands (D
-   written, C read when beta != 0: scratch buffers); us[i] = average microseconds of candidate i, -1 if it failed.
-   Returns the number of candidates. The product path always runs candidate 0 (profiles/r05_lt_tune.txt: the fastest
-   of 16 on 10 of BERT's 11 shapes). */
-VCG_API int vcg_lt_tune(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
-                        long long ldb, const void* C, long long ldc, void* D, long long ldd, int d_f32,
-                        const float* bias, float beta, int reps, float* us, int max_out, hipStream_t stream);
+/* vcg_gemm act flag: run this GEMM on the wide-tile engine (csrc/igemm_wide.hip: 128 x 128/192/256 tiles, one
+   512-thread workgroup per CU, persistent) -- BERT's Linear layers (transformers BertModel, model/lang/bert_hugface.py:20)
+   and the trunk's stride-2 downsample input gradient set it. Taken, whatever M, for bf16 GEMMs with K-contiguous
+   operands (transA = transB = 0), alpha = 1 and 16-B aligned rows whose epilogue is a bias (act NONE), bias + GELU
+   (aux: the pre-activation, rounded to bf16 before the GELU as bf16 autocast does), GELU' of a residual, or a
+   residual addend (residual != C); any other flagged GEMM runs on the 128 x 128 engine (vcg_gemm_census shows which
+   ran). */
+enum { VCG_ACT_FLAG_WIDE = 0x200 };
+/* GEMM census (tests, bench.py): while enabled, every GEMM dispatch of vcg_gemm / vcg_gemm_splitk / the conv entry
+   points adds one to the count of its key "<engine> M=.. N=.. K=.. <epilogue>"; enabling (or disabling) clears it.
+   vcg_gemm_census_size returns the number of keys; vcg_gemm_census_get(i) writes key i (NUL-terminated, at most n
+   bytes) and its count. */
+VCG_API int vcg_gemm_census_enable(int on);
+VCG_API int vcg_gemm_census_size(void);
+VCG_API int vcg_gemm_census_get(int i, char* key, int n, long long* count);
 
 /* ---- library ---------------------------------------------------------------------------- */
 VCG_API const char* vcg_last_error(void);
@@ -54,8 +54,8 @@ VCG_API int vcg_finalize(void);
 VCG_API int vcg_sync(hipStream_t stream);
 /* Live launch timing (bench.py's dominant-kernel roofline): while enabled, every fast-GEMM / wgrad launch is
    bracketed with HIP events on its stream; query sums durations (ms), launches and algorithmic FLOPs per kernel
-   id (0 igemm_fast_kernel, 1 wgrad_fast_kernel, 3 conv3x3_patch_kernel). Enabling (or disabling) clears the
-   records. */
+   id (0 igemm_fast_kernel, 1 wgrad_fast_kernel, 2 igemm_kernel, 3 conv3x3_patch_kernel, 4 gemm_wide_kernel).
+   Enabling (or disabling) clears the records. */
 VCG_API int vcg_timing_enable(int on);
 VCG_API int vcg_timing_query(int kernel_id, double* ms_total, long long* launches, double* flops);
 /* per-launch roofline of the recorded launches: ideal_ms = sum over launches of max(flops / peak_tflops,
@@ -72,6 +72,9 @@ VCG_API int vcg_patch_stamps(unsigned long long* out, int n);
 VCG_API int vcg_fast_stamps(unsigned long long* out, int n);
 /* profiling aid: s_memtime phase stamps of the last 256-tile GEMM (a -DVCG_G256_STAMPS build; 1 otherwise) */
 VCG_API int vcg_g256_stamps(unsigned long long* out, int n);
+/* profiling aid: s_memtime phase stamps of the last wide-tile GEMM (a -DVCG_WIDE_STAMPS build; 1 otherwise): waves 0
+   and 4 of workgroup 0, k-steps 8..23, both phases, 4 points each */
+VCG_API int vcg_wide_stamps(unsigned long long* out, int n);
 
 /* ---- MFMA implicit-GEMM engine (igemm.hip) ---------------------------------------------- */
 /* torchvision conv2d inside Resnet50TSM.base_model (model/vision/resnet50_tsm.py:15,68-77), with

@@ -20,6 +20,7 @@ Tolerances (bf16 activations / MFMA operands, fp32 accumulation and statistics; 
     BN-adjacent parameter gradients); total gradient norm within 3e-2.
 """
 import os
+import re
 
 import numpy as np
 import pytest
@@ -245,6 +246,31 @@ def test_pooled_stem_sums_step(prec):
             assert cos >= 0.999, (n, cos)
 
 
+@pytest.mark.parametrize("wgrad_stream,ds_stream", [(True, False), (False, False), (False, True)])
+def test_side_stream_settings_identical(wgrad_stream, ds_stream):
+    """The trunk backward's side-stream settings change where kernels run, never what they compute: with the
+    weight-gradient stream on and the downsample stream off (the downsample BN's backward apply then runs inline,
+    because conv1's fused dgrad on the main stream reads its dyd) and the other combinations, one C1-shape bf16
+    train step gives bit-identical loss and gradients to the default (both side streams on)."""
+    from vcg_hip import synth
+    from vcg_hip.trunk import ResNetTrunk
+    frames, ids, mask, labels = synth.clip_batch(2, 4, 112, 112, 32, seed=17, device=DEV)
+    saved = ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream
+    res = {}
+    try:
+        for tag, (wg, ds) in (("default", (True, True)), ("alt", (wgrad_stream, ds_stream))):
+            ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream = wg, ds
+            m = _model(4, "bf16")
+            res[tag] = _step(m, frames, ids, mask, labels)
+            del m
+    finally:
+        ResNetTrunk.wgrad_stream, ResNetTrunk.ds_stream = saved
+    (la, lga, ga, _), (lb, lgb, gb, _) = res["default"], res["alt"]
+    assert la == lb and torch.equal(lga, lgb)
+    diff = [n for n in ga if not torch.equal(ga[n], gb[n])]
+    assert not diff, f"gradients differ with wgrad_stream={wgrad_stream} ds_stream={ds_stream}: {diff[:6]}"
+
+
 def test_c1_loss_and_conditioning():
     """C1 bf16 step: loss / logits within bf16 tolerance of the exact fixture. (Its vision gradients are NOT
     compared element-wise with fp32: at C1 the BatchNorm statistics run over 8 frames of 4x4..56x56 maps and the
@@ -331,8 +357,14 @@ def test_full_res_train_step_vs_oracle():
     (batch-stat BatchNorm through 16 bottlenecks: the fp32 oracle's own vision gradients are ~2 % off exact,
     bf16 autocast's ~100 %, its vision embeddings ~13 %), so the bf16 step is held to PyTorch-bf16's accuracy:
     logits / vision embeddings / every gradient group within 1.5x of autocast's error vs exact (+ a small floor),
-    loss within 1e-2; BERT's gradients within max(1.5 x autocast's error, 5e-2) of exact."""
-    from vcg_hip import synth
+    loss within 1e-2; BERT's gradients within 1.5 x autocast's error of exact (median and 90th percentile over its
+    tensors, no floor).
+
+    Kernel census: the GEMM kernels this B = 1 step ran (vcg_gemm_census, every GEMM-class launch) are the kernels a
+    B = 64 step (the bench's C3 configuration) runs -- kernel selection does not depend on the batch, so this
+    oracle-anchored step exercises the benchmarked GEMM path (BERT's Linear layers on the wide-tile engine, the layer-4
+    3x3 forward convs on the 256-tile engine, ...)."""
+    from vcg_hip import ops, synth
     B, T, HW, L = 1, 16, 224, 128
     l64, lg64, v64, g64 = _oracle_step(T, HW, L, B, seed=11, dtype=torch.float64)
     lo, lgo, vo, go = _oracle_step(T, HW, L, B, seed=11)
@@ -346,20 +378,30 @@ def test_full_res_train_step_vs_oracle():
         opt = m.configure_optimizers(_Cfg)
         opt.zero_grad()
         ResNetTrunk.census = [] if prec == "bf16" else None
+        ops.gemm_census_enable(prec == "bf16")
         try:
             lg, _, ve, _ = m(frames, ids, mask, return_emb=True)
             loss = cross_entropy(lg, labels)
             loss.backward()
             torch.cuda.synchronize()
             census = ResNetTrunk.census
+            gemms = ops.gemm_census()
         finally:
             ResNetTrunk.census = None
+            ops.gemm_census_enable(False)
         if prec == "bf16":  # the oracle-anchored bf16 step ran the benchmarked per-block paths
             _check_census(census)
+            anchored_kernels = _gemm_kernels(gemms)
+            bert_wide = [k for k in gemms if k.startswith("gemm_wide") and f"M={B * L} " in k]
+            assert len(bert_wide) >= 4, gemms  # QKV / out-proj / FFN1 / FFN2 forward and their input gradients
         res[prec] = (loss.item(), lg.detach().double().cpu(), ve.detach().double().cpu(),
                      {n: p.grad.detach().double().cpu() for n, p in m.named_parameters()})
         del m, opt
         torch.cuda.empty_cache()
+    bench_kernels = _bench_step_kernels(T, HW, L)
+    print("GEMM kernels, B=1 step:", sorted(anchored_kernels))
+    assert bench_kernels == anchored_kernels, ("the B=64 step runs kernels the anchored step does not",
+                                               sorted(bench_kernels ^ anchored_kernels))
     l32, lg32, v32, g32 = res["fp32"]
     l16, lg16, v16, g16 = res["bf16"]
     print(f"loss exact {l64:.6f} oracle32 {lo:.6f} autocast-bf16 {la:.6f} native fp32 {l32:.6f} bf16 {l16:.6f}")
@@ -383,9 +425,33 @@ def test_full_res_train_step_vs_oracle():
         eac = np.array([_rel(ga[n], g64[n]) for n in names])
         print(f"{group}: grad rel err vs exact median / p90: native bf16 {np.median(e16):.2e} / "
               f"{np.quantile(e16, 0.9):.2e}, autocast bf16 {np.median(eac):.2e} / {np.quantile(eac, 0.9):.2e}")
-        floor = {"vision_model": 1e-2, "lang_model": 5e-2, "fusion_head": 5e-2}[group]
+        floor = {"vision_model": 1e-2, "lang_model": 0.0, "fusion_head": 5e-2}[group]
         assert np.median(e16) <= max(1.5 * np.median(eac), floor), group
         assert np.quantile(e16, 0.9) <= max(1.5 * np.quantile(eac, 0.9), 2 * floor), group
+
+
+def _gemm_kernels(gemms):
+    """The GEMM kernels (census keys without shape and split count) of a step."""
+    return {re.sub(r" z\d+", "", k.split(" M=")[0]) for k in gemms}
+
+
+def _bench_step_kernels(T, HW, L, B=64):
+    """GEMM kernels of one bf16 train step at the bench's C3 configuration (B = 64 windows)."""
+    from vcg_hip import ops, synth
+    from vcg_hip.functions import cross_entropy
+    frames, ids, mask, labels = synth.clip_batch(B, T, HW, HW, L, seed=5, device=DEV)
+    m = _model(T, "bf16")
+    ops.gemm_census_enable(True)
+    try:
+        loss = cross_entropy(m(frames, ids, mask)[0], labels)
+        loss.backward()
+        torch.cuda.synchronize()
+        gemms = ops.gemm_census()
+    finally:
+        ops.gemm_census_enable(False)
+    del m, frames, loss
+    torch.cuda.empty_cache()
+    return _gemm_kernels(gemms)
 
 
 def _check_census(census):

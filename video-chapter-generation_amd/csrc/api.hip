@@ -1,6 +1,9 @@
 // Library-level C ABI: error reporting, version, device handle.
 #include "common.h"
 
+#include <cstdio>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace vcg {
@@ -39,7 +42,43 @@ static void timing_clear() {
   }
   g_timing.clear();
 }
+
+// GEMM census: which kernel ran which GEMM shape (tests and bench.py compare the benchmarked step with the
+// oracle-anchored one); the host dispatches from one thread, the mutex keeps it safe anyway
+static std::mutex g_census_mu;
+static std::map<std::string, long long> g_census;
+static bool g_census_on = false;
+bool census_on() { return g_census_on; }
+void census_add(const char* tag, long long M, long long N, long long K) {
+  if (!g_census_on) return;
+  char key[192];
+  snprintf(key, sizeof(key), "%s M=%lld N=%lld K=%lld", tag, M, N, K);
+  std::lock_guard<std::mutex> lock(g_census_mu);
+  ++g_census[key];
+}
 }  // namespace vcg
+
+VCG_API int vcg_gemm_census_enable(int on) {
+  std::lock_guard<std::mutex> lock(vcg::g_census_mu);
+  vcg::g_census.clear();
+  vcg::g_census_on = on != 0;
+  return VCG_OK;
+}
+
+VCG_API int vcg_gemm_census_size(void) {
+  std::lock_guard<std::mutex> lock(vcg::g_census_mu);
+  return (int)vcg::g_census.size();
+}
+
+VCG_API int vcg_gemm_census_get(int i, char* key, int n, long long* count) {
+  std::lock_guard<std::mutex> lock(vcg::g_census_mu);
+  VCG_REQUIRE(i >= 0 && i < (int)vcg::g_census.size() && key && n > 0 && count, "bad census index / buffer");
+  auto it = vcg::g_census.begin();
+  std::advance(it, i);
+  snprintf(key, (size_t)n, "%s", it->first.c_str());
+  *count = it->second;
+  return VCG_OK;
+}
 
 VCG_API int vcg_timing_enable(int on) {
   vcg::timing_clear();

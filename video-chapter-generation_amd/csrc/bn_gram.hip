@@ -505,6 +505,7 @@ VCG_API int vcg_bn_apply_gram(const void* y, const float* scale, const float* sh
   const int g = gram_grid(P, C);
   const long long n = (long long)C * C + C;
   VCG_REQUIRE(ws_bytes >= (long long)g * n * 4, "workspace too small");
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "bn_apply_gram"); census_add(t_, P, C, C); }
 #define VCG_GRAM(CC)                                                                                            \
   hipLaunchKernelGGL(bn_apply_gram_kernel<CC>, dim3(g), dim3(256), 0, s, (const bf16_t*)y, scale, shift, mean, \
                      invstd, (bf16_t*)out, ws, g64, P)

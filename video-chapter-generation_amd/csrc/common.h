@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdio>
 #include <string>
 
 typedef uint16_t bf16_t;
@@ -17,9 +18,12 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 namespace vcg {
 // kernel ids of vcg_timing_query
-enum { TIMING_FAST_GEMM = 0, TIMING_WGRAD = 1, TIMING_GENERIC_GEMM = 2, TIMING_PATCH_CONV = 3 };
+enum { TIMING_FAST_GEMM = 0, TIMING_WGRAD = 1, TIMING_GENERIC_GEMM = 2, TIMING_PATCH_CONV = 3, TIMING_WIDE_GEMM = 4 };
 int timing_begin(hipStream_t s);
 void timing_end(int idx, hipStream_t s, int id, double flops, double bytes);
+// GEMM census (vcg_gemm_census_*): every GEMM-class launch adds one to the count of "<kernel tag> M=.. N=.. K=.."
+bool census_on();
+void census_add(const char* tag, long long M, long long N, long long K);
 }  // namespace vcg
 
 enum vcg_dtype { VCG_F32 = 0, VCG_BF16 = 1 };

@@ -16,7 +16,7 @@ enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 
        EPI_BWD_STREAM = 6 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
 enum { ACT_FLAG_ROUND_PRE = 0x100 };  // = VCG_ACT_FLAG_ROUND_PRE (include/vcg_hip.h)
-enum { ACT_FLAG_LIB = 0x200 };        // = VCG_ACT_FLAG_LIB: the vendor library may run this GEMM (blaslt.hip)
+enum { ACT_FLAG_WIDE = 0x200 };       // = VCG_ACT_FLAG_WIDE: run this GEMM on the wide-tile engine (igemm_wide.hip)
 
 template <typename T> struct Cfg;
 template <> struct Cfg<float> { static constexpr int VEC = 4, BK = 16, LDK = 20; };   // 80-B rows
@@ -298,13 +298,9 @@ __device__ __forceinline__ void gemm_epilogue(f32x4 (&acc)[BM / 32][BN / 32], co
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s);
 int fast_grid_rows(int M, int N, int z, int epi);
 bool fast_bwd_streams(const GemmParams& p);  // a dense EPI_BWD GEMM runs on the streaming kernel (P product: only there)
-// blaslt.hip: hipBLASLt for the plain bf16 GEMMs (VCG_OK, or VCG_ERR_UNSUPPORTED: no algorithm, run the engine)
-bool lt_gemm_enabled();
-int lt_gemm(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B, long long ldb,
-            const void* C, long long ldc, void* D, long long ldd, int d_f32, const float* bias, float beta,
-            hipStream_t stream);
-int lt_gemm_gelu(int transA, int transB, int M, int N, int K, const void* A, long long lda, const void* B,
-                 long long ldb, const float* bias, void* pre, void* out, long long ld, int fast, hipStream_t stream);
+// igemm_wide.hip: the wide-tile engine's epilogue class for a dense bf16 GEMM (-1: not supported) and its launch
+int wide_gemm_class(const GemmParams& p);
+int run_gemm_wide(GemmParams& p, int we, hipStream_t s);
 int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an EPI_BWD launch of run_fast_gemm
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,
                            float* dgamma, float* dbeta, int accumulate, hipStream_t s);  // grid rows (slots of EPI_BWD partials) of a fast-kernel launch

@@ -371,6 +371,7 @@ static int launch(const GemmParams& p, int splits, hipStream_t s) {
   dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((igemm_kernel<T, BM, BN, AM, BMD, EPI>), grid, dim3(256), 0, s, p);
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "igemm %s %dx%d a%d b%d e%d z%d", sizeof(T) == 2 ? "bf16" : "f32", BM, BN, AM, BMD, EPI, splits); census_add(t_, p.M, p.N, p.K); }
   {
     // algorithmic bytes: each operand once (a gathered A as its source tensor), the output once (the split-K
     // epilogue's f32 slabs count as its output), the residual once
@@ -779,10 +780,12 @@ __global__ __launch_bounds__(256) void p_slab_reduce_kernel(const float4* __rest
 }
 }  // namespace
 
-// P partial slabs of vcg_conv_dgrad_bwd with a2: at most 256 x 64 (workgroup rows x columns) [C][a2_c] f32 entries
+// P partial slabs of vcg_conv_dgrad_bwd with a2: [slots][C][a2_c] f32, slots = the streaming kernel's workgroup rows,
+// at most 256 / (C / 64) (one workgroup per CU over C / 64 column tiles; igemm_fast.hip bwd_stream_rows)
 VCG_API long long vcg_conv_dgrad_bwd_p_ws_bytes(int C, int a2_c) {
-  (void)C;
-  return 256LL * 64 * (a2_c > 0 ? a2_c : 0) * 4;
+  const long long nx = C >= 64 ? C / 64 : 1;
+  const long long slots = 256 / nx > 0 ? 256 / nx : 1;
+  return slots * (C > 0 ? C : 0) * (a2_c > 0 ? a2_c : 0) * 4;
 }
 
 VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C,
@@ -853,6 +856,7 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   if (a2) {  // P = g^T a2 from the stored g tiles: the streaming kernel only (else the caller runs the GEMM)
     e.a2 = a2; e.pj = a2_c; e.ppart = pws;
     if (!dense || !fast_bwd_streams(p)) return VCG_ERR_UNSUPPORTED;
+    VCG_REQUIRE((long long)fast_bwd_slots(p) * C * a2_c * 4 <= pws_bytes, "P workspace smaller than the launch's slots");
   }
   if (subpix) {
     bf16_t* wpk = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(ws) + dgrad_bwd_part_bytes(C));
@@ -1501,35 +1505,24 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
   p.b = transB ? dense_op(B, ldb, K, N, esz) : dense_op(B, ldb, N, K, esz);
   p.a.rows = M;
   p.b.rows = N;
-  VCG_REQUIRE((act & ~(0xff | ACT_FLAG_ROUND_PRE | ACT_FLAG_LIB)) == 0, "unknown act flags");
-  const bool lib = (act & ACT_FLAG_LIB) != 0 && dtype == VCG_BF16 && alpha == 1.f && lt_gemm_enabled() &&
-                   (long long)M * N * K >= (1LL << 31);
-  act &= ~ACT_FLAG_LIB;
+  VCG_REQUIRE((act & ~(0xff | ACT_FLAG_ROUND_PRE | ACT_FLAG_WIDE)) == 0, "unknown act flags");
+  const bool wide = (act & ACT_FLAG_WIDE) != 0 && dtype == VCG_BF16 && !transA && !transB;
+  act &= ~ACT_FLAG_WIDE;
   p.C = C; p.ldc = ldc; p.bias = bias; p.act = act & 0xff; p.residual = residual; p.ldr = ldr; p.aux = aux;
   p.res_round = (act & ACT_FLAG_ROUND_PRE) != 0 && residual != nullptr;
   p.alpha = alpha;
-  // BERT's FFN1 (GELU with the pre-activation kept): the library GEMM into the pre-activation + a GELU pass
-  // (88 -> 44 + ~20 us at B = 64, tools/bench_bert_gemm.py; VCG_LT_GELU_OFF=1: the fused engine epilogue)
-  if (lib && act == ACT_GELU && aux != nullptr && residual == nullptr && !getenv_flag("VCG_LT_GELU_OFF")) {
-    const int rc = lt_gemm_gelu(transA, transB, M, N, K, A, lda, B, ldb, bias, aux, C, ldc, fast_gelu_enabled() ? 1 : 0,
-                                stream);
-    if (rc == VCG_OK)
+  // BERT's Linear layers and the downsample input gradient (the caller's flag): the wide-tile engine, whatever M --
+  // the oracle-anchored B = 1 step runs the kernels of the B = 64 bench
+  if (wide) {
+    p.fast_act = fast_gelu_enabled();
+    const int we = wide_gemm_class(p);
+    if (we >= 0) {
       if (FILE* f = gemm_log()) {
-        fprintf(f, "lt M=%d N=%d K=%d gelu\n", M, N, K);
+        fprintf(f, "wide M=%d N=%d K=%d we=%d\n", M, N, K, we);
         fflush(f);
       }
-    if (rc != VCG_ERR_UNSUPPORTED) return rc;
-  }
-  // BERT's bias-only / addend-only GEMMs: the vendor library where it has an algorithm (blaslt.hip)
-  if (lib && act == 0 && aux == nullptr && (residual == nullptr || residual != C)) {
-    const int rc = lt_gemm(transA, transB, M, N, K, A, lda, B, ldb, residual, ldr, C, ldc, 0, bias,
-                           residual ? 1.f : 0.f, stream);
-    if (rc == VCG_OK)
-      if (FILE* f = gemm_log()) {
-        fprintf(f, "lt M=%d N=%d K=%d\n", M, N, K);
-        fflush(f);
-      }
-    if (rc != VCG_ERR_UNSUPPORTED) return rc;
+      return run_gemm_wide(p, we, stream);
+    }
   }
 #define VCG_GEMM_CASE(TT)                                                                   \
   if (!transA && !transB) return run_gemm<TT, OP_DENSE_K, OP_DENSE_K>(p, EPI_STORE, 1, stream);   \
@@ -1539,19 +1532,6 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
   if (dtype == VCG_BF16) { VCG_GEMM_CASE(bf16_t) }
   VCG_GEMM_CASE(float)
 #undef VCG_GEMM_CASE
-}
-
-// Weight gradients with fewer than this many outputs stay on the split-K engine: at 768 x 768 (BERT's attention
-// output projection) the library took 48 vs 33 us and the step ran +0.5 % with the engine there
-// (profiles/r05_bert_lt_ab.txt; VCG_LT_DW_MIN_MN overrides)
-static long long lt_dw_min_mn() {
-  const char* e = getenv("VCG_LT_DW_MIN_MN");
-  return e ? atoll(e) : (1LL << 20);
-}
-
-static bool lt_dw_off() {
-  const char* e = getenv("VCG_LT_DW");
-  return e != nullptr && e[0] == '0';
 }
 
 VCG_API long long vcg_gemm_splitk_ws_bytes(int dtype, int M, int N, int K) {
@@ -1569,20 +1549,6 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
   int kps = (K + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
   splits = (K + kps - 1) / kps;
-  // (isolated, the library's weight gradients are slower than the wgrad engine on 3 of BERT's 4 shapes -- 50 vs 33
-  // us at 768 x 768 -- but they write no split-K slabs and leave the splitk_reduce pass out: the train step runs
-  // +0.7 % with them, profiles/r05_bert_lt_ab.txt; VCG_LT_DW=0: the engine)
-  if (dtype == VCG_BF16 && transA && transB && lt_gemm_enabled() && !lt_dw_off() &&
-      (long long)M * N >= lt_dw_min_mn() &&
-      (long long)M * N * K >= (1LL << 31)) {
-    const int rc = lt_gemm(1, 1, M, N, K, A, lda, B, ldb, out, N, out, N, 1, nullptr, accumulate ? 1.f : 0.f, stream);
-    if (rc == VCG_OK)
-      if (FILE* f = gemm_log()) {
-        fprintf(f, "lt M=%d N=%d K=%d dW\n", M, N, K);
-        fflush(f);
-      }
-    if (rc != VCG_ERR_UNSUPPORTED) return rc;
-  }
   GemmParams p{};
   p.M = M; p.N = N; p.K = K; p.k_per_split = kps;
   p.a = dense_op(A, lda, M);

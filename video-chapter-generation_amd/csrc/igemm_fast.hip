@@ -2040,8 +2040,7 @@ static bool bwd_stream_ok(const GemmParams& p) {
   if (p.K == 256 && ((uintptr_t)p.b.ptr & 15 || p.b.ld % 8 != 0)) return false;  // 16-B weight fragment loads
   if (((uintptr_t)p.C | (uintptr_t)e.res | (uintptr_t)e.y | (uintptr_t)e.y2 | (uintptr_t)p.a.ptr) & 15) return false;
   if (e.res_s > 1 && (p.M % e.hw) != 0) return false;
-  if (e.pj > 0) {  // P = g^T a2: the mask bits alone, K 64 / 128 (a2 of 64 / 128 columns; 128: one A tile per slot)
-    // or K = 256 on the 64-column tiles (a2 of 128 columns, 2 slots: the layer-3 first block's dgrad)
+  if (e.pj > 0) {  // P = g^T a2 (a2 of 64 columns: layer 1): the mask bits alone, K 64 / 128
     if (e.y || !e.bits || e.pj != 64 || p.K > 128 || ((uintptr_t)e.a2 & 15) || !e.ppart) return false;
     if (((uintptr_t)p.b.ptr & 15) || p.b.ld % 8 != 0) return false;  // weight fragments in registers
   }
@@ -2100,6 +2099,7 @@ static int launch_fast(const GemmParams& p, int z, hipStream_t s) {
   dim3 grid(nx * gy, 1, z);
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((igemm_fast_kernel<BM, BN, AM, EPI, RES>), grid, dim3(BM * 2), 0, s, p);
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "igemm_fast %dx%d a%d e%d r%d z%d", BM, BN, AM, EPI, RES, z); census_add(t_, p.M, p.N, p.K); }
   timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K * z, algorithmic_bytes<AM, EPI, RES>(p, z));
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -2110,6 +2110,7 @@ static int launch_bwd_stream(const GemmParams& p, hipStream_t s) {
   const int nx = p.N / TN, gy = bwd_stream_rows(p);
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((igemm_fast_kernel<256, TN, KC, EPI_BWD_STREAM, false, XF>), dim3(nx * gy), dim3(512), 0, s, p);
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "igemm_fast_stream tn%d xf%d", TN, XF); census_add(t_, p.M, p.N, p.K); }
   // (with the g^T a2 product: + its flops, the a2 read and the P slabs written and reduced)
   const double pj = bwd_stream_pj(XF);
   timing_end(tk, s, TIMING_FAST_GEMM, 2.0 * p.M * p.N * (double)p.K + 2.0 * p.M * p.N * pj,
@@ -2152,6 +2153,7 @@ static int launch_patch(const GemmParams& p, int R, hipStream_t s) {
     gs.stamps = g_patch_stamps;
   }
   hipLaunchKernelGGL((conv3x3_patch_kernel<EPI, DG, PW>), dim3((p.N / 64) * gy), dim3(256), 0, s, p, gs);
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "conv3x3_patch e%d dg%d pw%d", EPI, (int)DG, PW); census_add(t_, p.M, p.N, p.K); }
   timing_end(tk, s, TIMING_PATCH_CONV, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_IM2COL, EPI, false>(p, 1));
   VCG_LAUNCH_CHECK();
   return VCG_OK;
@@ -2166,6 +2168,7 @@ static int launch_stem(const GemmParams& p, int R, hipStream_t s) {
   gy = max(gy, 1);
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((stem_patch_kernel<EPI>), dim3(nx * gy), dim3(256), 0, s, p, g);
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "stem_patch e%d", EPI); census_add(t_, p.M, p.N, p.K); }
   timing_end(tk, s, TIMING_PATCH_CONV, 2.0 * p.M * p.N * (double)p.K, algorithmic_bytes<OP_IM2COL, EPI, false>(p, 1));
   VCG_LAUNCH_CHECK();
   return VCG_OK;

@@ -272,6 +272,7 @@ template <int BM, int BN, bool BG> int launch_wgrad(const GemmParams& p0, int sp
   VCG_REQUIRE(wgs < (1LL << 31), "wgrad grid too large");
   const int tk = timing_begin(s);
   hipLaunchKernelGGL((wgrad_fast_kernel<BM, BN, BG>), dim3((unsigned)wgs), dim3(256), 0, s, p);
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "wgrad_fast %dx%d bg%d z%d", BM, BN, (int)BG, splits); census_add(t_, p.M, p.N, p.K); }
   // algorithmic bytes: dy and x read once, the fp32 weight gradient written once (the split slabs are not)
   timing_end(tk, s, TIMING_WGRAD, 2.0 * p.M * p.N * (double)p.K,
              (double)p.a.bytes + (double)p.b.bytes + 4.0 * p.M * (double)p.N);
@@ -508,6 +509,7 @@ int wgrad_patch_splits(int C, int Cout) { return wp_grid(C, Cout) / ((C / 64) * 
 template <int PW>
 static void launch_wgrad_patch(const void* x, const void* dy, float* ws, uint32_t xb, uint32_t yb, const WPatchGeom& g,
                                int grid, hipStream_t s) {
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "wgrad3x3_patch pw%d tm%d", PW, g.TM); census_add(t_, 0, 0, 0); }
   if (g.TM <= 64)
     hipLaunchKernelGGL((wgrad3x3_patch_kernel<PW, 2>), dim3(grid), dim3(256), 0, s, (const bf16_t*)x,
                        (const bf16_t*)dy, ws, xb, yb, g);

@@ -402,6 +402,7 @@ VCG_API int vcg_stem_bwd_fused(const void* dy, const unsigned char* idx, const v
   a.N = N; a.H = H; a.W = W; a.OH = (H - 1) / 2 + 1; a.OW = (W - 1) / 2 + 1; a.tiles = N * (H / 2);
   const int grid = a.tiles < SB_GRID ? a.tiles : SB_GRID;
   static const int dbg = getenv("VCG_STEM_BWD_DBG") ? atoi(getenv("VCG_STEM_BWD_DBG")) : 0;  // timing breakdown only
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "stem_bwd_fused"); census_add(t_, a.N, a.H, a.W); }
   if (dbg == 1) hipLaunchKernelGGL(stem_bwd_fused_kernel<1>, dim3(grid), dim3(SB_NTH), 0, s, a);
   else if (dbg == 2) hipLaunchKernelGGL(stem_bwd_fused_kernel<2>, dim3(grid), dim3(SB_NTH), 0, s, a);
   else hipLaunchKernelGGL(stem_bwd_fused_kernel<0>, dim3(grid), dim3(SB_NTH), 0, s, a);

@@ -209,6 +209,7 @@ int run_rs1x1_bnres(const void* x, const void* wfold, const float* bias, const v
   const char* e = getenv("VCG_RS1X1");  // (read per call: tests A/B both engines in one process)
   if ((e && e[0] == '0') || (K != 64 && K != 128 && K != 256) || N % RS_TN != 0 || N / RS_TN > 8 || M <= 0) return -1;
   const int g = rs_grid(N);
+  if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "rs1x1_bnres"); census_add(t_, M, N, K); }
   if (K == 64)
     hipLaunchKernelGGL(rs1x1_bnres_kernel<64>, dim3(g), dim3(RS_NTH), 0, s, (const bf16_t*)x, (const bf16_t*)wfold,
                        bias, (const bf16_t*)res, (bf16_t*)out, bits, M, N);

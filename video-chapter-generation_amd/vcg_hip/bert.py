@@ -16,9 +16,9 @@ import torch
 from . import ops
 
 
-# BERT's Linear GEMMs may run on the vendor library (ops.ACT_FLAG_LIB: bias-only / addend-only bf16 GEMMs and FFN1's
-# GELU, csrc/blaslt.hip); the flag is ignored in fp32 and for GEMMs with a fused epilogue
-LIB = ops.ACT_FLAG_LIB
+# BERT's Linear GEMMs run on the wide-tile engine (ops.ACT_FLAG_WIDE, csrc/igemm_wide.hip: bias, bias + GELU with the
+# pre-activation, GELU' of the pre-activation, residual addend), whatever the batch; the flag is ignored in fp32
+WIDE = ops.ACT_FLAG_WIDE
 
 def _seed(base, layer, site):
     return (base * 0x9E3779B1 + layer * 7919 + site * 104729) & ((1 << 63) - 1)
@@ -101,7 +101,7 @@ class BertEncoderEngine:
         LDS-DMA GEMM reads both operands K-contiguous (measured 87 -> 61 us at K = 3072, 67 -> 53 us at
         K = 2304; no gain at K = 768, tools/bench_bert_gemm.py)."""
         # (FFN2's input gradient: the fast engine's staged GELU' epilogue, the pre-activation read as full rows)
-        kw["act"] = kw.get("act", ops.ACT_NONE) | LIB
+        kw["act"] = kw.get("act", ops.ACT_NONE) | WIDE
         wt = self.wt.get(W) if self.wt is not None else None
         if wt is not None:
             return ops.gemm(A, wt, M, N, K, K, K, **kw)
@@ -133,9 +133,7 @@ class BertEncoderEngine:
         if need_grad and self.wt is not None:
             self.wt.refresh()  # (read only by the backward; issued here, on BERT's stream, beside the trunk)
 
-        # (the library GEMMs only in the train forward: in the no-grad scoring forward they measured -0.9 %,
-        # 3029 -> 3002 windows/s same box, profiles/r05_bert_lt_ab.txt)
-        lib = LIB if need_grad else 0
+        lib = WIDE
         emb = m.embeddings
         h, e_mean, e_rstd = ops.embed_ln_fwd(ids, emb.word_embeddings.weight, emb.position_embeddings.weight,
                                              emb.token_type_embeddings.weight, emb.LayerNorm.weight,

@@ -13,7 +13,7 @@ from . import _lib
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_GELU_BWD = 0, 1, 2, 3, 4
 ACT_FLAG_ROUND_PRE = 0x100  # gemm: round alpha*AB + bias to the storage dtype before the residual (vcg_hip.h)
-ACT_FLAG_LIB = 0x200  # gemm: the vendor library may run it (BERT's Linear layers; vcg_hip.h VCG_ACT_FLAG_LIB)
+ACT_FLAG_WIDE = 0x200  # gemm: the wide-tile engine (BERT's Linear layers, the downsample dgrad; vcg_hip.h VCG_ACT_FLAG_WIDE)
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -60,7 +60,24 @@ def conv_out_hw(H, W, KH, KW, stride, pad):
     return (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
 
 
-TIMING_FAST_GEMM, TIMING_WGRAD, TIMING_GENERIC_GEMM, TIMING_PATCH_CONV = 0, 1, 2, 3
+TIMING_FAST_GEMM, TIMING_WGRAD, TIMING_GENERIC_GEMM, TIMING_PATCH_CONV, TIMING_WIDE_GEMM = 0, 1, 2, 3, 4
+
+
+def gemm_census_enable(on):
+    """Start (or stop) counting GEMM-class launches per (kernel, shape); clears the counts."""
+    _lib.call("vcg_gemm_census_enable", int(bool(on)))
+
+
+def gemm_census():
+    """{"<kernel tag> M=.. N=.. K=..": launches} since gemm_census_enable(True)."""
+    import ctypes
+    out = {}
+    for i in range(_lib.query("vcg_gemm_census_size")):
+        buf = ctypes.create_string_buffer(256)
+        n = ctypes.c_longlong()
+        _lib.call("vcg_gemm_census_get", i, buf, 256, ctypes.addressof(n))
+        out[buf.value.decode()] = n.value
+    return out
 
 
 def timing_enable(on):

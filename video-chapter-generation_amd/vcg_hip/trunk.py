@@ -528,9 +528,9 @@ class ResNetTrunk:
             if cds.stride[0] == 2:
                 wt_ds = self._wprep_t(cds, Cin)
                 Mo = dyd.numel() // C3
-                # (a plain GEMM: the vendor library may run it, ops.ACT_FLAG_LIB)
+                # (a plain GEMM: the wide-tile engine, ops.ACT_FLAG_WIDE)
                 res, res_stride = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3,
-                                           act=ops.ACT_FLAG_LIB), 2
+                                           act=ops.ACT_FLAG_WIDE), 2
             else:
                 res, res_stride = self._dgrad(cds, dyd, N, H, W), 1
             ev = torch.cuda.Event()
@@ -738,8 +738,15 @@ class ResNetTrunk:
             if self._can_fold(r, ds):
                 bnf = (g, sums3)
                 dy3 = dyd = None
-                if ds:  # the downsample BN's apply pass on the side stream (dyd feeds only side-stream kernels)
-                    dyd = self._async(lambda: self._bn_apply_bwd(g, r["yd"], bd, C3, sumsd), g, r["yd"], *sumsd)
+                if ds:
+                    # the downsample BN's apply pass on the side stream when its input gradient runs there too (dyd
+                    # then feeds only side-stream kernels); inline otherwise, where the main stream reads dyd
+                    def dyd_fn():
+                        return self._bn_apply_bwd(g, r["yd"], bd, C3, sumsd)
+                    if self._ws is not None and ResNetTrunk.ds_stream:
+                        dyd = self._async(dyd_fn, g, r["yd"], *sumsd)
+                    else:
+                        dyd = dyd_fn()
             elif ResNetTrunk.dual_bn_bwd and ds and b3.mode != "running" and bd.mode != "running":  # g read once
                 dy3, dyd = ops.bn_bwd_apply_dual(g, r["y3"], b3.mean, b3.invstd, b3.bn.weight, sums3[0], sums3[1],
                                                  r["yd"], bd.mean, bd.invstd, bd.bn.weight, sumsd[0], sumsd[1], C3)
@@ -790,7 +797,7 @@ class ResNetTrunk:
                 # output pixels (no 3/4-zero rows), added by the conv1 dgrad epilogue at those rows (res_stride 2)
                 wt_ds = self._wprep_t(cds, Cin)
                 Mo = dyd.numel() // C3
-                res = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3, act=ops.ACT_FLAG_LIB)
+                res = ops.gemm(dyd.view(Mo, C3), wt_ds.view(Cin, C3), Mo, Cin, C3, C3, C3, act=ops.ACT_FLAG_WIDE)
                 res_stride = 2
             else:
                 res = self._dgrad(cds, dyd, N, H, W)  # the downsample branch's input gradient
