@@ -403,6 +403,9 @@ def main():
     ap.add_argument("--no-roofline-step", action="store_true",
                     help="skip the instrumented step after the timed region (profiling runs: the trace then ends with "
                          "the timed steps); the line then has no dominant-kernel roofline")
+    ap.add_argument("--one-stream", action="store_true",
+                    help="every kernel on one HIP stream (BERT, the trunk's weight gradients and downsample branch "
+                         "inline): the one-stream rocprof profiles, whose per-kernel durations are unshared")
     ap.add_argument("--launch-check", action="store_true",
                     help="rehearse the rank launch only (gloo, no GPU): every rank joins the process group and "
                          "rank 0 prints the line's n_gpus / rank layout")
@@ -452,6 +455,9 @@ def main():
     torch.manual_seed(123)
     model = build_two_stream(clip_frame_num=T, seed=123, device=dev, precision=args.precision)
     model.train(args.mode == "train")
+    if args.one_stream:
+        from vcg_hip.trunk import ResNetTrunk
+        model.overlap_streams = ResNetTrunk.wgrad_stream = ResNetTrunk.ds_stream = False
     if args.mode == "fwd" and args.bn == "batch":
         from test_video_segment_point import drop_bn_running_stats
         drop_bn_running_stats(model)

@@ -88,7 +88,7 @@ def test_fused_attention_matches_fp64_and_unfused(B, L, p):
 
 
 def test_fused_attention_in_bert_step_matches_unfused(monkeypatch):
-    """A whole bf16 text-only train step (BERT + head, dropout 0.1) with the fused kernels vs VCG_FUSED_ATTN=0 (same
+    """A whole bf16 text-only train step (BERT + head, dropout 0.1) with the fused kernels vs the unfused ones (same
     weights, inputs and dropout seeds): logits and every BERT parameter gradient within bf16 tolerance."""
     from vcg_hip import _lib, synth
     from vcg_hip.build import build_model
@@ -97,8 +97,9 @@ def test_fused_attention_in_bert_step_matches_unfused(monkeypatch):
     _, ids, mask, labels = synth.clip_batch(4, 1, 8, 8, 128, seed=7, device=DEV)
     mask[1, 70:] = 0
     res = {}
+    from vcg_hip.bert import BertEncoderEngine
     for flag in ("1", "0"):
-        monkeypatch.setenv("VCG_FUSED_ATTN", flag)
+        monkeypatch.setattr(BertEncoderEngine, "fused_attn", flag == "1")
         m = build_model("text", seed=7, device=DEV, precision="bf16", dropout=0.1).train()
         torch.manual_seed(11)  # the dropout seeds (vcg_hip.nn.new_seed) come from torch's RNG
         logits, _ = m(ids, mask)

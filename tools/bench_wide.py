@@ -1,7 +1,7 @@
 """Times the wide-tile engine on BERT-base's dense GEMMs at B=64 x L=128 (8192 rows), HIP events, 20 reps each, with
-the library and environment it is started with (VCG_LIB_PATH, VCG_WIDE_PIPE, VCG_WIDE_BN): one line per shape plus
+the library and environment it is started with (VCG_LIB_PATH, VCG_WIDE_BN): one line per shape plus
 the sum over one BERT layer's forward + input gradients (x12 = per step).
-usage: python tools/bench_wide.py [tag]"""
+usage: python tools/bench_wide.py [tag] [--only <shape name prefix>]"""
 import os
 import sys
 
@@ -25,7 +25,9 @@ def timeit(fn, iters=20):
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else os.environ.get("VCG_WIDE_PIPE", "default")
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    args = [a for i, a in enumerate(sys.argv[1:], 1) if a != "--only" and sys.argv[i - 1] != "--only"]
+    tag = args[0] if args else "default"
     dt, dev, W_ = torch.bfloat16, "cuda", ops.ACT_FLAG_WIDE
     R, H, I = 8192, 768, 3072
     g = torch.Generator(device=dev).manual_seed(0)
@@ -61,6 +63,8 @@ def main():
     tot = 0.0
     parts = []
     for name, fl, fn in shapes:
+        if only and not name.startswith(only):
+            continue
         t = timeit(fn)
         tot += t
         parts.append(f"{name} {t:6.1f}us/{fl / t / 1e6:4.0f}")

@@ -13,5 +13,5 @@ timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpur
 tail -1 gpurun_out/${TAG}_bench.log
 export TMPDIR=/tmp
 rm -f gpurun_out/${TAG}_gemm.log
-VCG_OVERLAP=0 VCG_WGRAD_STREAM=0 VCG_DS_STREAM=0 VCG_GEMM_LOG=gpurun_out/${TAG}_gemm.log timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/${TAG}_prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || { echo "profile failed"; tail -20 gpurun_out/${TAG}_prof.log; exit 3; }
+VCG_GEMM_LOG=gpurun_out/${TAG}_gemm.log timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/${TAG}_prof -o run -- python bench.py --one-stream --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || { echo "profile failed"; tail -20 gpurun_out/${TAG}_prof.log; exit 3; }
 echo done

@@ -16,7 +16,7 @@ ST=$(find gpurun_out/${TAG}_trace -name "*kernel_stats.csv" | head -1)
 python3 tools/trace_gaps.py "$KT" --last-ms 300 | tee gpurun_out/${TAG}_gaps.txt
 head -25 "$ST" | cut -d, -f1-5
 rm -f gpurun_out/${TAG}_gemm.log
-VCG_OVERLAP=0 VCG_WGRAD_STREAM=0 VCG_DS_STREAM=0 VCG_GEMM_LOG=gpurun_out/${TAG}_gemm.log timeout -k 10 600 \
+VCG_GEMM_LOG=gpurun_out/${TAG}_gemm.log timeout -k 10 600 \
   rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_one -o run -- \
   python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/${TAG}_one.log 2>&1 || { echo "one-stream profile failed"; tail -20 gpurun_out/${TAG}_one.log; exit 4; }
 KT1=$(find gpurun_out/${TAG}_one -name "*kernel_trace.csv" | head -1)

@@ -111,7 +111,6 @@ struct GemmParams {
   // batched mode (batch_inner > 0): blockIdx.z = zo * batch_inner + zi selects element offsets
   int batch_inner;
   long long a_so, a_si, b_so, b_si, c_so, c_si;
-  int stage_kt;  // fast kernel: stage the output tile through LDS when the tile has <= stage_kt k-steps
   int res_round; // residual epilogue: round alpha*AB + bias to bf16 before adding the residual (VCG_ACT_FLAG_ROUND_PRE)
   int fast_act;  // bf16 epilogues: GELU / GELU' through erf_fast (common.h) instead of erff (VCG_FAST_GELU=0: off)
   BwdEpi bwd;    // EPI_BWD

@@ -352,19 +352,8 @@ static OpArgs dense_op(const void* ptr, long long ld, int rows, long long K = 0,
   return a;
 }
 
-static bool getenv_flag(const char* name) {
-  const char* e = getenv(name);
-  return e && e[0] == '1';
-}
-
-static bool fast_gemm_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("VCG_FAST_GEMM");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
+// the bf16 LDS-DMA engines (igemm_fast.hip and the kernels beside it) run every bf16 GEMM they support
+static constexpr bool fast_gemm_enabled() { return true; }
 
 template <typename T, int BM, int BN, int AM, int BMD, int EPI>
 static int launch(const GemmParams& p, int splits, hipStream_t s) {
@@ -569,16 +558,9 @@ static void splitk_reduce(hipStream_t stream, const float* ws, int splits, long 
                      G, N, out, accumulate, conv_perm, KH, KW, Cpad, Cin, scale, KWp, pwp, pad);
 }
 
-// Split-K target: tiles x splits ~ this many workgroups (VCG_SPLITK_WG, read once; default 1024 = 2 rounds of 2
-// workgroups per CU). Fewer splits write and re-read fewer fp32 slabs.
-static int splitk_target() {
-  static int t = 0;
-  if (t == 0) {
-    const char* e = getenv("VCG_SPLITK_WG");
-    t = e && atoi(e) > 0 ? atoi(e) : 1024;
-  }
-  return t;
-}
+// Split-K target: tiles x splits ~ this many workgroups (2 rounds of 2 workgroups per CU; 512 and 2048 measured
+// -2.4 % / -1.3 % per step, profiles/r05_splitk_target_ab.txt). Fewer splits write and re-read fewer fp32 slabs.
+static int splitk_target() { return 1024; }
 
 static int choose_splits(int M, int N, int K, int BK) {
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
@@ -820,7 +802,7 @@ VCG_API int vcg_conv_dgrad_bwd(int dtype, const void* dy, const void* wt, void* 
   // stride-2 3x3: four sub-pixel classes (dx pixels of one (h, w) parity), each a GEMM over only the taps that
   // reach it (4 / 2 / 2 / 1 of 9) instead of one GEMM over all 9 with 3/4 of the tap rows masked to zero
   const bool subpix = stride == 2 && KH == 3 && KW == 3 && pad == 1 && tsm_fold == 0 && res_stride == 1 &&
-                      H % 2 == 0 && W % 2 == 0 && !getenv_flag("VCG_NO_SUBPIXEL");
+                      H % 2 == 0 && W % 2 == 0;
   GemmParams p{};
   p.M = N * H * W;
   p.N = C;
@@ -1544,6 +1526,7 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
                             const void* B, long long ldb, float* out, int accumulate, float* ws, long long ws_bytes,
                             hipStream_t stream) {
   const int BK = dtype == VCG_BF16 ? 32 : 16;
+  // (the Linear weight gradients with a 256-workgroup target: -2.1 % per step, profiles/r06_vs_r05_same_box.txt)
   int splits = choose_splits(M, N, K, BK);
   VCG_REQUIRE(ws_bytes >= (long long)splits * M * N * 4, "workspace too small");
   int kps = (K + splits - 1) / splits;
@@ -1559,7 +1542,7 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
   // bf16 dW = A^T B with both operands row-major over K (the Linear weight gradients): the LDS-DMA wgrad kernel
   // with a dense B operand; k per split in its 64-row steps (never more splits than the workspace query allows)
   const long long a_ext = ((long long)(K - 1) * lda + M) * 2, b_ext = ((long long)(K - 1) * ldb + N) * 2;
-  if (dtype == VCG_BF16 && transA && transB && fast_gemm_enabled() && !getenv_flag("VCG_NO_FAST_DW") &&
+  if (dtype == VCG_BF16 && transA && transB && fast_gemm_enabled() &&
       M % 8 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && a_ext < 0xFFFFFF00LL && b_ext < 0xFFFFFF00LL) {
     p.a.bytes = a_ext;  // [K][lda] operands: the LDS-DMA loaders' buffer range
     p.b.bytes = b_ext;

@@ -1348,8 +1348,8 @@ __device__ __forceinline__ void igemm_fast_body(const GemmParams& p) {
       const int mt = by + tile * gy;
       bf16_t* stA = As + cur * AE;  // the finished stage holds the output rounds (see stage_put)
       bf16_t* stB = BM == 256 ? stA + 64 * BN : Bs + cur * BE;
-      // output tiles go through the LDS stage for full-row 16-B stores (VCG_STAGE_KT can limit it)
-      const bool staged = ntiles <= p.stage_kt;
+      // output tiles go through the LDS stage for full-row 16-B stores
+      const bool staged = true;
       if constexpr (BWD) {
 #pragma unroll
         for (int h = 0; h < BM / 128; ++h) {
@@ -2175,11 +2175,8 @@ static int launch_stem(const GemmParams& p, int R, hipStream_t s) {
 }
 
 // Entry from igemm.hip's dispatcher (bf16, K-contiguous A and B, no split-K).
-// VCG_STAGE_KT (default: all): largest k-step count per tile whose output goes through the LDS stage
-// (A/B in one process, tools/bench_gemm.py with VCG_BENCH_AB=1: staging never loses).
+// (Every output tile goes through the LDS stage: measured never slower, tools/bench_gemm.py, round 2.)
 int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
-  const char* e = getenv("VCG_STAGE_KT");
-  p.stage_kt = e && e[0] ? atoi(e) : 1 << 30;
   if (p.a.ptr2) {  // a BatchNorm backward folded into this input gradient: A = [g | y] (light epilogue only)
     if (amode != OP_DENSE_K || epi != EPI_BWD || z != 1 || !bwd_light(p) || p.a.split2 % FBK != 0) return -1;
     return fast_bn<OP_DENSE_K2, EPI_BWD_AFF>(p, z, s);
@@ -2236,7 +2233,7 @@ int run_fast_gemm(GemmParams& p, int amode, int epi, int z, hipStream_t s) {
   // GEMMs by ~10 % (2.72-2.76 K vs 3.06 K windows/s, bisected to that change)
   if (p.residual) return p.act == ACT_GELU_BWD ? fast_bn<OP_DENSE_K, EPI_STORE, 2>(p, z, s)
                                                : fast_bn<OP_DENSE_K, EPI_STORE, 1>(p, z, s);
-  if (p.aux && amode == OP_DENSE_K && (p.ldc & 7) == 0 && !getenv("VCG_NO_AUX_STAGE"))  // BERT FFN1 (GELU input)
+  if (p.aux && amode == OP_DENSE_K && (p.ldc & 7) == 0)  // a GELU input kept for the backward
     return fast_bn<OP_DENSE_K, EPI_STORE_AUX>(p, z, s);
   if (amode == OP_IM2COL_SMALLC) return fast_bn<OP_IM2COL_SMALLC, EPI_STORE>(p, z, s);
   if (amode == OP_IM2COL_TSM) return fast_bn<OP_IM2COL_TSM, EPI_STORE>(p, z, s);

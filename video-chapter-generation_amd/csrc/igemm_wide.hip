@@ -133,9 +133,9 @@ __device__ __forceinline__ void wide_wait(int ahead) {
 // (a "piece"), PA = BM / 64 A pieces and PB = BN / 64 B pieces per wave and k-step; 16-B chunk c of row r at slot
 // c ^ ((r >> 1) & 7) (fast_frag's swizzle, pre-applied on the global source address). The per-row offsets are computed
 // once per tile, so a piece is one select and one buffer_load ... lds.
-template <int BM, int BN>
+template <int BM, int BN, int NW = 8>
 struct WideLoader {
-  static constexpr int PA = BM / 64, PB = BN / 64, P = PA + PB, AE = BM * FBK;
+  static constexpr int PA = BM / (8 * NW), PB = BN / (8 * NW), P = PA + PB, AE = BM * FBK;
   __amdgpu_buffer_rsrc_t ra, rb;
   uint32_t oa, ob;  // offsets past the buffers' ranges: the load returns zeros
   int off[P];       // element offset of the piece row's chunk (k = 0), -1 = a row beyond M / N
@@ -164,27 +164,25 @@ struct WideLoader {
     bf16_t* slice = stage + (isa ? 0 : AE) + (wave * (isa ? PA : PB) + (isa ? Q : Q - PA)) * 512;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(isa ? ra : rb, (lds_void_t*)slice, 16, voff, 0, 0, 0);
   }
+  template <int Q = 0>
   __device__ __forceinline__ void all(int k0, int K, bf16_t* stage, int wave) const {
-    piece<0>(k0, K, stage, wave);
-    if constexpr (P > 1) piece<1>(k0, K, stage, wave);
-    if constexpr (P > 2) piece<2>(k0, K, stage, wave);
-    if constexpr (P > 3) piece<3>(k0, K, stage, wave);
-    if constexpr (P > 4) piece<4>(k0, K, stage, wave);
-    if constexpr (P > 5) piece<5>(k0, K, stage, wave);
-    static_assert(P <= 6, "pieces");
+    if constexpr (Q < P) {
+      piece<Q>(k0, K, stage, wave);
+      all<Q + 1>(k0, K, stage, wave);
+    }
   }
 };
 
-// ST stages (prefetch distance ST - 1). DC: where each group issues its LDS-DMA pieces of step s + ST - 1 -- 0 in its
-// read phase after the fragment reads, 1 in its compute phase between the two k32 halves, 2 in its compute phase one
-// piece every few MFMAs
-template <int BM, int BN, int WE, int ST, int DC>
+// ST = 3 stages (prefetch distance 2); each group issues its LDS-DMA pieces of step s + 2 in its read phase, after the
+// fragment reads. (Measured and rejected, profiles/r06_wide_engine_ab.txt: 4 stages, the pieces in the compute phase
+// -- between the two k32 halves or one every few MFMAs --, no s_setprio or the read phase at priority 1, no stagger,
+// and a 4-wave 64 x 96 form with in-wave software pipelining: all equal or slower.)
+template <int BM, int BN, int WE, int ST = 3>
 __global__ __launch_bounds__(512) void gemm_wide_kernel(GemmParams p) {
   constexpr int MT = BM / 32, NT = BN / 64;          // the wave's (BM / 2) x (BN / 4) sub-tile in 16 x 16 fragments
   constexpr int AE = BM * FBK, BE = BN * FBK, SE = AE + BE;
   constexpr int PIECES = BM / 64 + BN / 64;          // LDS-DMA instructions per wave per k-step
   constexpr int PF = ST - 1;
-  constexpr int NMF = 2 * MT * NT, SP = NMF / (PIECES + 1);  // MFMAs per phase; DC 2: a piece after every SP
   static_assert(ST * SE * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(1024))) bf16_t smem[ST * SE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -244,7 +242,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(GemmParams p) {
       istage = smem + (cur == 0 ? ST - 1 : cur - 1) * SE;
     }
     const int ik0 = ikt * FBK;
-    // ---- read phase: this k-step's fragments (and, DC 0, the DMA of step s + PF)
+    // ---- read phase: this k-step's fragments, the DMA of step s + PF
     W_STAMP(s, 0, 0);
     if (VCG_WIDE_ABL != 3 || s == 0) {
 #pragma unroll
@@ -255,7 +253,7 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(GemmParams p) {
         for (int i = 0; i < MT; ++i) af[i][s2] = fast_frag(Ac, grp * (BM / 2) + i * 16, lane, s2);
       }
     }
-    if (DC == 0 && pre && VCG_WIDE_ABL != 1) ld.all(ik0, p.K, istage, wave);
+    if (pre && VCG_WIDE_ABL != 1) ld.all(ik0, p.K, istage, wave);
     W_STAMP(s, 0, 1);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the reads have landed before the barrier (the other group
                                          // refills this stage PF - 1 phases from now)
@@ -263,40 +261,21 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(GemmParams p) {
     // waves 4-7 end their read phase with step s + 1 landed (their pieces of it); waves 0-3 read it after the
     // next barrier. Younger pieces in flight: steps s + 2 .. (the last issued)
     if (grp == 1 && s + 1 < steps && VCG_WIDE_ABL != 1)
-      wide_wait<PIECES>(min(s + (DC ? PF - 1 : PF), steps - 1) - (s + 1));
+      wide_wait<PIECES>(min(s + PF, steps - 1) - (s + 1));
     W_STAMP(s, 0, 3);
     __builtin_amdgcn_s_barrier();
     // ---- compute phase
     W_STAMP(s, 1, 0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    if (VCG_WIDE_ABL != 2) {
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+      for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          if (VCG_WIDE_ABL != 2)
+          for (int j = 0; j < NT; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j][s2], af[i][s2], acc[i][j], 0, 0, 0);
-          const int idx = (s2 * MT + i) * NT + j + 1;  // MFMAs issued so far
-          if (DC == 2 && idx % SP == 0 && idx / SP <= PIECES && pre && VCG_WIDE_ABL != 1) {
-            __builtin_amdgcn_sched_barrier(0);
-            switch (idx / SP - 1) {
-              case 0: ld.template piece<0>(ik0, p.K, istage, wave); break;
-              case 1: ld.template piece<1>(ik0, p.K, istage, wave); break;
-              case 2: ld.template piece<2 < PIECES ? 2 : 0>(ik0, p.K, istage, wave); break;
-              case 3: ld.template piece<3 < PIECES ? 3 : 0>(ik0, p.K, istage, wave); break;
-              case 4: ld.template piece<4 < PIECES ? 4 : 0>(ik0, p.K, istage, wave); break;
-              default: ld.template piece<5 < PIECES ? 5 : 0>(ik0, p.K, istage, wave); break;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      if (DC == 1 && s2 == 0 && pre && VCG_WIDE_ABL != 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        ld.all(ik0, p.K, istage, wave);
-        __builtin_amdgcn_sched_barrier(0);
-      }
     }
     __builtin_amdgcn_s_setprio(0);
     if (pre) advance();
@@ -359,29 +338,12 @@ int wide_bn_for(const GemmParams& p) {
   return best;
 }
 
-// pipeline variant (measurement aid, read per call): VCG_WIDE_PIPE = 10 * DC + stages (3 / 4); default 3
-int wide_pipe() {
-  const char* e = getenv("VCG_WIDE_PIPE");
-  const int v = e ? atoi(e) : 3;
-  return (v % 10 == 3 || v % 10 == 4) && v / 10 <= 2 ? v : 3;
-}
-
 template <int BN, int WE>
 void launch_wide(const GemmParams& p, hipStream_t s) {
   constexpr int BM = 128;
   const long long tiles = (long long)((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int grid = (int)(tiles < wide_cus() ? tiles : wide_cus());
-  int pipe = wide_pipe();
-  if (BN > 192) pipe = pipe / 10 * 10 + 3;  // (4 stages of 128 + 256 rows exceed the LDS)
-  const dim3 g(grid), b(512);
-  switch (pipe) {
-    case 4: if constexpr (BN <= 192) hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WE, 4, 0>), g, b, 0, s, p); break;
-    case 14: if constexpr (BN <= 192) hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WE, 4, 1>), g, b, 0, s, p); break;
-    case 24: if constexpr (BN <= 192) hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WE, 4, 2>), g, b, 0, s, p); break;
-    case 13: hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WE, 3, 1>), g, b, 0, s, p); break;
-    case 23: hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WE, 3, 2>), g, b, 0, s, p); break;
-    default: hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WE, 3, 0>), g, b, 0, s, p); break;
-  }
+  hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WE>), dim3(grid), dim3(512), 0, s, p);
 }
 
 template <int BN>

@@ -22,6 +22,10 @@
 // the slabs in a fixed order (deterministic) into the OIHW weight gradient.
 #include "igemm.h"
 
+#ifndef VCG_STEM_BWD_DBG
+#define VCG_STEM_BWD_DBG 0
+#endif
+
 namespace vcg {
 namespace {
 
@@ -401,11 +405,9 @@ VCG_API int vcg_stem_bwd_fused(const void* dy, const unsigned char* idx, const v
   a.sum_gx = sum_gx; a.inv_count = 1.f / (float)count; a.train = train_stats; a.ws = ws;
   a.N = N; a.H = H; a.W = W; a.OH = (H - 1) / 2 + 1; a.OW = (W - 1) / 2 + 1; a.tiles = N * (H / 2);
   const int grid = a.tiles < SB_GRID ? a.tiles : SB_GRID;
-  static const int dbg = getenv("VCG_STEM_BWD_DBG") ? atoi(getenv("VCG_STEM_BWD_DBG")) : 0;  // timing breakdown only
   if (census_on()) { char t_[96]; snprintf(t_, sizeof(t_), "stem_bwd_fused"); census_add(t_, a.N, a.H, a.W); }
-  if (dbg == 1) hipLaunchKernelGGL(stem_bwd_fused_kernel<1>, dim3(grid), dim3(SB_NTH), 0, s, a);
-  else if (dbg == 2) hipLaunchKernelGGL(stem_bwd_fused_kernel<2>, dim3(grid), dim3(SB_NTH), 0, s, a);
-  else hipLaunchKernelGGL(stem_bwd_fused_kernel<0>, dim3(grid), dim3(SB_NTH), 0, s, a);
+  // (timing breakdown: a -DVCG_STEM_BWD_DBG=1 / 2 build compiles one phase out, tools/bench_stem_bwd.py)
+  hipLaunchKernelGGL(stem_bwd_fused_kernel<VCG_STEM_BWD_DBG>, dim3(grid), dim3(SB_NTH), 0, s, a);
   VCG_LAUNCH_CHECK();
   hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(64 * SB_N / 4 / SR_Q), dim3(256), 0, s, ws, grid, dw, accumulate);
   VCG_LAUNCH_CHECK();

@@ -1299,11 +1299,7 @@ VCG_API int vcg_bn_relu_maxpool(int dtype, const void* y, const float* scale, co
   const int lcpr = ilog2i(C / VN);
   const long long TV = (long long)N * OH * OW * (C / VN);
   VCG_REQUIRE((long long)N * H * W < (1LL << 31), "too many pixels");
-  static const bool two = [] {
-    const char* e = getenv("VCG_MAXPOOL_PAIR");
-    return !(e && e[0] == '0');
-  }();
-  if (dtype == VCG_BF16 && two) {  // two outputs per thread (maxpool_fwd2_kernel)
+  if (dtype == VCG_BF16) {  // two outputs per thread (maxpool_fwd2_kernel)
     const int OW2 = (OW + 1) / 2;
     const long long TV2 = (long long)N * OH * OW2 * (C / VN);
     hipLaunchKernelGGL((maxpool_fwd2_kernel<bf16_t, true>), dim3(blocks_for(TV2, 256)), dim3(256), 0, s,

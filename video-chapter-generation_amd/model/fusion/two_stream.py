@@ -7,7 +7,6 @@ return_emb=False) -> (logits [B,2], prob [B,2]) (+ vision_emb [B,T,2048], lang_e
 accumulation and statistics); the default "fp32" is the parity mode.
 """
 import math
-import os
 
 import torch
 from torch import nn
@@ -119,7 +118,8 @@ class TwoStream(NativeRoot, nn.Module):
     def configure_optimizers(self, train_config):
         return configure_adamw(self, train_config)
 
-    overlap_streams = os.environ.get("VCG_OVERLAP", "1") != "0"
+    # BERT on a side HIP stream beside the trunk (bench.py --one-stream and the instrumented step set it False)
+    overlap_streams = True
 
     def _side_stream(self, dev):
         """The BERT side stream (None: one stream), created once per device."""

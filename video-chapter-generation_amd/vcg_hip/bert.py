@@ -9,7 +9,6 @@ batched PV) -> out-proj GEMM -> LN(dropout(.)+res) -> FFN1 GEMM with erf-GELU
 epilogue -> FFN2 GEMM -> LN(dropout(.)+res); pooler = tanh(W h[:,0] + b).
 """
 import math
-import os
 
 import torch
 
@@ -75,12 +74,15 @@ class _LinearT:
 
 
 class BertEncoderEngine:
+    # bf16 L <= 128: the fused attention kernels (bert_attn.hip); False: the unfused kernels (tests compare both)
+    fused_attn = True
+
     def __init__(self, model, flat, dtype):
         self.m = model
         self.flat = flat
         self.dtype = dtype
         self.wt = None
-        if dtype == torch.bfloat16 and flat is not None and os.environ.get("VCG_BERT_WT", "1") != "0":
+        if dtype == torch.bfloat16 and flat is not None:
             wt = getattr(model, "_vcg_bert_wt", None)
             if wt is None or wt.flat is not flat:
                 wt = _LinearT(model, flat, dtype)
@@ -88,9 +90,8 @@ class BertEncoderEngine:
             self.wt = wt
 
     def _fused_attn(self, L, dh):
-        # VCG_FUSED_ATTN=0: the unfused kernels (A/B and tests); the fp32 parity mode always runs unfused
-        return (self.dtype == torch.bfloat16 and L <= 128 and dh == 64
-                and os.environ.get("VCG_FUSED_ATTN", "1") != "0")
+        # (the fp32 parity mode always runs unfused)
+        return self.dtype == torch.bfloat16 and L <= 128 and dh == 64 and BertEncoderEngine.fused_attn
 
     def _w(self, p):
         return self.flat.compute_view(p, self.dtype)
@@ -100,8 +101,10 @@ class BertEncoderEngine:
         (QKV, FFN1 input gradients: K = 2304 / 3072, N = 768): W^T is materialised (tiled transpose) so the
         LDS-DMA GEMM reads both operands K-contiguous (measured 87 -> 61 us at K = 3072, 67 -> 53 us at
         K = 2304; no gain at K = 768, tools/bench_bert_gemm.py)."""
-        # (FFN2's input gradient: the fast engine's staged GELU' epilogue, the pre-activation read as full rows)
-        kw["act"] = kw.get("act", ops.ACT_NONE) | WIDE
+        # (FFN2's input gradient with the GELU' epilogue stays on the 128 x 128 engine, whose staged epilogue reads the
+        # pre-activation as full rows: 71 vs 82 us on the wide engine, profiles/r06_bert_gemm.txt)
+        if kw.get("act", ops.ACT_NONE) != ops.ACT_GELU_BWD:
+            kw["act"] = kw.get("act", ops.ACT_NONE) | WIDE
         wt = self.wt.get(W) if self.wt is not None else None
         if wt is not None:
             return ops.gemm(A, wt, M, N, K, K, K, **kw)

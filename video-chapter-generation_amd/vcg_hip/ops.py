@@ -574,10 +574,8 @@ IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
 def stem_cpad(dtype):
-    """Channels of the stem's NHWC input: bf16 -> 4 (RGB0, the pair-packed stem: two stride-2 taps per 16-B
-    chunk, vcg_conv_fwd) unless VCG_NO_STEM_PAIR=1 (8: one tap per chunk); fp32 -> 4."""
-    if dtype == torch.bfloat16 and os.environ.get("VCG_NO_STEM_PAIR", "0") == "1":
-        return 8
+    """Channels of the stem's NHWC input: 4 (RGB0; bf16: the pair-packed stem, two stride-2 taps per 16-B chunk,
+    vcg_conv_fwd)."""
     return 4
 
 

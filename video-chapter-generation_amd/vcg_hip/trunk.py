@@ -108,50 +108,50 @@ class ResNetTrunk:
     # the reference path the fused conv_dgrad_bwd engine is checked against (tests/test_gpu_bf16_train.py)
     fused_bwd = True
     # bf16 backward: the weight gradients run on a side stream (one per device, _WSTREAMS), concurrently with the
-    # input-gradient chain they branch off (each wgrad waits only for its dy); VCG_WGRAD_STREAM=0: one stream
-    wgrad_stream = os.environ.get("VCG_WGRAD_STREAM", "1") != "0"
-    # forward of a layer's first bottleneck: the downsample conv on the side stream (VCG_DS_STREAM=0: inline)
-    ds_stream = os.environ.get("VCG_DS_STREAM", "1") != "0"
+    # input-gradient chain they branch off (each wgrad waits only for its dy); False: one stream
+    wgrad_stream = True
+    # forward of a layer's first bottleneck: the downsample conv on the side stream (False: inline)
+    ds_stream = True
     # the first bottleneck of a layer: bn3's and the downsample BN's backward applies in one pass over g
-    dual_bn_bwd = os.environ.get("VCG_BN_DUAL", "1") != "0"
+    dual_bn_bwd = True
     # bf16 scoring forward (running-statistics BN, no autograd): bn3 folded into conv3 (1x1 GEMM with the BN scale in
     # the weight rows, the shift as bias, + identity, ReLU in the epilogue) -- no y3 tensor, no bn3 pass
-    fold_eval = os.environ.get("VCG_FOLD_BN", "1") != "0"
+    fold_eval = True
     # bf16 training backward: bn3's batch-statistics backward folded into conv3's two gradients (dy3 = A g + B y3 + C
     # is never stored: the input gradient is one GEMM over [g | y3], the weight gradient one GEMM with 2 C3 rows;
-    # ops.conv_dgrad_bwd_bnfold / conv_wgrad_bnfold); VCG_BN_FOLD=0: the bn_bwd_apply pass
-    bn_fold_bwd = os.environ.get("VCG_BN_FOLD", "1") != "0"
+    # ops.conv_dgrad_bwd_bnfold / conv_wgrad_bnfold); False: the bn_bwd_apply pass
+    bn_fold_bwd = True
     # ... for blocks with C3 <= this many channels (layers 1-3; layer 4's MFMA-bound conv3 gradients lose more to the
     # extra K than the pass costs: measured with the y3 drop, 78.6 vs 78.0 ms per step)
-    bn_fold_max_c3 = int(os.environ.get("VCG_BN_FOLD_MAXC3", "1024"))
+    bn_fold_max_c3 = 1024
     # ... with conv3's input a2 (C3 / 4 channels) as the second GEMM source instead of y3 (y3 = a2 w3^T: the input
     # gradient reads [g | a2] against [A w | w3^T diag(B) w3], the weight gradient is A (g^T a2) + B w3 (a2^T a2) + C
-    # colsum(a2)); VCG_BN_FOLD_A2=0: the y3 form
-    bn_fold_a2 = os.environ.get("VCG_BN_FOLD_A2", "1") != "0"
+    # colsum(a2)); False: the y3 form
+    bn_fold_a2 = True
     # ... and with both (non-first blocks): y3 is not stored at all -- conv3's forward GEMM keeps only the BN
     # statistics (ops.conv1x1_stats), the next block's conv1 dgrad reduces only sum g, and sum_gx comes from g^T a2
-    # (ops.bn_bwd_sumgx_from_wgrad), which is also the weight gradient's first product; VCG_Y3_DROP=0: stored
-    y3_drop = os.environ.get("VCG_Y3_DROP", "1") != "0"
+    # (ops.bn_bwd_sumgx_from_wgrad), which is also the weight gradient's first product; False: stored
+    y3_drop = True
     # batch-statistics forward of a non-first bottleneck with C3 <= this many channels: bn3 + identity + ReLU as a
     # second pass of conv3's GEMM (scale folded into its weight rows, shift as bias; ops.conv1x1_bn_res_relu)
     # instead of reading y3 back in the bn_apply pass (0: off)
-    bn3_gemm_max_c3 = int(os.environ.get("VCG_BN3_GEMM_MAXC3", "1024"))
+    bn3_gemm_max_c3 = 1024
     # bf16 batch statistics: the bn2 apply pass also returns colsum(a2) and a2^T a2 (ops.bn_apply_gram), from which
     # bn3's statistics follow where y3 is not stored (no statistics-only conv3 pass over a2) and the a2-form fold
     # takes its Gram term (no a2^T a2 GEMM in the backward); False: the conv3 statistics GEMM (tests compare both)
-    gram_stats = os.environ.get("VCG_GRAM_STATS", "1") != "0"
+    gram_stats = True
     # the stem BN-backward sums from the pooled activation (ops.maxpool_bwd_bn_sums_pooled) instead of a pass over
     # the pre-pool conv output; False: the per-pixel pass (tests compare both)
-    pooled_stem_sums = os.environ.get("VCG_POOLED_STEM_SUMS", "1") != "0"
+    pooled_stem_sums = True
     # the stem's BN-backward apply and conv1 weight gradient as one pass (ops.stem_bwd_fused); False: the apply pass
     # writes dy0 and the im2col weight-gradient GEMM reads it (tests compare both)
-    fused_stem_bwd = os.environ.get("VCG_FUSED_STEM_BWD", "1") != "0"
+    fused_stem_bwd = True
     # a y3-drop block's P = g^T a2 formed by the next block's streaming conv1 dgrad (layers 1-2); False: the weight-
     # gradient GEMM (tests compare both)
-    dgrad_p = os.environ.get("VCG_DGRAD_P", "1") != "0"
+    dgrad_p = True
     # bn3's statistics, finalize and the GEMM pass's folded weight as one launch (ops.bn_finalize_from_gram) where the
     # Gram statistics apply; False: bn_stats_from_gram + bn_finalize + weight_fold (tests compare both)
-    gram_fin = os.environ.get("VCG_GRAM_FIN", "1") != "0"
+    gram_fin = True
 
     def __init__(self, net, dtype):
         self.net = net
