@@ -24,6 +24,10 @@ extern "C" {
 
 #define VCG_API
 enum { VCG_F32 = 0, VCG_BF16 = 1 };
+/* vcg_ln_bwd / vcg_embed_ln_bwd dtype flag (VCG_BF16 | VCG_GRAD_F32): the incoming gradient dout and the residual
+   gradient dres are fp32 while x / res / dx stay bf16 -- BERT's residual-gradient stream kept in fp32 between its
+   LayerNorm backwards, as torch autocast keeps it (the LayerNorm outputs it flows back into are fp32 there) */
+enum { VCG_GRAD_F32 = 0x10 };
 enum { VCG_OK = 0, VCG_ERR_INVALID = -1, VCG_ERR_UNSUPPORTED = -2, VCG_ERR_HIP = -3 };
 enum { VCG_ACT_NONE = 0, VCG_ACT_RELU = 1, VCG_ACT_GELU = 2, VCG_ACT_TANH = 3, VCG_ACT_GELU_BWD = 4 };
 /* vcg_gemm act flag: with a residual, round alpha * AB + bias to the storage dtype BEFORE adding the residual (the
@@ -34,10 +38,13 @@ enum { VCG_ACT_FLAG_ROUND_PRE = 0x100 };
    512-thread workgroup per CU, persistent) -- BERT's Linear layers (transformers BertModel, model/lang/bert_hugface.py:20)
    and the trunk's stride-2 downsample input gradient set it. Taken, whatever M, for bf16 GEMMs with K-contiguous
    operands (transA = transB = 0), alpha = 1 and 16-B aligned rows whose epilogue is a bias (act NONE), bias + GELU
-   (aux: the pre-activation, rounded to bf16 before the GELU as bf16 autocast does), GELU' of a residual, or a
+   (aux: the bf16 pre-activation; the GELU of the unrounded value, as the 128 x 128 engine), GELU' of a residual, or a
    residual addend (residual != C); any other flagged GEMM runs on the 128 x 128 engine (vcg_gemm_census shows which
    ran). */
 enum { VCG_ACT_FLAG_WIDE = 0x200 };
+/* vcg_gemm act flag with VCG_ACT_FLAG_WIDE and a residual: the residual and the output C are fp32 (the operands bf16):
+   BERT's input gradients added to its fp32 residual-gradient stream (C = A B^T + residual, one rounding to fp32) */
+enum { VCG_ACT_FLAG_F32_OUT = 0x400 };
 /* GEMM census (tests, bench.py): while enabled, every GEMM dispatch of vcg_gemm / vcg_gemm_splitk / the conv entry
    points adds one to the count of its key "<engine> M=.. N=.. K=.. <epilogue>"; enabling (or disabling) clears it.
    vcg_gemm_census_size returns the number of keys; vcg_gemm_census_get(i) writes key i (NUL-terminated, at most n

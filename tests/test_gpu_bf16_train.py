@@ -425,6 +425,8 @@ def test_full_res_train_step_vs_oracle():
         eac = np.array([_rel(ga[n], g64[n]) for n in names])
         print(f"{group}: grad rel err vs exact median / p90: native bf16 {np.median(e16):.2e} / "
               f"{np.quantile(e16, 0.9):.2e}, autocast bf16 {np.median(eac):.2e} / {np.quantile(eac, 0.9):.2e}")
+        worst = sorted(zip(e16, eac, names), key=lambda t: -t[0])[:10]
+        print(f"{group} worst:", [(n.split(".", 1)[1][-40:], f"{a:.2e}", f"{b:.2e}") for a, b, n in worst])
         floor = {"vision_model": 1e-2, "lang_model": 0.0, "fusion_head": 5e-2}[group]
         assert np.median(e16) <= max(1.5 * np.median(eac), floor), group
         assert np.quantile(e16, 0.9) <= max(1.5 * np.quantile(eac, 0.9), 2 * floor), group

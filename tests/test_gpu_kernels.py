@@ -680,6 +680,34 @@ def test_layernorm_fwd_bwd(K, dtype, H, rows):
     _close(cs - 0.25, dx.double().sum(0), torch.float32, "colsum")
 
 
+@pytest.mark.parametrize("H,rows", [(768, 37), (768, 2085), (512, 300)])
+def test_layernorm_bwd_fp32_gradient_stream(K, H, rows):
+    """LN backward with bf16 x / res and an fp32 incoming gradient (VCG_GRAD_F32, BERT's fp32 residual-gradient
+    stream): dres comes back fp32 and dx bf16; both closer to float64 autograd than the all-bf16 call on the
+    bf16-rounded gradient (dres to fp32 rounding of the same arithmetic), dgamma / dbeta likewise."""
+    x = _rand((rows, H), torch.bfloat16, 171)
+    r = _rand((rows, H), torch.bfloat16, 172)
+    g0 = torch.Generator().manual_seed(173)
+    gamma = torch.rand(H, generator=g0) + 0.5
+    beta = torch.randn(H, generator=g0) * 0.1
+    dout = torch.randn(rows, H, generator=g0)  # fp32
+    xd, rd = x.double().requires_grad_(), r.double().requires_grad_()
+    y = F.layer_norm(xd + rd, (H,), gamma.double(), beta.double(), eps=1e-12)
+    dx_ref, dr_ref = torch.autograd.grad(y, (xd, rd), dout.double())
+    _, mean, rstd = K.ln_fwd(x.to(DEV), r.to(DEV), gamma.to(DEV), beta.to(DEV), rows, H, 1e-12)
+    res = {}
+    for tag, d in (("f32", dout.to(DEV)), ("bf16", dout.to(torch.bfloat16).to(DEV))):
+        gg, gb = torch.zeros(H, device=DEV), torch.zeros(H, device=DEV)
+        dx, dres = K.ln_bwd(d, x.to(DEV), r.to(DEV), gamma.to(DEV), mean, rstd, gg, gb, rows, H)
+        res[tag] = (dx, dres)
+    dx32, dres32 = res["f32"]
+    assert dx32.dtype == torch.bfloat16 and dres32.dtype == torch.float32
+    e = {t: ((res[t][1].double().cpu() - dr_ref).norm() / dr_ref.norm()).item() for t in res}
+    assert e["f32"] < 1e-5, e  # the fp32 stream: fp32 rounding only
+    assert e["f32"] < 0.1 * e["bf16"], e
+    _close(dx32, dx_ref, torch.bfloat16, "ln bwd dx (fp32 dout)")
+
+
 def test_maxpool_bwd_bn(K):
     """maxpool backward fused with the stem BN mask + reduction == maxpool_bwd, masked; sums in float64."""
     dtype = torch.bfloat16

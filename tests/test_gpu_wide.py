@@ -72,8 +72,9 @@ def test_forward_bias(M, N, K):
 
 @pytest.mark.parametrize("M", [R, 128])
 def test_ffn1_gelu_aux(M):
-    """pre = bf16(x W^T + b) (the pre-activation the backward keeps), out = bf16(gelu(pre)): pre within bf16
-    rounding of float64, out equal to the float64 GELU of the stored pre within one bf16 ulp."""
+    """pre = bf16(x W^T + b) (the pre-activation the backward keeps), out = bf16(gelu(x W^T + b)) of the unrounded
+    value: pre within bf16 rounding of float64, out equal to the float64 GELU of the exact pre-activation within bf16
+    rounding, and to the 128 x 128 engine's fused epilogue within one bf16 ulp."""
     gen = torch.Generator().manual_seed(11 + M)
     A, W = _bf((M, H), gen), _bf((I, H), gen, 0.02)
     b = (torch.randn(I, generator=gen) * 0.1).to(DEV)
@@ -82,9 +83,11 @@ def test_ffn1_gelu_aux(M):
     assert keys and "we1" in keys[0], keys
     ref_pre = A.double() @ W.double().t() + b.double()
     assert _rel(pre, ref_pre) < 4e-3
-    g = _gelu64(pre.double())
-    err = (out.double() - g).abs()
-    assert (err <= g.abs() * 2.0 ** -7 + 1e-6).all(), err.max().item()
+    g = _gelu64(ref_pre)
+    assert _rel(out, g) < 4e-3
+    eng = ops.gemm(A, W, M, I, H, H, H, bias=b, act=ops.ACT_GELU)
+    err = (out.double() - eng.double()).abs()
+    assert (err <= eng.double().abs() * 2.0 ** -7 + 1e-6).all(), err.max().item()
     # no pre-activation copy: the same output
     out2 = ops.gemm(A, W, M, I, H, H, H, bias=b, act=ops.ACT_GELU | WIDE)
     torch.cuda.synchronize()
@@ -122,6 +125,24 @@ def test_input_gradient_residual(M, N, K):
     assert e_w < 1.5 * e_e + 4e-3
 
 
+@pytest.mark.parametrize("M", [R, 128])
+@pytest.mark.parametrize("N,K", [(H, I), (H, 3 * H)])
+def test_input_gradient_fp32_stream(M, N, K):
+    """dX + the fp32 residual-gradient stream, written fp32 (VCG_ACT_FLAG_F32_OUT): within fp32 rounding of
+    (bf16 operands' exact product + residual), i.e. far inside the bf16-output error."""
+    gen = torch.Generator().manual_seed(N + K + 5 * M)
+    dY, Wt = _bf((M, K), gen, 0.05), _bf((N, K), gen, 0.02)
+    r = (torch.randn(M, N, generator=gen) * 0.01).to(DEV)
+    out = torch.empty((M, N), dtype=torch.float32, device=DEV)
+    _, keys = _wide(lambda: ops.gemm(dY, Wt, M, N, K, K, K, out=out, ldc=N, residual=r, ldr=N,
+                                     act=WIDE | ops.ACT_FLAG_F32_OUT))
+    assert keys and "we4" in keys[0], keys
+    ref = dY.double() @ Wt.double().t() + r.double()
+    assert _rel(out, ref) < 1e-5
+    with pytest.raises(Exception):  # only with the wide flag and a residual
+        ops.gemm(dY, Wt, M, N, K, K, K, out=out, ldc=N, act=ops.ACT_FLAG_F32_OUT)
+
+
 @pytest.mark.parametrize("bn", ["128", "192", "256"])
 @pytest.mark.parametrize("M,N,K", [(1000, 200, 136), (130, 776, 72), (1, 8, 8), (4099, 1032, 520)])
 def test_ragged_all_widths(monkeypatch, bn, M, N, K):
@@ -142,14 +163,16 @@ def test_ragged_all_widths(monkeypatch, bn, M, N, K):
     assert _rel(o2, ref + r.double()) < 4e-3
 
 
-def test_tile_width_choice():
-    """The cost rule picks 192 columns at N = 768 / 2304 and 256 at N = 3072 (M = 8192), whatever was forced before."""
+@pytest.mark.parametrize("M", [R, 128, 1])
+def test_tile_width_choice(M):
+    """The tile width follows N alone (192 columns at N = 768 / 2304, 256 at N = 3072, 128 at the downsample's 256 /
+    512 / 1024), the same at every M."""
     gen = torch.Generator().manual_seed(3)
-    A = _bf((R, H), gen)
-    for N, bn in ((H, 192), (3 * H, 192), (I, 256)):
+    A = _bf((M, H), gen)
+    for N, bn in ((H, 192), (3 * H, 192), (I, 256), (256, 128), (512, 128), (1024, 128)):
         W = _bf((N, H), gen, 0.02)
-        _, keys = _wide(lambda: ops.gemm(A, W, R, N, H, H, H, act=WIDE))
-        assert keys == [f"gemm_wide 128x{bn} we0 M={R} N={N} K={H}"], keys
+        _, keys = _wide(lambda: ops.gemm(A, W, M, N, H, H, H, act=WIDE))
+        assert keys == [f"gemm_wide 128x{bn} we0 M={M} N={N} K={H}"], keys
 
 
 def test_unflagged_and_fp32_stay_off():

@@ -545,13 +545,14 @@ __global__ __launch_bounds__(256) void ln_fwd_rw_kernel(const T* __restrict__ x,
 
 // LN backward, rows strided over the grid's waves; per-block column partials part[block][NRED][H]:
 // dgamma (sum dout * xhat), dbeta (sum dout) and (NRED = 3) the column sums of dx (the bias gradient of the
-// dense layer in front of the LayerNorm).
-template <typename T, int NQ, int NRED>
-__global__ __launch_bounds__(256) void ln_bwd_rw_kernel(const T* __restrict__ dout, const T* __restrict__ x,
+// dense layer in front of the LayerNorm). TD: the storage type of the incoming gradient dout and the residual
+// gradient dres (fp32 for BERT's bf16 residual-gradient stream, as torch autocast keeps it), T that of x / res / dx.
+template <typename T, typename TD, int NQ, int NRED>
+__global__ __launch_bounds__(256) void ln_bwd_rw_kernel(const TD* __restrict__ dout, const T* __restrict__ x,
                                                         const T* __restrict__ res, const float* __restrict__ gamma,
                                                         const float* __restrict__ mean_in,
                                                         const float* __restrict__ rstd_in, T* __restrict__ dx,
-                                                        T* __restrict__ dres, float* __restrict__ part, int rows,
+                                                        TD* __restrict__ dres, float* __restrict__ part, int rows,
                                                         float p, uint64_t seed) {
   constexpr int H = 256 * NQ;
   __shared__ float red[4][NRED][H];
@@ -576,7 +577,7 @@ __global__ __launch_bounds__(256) void ln_bwd_rw_kernel(const T* __restrict__ do
       const int c = 4 * (lane + 64 * q);
       ld4<T>(x + rb + c, nx[q]);
       if (res) ld4<T>(res + rb + c, nr[q]);
-      ld4<T>(dout + rb + c, nd[q]);
+      ld4<TD>(dout + rb + c, nd[q]);
     }
   };
   if (blockIdx.x * 4 + wave < rows) load_row(blockIdx.x * 4 + wave);
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(256) void ln_bwd_rw_kernel(const T* __restrict__ do
         od[i] = (p > 0.f) ? (((kb >> (4 * q + i)) & 1u) ? o[i] / (1.f - p) : 0.f) : o[i];
         if (NRED > 2) pd[q][i] += bf_round<T>(od[i]);
       }
-      if (dres) st4<T>(dres + rb + c, o);
+      if (dres) st4<TD>(dres + rb + c, o);
       if (dx) st4<T>(dx + rb + c, od);
     }
   }
@@ -804,6 +805,7 @@ VCG_API int vcg_embed_ln_bwd(int dtype, const void* dout, const long long* ids, 
   const int rows = B * L;
   VCG_REQUIRE(ws_bytes >= vcg_ln_bwd_ws_bytes(rows, H), "workspace too small");
   VCG_REQUIRE(H <= SCAT_MAXE * 256, "hidden size > 1024 not supported by the word-grad reduction");
+  if (dtype & VCG_GRAD_F32) dtype = VCG_F32;  // (only dout is read in the storage dtype here)
   int rpb;
   const int nb = row_blocks(rows, &rpb);
   float* part = ws;
@@ -870,28 +872,34 @@ VCG_API int vcg_ln_bwd(int dtype, const void* dout, const void* x, const void* r
                        const float* mean, const float* rstd, void* dx, void* dres, float* gamma_grad,
                        float* beta_grad, float* bias_grad, float* ws, long long ws_bytes, int rows, int H,
                        float dropout_p, unsigned long long seed, hipStream_t s) {
+  const bool g32 = (dtype & VCG_GRAD_F32) != 0;  // dout / dres in fp32 (bf16 x / res / dx)
+  dtype &= ~VCG_GRAD_F32;
+  VCG_REQUIRE(!g32 || (dtype == VCG_BF16 && H % 256 == 0 && H <= 1024), "VCG_GRAD_F32: bf16 with H % 256 == 0, <= 1024");
   int rpb;
   const int nb = row_blocks(rows, &rpb);
   VCG_REQUIRE(ws_bytes >= (long long)nb * 2 * H * 4, "workspace too small");
   VCG_REQUIRE(!bias_grad || dx, "bias_grad is the column sum of dx");
   const int nq = H % 256 == 0 ? H / 256 : 0;
   const int nbr = (rows + 3) / 4 < 256 ? (rows + 3) / 4 : 256;  // one wave per row, <= 8 rows per wave at 8192
-  if (nq >= 1 && nq <= 4 && rows > 0 && (long long)nbr * 3 * H <= (long long)nb * 2 * H) {
+  if (nq >= 1 && nq <= 4 && rows > 0 && ((long long)nbr * 3 * H <= (long long)nb * 2 * H || g32)) {
     const int nred = bias_grad ? 3 : 2;
-#define VCG_LNB(T, NQ, NR)                                                                                        \
-  hipLaunchKernelGGL((ln_bwd_rw_kernel<T, NQ, NR>), dim3(nbr), dim3(256), 0, s, (const T*)dout, (const T*)x,         \
-                     (const T*)res, gamma, mean, rstd, (T*)dx, (T*)dres, ws, rows, dropout_p, (uint64_t)seed)
-#define VCG_LNB_Q(T, NR)                     \
-  switch (nq) {                              \
-    case 1: VCG_LNB(T, 1, NR); break;        \
-    case 2: VCG_LNB(T, 2, NR); break;        \
-    case 3: VCG_LNB(T, 3, NR); break;        \
-    default: VCG_LNB(T, 4, NR); break;       \
+    VCG_REQUIRE((long long)nbr * nred * H * 4 <= ws_bytes, "workspace too small");
+#define VCG_LNB(T, TD, NQ, NR)                                                                                     \
+  hipLaunchKernelGGL((ln_bwd_rw_kernel<T, TD, NQ, NR>), dim3(nbr), dim3(256), 0, s, (const TD*)dout, (const T*)x,   \
+                     (const T*)res, gamma, mean, rstd, (T*)dx, (TD*)dres, ws, rows, dropout_p, (uint64_t)seed)
+#define VCG_LNB_Q(T, TD, NR)                     \
+  switch (nq) {                                  \
+    case 1: VCG_LNB(T, TD, 1, NR); break;        \
+    case 2: VCG_LNB(T, TD, 2, NR); break;        \
+    case 3: VCG_LNB(T, TD, 3, NR); break;        \
+    default: VCG_LNB(T, TD, 4, NR); break;       \
   }
-    if (dtype == VCG_BF16) {
-      if (nred == 3) { VCG_LNB_Q(bf16_t, 3) } else { VCG_LNB_Q(bf16_t, 2) }
+    if (dtype == VCG_BF16 && g32) {
+      if (nred == 3) { VCG_LNB_Q(bf16_t, float, 3) } else { VCG_LNB_Q(bf16_t, float, 2) }
+    } else if (dtype == VCG_BF16) {
+      if (nred == 3) { VCG_LNB_Q(bf16_t, bf16_t, 3) } else { VCG_LNB_Q(bf16_t, bf16_t, 2) }
     } else {
-      if (nred == 3) { VCG_LNB_Q(float, 3) } else { VCG_LNB_Q(float, 2) }
+      if (nred == 3) { VCG_LNB_Q(float, float, 3) } else { VCG_LNB_Q(float, float, 2) }
     }
 #undef VCG_LNB_Q
 #undef VCG_LNB

@@ -27,6 +27,7 @@ void census_add(const char* tag, long long M, long long N, long long K);
 }  // namespace vcg
 
 enum vcg_dtype { VCG_F32 = 0, VCG_BF16 = 1 };
+enum { VCG_GRAD_F32 = 0x10 };  // vcg_ln_bwd / vcg_embed_ln_bwd dtype flag (include/vcg_hip.h)
 enum vcg_status {
   VCG_OK = 0,
   VCG_ERR_INVALID = -1,

@@ -17,6 +17,7 @@ enum { EPI_STORE = 0, EPI_STATS = 1, EPI_SPLITK = 2, EPI_BWD = 3, EPI_BWD_AFF = 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_GELU_BWD = 4 };
 enum { ACT_FLAG_ROUND_PRE = 0x100 };  // = VCG_ACT_FLAG_ROUND_PRE (include/vcg_hip.h)
 enum { ACT_FLAG_WIDE = 0x200 };       // = VCG_ACT_FLAG_WIDE: run this GEMM on the wide-tile engine (igemm_wide.hip)
+enum { ACT_FLAG_F32_OUT = 0x400 };    // = VCG_ACT_FLAG_F32_OUT: fp32 residual and output (wide engine, bf16 operands)
 
 template <typename T> struct Cfg;
 template <> struct Cfg<float> { static constexpr int VEC = 4, BK = 16, LDK = 20; };   // 80-B rows
@@ -299,6 +300,7 @@ int fast_grid_rows(int M, int N, int z, int epi);
 bool fast_bwd_streams(const GemmParams& p);  // a dense EPI_BWD GEMM runs on the streaming kernel (P product: only there)
 // igemm_wide.hip: the wide-tile engine's epilogue class for a dense bf16 GEMM (-1: not supported) and its launch
 int wide_gemm_class(const GemmParams& p);
+int wide_gemm_class_f32(const GemmParams& p);  // the fp32-residual / fp32-output class (ACT_FLAG_F32_OUT), or -1
 int run_gemm_wide(GemmParams& p, int we, hipStream_t s);
 int fast_bwd_slots(const GemmParams& p);  // partial-sum slots (grid rows) of an EPI_BWD launch of run_fast_gemm
 int bn_bwd_finalize_launch(const float* partial, int nb, int C, long long ld, int gx_off, float* sum_g, float* sum_gx,

@@ -1487,9 +1487,12 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
   p.b = transB ? dense_op(B, ldb, K, N, esz) : dense_op(B, ldb, N, K, esz);
   p.a.rows = M;
   p.b.rows = N;
-  VCG_REQUIRE((act & ~(0xff | ACT_FLAG_ROUND_PRE | ACT_FLAG_WIDE)) == 0, "unknown act flags");
+  VCG_REQUIRE((act & ~(0xff | ACT_FLAG_ROUND_PRE | ACT_FLAG_WIDE | ACT_FLAG_F32_OUT)) == 0, "unknown act flags");
   const bool wide = (act & ACT_FLAG_WIDE) != 0 && dtype == VCG_BF16 && !transA && !transB;
-  act &= ~ACT_FLAG_WIDE;
+  const bool f32out = (act & ACT_FLAG_F32_OUT) != 0;
+  VCG_REQUIRE(!f32out || (wide && residual && (act & 0xff) == 0 && !aux && alpha == 1.f),
+              "VCG_ACT_FLAG_F32_OUT: a wide-engine bf16 GEMM with a residual addend only");
+  act &= ~(ACT_FLAG_WIDE | ACT_FLAG_F32_OUT);
   p.C = C; p.ldc = ldc; p.bias = bias; p.act = act & 0xff; p.residual = residual; p.ldr = ldr; p.aux = aux;
   p.res_round = (act & ACT_FLAG_ROUND_PRE) != 0 && residual != nullptr;
   p.alpha = alpha;
@@ -1497,7 +1500,8 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
   // the oracle-anchored B = 1 step runs the kernels of the B = 64 bench
   if (wide) {
     p.fast_act = fast_gelu_enabled();
-    const int we = wide_gemm_class(p);
+    const int we = f32out ? wide_gemm_class_f32(p) : wide_gemm_class(p);
+    VCG_REQUIRE(!f32out || we >= 0, "VCG_ACT_FLAG_F32_OUT: unsupported shape / alignment");
     if (we >= 0) {
       if (FILE* f = gemm_log()) {
         fprintf(f, "wide M=%d N=%d K=%d we=%d\n", M, N, K, we);

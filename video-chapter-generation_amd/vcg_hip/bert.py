@@ -96,7 +96,7 @@ class BertEncoderEngine:
     def _w(self, p):
         return self.flat.compute_view(p, self.dtype)
 
-    def _gemm_dx(self, A, W, M, N, K, **kw):
+    def _gemm_dx(self, A, W, M, N, K, f32_out=False, **kw):
         """A [M, K] @ W [K, N] (W = a Linear weight [out=K, in=N]: the input gradient). bf16 with a long K
         (QKV, FFN1 input gradients: K = 2304 / 3072, N = 768): W^T is materialised (tiled transpose) so the
         LDS-DMA GEMM reads both operands K-contiguous (measured 87 -> 61 us at K = 3072, 67 -> 53 us at
@@ -106,6 +106,10 @@ class BertEncoderEngine:
         if kw.get("act", ops.ACT_NONE) != ops.ACT_GELU_BWD:
             kw["act"] = kw.get("act", ops.ACT_NONE) | WIDE
         wt = self.wt.get(W) if self.wt is not None else None
+        if f32_out:  # + the fp32 residual-gradient stream, written in fp32 (bf16: W^T is resident)
+            kw["act"] |= ops.ACT_FLAG_F32_OUT
+            return ops.gemm(A, wt, M, N, K, K, K, out=torch.empty((M, N), dtype=torch.float32, device=A.device),
+                            ldc=N, **kw)
         if wt is not None:
             return ops.gemm(A, wt, M, N, K, K, K, **kw)
         if self.dtype == torch.bfloat16 and K >= 2 * N:
@@ -183,10 +187,15 @@ class BertEncoderEngine:
         rows = B * L
         p_h, p_a, scale, seed = sv["p_h"], sv["p_a"], sv["scale"], sv["seed"]
         dev = sv["ids"].device
+        # the residual-gradient stream (the gradient w.r.t. each LayerNorm output, summed over the skip and the next
+        # layer's input gradient) stays fp32 between the LayerNorm backwards, as torch autocast keeps it (its
+        # LayerNorm outputs are fp32): bf16 roundings of it compounded over 24 LayerNorms
+        g32 = dt == torch.bfloat16 and self.wt is not None
+        gd = torch.float32 if g32 else dt
         if d_last is not None:
-            dh_ = d_last.to(dt).contiguous().clone()
+            dh_ = d_last.to(gd).contiguous().clone()
         else:
-            dh_ = torch.zeros((rows, H), dtype=dt, device=dev)
+            dh_ = torch.zeros((rows, H), dtype=gd, device=dev)
         if d_pooled is not None and m.pooler is not None:
             pd = m.pooler.dense
             dpp = ops.tanh_bwd(d_pooled.to(dt).contiguous(), sv["pooled"])
@@ -194,8 +203,9 @@ class BertEncoderEngine:
             if pd.weight.requires_grad:
                 ops.gemm_splitk(dpp, h_last, pd.weight.grad, H, H, B, H, L * H, transA=True, transB=True)
                 ops.colsum(dpp, H, B, H, pd.bias.grad)
-            # dh[b*L] += dpp @ Wp
-            ops.gemm(dpp, self._w(pd.weight), B, H, H, H, H, transB=True, out=dh_, ldc=L * H, residual=dh_, ldr=L * H)
+            # dh[b*L] += dpp @ Wp (B rows: an fp32 GEMM on the fp32 stream)
+            dpw = (dpp.float(), pd.weight.data) if g32 else (dpp, self._w(pd.weight))
+            ops.gemm(dpw[0], dpw[1], B, H, H, H, H, transB=True, out=dh_, ldc=L * H, residual=dh_, ldr=L * H)
             if hooks is not None:
                 hooks(list(m.pooler.parameters()))
         for i in reversed(range(len(sv["layers"]))):
@@ -212,7 +222,7 @@ class BertEncoderEngine:
             del dfo
             ops.gemm_splitk(dpre, s["h1"], inter.weight.grad, I, H, rows, I, H, transA=True, transB=True)
             ops.colsum(dpre, I, rows, I, inter.bias.grad)
-            dh1 = self._gemm_dx(dpre, self._w(inter.weight), rows, H, I, residual=dh1_res, ldr=H)
+            dh1 = self._gemm_dx(dpre, self._w(inter.weight), rows, H, I, f32_out=g32, residual=dh1_res, ldr=H)
             del dpre, dh1_res
             ln1 = at.output.LayerNorm
             od = at.output.dense
@@ -233,7 +243,7 @@ class BertEncoderEngine:
                 ops.gemm_splitk(dqkv, s["h"], gW, 3 * H, H, rows, 3 * H, H, transA=True, transB=True)
                 ops.colsum(dqkv, 3 * H, rows, 3 * H, gb)
             Wqkv = flat.compute_contiguous([sq.weight, sk.weight, svv.weight], (3 * H, H), dt)
-            dh_ = self._gemm_dx(dqkv, Wqkv, rows, H, 3 * H, residual=dh_res, ldr=H)
+            dh_ = self._gemm_dx(dqkv, Wqkv, rows, H, 3 * H, f32_out=g32, residual=dh_res, ldr=H)
             del dqkv, dh_res, s
             if hooks is not None:
                 hooks(list(layer.parameters()))

@@ -14,6 +14,8 @@ F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_GELU_BWD = 0, 1, 2, 3, 4
 ACT_FLAG_ROUND_PRE = 0x100  # gemm: round alpha*AB + bias to the storage dtype before the residual (vcg_hip.h)
 ACT_FLAG_WIDE = 0x200  # gemm: the wide-tile engine (BERT's Linear layers, the downsample dgrad; vcg_hip.h VCG_ACT_FLAG_WIDE)
+ACT_FLAG_F32_OUT = 0x400  # gemm (wide, bf16 operands): fp32 residual and output (vcg_hip.h VCG_ACT_FLAG_F32_OUT)
+GRAD_F32 = 0x10  # ln_bwd dtype flag: fp32 dout / dres beside bf16 x / res / dx (vcg_hip.h VCG_GRAD_F32)
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -721,12 +723,18 @@ def ln_fwd(x, res, gamma, beta, rows, H, eps, p=0.0, seed=0):
 def ln_bwd(dout, x, res, gamma, mean, rstd, gamma_grad, beta_grad, rows, H, p=0.0, seed=0, want_dx=True,
            want_dres=True, bias_grad=None):
     """LayerNorm(dropout(x) + res) backward. bias_grad (optional, accumulated): column sums of dx, i.e. the
-    bias gradient of the dense layer that produced x."""
-    dx = torch.empty_like(dout) if want_dx else None
+    bias gradient of the dense layer that produced x. dx has x's dtype, dres dout's: a bf16 x with an fp32 dout keeps
+    the residual gradient in fp32 (VCG_GRAD_F32)."""
+    dx = torch.empty_like(x) if want_dx else None
     dres = torch.empty_like(dout) if want_dres else None
     nbytes = _lib.query("vcg_ln_bwd_ws_bytes", rows, H)
     w = ws(nbytes, dout.device)
-    _lib.call("vcg_ln_bwd", dt_code(dout.dtype), P(dout), P(x), P(res), P(gamma), P(mean), P(rstd), P(dx), P(dres),
+    code = dt_code(x.dtype)
+    if dout.dtype != x.dtype:
+        if not (x.dtype == torch.bfloat16 and dout.dtype == torch.float32):
+            raise TypeError(f"ln_bwd: dout {dout.dtype} with x {x.dtype}")
+        code |= GRAD_F32
+    _lib.call("vcg_ln_bwd", code, P(dout), P(x), P(res), P(gamma), P(mean), P(rstd), P(dx), P(dres),
               P(gamma_grad), P(beta_grad), P(bias_grad), P(w), w.numel() * 4, rows, H, float(p),
               int(seed) & (2**64 - 1), stream())
     return dx, dres
