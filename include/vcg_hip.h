@@ -273,7 +273,8 @@ VCG_API int vcg_attn_softmax_fwd(int dtype, const void* S, const long long* mask
 VCG_API int vcg_attn_softmax_bwd(int dtype, const void* dPd, const void* P, void* dS, int Z, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
 /* fused self-attention (bert_attn.hip), bf16, L <= 128, head dim 64: ctx = dropout(softmax(scale QK^T + mask)) V
    per (sequence, head) in one workgroup, nothing L x L in HBM; stats [B*nh][128] float2 (row max, 1 / row sum)
-   for the backward, which recomputes P and writes dQ | dK | dV into dqkv [B*L][3*H]. Same semantics and dropout
+   for the backward, which recomputes P and writes dQ | dK | dV into dqkv [B*L][3*H] (its ctx argument may be
+   NULL: the row term rowsum(dP o P) comes from the fp32 products, not from the forward's output). Same semantics and dropout
    mask as vcg_attn_softmax_fwd/bwd + the batched GEMMs (HF BertSelfAttention, bert_hugface.py:20). */
 VCG_API int vcg_bert_attn_fwd(const void* qkv, const long long* mask, void* ctx, void* stats, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API int vcg_bert_attn_bwd(const void* qkv, const void* dctx, const void* ctx, const long long* mask, const void* stats, void* dqkv, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);

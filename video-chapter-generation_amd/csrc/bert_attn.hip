@@ -4,7 +4,9 @@
 //   forward : S = Q K^T, P = softmax(scale * S + mask_add) (a row with no valid key is uniform over the L keys, as
 //             HF's finfo.min bias gives), Pd = dropout(P), ctx = Pd V; saved: (row max, 1 / row sum) per query
 //   backward: S and P recomputed from Q, K and the saved row statistics, dPd = dO V^T, dP = dropout'(dPd),
-//             D = rowsum(dO o O) (= rowsum(dP o P)), dS = scale * P o (dP - D); dQ = dS K, dK = dS^T Q, dV = Pd^T dO
+//             D = rowsum(dP o P) from the fp32 products (not rowsum(dO o O) of the bf16-rounded ctx: the same dP
+//             then enters both terms of dP - D, so each dS row sums to zero as the exact softmax gradient does and the
+//             rounding of O does not leak into dQ / dK), dS = scale * P o (dP - D); dQ = dS K, dK = dS^T Q, dV = Pd^T dO
 //
 // Nothing of size L x L touches HBM (the unfused path writes S, P and Pd per layer and reads them back): the
 // forward reads Q, K, V once and writes ctx; the backward reads Q, K, V, dO, O once and writes dQ, dK, dV.
@@ -210,10 +212,9 @@ __global__ __launch_bounds__(256) void bert_attn_fwd_kernel(const bf16_t* __rest
 // ------------------------------------------------------------------------------------------------ backward
 // 4 waves; wave w owns keys 32 w .. 32 w + 31 for S, dPd, dV and dK (A = Q / dO rows, Q^T / dO^T from LDS, B = the
 // wave's K / V rows from HBM, and its P / dS fragments from registers), then queries 32 w .. 32 w + 31 for dQ
-// (A = K^T from LDS, B = dS rows from the LDS copy every wave wrote).
+// (A = K^T from LDS, B = dS rows from the LDS copy every wave wrote). The forward's ctx is not read.
 __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __restrict__ qkv,
                                                             const bf16_t* __restrict__ dctx,
-                                                            const bf16_t* __restrict__ ctx,
                                                             const long long* __restrict__ mask,
                                                             const float2* __restrict__ stats,
                                                             bf16_t* __restrict__ dqkv, int nh, int L, int Lp,
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
   __shared__ __attribute__((aligned(16))) bf16_t Kt[DH * TP];
   __shared__ __attribute__((aligned(16))) bf16_t dSm[LT * TP];
   __shared__ float2 st[LT];
-  __shared__ float Dq[LT];
+  __shared__ float Dp[4 * LT];  // per-wave partial rowsum(dP o P) over the wave's 32 keys
   __shared__ uint8_t kval[LT];
   const int z = blockIdx.x, b = z / nh, h = z - b * nh;
   const int H = nh * DH;
@@ -233,29 +234,11 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const bf16_t* base = qkv + (long long)b * L * ld + h * DH;
   const bf16_t* dob = dctx + (long long)b * L * H + h * DH;
-  const bf16_t* ob = ctx + (long long)b * L * H + h * DH;
   bf16_t* gq = dqkv + (long long)b * L * ld + h * DH;
 
   load_transpose(base, ld, L, Qt, Qs, tid);
   load_transpose(dob, H, L, dOt, dOs, tid);
   load_transpose(base + H, ld, L, Kt, nullptr, tid);
-  {
-    // D[q] = dO[q] . O[q] (two threads per query, 32 elements each)
-    const int q = tid >> 1, hf = tid & 1;
-    float acc = 0.f;
-    if (q < L) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float x[8], y[8];
-        load16<bf16_t>(dob + (long long)q * H + 32 * hf + 8 * c, x);
-        load16<bf16_t>(ob + (long long)q * H + 32 * hf + 8 * c, y);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc = fmaf(x[e], y[e], acc);
-      }
-    }
-    acc += __shfl_xor(acc, 1, 64);
-    if (hf == 0) Dq[q] = acc;
-  }
   if (tid < LT) {
     kval[tid] = tid < L && (mask == nullptr || mask[(long long)b * L + tid] != 0);
     st[tid] = tid < L ? stats[(long long)z * LT + tid] : make_float2(0.f, 0.f);
@@ -297,14 +280,15 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
     keyi[kt] = 32 * w + 16 * kt + i;
     kv[kt] = kval[keyi[kt]] != 0;
   }
+  uint64_t keepb = 0;  // bit 8 qt + 2 r + kt: element (query 16 qt + 4 g + r, key keyi[kt]) kept by dropout
 #pragma unroll
   for (int qt = 0; qt < 8; ++qt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = 16 * qt + 4 * g + r;
       const float2 mi = st[q];
-      const float D = Dq[q];
       const uint64_t rowi = ((uint64_t)z * L + q) * (uint64_t)Lp;
+      float part = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         const int key = keyi[kt];
@@ -315,10 +299,31 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
         }
         const bool keep = q < L && key < L && dropout_keep(seed, rowi + key, p);
         const float dP = keep ? pacc[qt][kt][r] * rs : 0.f;
-        sacc[qt][kt][r] = keep ? P * rs : 0.f;            // Pd
-        const float dS = scale * P * (dP - D);
+        keepb |= keep ? (1ull << (8 * qt + 2 * r + kt)) : 0ull;
+        sacc[qt][kt][r] = P;
+        pacc[qt][kt][r] = dP;
+        part = fmaf(P, dP, part);
+      }
+      part += __shfl_xor(part, 1, 64);
+      part += __shfl_xor(part, 2, 64);
+      part += __shfl_xor(part, 4, 64);
+      part += __shfl_xor(part, 8, 64);
+      if (i == 0) Dp[w * LT + q] = part;
+    }
+  __syncthreads();  // Dp complete
+#pragma unroll
+  for (int qt = 0; qt < 8; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = 16 * qt + 4 * g + r;
+      const float D = (Dp[q] + Dp[LT + q]) + (Dp[2 * LT + q] + Dp[3 * LT + q]);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const float P = sacc[qt][kt][r];
+        const float dS = scale * P * (pacc[qt][kt][r] - D);
+        sacc[qt][kt][r] = ((keepb >> (8 * qt + 2 * r + kt)) & 1ull) ? P * rs : 0.f;  // Pd
         pacc[qt][kt][r] = dS;
-        dSm[q * TP + key] = f2bf(dS);
+        dSm[q * TP + keyi[kt]] = f2bf(dS);
       }
     }
 
@@ -427,7 +432,8 @@ VCG_API int vcg_bert_attn_bwd(const void* qkv, const void* dctx, const void* ctx
                               const void* stats, void* dqkv, int B, int nh, int L, int Lp, float scale,
                               float dropout_p, unsigned long long seed, hipStream_t s) {
   if (B == 0 || L == 0) return VCG_OK;
-  if (!qkv || !dctx || !ctx || !stats || !dqkv || B < 0 || nh <= 0 || L < 0 || Lp < L) {
+  (void)ctx;  // (kept in the signature: the backward no longer needs the forward's output)
+  if (!qkv || !dctx || !stats || !dqkv || B < 0 || nh <= 0 || L < 0 || Lp < L) {
     set_error("vcg_bert_attn_bwd: invalid arguments");
     return VCG_ERR_INVALID;
   }
@@ -435,8 +441,8 @@ VCG_API int vcg_bert_attn_bwd(const void* qkv, const void* dctx, const void* ctx
     set_error("vcg_bert_attn_bwd: L > 128 is not supported by the fused kernel");
     return VCG_ERR_UNSUPPORTED;
   }
-  hipLaunchKernelGGL(bert_attn_bwd_kernel, dim3(B * nh), dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)dctx,
-                     (const bf16_t*)ctx, mask, (const float2*)stats, (bf16_t*)dqkv, nh, L, Lp, scale, dropout_p,
+  hipLaunchKernelGGL(bert_attn_bwd_kernel, dim3(B * nh), dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)dctx, mask,
+                     (const float2*)stats, (bf16_t*)dqkv, nh, L, Lp, scale, dropout_p,
                      (uint64_t)seed);
   VCG_CHECK_HIP(hipGetLastError());
   return VCG_OK;
