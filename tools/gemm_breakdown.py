@@ -1,12 +1,12 @@
 """Join a VCG_GEMM_LOG dispatch log with a rocprofv3 kernel_trace.csv (igemm launches pair up in
-order; "lt ..." lines are the hipBLASLt GEMMs, one Cijk_* kernel each) and print time per GEMM shape.
+order; "wide ..." lines are the wide-tile engine's gemm_wide_kernel launches) and print time per GEMM shape.
 usage: gemm_breakdown.py LOG TRACE_CSV [n_steps]"""
 import collections
 import csv
 import sys
 
 log = [l.strip() for l in open(sys.argv[1]) if l.strip()]
-rows = [r for r in csv.DictReader(open(sys.argv[2])) if any(k in r["Kernel_Name"] for k in ("igemm", "gemm256", "wgrad_fast", "wgrad3x3_patch", "conv3x3_patch", "stem_patch", "rs1x1", "Cijk_"))]
+rows = [r for r in csv.DictReader(open(sys.argv[2])) if any(k in r["Kernel_Name"] for k in ("igemm", "gemm256", "wgrad_fast", "wgrad3x3_patch", "conv3x3_patch", "stem_patch", "rs1x1", "gemm_wide"))]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 steps = float(sys.argv[3]) if len(sys.argv) > 3 else 3.0
 if len(log) != len(rows):
