@@ -141,8 +141,6 @@ __device__ __forceinline__ void wide_wait(int ahead) {
 // (a "piece"), PA = BM / 64 A pieces and PB = BN / 64 B pieces per wave and k-step; 16-B chunk c of row r at slot
 // c ^ ((r >> 1) & 7) (fast_frag's swizzle, pre-applied on the global source address). The per-row offsets are computed
 // once per tile, so a piece is one select and one buffer_load ... lds.
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-
 template <int BM, int BN, int NW = 8>
 struct WideLoader {
   static constexpr int PA = BM / (8 * NW), PB = BN / (8 * NW), P = PA + PB, AE = BM * FBK;
@@ -181,30 +179,13 @@ struct WideLoader {
       all<Q + 1>(k0, K, stage, wave);
     }
   }
-  // register staging (VCG_WIDE_REG): the same pieces loaded into VGPRs (fetch), written to the stage later (commit:
-  // lane l's 16 B at the piece slice + 16 l, the LDS image the DMA writes)
-  __device__ __forceinline__ void fetch(int k0, int K, u32x4_t (&rg)[P]) const {
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const bool isa = q < PA;
-      const uint32_t voff = (off[q] >= 0 && k0 + kc[q] < K) ? (uint32_t)(off[q] + k0) * 2u : (isa ? oa : ob);
-      rg[q] = __builtin_amdgcn_raw_buffer_load_b128(isa ? ra : rb, voff, 0, 0);
-    }
-  }
-  __device__ __forceinline__ void commit(const u32x4_t (&rg)[P], bf16_t* stage, int wave, int lane) const {
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const bool isa = q < PA;
-      bf16_t* slice = stage + (isa ? 0 : AE) + (wave * (isa ? PA : PB) + (isa ? q : q - PA)) * 512;
-      *reinterpret_cast<u32x4_t*>(slice + 8 * lane) = rg[q];
-    }
-  }
 };
 
 // ST = 3 stages (prefetch distance 2); each group issues its LDS-DMA pieces of step s + 2 in its read phase, after the
 // fragment reads. (Measured and rejected, profiles/r06_wide_engine_ab.txt: 4 stages, the pieces in the compute phase
 // -- between the two k32 halves or one every few MFMAs --, no s_setprio or the read phase at priority 1, no stagger,
-// and a 4-wave 64 x 96 form with in-wave software pipelining: all equal or slower.)
+// a 4-wave 64 x 96 form with in-wave software pipelining, and register staging (buffer_load to VGPRs one k-step ahead,
+// ds_write_b128 into the stage, 2 or 3 stages: 6-7 % slower): all equal or slower.)
 template <int BM, int BN, int WE, int ST = 3>
 __global__ __launch_bounds__(512) void gemm_wide_kernel(GemmParams p) {
   constexpr int MT = BM / 32, NT = BN / 64;          // the wave's (BM / 2) x (BN / 4) sub-tile in 16 x 16 fragments
@@ -329,106 +310,6 @@ __global__ __launch_bounds__(512) void gemm_wide_kernel(GemmParams p) {
   if (grp == 0) __builtin_amdgcn_s_barrier();  // (the stagger's barrier count)
 }
 
-// Register-staged form (VCG_WIDE_REG builds): the pieces of step s + ST are fetched into VGPRs in the read phase of step
-// s - 1 ... ST - 1 phases ahead and written to their stage (ds_write_b128, the DMA's LDS image) in the read phase of
-// step s; the lgkmcnt(0) before each phase-ending barrier orders the writes before the reads two phases later.
-template <int BM, int BN, int WE, int ST = 3>
-__global__ __launch_bounds__(512) void gemm_wide_reg_kernel(GemmParams p) {
-  constexpr int MT = BM / 32, NT = BN / 64;
-  constexpr int AE = BM * FBK, BE = BN * FBK, SE = AE + BE;
-  constexpr int PF = ST - 1;
-  static_assert(ST * SE * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) bf16_t smem[ST * SE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2, wc = wave & 3;
-  const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM, ntiles = ntn * ntm;
-  const int G = gridDim.x;
-  const int slot = w_xcd_slot(blockIdx.x, G);
-  const int mine = slot < ntiles ? (ntiles - 1 - slot) / G + 1 : 0;
-  const int nk = (p.K + FBK - 1) / FBK;
-  const int steps = mine * nk;
-  if (steps == 0) return;
-
-  using LD = WideLoader<BM, BN>;
-  LD ld;
-  ld.init(p);
-  int ikt = 0, itile = 0;  // the next step to fetch
-  auto fetch_next = [&](u32x4_t (&rg)[LD::P]) {
-    if (ikt == 0) {
-      const int L = slot + itile * G, mt = L / ntn, nt = L - mt * ntn;
-      ld.tile(p, mt * BM, nt * BN, wave, lane);
-    }
-    ld.fetch(ikt * FBK, p.K, rg);
-    if (++ikt == nk) {
-      ikt = 0;
-      ++itile;
-    }
-  };
-
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  u32x4_t rg[LD::P];
-#pragma unroll
-  for (int t = 0; t < PF; ++t)
-    if (t < steps) {
-      fetch_next(rg);
-      ld.commit(rg, smem + t * SE, wave, lane);
-    }
-  if (PF < steps) fetch_next(rg);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_s_barrier();
-  if (grp == 1) __builtin_amdgcn_s_barrier();
-
-  int cur = 0, kt = 0, tile = 0;
-  s16x8 af[MT][2], bq[NT][2];
-  for (int s = 0; s < steps; ++s) {
-    const bf16_t* Ac = smem + cur * SE;
-    const bf16_t* Bc = Ac + AE;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-      for (int j = 0; j < NT; ++j) bq[j][s2] = fast_frag(Bc, wc * (BN / 4) + j * 16, lane, s2);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) af[i][s2] = fast_frag(Ac, grp * (BM / 2) + i * 16, lane, s2);
-    }
-    if (s + PF < steps) {  // step s + PF into the stage step s - 1 used
-      ld.commit(rg, smem + (cur == 0 ? ST - 1 : cur - 1) * SE, wave, lane);
-      if (s + PF + 1 < steps) fetch_next(rg);
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): reads and stage writes done before the barrier
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j][s2], af[i][s2], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (++kt == nk) {
-      const int L = slot + tile * G, mt = L / ntn, nt = L - mt * ntn;
-      wide_epilogue<MT, NT, WE>(acc, p, mt * BM + grp * (BM / 2) + (lane & 15), nt * BN + wc * (BN / 4) + 4 * (lane >> 4));
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      kt = 0;
-      ++tile;
-    }
-    __builtin_amdgcn_s_barrier();
-    cur = cur == ST - 1 ? 0 : cur + 1;
-  }
-  if (grp == 0) __builtin_amdgcn_s_barrier();
-}
-
 namespace {
 
 int wide_cus() {
@@ -463,11 +344,7 @@ void launch_wide(const GemmParams& p, hipStream_t s) {
   constexpr int BM = 128;
   const long long tiles = (long long)((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int grid = (int)(tiles < wide_cus() ? tiles : wide_cus());
-#if defined(VCG_WIDE_REG) && VCG_WIDE_REG > 0
-  hipLaunchKernelGGL((gemm_wide_reg_kernel<BM, BN, WE, VCG_WIDE_REG>), dim3(grid), dim3(512), 0, s, p);
-#else
   hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WE>), dim3(grid), dim3(512), 0, s, p);
-#endif
 }
 
 template <int BN>
