@@ -205,6 +205,7 @@ def long_video_bench(args):
     win, idx, ids, mask = lv.window_inputs(F, T, args.stride, subtitles, HashTokenizer(), L)
     idx, ids, mask = (torch.from_numpy(a).to(dev) for a in (idx, ids, mask))
     K = args.scoring_streams
+    G = args.bn_groups
     # re-bias the random-init 2-way head (untimed, as tests/test_gpu_long_video.py does) so its decisions split
     # about evenly: otherwise every window sits on one side of 0.5, no cut point is predicted and F is 0 / undefined
     samp = torch.from_numpy(np.linspace(0, len(win) - 1, 256).astype(np.int64)).to(dev)
@@ -214,10 +215,11 @@ def long_video_bench(args):
         shift = -torch.log(pr / (1 - pr)).median().item()
         model.fusion_head.head.bias.data[1] += shift
         model.native_flat().refresh_shadow(force=True)
-    lv.score_windows(model, frames, idx[:B * max(2, K)], ids[:B * max(2, K)], mask[:B * max(2, K)], B, streams=K)
+    W0 = B * max(2, K, G)
+    lv.score_windows(model, frames, idx[:W0], ids[:W0], mask[:W0], B, streams=K, groups=G)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scores, labels = lv.score_windows(model, frames, idx, ids, mask, B, streams=K)
+    scores, labels = lv.score_windows(model, frames, idx, ids, mask, B, streams=K, groups=G)
     torch.cuda.synchronize()
     sec = time.perf_counter() - t0
     lab = labels.cpu().tolist()
@@ -253,8 +255,9 @@ def long_video_bench(args):
         "higher_is_better": True, "dtype": args.precision,
         "data": "synthetic 1 fps video (seeded u8 frames in HBM, random-init weights)",
         "config": {"workload": f"{F} frames {HW}^2, T={T}, L={L}, stride {args.stride} s, batch {B}, "
-                               f"{args.bn}-stats BN" + (f", batches on {K} streams" if K > 1 else ""),
-                   "bn": args.bn, "stride": args.stride, "scoring_streams": K,
+                               f"{args.bn}-stats BN" + (f", batches on {K} streams" if K > 1 else "")
+                               + (f", {G} batches per forward (per-batch statistics)" if G > 1 else ""),
+                   "bn": args.bn, "stride": args.stride, "scoring_streams": K, "bn_groups": G,
                    "frames": F, "clip_frame_num": T, "seq_len": L, "resolution": HW},
         "cpu_baseline": cpu,
         "roofline_step": {"bound": "hbm", "achieved": round(nbytes * n / sec / 1e9, 2), "peak": HBM_PEAK_GBS,
@@ -394,10 +397,17 @@ def main():
     ap.add_argument("--scoring-streams", type=int, default=1,
                     help="long_video: scoring batches round-robin over this many HIP streams (long_video.score_windows); "
                          "fwd: a step scores this many batches of --batch windows, one per HIP stream")
+    ap.add_argument("--bn-groups", type=int, default=1,
+                    help="batch-statistics scoring (--bn batch): this many batches of --batch windows form ONE forward "
+                         "with per-batch BatchNorm statistics (TwoStream.bn_group: the trunk per batch, BERT and the "
+                         "head once over all of them); fwd: a step is that forward; long_video: score_windows(groups)")
     ap.add_argument("--bn", default="running", choices=["running", "batch"],
                     help="scoring modes (fwd / long_video): BN with running statistics (model.eval(), the trainer's "
                          "val and convert2vision_emb) or with the batch's statistics (test_video_segment_point.py:"
                          "116-122, which scores batches of 16 windows: pass --batch 16)")
+    ap.add_argument("--bn-group-streams", type=int, default=0,
+                    help="with --bn-groups: the groups' trunks round-robin on this many HIP streams "
+                         "(TwoStream.bn_group_streams; 0: the model's default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-roofline-step", action="store_true",
@@ -413,6 +423,9 @@ def main():
     if args.batch is None:
         args.batch = 16 if (args.bn == "batch" and args.mode != "train") else 64
 
+    if args.bn_groups > 1 and (args.bn != "batch" or args.mode == "train" or args.scoring_streams > 1):
+        raise SystemExit("bench.py: --bn-groups applies to batch-statistics scoring (--bn batch, fwd / long_video) "
+                         "on one stream")
     if args.mode == "long_video" and args.gpus > 1:
         raise SystemExit("bench.py: --mode long_video is a one-GPU benchmark (config 5); run it with --gpus 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -486,7 +499,13 @@ def main():
     # main stream first in the first step, so one-time weight preparation is ordered before the others): the
     # batch-statistics mode scores batches of 16 (BN couples only the windows of one batch), which underfill the chip
     K = args.scoring_streams if args.mode == "fwd" else 1
-    frames, ids, mask, labels = synth.clip_batch(B * K, T, HW, HW, L, seed=123 + rank, device=dev)
+    # fwd with --bn-groups G: a step is ONE forward over G batches of B windows, BatchNorm statistics per batch
+    G = args.bn_groups if args.mode == "fwd" else 1
+    if G > 1:
+        model.bn_group = B
+        if args.bn_group_streams > 0:
+            model.bn_group_streams = args.bn_group_streams
+    frames, ids, mask, labels = synth.clip_batch(B * K * G, T, HW, HW, L, seed=123 + rank, device=dev)
     chunks = [(frames[k * B:(k + 1) * B], ids[k * B:(k + 1) * B], mask[k * B:(k + 1) * B]) for k in range(K)]
     pool = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(K - 1)]
     comm_events = None  # [(backward done, finish joined)] per timed step (world > 1)
@@ -630,12 +649,12 @@ def main():
                                "torch.distributed")
 
     if rank == 0:
-        windows = B * K * world
+        windows = B * K * G * world
         value = windows / (ms / 1000.0)
         s_bytes = 2 if args.precision == "bf16" else 4
         nbytes, nflops = window_costs(T, HW, L, B, s_bytes, args.mode == "train")
-        achieved = nbytes * B * K / (ms / 1000.0) / 1e9  # per GPU
-        tflops = nflops * B * K / (ms / 1000.0) / 1e12
+        achieved = nbytes * B * K * G / (ms / 1000.0) / 1e9  # per GPU
+        tflops = nflops * B * K * G / (ms / 1000.0) / 1e12
         traffic = kern_traffic = mfma_busy = None
         tf = os.path.join(REPO, "profiles", f"traffic_{args.mode}_{args.precision}_b{B}.json")
         if os.path.exists(tf):
@@ -693,6 +712,7 @@ def main():
                                    + (", fused clip+AdamW" if args.mode == "train" else ""),
                        "global_batch": windows, "seq_len": L, "frames": T, "resolution": HW,
                        **({"batches_per_step": K, "batch": B, "scoring_streams": K} if K > 1 else {}),
+                       **({"batches_per_step": G, "batch": B, "bn_groups": G} if G > 1 else {}),
                        "parallelism": f"dp{world}", **({"bn": args.bn} if args.mode == "fwd" else {})},
             "roofline": dom,
             **ddp,

@@ -273,3 +273,31 @@ def test_c5_stride4_f1_vs_oracle_golden():
         assert m32["pred_cut_points"] == g["pred_cut_points"].tolist()
         for k in ("recall", "recall_3", "recall_5", "precision", "precision_3", "precision_5", "f", "f_3", "f_5"):
             assert m32[k] == float(g["metric_" + k]), k
+
+
+@pytest.mark.parametrize("precision,streams", [("bf16", 2), ("bf16", 1), ("fp32", 2)])
+def test_score_windows_groups_identical(precision, streams):
+    """Batch-statistics scoring with 4 batches of 16 windows per forward (TwoStream.bn_group: the trunk per batch with
+    its own BatchNorm statistics -- the groups' trunks on `streams` HIP streams --, BERT and the head once over all 64
+    windows) gives bit-identical scores / labels to one forward per batch (test_video_segment_point.py:41,116-122);
+    the final ragged batch included."""
+    import long_video as lv
+    from data.synthetic_dataset import HashTokenizer
+    from test_video_segment_point import drop_bn_running_stats
+    from vcg_hip.build import build_two_stream
+    F, T, HW, L = 80, 4, 112, 32
+    model = build_two_stream(clip_frame_num=T, seed=123, device=DEV, precision=precision, dropout=0.0).eval()
+    drop_bn_running_stats(model)
+    model.bn_group_streams = streams
+    frames, _, subtitles = lv.synthetic_long_video(F, HW, HW, chapter_every=12, seed=8, device=DEV)
+    win, idx, ids, mask = lv.window_inputs(F, T, 1, subtitles, HashTokenizer(), L)
+    assert len(win) % 16 != 0  # a ragged last batch
+    args = [torch.from_numpy(a).to(DEV) for a in (idx, ids, mask)]
+    s1, l1 = lv.score_windows(model, frames, *args, batch_size=16)
+    s4, l4 = lv.score_windows(model, frames, *args, batch_size=16, groups=4)
+    torch.cuda.synchronize()
+    assert model.bn_group is None
+    assert torch.equal(s1, s4) and torch.equal(l1, l4)
+    # and not what one batch of 64 gives (the statistics do span only each group)
+    s64, _ = lv.score_windows(model, frames, *args, batch_size=64)
+    assert not torch.equal(s1, s64)

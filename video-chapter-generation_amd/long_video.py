@@ -73,14 +73,15 @@ def window_inputs(n_frames, clip_frame_num, stride, subtitles, tokenizer, max_te
 
 
 @torch.no_grad()
-def score_windows(model, frames_u8, idx, ids, mask, batch_size, export=None, streams=1):
+def score_windows(model, frames_u8, idx, ids, mask, batch_size, export=None, streams=1, groups=1):
     """GPU part: per batch, frame gather + normalisation (ops.window_frames_u8) and the TwoStream forward.
     idx / ids / mask are device tensors. Returns (pred_score f32 [n], pred_label i64 [n]) on the device.
     export(b0, vision_emb [b, T, 2048]) is called per batch when given.
     streams > 1: consecutive batches go round-robin to that many HIP streams, so the small batches of the
     batch-statistics mode (16 windows: BN couples only the windows of one batch) run concurrently; every batch is
-    still one forward over exactly its own windows, so the results are those of streams = 1."""
-    from vcg_hip import ops
+    still one forward over exactly its own windows, so the results are those of streams = 1.
+    groups > 1: `groups` consecutive batches form one forward with per-batch BatchNorm statistics (TwoStream.bn_group
+    = batch_size): BERT and the head run once over all of them; the results are those of groups = 1."""
     dt = model.compute_dtype()
     n = idx.shape[0]
     dev = frames_u8.device
@@ -88,8 +89,23 @@ def score_windows(model, frames_u8, idx, ids, mask, batch_size, export=None, str
     labels = torch.empty(n, dtype=torch.int64, device=dev)
     main = torch.cuda.current_stream(dev)
     pool = [main] if streams <= 1 or export is not None else [torch.cuda.Stream(device=dev) for _ in range(streams)]
-    for k, b0 in enumerate(range(0, n, batch_size)):
-        b1 = min(n, b0 + batch_size)
+    step = batch_size * max(1, groups)
+    if groups > 1:
+        if not hasattr(model, "bn_group"):
+            raise ValueError("score_windows(groups > 1) needs a TwoStream model (per-group BatchNorm statistics)")
+        saved_group, model.bn_group = model.bn_group, batch_size
+    try:
+        _score_batches(model, frames_u8, idx, ids, mask, n, step, dt, main, pool, scores, labels, export)
+    finally:
+        if groups > 1:
+            model.bn_group = saved_group
+    return scores, labels
+
+
+def _score_batches(model, frames_u8, idx, ids, mask, n, step, dt, main, pool, scores, labels, export):
+    from vcg_hip import ops
+    for k, b0 in enumerate(range(0, n, step)):
+        b1 = min(n, b0 + step)
         if k == 1 and len(pool) > 1:
             # batch 0 ran on the caller's stream: whatever the first forward prepares once (the bf16 weight shadow /
             # GEMM layouts / folded weights) is ordered before every stream's batches
@@ -106,7 +122,6 @@ def score_windows(model, frames_u8, idx, ids, mask, batch_size, export=None, str
     for s in pool:
         if s is not main:
             main.wait_stream(s)
-    return scores, labels
 
 
 def boundary_metrics(labels, timestamps, n_frames, clip_frame_num, stride):

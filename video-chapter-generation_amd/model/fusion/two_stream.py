@@ -120,6 +120,18 @@ class TwoStream(NativeRoot, nn.Module):
 
     # BERT on a side HIP stream beside the trunk (bench.py --one-stream and the instrumented step set it False)
     overlap_streams = True
+    # batch-statistics scoring of several batches in ONE forward (long_video.score_windows(groups=K), bench.py
+    # --bn-groups K): with bn_group = G windows, a no-grad forward whose trunk BatchNorms use batch statistics runs the
+    # trunk once per consecutive group of G windows (each group its own statistics: the reference harness's batches,
+    # test_video_segment_point.py:41,116-122), and BERT and the head -- no BatchNorm, per-window results independent
+    # of the batch -- once over all windows at full chip fill. Bit-identical to forwarding the groups one by one.
+    # None: the statistics span the whole batch (the reference forward).
+    bn_group = None
+    # ... the groups' trunks round-robin on this many HIP streams (1: one after another on the caller's stream); a
+    # concurrent group's downsample branches run inline (the trunk's shared side stream would couple the groups).
+    # 4 x 16 windows (profiles/r06_scoring_groups.txt): 1 stream 2154, 2 streams 2553, 4 streams 2555 windows/s;
+    # one batch of 64 (the bound) 2617; one forward per batch of 16: 2090
+    bn_group_streams = 2
 
     def _side_stream(self, dev):
         """The BERT side stream (None: one stream), created once per device."""
@@ -130,6 +142,22 @@ class TwoStream(NativeRoot, nn.Module):
             s = torch.cuda.Stream(device=dev)
             object.__setattr__(self, "_vcg_side", s)
         return s
+
+    def _group_streams(self, dev):
+        """The streams of concurrent per-group trunks ([]: the caller's stream only)."""
+        n = self.bn_group_streams
+        if n <= 1 or dev.type != "cuda":
+            return []
+        pool = getattr(self, "_vcg_group_streams", None)
+        if pool is None or len(pool) != n or pool[0].device != dev:
+            pool = [torch.cuda.Stream(device=dev) for _ in range(n)]
+            object.__setattr__(self, "_vcg_group_streams", pool)
+        return pool
+
+    def _trunk_batch_stats(self):
+        """Some trunk BatchNorm normalises with the statistics of its batch (train mode, or no running buffers)."""
+        from vcg_hip.trunk import bn_mode
+        return any(bn_mode(m) != "running" for m in self.vision_model.modules() if isinstance(m, nn.BatchNorm2d))
 
     def set_grad_hooks(self, hooks):
         """hooks(tag) is called from the backward when a branch's gradients are final."""
@@ -181,9 +209,30 @@ class TwoStream(NativeRoot, nn.Module):
                 t.record_stream(side)
             with torch.cuda.stream(side):
                 lang_emb, _ = BertFn.apply(text_ids, attention_mask, anchor, bert, need_grad, new_seed(), hooks, main)
-        trunk = ResNetTrunk(self.vision_model, dt)
-        trunk.staged = staged
-        vision_emb = TrunkFn.apply(img, anchor, trunk, need_grad, hooks)
+        G = self.bn_group
+        if G is not None and not need_grad and 0 < G < batch_size and self._trunk_batch_stats():
+            T = img.shape[0] // batch_size
+            main = torch.cuda.current_stream(dev)
+            pool = self._group_streams(dev)
+            embs = []
+            for k, g0 in enumerate(range(0, batch_size, G)):
+                trunk = ResNetTrunk(self.vision_model, dt)
+                trunk.staged = staged
+                st = pool[k % len(pool)] if pool else main
+                if st is not main:
+                    trunk.ds_stream = False
+                    st.wait_stream(main)
+                with torch.cuda.stream(st):
+                    embs.append(TrunkFn.apply(img[g0 * T:min(batch_size, g0 + G) * T], anchor, trunk, False, hooks))
+                if st is not main:
+                    embs[-1].record_stream(main)  # (allocated on st, read and freed on main)
+            for st in pool:
+                main.wait_stream(st)
+            vision_emb = torch.cat(embs)
+        else:
+            trunk = ResNetTrunk(self.vision_model, dt)
+            trunk.staged = staged
+            vision_emb = TrunkFn.apply(img, anchor, trunk, need_grad, hooks)
         if side is not None:
             main.wait_stream(side)
             lang_emb.record_stream(main)

@@ -300,7 +300,7 @@ class ResNetTrunk:
         yd = bd = side = None
         cur = torch.cuda.current_stream() if x.is_cuda else None
         if blk.downsample is not None:
-            side = self._wside(x.device) if ResNetTrunk.ds_stream else None
+            side = self._wside(x.device) if self.ds_stream else None  # (an instance may turn it off)
             if side is not None:
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):
@@ -743,7 +743,7 @@ class ResNetTrunk:
                     # then feeds only side-stream kernels); inline otherwise, where the main stream reads dyd
                     def dyd_fn():
                         return self._bn_apply_bwd(g, r["yd"], bd, C3, sumsd)
-                    if self._ws is not None and ResNetTrunk.ds_stream:
+                    if self._ws is not None and self.ds_stream:
                         dyd = self._async(dyd_fn, g, r["yd"], *sumsd)
                     else:
                         dyd = dyd_fn()
@@ -760,7 +760,7 @@ class ResNetTrunk:
         # the downsample branch's input gradient needs only dyd: on the side stream ahead of the weight gradients,
         # joined (by its own event) just before conv1's fused dgrad adds it
         ds_res = None
-        if ds and self._ws is not None and ResNetTrunk.ds_stream:
+        if ds and self._ws is not None and self.ds_stream:
             ds_res = self._ds_dgrad_side(blk.downsample[0], dyd, N, H, W, Cin, C3)
         if bnf is not None and not self._fold_conv3(r, *bnf):  # (the engine does not apply: the pass on dy3)
             dy3 = self._bn_apply_bwd(bnf[0], self._y3(r), r["b3"], C3, bnf[1])
