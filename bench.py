@@ -408,6 +408,9 @@ def main():
     ap.add_argument("--bn-group-streams", type=int, default=0,
                     help="with --bn-groups: the groups' trunks round-robin on this many HIP streams "
                          "(TwoStream.bn_group_streams; 0: the model's default)")
+    ap.add_argument("--full-text", action="store_true",
+                    help="synthetic subtitles fill all --tokens positions (default: n_valid uniform in [L/2, L], "
+                         "vcg_hip.synth.clip_batch): the BERT work without any padded rows to drop")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-roofline-step", action="store_true",
@@ -506,6 +509,9 @@ def main():
         if args.bn_group_streams > 0:
             model.bn_group_streams = args.bn_group_streams
     frames, ids, mask, labels = synth.clip_batch(B * K * G, T, HW, HW, L, seed=123 + rank, device=dev)
+    if args.full_text:  # every window's subtitle fills all L tokens (no padding for BERT to drop)
+        ids[ids == 0] = 1000
+        mask.fill_(1)
     chunks = [(frames[k * B:(k + 1) * B], ids[k * B:(k + 1) * B], mask[k * B:(k + 1) * B]) for k in range(K)]
     pool = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(K - 1)]
     comm_events = None  # [(backward done, finish joined)] per timed step (world > 1)
@@ -711,6 +717,7 @@ def main():
                                    f"B={B} windows/GPU of {T}x{HW}^2 frames + {L} tokens"
                                    + (", fused clip+AdamW" if args.mode == "train" else ""),
                        "global_batch": windows, "seq_len": L, "frames": T, "resolution": HW,
+                       "text_fill": "full" if args.full_text else "n_valid ~ U[L/2, L]",
                        **({"batches_per_step": K, "batch": B, "scoring_streams": K} if K > 1 else {}),
                        **({"batches_per_step": G, "batch": B, "bn_groups": G} if G > 1 else {}),
                        "parallelism": f"dp{world}", **({"bn": args.bn} if args.mode == "fwd" else {})},

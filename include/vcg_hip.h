@@ -278,6 +278,12 @@ VCG_API int vcg_attn_softmax_bwd(int dtype, const void* dPd, const void* P, void
    mask as vcg_attn_softmax_fwd/bwd + the batched GEMMs (HF BertSelfAttention, bert_hugface.py:20). */
 VCG_API int vcg_bert_attn_fwd(const void* qkv, const long long* mask, void* ctx, void* stats, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API int vcg_bert_attn_bwd(const void* qkv, const void* dctx, const void* ctx, const long long* mask, const void* stats, void* dqkv, int B, int nh, int L, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
+/* packed (unpadded) sequences -- BERT with the padded positions dropped (they feed neither the pooler's CLS row nor any
+   kept row: masked keys), reference HF BertModel via bert_hugface.py:20 / two_stream.py:178-179: sequence b's rows are
+   seq[b] .. seq[b+1]-1 (int32 [B+1] prefix offsets, each <= Lmax <= 128 rows) of qkv [rows][3H] / ctx / dqkv, mask the
+   key flag of every packed row (NULL: all keys); stats and the dropout counters keep the padded [B*nh][Lmax] space */
+VCG_API int vcg_bert_attn_fwd_varlen(const void* qkv, const long long* mask, const int* seq, void* ctx, void* stats, int B, int nh, int Lmax, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
+VCG_API int vcg_bert_attn_bwd_varlen(const void* qkv, const void* dctx, const long long* mask, const int* seq, const void* stats, void* dqkv, int B, int nh, int Lmax, int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s);
 VCG_API int vcg_tanh_bwd(int dtype, const void* dy, const void* t, void* dx, long long n, hipStream_t s);
 
 /* ---- fusion head + loss (head.hip): ChapterHead mlp (two_stream.py:51-95), softmax (:189),

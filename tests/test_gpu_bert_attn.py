@@ -121,3 +121,81 @@ def test_fused_attention_in_bert_step_matches_unfused(monkeypatch):
     errs = sorted((rel(g1[n], g0[n]), n) for n in g1 if n not in kb and g0[n].norm() > 0)
     print("grad rel errors: median %.3e, worst %s" % (errs[len(errs) // 2][0], errs[-3:]))
     assert errs[len(errs) // 2][0] < 3e-2 and errs[-1][0] < 1e-1
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_varlen_attention_matches_padded(p):
+    """Packed (unpadded) sequences (vcg_bert_attn_fwd/bwd_varlen, bert.Packing): the kept rows' ctx and dQ | dK | dV
+    equal the padded kernels' bit for bit where the kept rows are a prefix of the padded ones (same key positions and
+    dropout counters), given the dropped rows' upstream gradient is zero as in the model; a sequence with a masked hole
+    matches within rounding without dropout; a sequence without any key keeps all its rows (uniform attention, as HF)."""
+    from vcg_hip import _lib
+    from vcg_hip.bert import Packing, attention_bwd, attention_fwd
+    _lib.call("vcg_init", 0)
+    B, L, nh, H = 5, 128, 12, 768
+    Lp = L
+    lens = [128, 77, 1, 50]
+    mask_np = np.zeros((B, L), np.int64)
+    for b, n in enumerate(lens):
+        mask_np[b, :n] = 1
+    mask_np[4, :10] = 1
+    mask_np[4, 16:40] = 1                  # a hole: kept rows 0-9, 16-39 (positions shift when packed)
+    mask_np[2, :] = 0                      # no key at all: every row kept
+    pk = Packing(mask_np.copy(), DEV)
+    rows = pk.rows.cpu()
+    assert pk.R == 128 + 77 + 128 + 50 + 34
+    g = torch.Generator().manual_seed(5)
+    qkv = (torch.randn(B * L + 8, 3 * H, generator=g) * 1.5).to(torch.bfloat16)
+    dctx = torch.randn(B * L, H, generator=g).to(torch.bfloat16)
+    drop = torch.ones(B * L, dtype=torch.bool)
+    drop[rows] = False
+    dctx[drop] = 0
+    seed = 0xABCDEF + int(p * 10)
+    mask = torch.from_numpy(mask_np).to(DEV)
+    ctx_p, att_p = attention_fwd(qkv.to(DEV), mask, B, nh, L, Lp, 64, 0.125, p, seed, True)
+    dqkv_p = attention_bwd(qkv.to(DEV), dctx.to(DEV), ctx_p, mask, att_p, B, nh, L, Lp, 64, 0.125, p, seed)
+    qkv_k = torch.cat([qkv[rows], torch.zeros(8, 3 * H, dtype=qkv.dtype)]).to(DEV)
+    ctx_k, att_k = attention_fwd(qkv_k, pk.keys, B, nh, L, Lp, 64, 0.125, p, seed, True, seq=pk.seq, rows=pk.R)
+    dqkv_k = attention_bwd(qkv_k, dctx[rows].to(DEV), ctx_k, pk.keys, att_k, B, nh, L, Lp, 64, 0.125, p, seed,
+                           seq=pk.seq, rows=pk.R)
+    torch.cuda.synchronize()
+    ctx_p, dqkv_p, ctx_k, dqkv_k = (t.cpu() for t in (ctx_p, dqkv_p, ctx_k, dqkv_k))
+    seq = pk.seq.cpu().tolist()
+    for b in range(B):
+        kr = rows[seq[b]:seq[b + 1]]
+        a, c = slice(seq[b], seq[b + 1]), kr
+        if b == 4:  # (with dropout its shifted key positions draw other dropout counters: another valid sample)
+            if p == 0:
+                assert rel(ctx_k[a], ctx_p[c]) < 5e-3 and rel(dqkv_k[a], dqkv_p[c]) < 5e-3, b
+        else:
+            assert torch.equal(ctx_k[a], ctx_p[c]) and torch.equal(dqkv_k[a], dqkv_p[c]), b
+
+
+def test_unpadded_bert_in_two_stream_step(monkeypatch):
+    """A whole bf16 TwoStream train step (dropout 0) with BERT's padded rows dropped (BertEncoderEngine.unpad) vs
+    every row computed: logits bit-identical (prefix masks: the kept rows see the padded computation exactly), every
+    parameter gradient within fp32 summation-order rounding (the weight-gradient and bias sums run over fewer rows)."""
+    from vcg_hip import _lib, synth
+    from vcg_hip.bert import BertEncoderEngine, PackingRequest
+    from vcg_hip.build import build_two_stream
+    from vcg_hip.functions import cross_entropy
+    _lib.call("vcg_init", 0)
+    T, HW, L = 2, 64, 128
+    frames, ids, mask, labels = synth.clip_batch(6, T, HW, HW, L, seed=21, device=DEV)
+    assert (mask == 0).any()
+    res = {}
+    for unpad in (True, False):
+        monkeypatch.setattr(BertEncoderEngine, "unpad", unpad)
+        PackingRequest._last = None
+        m = build_two_stream(clip_frame_num=T, seed=5, device=DEV, precision="bf16", dropout=0.0).train()
+        logits, _ = m(frames, ids, mask)
+        cross_entropy(logits, labels).backward()
+        torch.cuda.synchronize()
+        res[unpad] = (logits.detach().float().cpu(),
+                      {n: p.grad.detach().double().cpu().clone() for n, p in m.named_parameters() if p.grad is not None})
+    (l1, g1), (l0, g0) = res[True], res[False]
+    assert torch.equal(l1, l0)
+    assert g1.keys() == g0.keys()
+    errs = sorted((rel(g1[n], g0[n]), n) for n in g1 if g0[n].norm() > 1e-3 * max(v.norm() for v in g0.values()))
+    print("unpadded vs padded grad rel errors: median %.3e, worst %s" % (errs[len(errs) // 2][0], errs[-3:]))
+    assert errs[-1][0] < 2e-3, errs[-3:]

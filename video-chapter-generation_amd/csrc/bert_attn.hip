@@ -88,8 +88,8 @@ __device__ __forceinline__ void load_transpose(const bf16_t* src, long long ld, 
 __global__ __launch_bounds__(256) void bert_attn_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                             const long long* __restrict__ mask,
                                                             bf16_t* __restrict__ ctx, float2* __restrict__ stats,
-                                                            int nh, int L, int Lp, float scale, float p,
-                                                            uint64_t seed) {
+                                                            const int* __restrict__ seq, int nh, int Lmax, int Lp,
+                                                            float scale, float p, uint64_t seed) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[LT * DH];
   __shared__ __attribute__((aligned(16))) bf16_t Vt[DH * TP];
   __shared__ uint8_t kval[LT];
@@ -97,14 +97,17 @@ __global__ __launch_bounds__(256) void bert_attn_fwd_kernel(const bf16_t* __rest
   const int H = nh * DH;
   const long long ld = 3LL * H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const bf16_t* base = qkv + (long long)b * L * ld + h * DH;  // Q of (b, h); K at + H, V at + 2 H
+  // sequence b: rows row0 .. row0 + L - 1 (packed: seq[b] .. seq[b + 1] - 1; else b Lmax .. + Lmax - 1)
+  const int row0 = seq ? seq[b] : b * Lmax;
+  const int L = seq ? seq[b + 1] - row0 : Lmax;
+  const bf16_t* base = qkv + (long long)row0 * ld + h * DH;  // Q of (b, h); K at + H, V at + 2 H
 
   for (int c = tid; c < LT * 8; c += 256) {
     const int r = c >> 3, ch = c & 7;
     *reinterpret_cast<uint4*>(Ks + r * DH + 8 * swz(r, ch)) = ld16(base + r * ld + H + 8 * ch, r < L);
   }
   load_transpose(base + 2 * H, ld, L, Vt, nullptr, tid);
-  if (tid < LT) kval[tid] = tid < L && (mask == nullptr || mask[(long long)b * L + tid] != 0);
+  if (tid < LT) kval[tid] = tid < L && (mask == nullptr || mask[(long long)row0 + tid] != 0);
   s16x8 qf[2][2];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(256) void bert_attn_fwd_kernel(const bf16_t* __rest
     sum += __shfl_xor(sum, 32, 64);
     const float inv = 1.f / sum;
     if (g == 0 && q < L) stats[(long long)z * LT + q] = make_float2(mx, inv);
-    const uint64_t rowi = ((uint64_t)z * L + q) * (uint64_t)Lp;
+    const uint64_t rowi = ((uint64_t)z * Lmax + q) * (uint64_t)Lp;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       float a[4], c[4];
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(256) void bert_attn_fwd_kernel(const bf16_t* __rest
   for (int qt = 0; qt < 2; ++qt) {
     const int q = 32 * w + 16 * qt + i;
     if (q < L) {
-      bf16_t* o = ctx + ((long long)b * L + q) * H + h * DH + 4 * g;
+      bf16_t* o = ctx + ((long long)row0 + q) * H + h * DH + 4 * g;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
         *reinterpret_cast<uint2*>(o + 16 * dt) =
@@ -217,8 +220,9 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ dctx,
                                                             const long long* __restrict__ mask,
                                                             const float2* __restrict__ stats,
-                                                            bf16_t* __restrict__ dqkv, int nh, int L, int Lp,
-                                                            float scale, float p, uint64_t seed) {
+                                                            bf16_t* __restrict__ dqkv, const int* __restrict__ seq,
+                                                            int nh, int Lmax, int Lp, float scale, float p,
+                                                            uint64_t seed) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[LT * DH];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[LT * DH];
   __shared__ __attribute__((aligned(16))) bf16_t Qt[DH * TP];
@@ -232,15 +236,17 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
   const int H = nh * DH;
   const long long ld = 3LL * H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const bf16_t* base = qkv + (long long)b * L * ld + h * DH;
-  const bf16_t* dob = dctx + (long long)b * L * H + h * DH;
-  bf16_t* gq = dqkv + (long long)b * L * ld + h * DH;
+  const int row0 = seq ? seq[b] : b * Lmax;
+  const int L = seq ? seq[b + 1] - row0 : Lmax;
+  const bf16_t* base = qkv + (long long)row0 * ld + h * DH;
+  const bf16_t* dob = dctx + (long long)row0 * H + h * DH;
+  bf16_t* gq = dqkv + (long long)row0 * ld + h * DH;
 
   load_transpose(base, ld, L, Qt, Qs, tid);
   load_transpose(dob, H, L, dOt, dOs, tid);
   load_transpose(base + H, ld, L, Kt, nullptr, tid);
   if (tid < LT) {
-    kval[tid] = tid < L && (mask == nullptr || mask[(long long)b * L + tid] != 0);
+    kval[tid] = tid < L && (mask == nullptr || mask[(long long)row0 + tid] != 0);
     st[tid] = tid < L ? stats[(long long)z * LT + tid] : make_float2(0.f, 0.f);
   }
   s16x8 kf[2][2], vf[2][2];
@@ -287,7 +293,7 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
     for (int r = 0; r < 4; ++r) {
       const int q = 16 * qt + 4 * g + r;
       const float2 mi = st[q];
-      const uint64_t rowi = ((uint64_t)z * L + q) * (uint64_t)Lp;
+      const uint64_t rowi = ((uint64_t)z * Lmax + q) * (uint64_t)Lp;
       float part = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -411,19 +417,41 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
 
 }  // namespace
 
-VCG_API int vcg_bert_attn_fwd(const void* qkv, const long long* mask, void* ctx, void* stats, int B, int nh, int L,
-                              int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s) {
-  if (B == 0 || L == 0) return VCG_OK;
-  if (!qkv || !ctx || !stats || B < 0 || nh <= 0 || L < 0 || Lp < L) {
-    set_error("vcg_bert_attn_fwd: invalid arguments");
+VCG_API int vcg_bert_attn_fwd_varlen(const void* qkv, const long long* mask, const int* seq, void* ctx, void* stats,
+                                     int B, int nh, int Lmax, int Lp, float scale, float dropout_p,
+                                     unsigned long long seed, hipStream_t s);
+VCG_API int vcg_bert_attn_bwd_varlen(const void* qkv, const void* dctx, const long long* mask, const int* seq,
+                                     const void* stats, void* dqkv, int B, int nh, int Lmax, int Lp, float scale,
+                                     float dropout_p, unsigned long long seed, hipStream_t s);
+
+static int attn_check(const char* fn, const void* qkv, const void* out, const void* stats, int B, int nh, int L, int Lp) {
+  if (!qkv || !out || !stats || B < 0 || nh <= 0 || L < 0 || Lp < L) {
+    set_error(std::string(fn) + ": invalid arguments");
     return VCG_ERR_INVALID;
   }
   if (L > LT) {
-    set_error("vcg_bert_attn_fwd: L > 128 is not supported by the fused kernel");
+    set_error(std::string(fn) + ": L > 128 is not supported by the fused kernel");
     return VCG_ERR_UNSUPPORTED;
   }
+  return VCG_OK;
+}
+
+VCG_API int vcg_bert_attn_fwd(const void* qkv, const long long* mask, void* ctx, void* stats, int B, int nh, int L,
+                              int Lp, float scale, float dropout_p, unsigned long long seed, hipStream_t s) {
+  return vcg_bert_attn_fwd_varlen(qkv, mask, nullptr, ctx, stats, B, nh, L, Lp, scale, dropout_p, seed, s);
+}
+
+// Packed (unpadded) sequences: sequence b's rows are seq[b] .. seq[b + 1] - 1 of qkv / ctx (at most Lmax <= 128 of
+// them), mask the key flags of those rows (NULL: every row is a key); stats and the dropout counters keep the padded
+// [B][nh][Lmax] index space, so a sequence whose kept rows are a prefix of its padded rows gets the padded result.
+VCG_API int vcg_bert_attn_fwd_varlen(const void* qkv, const long long* mask, const int* seq, void* ctx, void* stats,
+                                     int B, int nh, int Lmax, int Lp, float scale, float dropout_p,
+                                     unsigned long long seed, hipStream_t s) {
+  if (B == 0 || Lmax == 0) return VCG_OK;
+  const int rc = attn_check("vcg_bert_attn_fwd", qkv, ctx, stats, B, nh, Lmax, Lp);
+  if (rc != VCG_OK) return rc;
   hipLaunchKernelGGL(bert_attn_fwd_kernel, dim3(B * nh), dim3(256), 0, s, (const bf16_t*)qkv, mask, (bf16_t*)ctx,
-                     (float2*)stats, nh, L, Lp, scale, dropout_p, (uint64_t)seed);
+                     (float2*)stats, seq, nh, Lmax, Lp, scale, dropout_p, (uint64_t)seed);
   VCG_CHECK_HIP(hipGetLastError());
   return VCG_OK;
 }
@@ -431,19 +459,22 @@ VCG_API int vcg_bert_attn_fwd(const void* qkv, const long long* mask, void* ctx,
 VCG_API int vcg_bert_attn_bwd(const void* qkv, const void* dctx, const void* ctx, const long long* mask,
                               const void* stats, void* dqkv, int B, int nh, int L, int Lp, float scale,
                               float dropout_p, unsigned long long seed, hipStream_t s) {
-  if (B == 0 || L == 0) return VCG_OK;
   (void)ctx;  // (kept in the signature: the backward no longer needs the forward's output)
-  if (!qkv || !dctx || !stats || !dqkv || B < 0 || nh <= 0 || L < 0 || Lp < L) {
+  return vcg_bert_attn_bwd_varlen(qkv, dctx, mask, nullptr, stats, dqkv, B, nh, L, Lp, scale, dropout_p, seed, s);
+}
+
+VCG_API int vcg_bert_attn_bwd_varlen(const void* qkv, const void* dctx, const long long* mask, const int* seq,
+                                     const void* stats, void* dqkv, int B, int nh, int Lmax, int Lp, float scale,
+                                     float dropout_p, unsigned long long seed, hipStream_t s) {
+  if (B == 0 || Lmax == 0) return VCG_OK;
+  if (!dctx) {
     set_error("vcg_bert_attn_bwd: invalid arguments");
     return VCG_ERR_INVALID;
   }
-  if (L > LT) {
-    set_error("vcg_bert_attn_bwd: L > 128 is not supported by the fused kernel");
-    return VCG_ERR_UNSUPPORTED;
-  }
+  const int rc = attn_check("vcg_bert_attn_bwd", qkv, dqkv, stats, B, nh, Lmax, Lp);
+  if (rc != VCG_OK) return rc;
   hipLaunchKernelGGL(bert_attn_bwd_kernel, dim3(B * nh), dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)dctx, mask,
-                     (const float2*)stats, (bf16_t*)dqkv, nh, L, Lp, scale, dropout_p,
-                     (uint64_t)seed);
+                     (const float2*)stats, (bf16_t*)dqkv, seq, nh, Lmax, Lp, scale, dropout_p, (uint64_t)seed);
   VCG_CHECK_HIP(hipGetLastError());
   return VCG_OK;
 }

@@ -137,6 +137,22 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
   const int ksteps = (2 * W + 31) / 32;  // k = the tile's 2W pixels, padded to 32 with zero dy0 rows
   for (int i = 2 * W * 8 + tid; i < ksteps * 32 * 8; i += SB_NTH)  // (the pad rows, never DMA'd)
     *reinterpret_cast<uint4*>(smem + 16 * i) = uint4{0u, 0u, 0u, 0u};
+  // a thread's phase-1 items keep one 8-channel chunk c8 for the whole kernel: its 5 x 8 parameters live in registers
+  // (read once here, before any LDS-DMA is in flight, instead of 10 ds_read_b128 per item and tile)
+  __syncthreads();
+  float sc[8], sh[8], A[8], Bc[8], Cc[8];
+  {
+    float* dst[5] = {sc, sh, A, Bc, Cc};
+#pragma unroll
+    for (int v = 0; v < 5; ++v) {
+      const uint4 lo = sb_ld16(&prm[v][8 * c8]), hi = sb_ld16(&prm[v][8 * c8 + 4]);
+      sb_lgkm0();
+      dst[v][0] = __uint_as_float(lo.x); dst[v][1] = __uint_as_float(lo.y);
+      dst[v][2] = __uint_as_float(lo.z); dst[v][3] = __uint_as_float(lo.w);
+      dst[v][4] = __uint_as_float(hi.x); dst[v][5] = __uint_as_float(hi.y);
+      dst[v][6] = __uint_as_float(hi.z); dst[v][7] = __uint_as_float(hi.w);
+    }
+  }
 
   // tile lt's DMAs into the slot: instruction i = wave, wave + 4, ... of Y | D | I | P
   auto issue = [&](int lt) {
@@ -174,17 +190,10 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
     const bf16_t* Dg = reinterpret_cast<const bf16_t*>(S + SB_YB);
     const uint8_t* Ib = reinterpret_cast<const uint8_t*>(S + SB_YB + SB_DB);
     bf16_t* Y = reinterpret_cast<bf16_t*>(S);
-    float sc[8], sh[8], A[8], Bc[8], Cc[8];
     uint4 g4[4], y4s[4];
     uint2 w2[4];
     bool use[4];
     {
-      uint4 pr4[10];
-#pragma unroll
-      for (int v = 0; v < 5; ++v) {
-        pr4[2 * v] = sb_ld16(&prm[v][8 * c8]);
-        pr4[2 * v + 1] = sb_ld16(&prm[v][8 * c8 + 4]);
-      }
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         const int rr = qq >> 1, col = min(jj + (qq & 1), OW - 1);
@@ -198,15 +207,6 @@ void stem_bwd_fused_kernel(StemBwdArgs a) {
         y4s[p4] = sb_ld16(Y + pix * 64 + 8 * sb_swz(pix, c8));
       }
       sb_lgkm0();
-      float* dst[5] = {sc, sh, A, Bc, Cc};
-#pragma unroll
-      for (int v = 0; v < 5; ++v) {
-        const uint4 lo = pr4[2 * v], hi = pr4[2 * v + 1];
-        dst[v][0] = __uint_as_float(lo.x); dst[v][1] = __uint_as_float(lo.y);
-        dst[v][2] = __uint_as_float(lo.z); dst[v][3] = __uint_as_float(lo.w);
-        dst[v][4] = __uint_as_float(hi.x); dst[v][5] = __uint_as_float(hi.y);
-        dst[v][6] = __uint_as_float(hi.z); dst[v][7] = __uint_as_float(hi.w);
-      }
     }
 #pragma unroll
     for (int p4 = 0; p4 < 4; ++p4) {

@@ -177,7 +177,7 @@ class TwoStream(NativeRoot, nn.Module):
         return self._forward(frames, text_ids.shape[0], text_ids, attention_mask, return_emb, staged=True)
 
     def _forward(self, img, batch_size, text_ids, attention_mask, return_emb, staged):
-        from vcg_hip.bert import BertEncoderEngine
+        from vcg_hip.bert import BertEncoderEngine, PackingRequest
         from vcg_hip.functions import BertFn, HeadFn, TrunkFn
         from vcg_hip.head import HeadEngine
         from vcg_hip.trunk import ResNetTrunk
@@ -194,6 +194,9 @@ class TwoStream(NativeRoot, nn.Module):
         if attention_mask is None:
             attention_mask = torch.ones_like(text_ids)
         bert = BertEncoderEngine(self.lang_model, f, dt)
+        bert.pooled_only = True  # (the pooler output is the only one read: padded token rows may be dropped)
+        if bert.packs(text_ids):
+            bert.packing = PackingRequest(attention_mask)
         side = self._side_stream(dev)
         if side is None:
             lang_emb, _ = BertFn.apply(text_ids, attention_mask, anchor, bert, need_grad, new_seed(), hooks)

@@ -7,9 +7,18 @@ Reference use: TwoStream.forward -> lang_model(input_ids, attention_mask).pooler
 kernel per direction, bert_attn.hip, nothing L x L in HBM; otherwise batched QK^T -> masked softmax (+dropout) ->
 batched PV) -> out-proj GEMM -> LN(dropout(.)+res) -> FFN1 GEMM with erf-GELU
 epilogue -> FFN2 GEMM -> LN(dropout(.)+res); pooler = tanh(W h[:,0] + b).
+
+Unpadded sequences (Packing, bf16 with the fused attention, callers that read only the pooler output -- TwoStream,
+two_stream.py:178-179): a padded position (attention_mask 0) is a masked key, so no kept row ever reads it, and the
+pooler reads only row 0; its rows are therefore dropped from every GEMM, LayerNorm and attention of the encoder (the
+embedding LayerNorm still runs padded, then the kept rows are gathered; its gradient is scattered back with zeros at
+the padded rows, which is what they receive in the padded computation). With prefix masks every kept row sees
+exactly the padded computation (same attention key positions and dropout counters).
 """
 import math
+import weakref
 
+import numpy as np
 import torch
 
 from . import ops
@@ -73,15 +82,70 @@ class _LinearT:
         return self.t.get(W.data_ptr())
 
 
+class Packing:
+    """The kept rows of a padded [B, L] batch: every position with attention_mask != 0, plus position 0 (the pooler's
+    row, even if masked), plus every row of a sequence without any key (HF then attends uniformly to all L rows).
+    rows: flat b*L + t of the kept rows in order (int64 [R]); seq: int32 [B+1] prefix offsets; keys: the kept rows'
+    mask values (int64 [R], the fused attention's key flags); cls: the packed row of each sequence's position 0."""
+
+    def __init__(self, mask_np, device):
+        B, L = mask_np.shape
+        keep = mask_np != 0
+        keep[~keep.any(1)] = True
+        keep[:, 0] = True
+        n = keep.sum(1)
+        seq = np.zeros(B + 1, dtype=np.int32)
+        seq[1:] = np.cumsum(n)
+        rows = np.flatnonzero(keep.reshape(-1)).astype(np.int64)
+        self.B, self.L, self.R = B, L, int(seq[-1])
+        host = [torch.from_numpy(a).pin_memory() for a in (rows, seq, mask_np.reshape(-1)[rows].astype(np.int64),
+                                                           seq[:-1].astype(np.int64))]
+        self.rows, self.seq, self.keys, self.cls = (t.to(device, non_blocking=True) for t in host)
+        self._host = host  # (the pinned sources stay alive until the copies have run: the engine holds the Packing)
+
+
+class PackingRequest:
+    """The packing of a device attention mask without stalling the GPU: the mask's device-to-host copy is issued on
+    the caller's stream now (behind whatever produced the mask), the host waits for it only in get() -- TwoStream
+    enqueues the trunk forward in between. The result is cached per mask tensor object and version, so a batch fed
+    again (bench.py's synthetic step) costs no copy."""
+    _last = None  # (weakref to the mask, its _version, Packing)
+
+    def __init__(self, mask):
+        last = PackingRequest._last
+        if last is not None and last[0]() is mask and last[1] == mask._version:
+            self.pk, self.ev = last[2], None
+            return
+        self.mask = mask
+        self.host = torch.empty(mask.shape, dtype=mask.dtype, pin_memory=True)
+        self.host.copy_(mask, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+        self.pk = None
+
+    def get(self):
+        if self.pk is None:
+            self.ev.synchronize()
+            self.pk = Packing(self.host.numpy(), self.mask.device)
+            PackingRequest._last = (weakref.ref(self.mask), self.mask._version, self.pk)
+            self.mask = self.host = None
+        return self.pk
+
+
 class BertEncoderEngine:
     # bf16 L <= 128: the fused attention kernels (bert_attn.hip); False: the unfused kernels (tests compare both)
     fused_attn = True
+    # unpadded sequences (Packing) where the caller reads only the pooler output and the fused attention applies;
+    # False: every padded row is computed (tests compare both)
+    unpad = True
 
     def __init__(self, model, flat, dtype):
         self.m = model
         self.flat = flat
         self.dtype = dtype
         self.wt = None
+        self.pooled_only = False  # the caller reads only the pooler output (TwoStream): the rows may be unpadded
+        self.packing = None  # forward()'s default packing (a Packing / PackingRequest the caller made)
         if dtype == torch.bfloat16 and flat is not None:
             wt = getattr(model, "_vcg_bert_wt", None)
             if wt is None or wt.flat is not flat:
@@ -116,15 +180,29 @@ class BertEncoderEngine:
             return ops.gemm(A, ops.transpose(W), M, N, K, K, K, **kw)
         return ops.gemm(A, W, M, N, K, K, N, transB=True, **kw)
 
-    def forward(self, ids, mask, need_grad, seed):
+    def packs(self, ids):
+        """forward() would run unpadded (a PackingRequest is worth making)."""
+        cfg = self.m.config
+        return (BertEncoderEngine.unpad and self.pooled_only and self.m.pooler is not None and ids.is_cuda
+                and self._fused_attn(ids.shape[1], cfg.hidden_size // cfg.num_attention_heads))
+
+    def forward(self, ids, mask, need_grad, seed, packing=None):
+        """packing: a Packing or PackingRequest of `mask` (only where packs()); its kept rows are computed, and the
+        second output (the last hidden state) is then empty."""
         m, dt, flat = self.m, self.dtype, self.flat
+        if packing is None:
+            packing = self.packing
         cfg = m.config
         B, L = ids.shape
         H = cfg.hidden_size
         nh = cfg.num_attention_heads
         dh = H // nh
         Lp = (L + 7) // 8 * 8
-        rows = B * L
+        if isinstance(packing, PackingRequest):
+            packing = packing.get()
+        if packing is not None and packing.R == B * L:  # nothing to drop
+            packing = None
+        rows = B * L if packing is None else packing.R
         # dropout rates from the nn.Dropout modules, as HF's BertModel applies them (a caller may change .p after
         # construction); hidden dropout sites share one rate, attention-probability sites another
         hid = [emb_d for emb_d in [m.embeddings.dropout] + [d for lyr in m.encoder.layer
@@ -145,6 +223,9 @@ class BertEncoderEngine:
         h, e_mean, e_rstd = ops.embed_ln_fwd(ids, emb.word_embeddings.weight, emb.position_embeddings.weight,
                                              emb.token_type_embeddings.weight, emb.LayerNorm.weight,
                                              emb.LayerNorm.bias, B, L, H, eps, dt, p_h, _seed(seed, 0, 0))
+        if packing is not None:
+            h = h.index_select(0, packing.rows)
+        att_mask, seq = (mask, None) if packing is None else (packing.keys, packing.seq)
         saved_layers = []
         for i, layer in enumerate(m.encoder.layer):
             at = layer.attention
@@ -155,7 +236,8 @@ class BertEncoderEngine:
             qkv = qkv_buf[:rows]
             ops.gemm(h, Wqkv, rows, 3 * H, H, H, H, out=qkv, ldc=3 * H, bias=bqkv, act=lib)
             sa = _seed(seed, i + 1, 1)
-            ctx, att = attention_fwd(qkv_buf, mask, B, nh, L, Lp, dh, scale, p_a, sa, self._fused_attn(L, dh))
+            ctx, att = attention_fwd(qkv_buf, att_mask, B, nh, L, Lp, dh, scale, p_a, sa, self._fused_attn(L, dh),
+                                     seq=seq, rows=rows)
             ao = ops.gemm(ctx, self._w(at.output.dense.weight), rows, H, H, H, H, bias=at.output.dense.bias, act=lib)
             s1 = _seed(seed, i + 1, 2)
             h1, m1, r1 = ops.ln_fwd(ao, h, at.output.LayerNorm.weight, at.output.LayerNorm.bias, rows, H, eps, p_h, s1)
@@ -172,19 +254,27 @@ class BertEncoderEngine:
                                          fo=fo, m1=m1, r1=r1, m2=m2, r2=r2, sa=sa, s1=s1, s2=s2))
             h = h2
         pooled = None
+        cls = h if packing is None else h.index_select(0, packing.cls)  # (packed: the B position-0 rows)
+        lda = L * H if packing is None else H
         if m.pooler is not None:
             pd = m.pooler.dense
-            pooled = ops.gemm(h, self._w(pd.weight), B, H, H, L * H, H, bias=pd.bias, act=ops.ACT_TANH)
+            pooled = ops.gemm(cls, self._w(pd.weight), B, H, H, lda, H, bias=pd.bias, act=ops.ACT_TANH)
         saved = None
         if need_grad:
-            saved = dict(ids=ids, mask=mask, layers=saved_layers, e_mean=e_mean, e_rstd=e_rstd, h_last=h, pooled=pooled, B=B,
-                         L=L, Lp=Lp, H=H, nh=nh, dh=dh, p_h=p_h, p_a=p_a, scale=scale, seed=seed)
+            saved = dict(ids=ids, mask=att_mask, seq=seq, packing=packing, layers=saved_layers, e_mean=e_mean,
+                         e_rstd=e_rstd, h_last=cls, lda=lda, pooled=pooled, B=B, L=L, Lp=Lp, H=H, nh=nh, dh=dh,
+                         p_h=p_h, p_a=p_a, scale=scale, seed=seed)
+        if packing is not None:
+            h = h.new_empty((0, H))  # (the padded rows' hidden states were not computed)
         return pooled, h, saved
 
     def backward(self, d_pooled, d_last, sv, hooks=None):
         m, dt, flat = self.m, self.dtype, self.flat
         B, L, Lp, H, nh, dh = sv["B"], sv["L"], sv["Lp"], sv["H"], sv["nh"], sv["dh"]
-        rows = B * L
+        packing = sv["packing"]
+        rows = B * L if packing is None else packing.R
+        if packing is not None and d_last is not None and d_last.numel():
+            raise RuntimeError("BertEncoderEngine: the unpadded forward has no last hidden state to differentiate")
         p_h, p_a, scale, seed = sv["p_h"], sv["p_a"], sv["scale"], sv["seed"]
         dev = sv["ids"].device
         # the residual-gradient stream (the gradient w.r.t. each LayerNorm output, summed over the skip and the next
@@ -192,20 +282,24 @@ class BertEncoderEngine:
         # LayerNorm outputs are fp32): bf16 roundings of it compounded over 24 LayerNorms
         g32 = dt == torch.bfloat16 and self.wt is not None
         gd = torch.float32 if g32 else dt
-        if d_last is not None:
+        if d_last is not None and d_last.numel():
             dh_ = d_last.to(gd).contiguous().clone()
         else:
             dh_ = torch.zeros((rows, H), dtype=gd, device=dev)
         if d_pooled is not None and m.pooler is not None:
             pd = m.pooler.dense
             dpp = ops.tanh_bwd(d_pooled.to(dt).contiguous(), sv["pooled"])
-            h_last = sv["h_last"]
+            h_last, lda = sv["h_last"], sv["lda"]
             if pd.weight.requires_grad:
-                ops.gemm_splitk(dpp, h_last, pd.weight.grad, H, H, B, H, L * H, transA=True, transB=True)
+                ops.gemm_splitk(dpp, h_last, pd.weight.grad, H, H, B, H, lda, transA=True, transB=True)
                 ops.colsum(dpp, H, B, H, pd.bias.grad)
             # dh[b*L] += dpp @ Wp (B rows: an fp32 GEMM on the fp32 stream)
             dpw = (dpp.float(), pd.weight.data) if g32 else (dpp, self._w(pd.weight))
-            ops.gemm(dpw[0], dpw[1], B, H, H, H, H, transB=True, out=dh_, ldc=L * H, residual=dh_, ldr=L * H)
+            if packing is None:
+                ops.gemm(dpw[0], dpw[1], B, H, H, H, H, transB=True, out=dh_, ldc=L * H, residual=dh_, ldr=L * H)
+            else:  # (dh_ is zero: the CLS rows receive the product)
+                dh_.index_copy_(0, packing.cls, ops.gemm(dpw[0], dpw[1], B, H, H, H, H, transB=True,
+                                                         out=torch.empty((B, H), dtype=gd, device=dev)))
             if hooks is not None:
                 hooks(list(m.pooler.parameters()))
         for i in reversed(range(len(sv["layers"]))):
@@ -234,7 +328,7 @@ class BertEncoderEngine:
             # ---- attention backward
             qkv_buf = s["qkv_buf"]
             dqkv = attention_bwd(qkv_buf, dctx, s["ctx"], sv["mask"], s["att"], B, nh, L, Lp, dh, scale, p_a,
-                                 s["sa"])
+                                 s["sa"], seq=sv["seq"], rows=rows)
             del dctx
             sq, sk, svv = at.self.query, at.self.key, at.self.value
             if sq.weight.requires_grad:
@@ -248,6 +342,9 @@ class BertEncoderEngine:
             if hooks is not None:
                 hooks(list(layer.parameters()))
         emb = m.embeddings
+        if packing is not None:  # back to the padded rows (zero gradient at the dropped ones)
+            dpad = torch.zeros((B * L, H), dtype=dh_.dtype, device=dev)
+            dh_ = dpad.index_copy_(0, packing.rows, dh_)
         ops.embed_ln_bwd(dh_, sv["ids"], emb.word_embeddings.weight, emb.position_embeddings.weight,
                          emb.token_type_embeddings.weight, emb.LayerNorm.weight, sv["e_mean"], sv["e_rstd"],
                          emb.word_embeddings.weight.grad, emb.position_embeddings.weight.grad,
@@ -258,18 +355,20 @@ class BertEncoderEngine:
             hooks(list(emb.parameters()))
 
 
-def attention_fwd(qkv_buf, mask, B, nh, L, Lp, dh, scale, p_a, seed, fused):
+def attention_fwd(qkv_buf, mask, B, nh, L, Lp, dh, scale, p_a, seed, fused, seq=None, rows=None):
     """ctx [B*L, H] of HF BertSelfAttention (eager) from the fused projection qkv_buf [B*L (+8), 3H] and the
     key mask [B, L]; returns (ctx, saved-for-backward). fused: bert_attn.hip (bf16, L <= 128, dh = 64: one kernel,
-    row statistics saved); else QK^T GEMM -> masked softmax (+dropout) -> PV GEMM with S, P, Pd in HBM."""
+    row statistics saved); else QK^T GEMM -> masked softmax (+dropout) -> PV GEMM with S, P, Pd in HBM.
+    seq: packed sequences (Packing.seq; fused only), `rows` rows, mask = the packed rows' key flags."""
     H = nh * dh
-    rows = B * L
+    rows = B * L if rows is None else rows
     dt, dev = qkv_buf.dtype, qkv_buf.device
     ctx = torch.empty((rows, H), dtype=dt, device=dev)
     if fused:
         stats = torch.empty((B * nh * 128, 2), dtype=torch.float32, device=dev)
-        ops.bert_attn_fwd(qkv_buf, mask, ctx, stats, B, nh, L, Lp, scale, p_a, seed)
+        ops.bert_attn_fwd(qkv_buf, mask, ctx, stats, B, nh, L, Lp, scale, p_a, seed, seq=seq)
         return ctx, dict(stats=stats)
+    assert seq is None, "packed sequences need the fused attention"
     Z = B * nh
     S = torch.empty((Z, L, Lp), dtype=dt, device=dev)
     ops.gemm_batched(qkv_buf, qkv_buf[:, H:], S, L, Lp, dh, 3 * H, 3 * H, Lp, L * 3 * H, dh, L * 3 * H, dh,
@@ -284,14 +383,14 @@ def attention_fwd(qkv_buf, mask, B, nh, L, Lp, dh, scale, p_a, seed, fused):
     return ctx, dict(P=Pm, Pd=Pd)
 
 
-def attention_bwd(qkv_buf, dctx, ctx, mask, att, B, nh, L, Lp, dh, scale, p_a, seed):
+def attention_bwd(qkv_buf, dctx, ctx, mask, att, B, nh, L, Lp, dh, scale, p_a, seed, seq=None, rows=None):
     """dqkv [B*L, 3H] (dQ | dK | dV) from dctx = d ctx, given attention_fwd's saved state."""
     H = nh * dh
-    rows = B * L
+    rows = B * L if rows is None else rows
     dt, dev = qkv_buf.dtype, qkv_buf.device
     dqkv = torch.empty((rows, 3 * H), dtype=dt, device=dev)
     if "stats" in att:
-        ops.bert_attn_bwd(qkv_buf, dctx, ctx, mask, att["stats"], dqkv, B, nh, L, Lp, scale, p_a, seed)
+        ops.bert_attn_bwd(qkv_buf, dctx, ctx, mask, att["stats"], dqkv, B, nh, L, Lp, scale, p_a, seed, seq=seq)
         return dqkv
     Z = B * nh
     dPd = torch.empty((Z, L, Lp), dtype=dt, device=dev)

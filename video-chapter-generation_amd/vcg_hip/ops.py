@@ -757,15 +757,25 @@ def attn_softmax_bwd(dPd, Pm, dS, Z, L, Lp, scale, p=0.0, seed=0):
               int(seed) & (2**64 - 1), stream())
 
 
-def bert_attn_fwd(qkv, mask, ctx, stats, B, nh, L, Lp, scale, p=0.0, seed=0):
-    """Fused attention forward (bf16): qkv [B*L(+pad), 3H] -> ctx [B*L, H]; stats [B*nh*128, 2] f32."""
-    _lib.call("vcg_bert_attn_fwd", P(qkv), P(mask), P(ctx), P(stats), B, nh, L, Lp, float(scale), float(p),
-              int(seed) & (2**64 - 1), stream())
+def bert_attn_fwd(qkv, mask, ctx, stats, B, nh, L, Lp, scale, p=0.0, seed=0, seq=None):
+    """Fused attention forward (bf16): qkv [B*L(+pad), 3H] -> ctx [B*L, H]; stats [B*nh*128, 2] f32.
+    seq (int32 [B+1]): packed sequences, rows seq[b] .. seq[b+1]-1 (L = the longest, mask = the packed rows' key
+    flags; vcg_bert_attn_fwd_varlen)."""
+    if seq is None:
+        _lib.call("vcg_bert_attn_fwd", P(qkv), P(mask), P(ctx), P(stats), B, nh, L, Lp, float(scale), float(p),
+                  int(seed) & (2**64 - 1), stream())
+    else:
+        _lib.call("vcg_bert_attn_fwd_varlen", P(qkv), P(mask), P(seq), P(ctx), P(stats), B, nh, L, Lp, float(scale),
+                  float(p), int(seed) & (2**64 - 1), stream())
 
 
-def bert_attn_bwd(qkv, dctx, ctx, mask, stats, dqkv, B, nh, L, Lp, scale, p=0.0, seed=0):
-    _lib.call("vcg_bert_attn_bwd", P(qkv), P(dctx), P(ctx), P(mask), P(stats), P(dqkv), B, nh, L, Lp, float(scale),
-              float(p), int(seed) & (2**64 - 1), stream())
+def bert_attn_bwd(qkv, dctx, ctx, mask, stats, dqkv, B, nh, L, Lp, scale, p=0.0, seed=0, seq=None):
+    if seq is None:
+        _lib.call("vcg_bert_attn_bwd", P(qkv), P(dctx), P(ctx), P(mask), P(stats), P(dqkv), B, nh, L, Lp, float(scale),
+                  float(p), int(seed) & (2**64 - 1), stream())
+    else:
+        _lib.call("vcg_bert_attn_bwd_varlen", P(qkv), P(dctx), P(mask), P(seq), P(stats), P(dqkv), B, nh, L, Lp,
+                  float(scale), float(p), int(seed) & (2**64 - 1), stream())
 
 
 def tanh_bwd(dy, t):
