@@ -19,13 +19,13 @@ run() {  # name, args...
 [ "${BENCH:-1}" = 1 ] && {
 run fwd_bf16_running --mode fwd --steps 10 --warmup 3
 run fwd_bf16_batch16 --mode fwd --bn batch --steps 20 --warmup 3
-run fwd_bf16_batch16_streams4 --mode fwd --bn batch --scoring-streams 4 --steps 10 --warmup 3
+run fwd_bf16_batch16_groups4 --mode fwd --bn batch --bn-groups 4 --steps 10 --warmup 3
 run fwd_fp32_running --mode fwd --precision fp32 --steps 5 --warmup 2
 run fwd_fp32_batch16 --mode fwd --precision fp32 --bn batch --steps 10 --warmup 2
 run train_fp32_b64 --precision fp32 --steps 3 --warmup 1 --no-cpu-baseline
 run c5_bf16_running --mode long_video
 run c5_bf16_batch16 --mode long_video --bn batch
-run c5_bf16_batch16_streams4 --mode long_video --bn batch --scoring-streams 4
+run c5_bf16_batch16_groups4 --mode long_video --bn batch --bn-groups 4
 run c5_fp32_batch16_stride4 --mode long_video --bn batch --precision fp32 --stride 4
 }
 [ "${SWEEP:-0}" = 1 ] || exit 0

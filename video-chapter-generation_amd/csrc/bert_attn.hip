@@ -118,6 +118,8 @@ __global__ __launch_bounds__(256) void bert_attn_fwd_kernel(const bf16_t* __rest
       qf[qt][s] = __builtin_bit_cast(s16x8, u);
     }
   __syncthreads();
+  // (a packed sequence shorter than 128 rows: tiles of keys / queries past its end add nothing and are skipped)
+  if (32 * w >= L) return;  // every query of this wave is past the end (no barrier follows)
 
   f32x4 sacc[2][8];
 #pragma unroll
@@ -126,11 +128,13 @@ __global__ __launch_bounds__(256) void bert_attn_fwd_kernel(const bf16_t* __rest
     for (int kt = 0; kt < 8; ++kt) sacc[qt][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt)
+    if (16 * kt < L) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const s16x8 kf = frag_rm(Ks, 16 * kt + i, 4 * s + g);
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 kf = frag_rm(Ks, 16 * kt + i, 4 * s + g);
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) sacc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][s], sacc[qt][kt], 0, 0, 0);
+        for (int qt = 0; qt < 2; ++qt) sacc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][s], sacc[qt][kt], 0, 0, 0);
+      }
     }
   // lane holds S^T[key 16 kt + 4 g + r][query 32 w + 16 qt + i]
   uint32_t vb = 0;  // bit 4 kt + r: key 16 kt + 4 g + r is valid
@@ -192,11 +196,13 @@ __global__ __launch_bounds__(256) void bert_attn_fwd_kernel(const bf16_t* __rest
     for (int qt = 0; qt < 2; ++qt) oacc[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 4; ++s)
+    if (32 * s < L) {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const s16x8 vf = frag_split(Vt, 16 * dt + i, 32 * s + 4 * g);
+      for (int dt = 0; dt < 4; ++dt) {
+        const s16x8 vf = frag_split(Vt, 16 * dt + i, 32 * s + 4 * g);
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) oacc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][s], oacc[dt][qt], 0, 0, 0);
+        for (int qt = 0; qt < 2; ++qt) oacc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][s], oacc[dt][qt], 0, 0, 0);
+      }
     }
   // lane holds O^T[d 16 dt + 4 g + r][query 32 w + 16 qt + i]
 #pragma unroll
@@ -265,16 +271,21 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
   for (int qt = 0; qt < 8; ++qt)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) sacc[qt][kt] = pacc[qt][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (tiles past the end of a packed sequence add nothing: skipped; a wave whose 32 keys are all past it keeps zeros,
+  // so its dS entries -- read by every wave's dQ -- are exact zeros)
+  const bool wkeys = 32 * w < L;
 #pragma unroll
   for (int qt = 0; qt < 8; ++qt)
+    if (wkeys && 16 * qt < L) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const s16x8 qa = frag_rm(Qs, 16 * qt + i, 4 * s + g);
-      const s16x8 da = frag_rm(dOs, 16 * qt + i, 4 * s + g);
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 qa = frag_rm(Qs, 16 * qt + i, 4 * s + g);
+        const s16x8 da = frag_rm(dOs, 16 * qt + i, 4 * s + g);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        sacc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kt][s], sacc[qt][kt], 0, 0, 0);
-        pacc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kt][s], pacc[qt][kt], 0, 0, 0);
+        for (int kt = 0; kt < 2; ++kt) {
+          sacc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kt][s], sacc[qt][kt], 0, 0, 0);
+          pacc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[kt][s], pacc[qt][kt], 0, 0, 0);
+        }
       }
     }
   // lane holds S / dPd [query 16 qt + 4 g + r][key 32 w + 16 kt + i]
@@ -341,6 +352,7 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
     for (int kt = 0; kt < 2; ++kt) dv[dt][kt] = dk[dt][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
+    if (!wkeys || 32 * s >= L) continue;
     s16x8 pb[2], sb[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -391,6 +403,7 @@ __global__ __launch_bounds__(256) void bert_attn_bwd_kernel(const bf16_t* __rest
     for (int qt = 0; qt < 2; ++qt) dq[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
+    if (32 * w >= L || 32 * s >= L) continue;  // (the wave's queries / this step's keys past the end)
     s16x8 sbq[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
