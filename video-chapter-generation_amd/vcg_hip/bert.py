@@ -82,6 +82,19 @@ class _LinearT:
         return self.t.get(W.data_ptr())
 
 
+def pack_rows(mask_np):
+    """Host side of Packing: (rows int64 [R] = flat b*L + t of the kept rows in order, seq int32 [B+1] prefix offsets,
+    keys int64 [R] = the kept rows' mask values, cls int64 [B] = the packed row of each sequence's position 0)."""
+    B, L = mask_np.shape
+    keep = mask_np != 0
+    keep[~keep.any(1)] = True
+    keep[:, 0] = True
+    seq = np.zeros(B + 1, dtype=np.int32)
+    seq[1:] = np.cumsum(keep.sum(1))
+    rows = np.flatnonzero(keep.reshape(-1)).astype(np.int64)
+    return rows, seq, mask_np.reshape(-1)[rows].astype(np.int64), seq[:-1].astype(np.int64)
+
+
 class Packing:
     """The kept rows of a padded [B, L] batch: every position with attention_mask != 0, plus position 0 (the pooler's
     row, even if masked), plus every row of a sequence without any key (HF then attends uniformly to all L rows).
@@ -90,16 +103,9 @@ class Packing:
 
     def __init__(self, mask_np, device):
         B, L = mask_np.shape
-        keep = mask_np != 0
-        keep[~keep.any(1)] = True
-        keep[:, 0] = True
-        n = keep.sum(1)
-        seq = np.zeros(B + 1, dtype=np.int32)
-        seq[1:] = np.cumsum(n)
-        rows = np.flatnonzero(keep.reshape(-1)).astype(np.int64)
+        rows, seq, keys, cls = pack_rows(mask_np)
         self.B, self.L, self.R = B, L, int(seq[-1])
-        host = [torch.from_numpy(a).pin_memory() for a in (rows, seq, mask_np.reshape(-1)[rows].astype(np.int64),
-                                                           seq[:-1].astype(np.int64))]
+        host = [torch.from_numpy(a).pin_memory() for a in (rows, seq, keys, cls)]
         self.rows, self.seq, self.keys, self.cls = (t.to(device, non_blocking=True) for t in host)
         self._host = host  # (the pinned sources stay alive until the copies have run: the engine holds the Packing)
 
