@@ -698,7 +698,8 @@ def main():
                    "per_launch_roofline": _per_launch(rl[dom_id]),
                    "wgrad_fast_kernel": _per_launch(rl[ops.TIMING_WGRAD]),
                    # the dense bf16 GEMMs of BERT's Linear layers and the downsample input gradient
-                   "gemm_wide_kernel": {**_per_launch(rl[ops.TIMING_WIDE_GEMM]), "launches_per_step": wide_n},
+                   "gemm_wide_kernel": ({**_per_launch(rl[ops.TIMING_WIDE_GEMM]), "launches_per_step": wide_n}
+                                        if _per_launch(rl[ops.TIMING_WIDE_GEMM]) else None),  # (fp32: none)
                    # round 4's category: every launch of the 128 x 128 / 256-tile engines AND the wide engine's (BERT's
                    # dense GEMMs were on the 128 x 128 engine then), so that moving GEMMs between engines does not
                    # read as kernel speed
