@@ -186,7 +186,7 @@ def test_unpadded_bert_in_two_stream_step(monkeypatch):
     res = {}
     for unpad in (True, False):
         monkeypatch.setattr(BertEncoderEngine, "unpad", unpad)
-        PackingRequest._last = None
+        PackingRequest._last = PackingRequest._mirror = None
         m = build_two_stream(clip_frame_num=T, seed=5, device=DEV, precision="bf16", dropout=0.0).train()
         logits, _ = m(frames, ids, mask)
         cross_entropy(logits, labels).backward()

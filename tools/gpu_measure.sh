@@ -13,7 +13,7 @@ if [ $# -gt 0 ]; then
 fi
 run() {  # name, args...
   local n=$1; shift
-  timeout -k 10 400 python bench.py "$@" > gpurun_out/${TAG}_$n.json 2> gpurun_out/${TAG}_$n.err || { echo "$n failed"; tail -5 gpurun_out/${TAG}_$n.err; exit 3; }
+  timeout -k 10 400 python bench.py "$@" > gpurun_out/${TAG}_$n.json 2> gpurun_out/${TAG}_$n.err || { echo "$n failed"; tail -5 gpurun_out/${TAG}_$n.err; exit 5; }
   echo "$n: $(tail -1 gpurun_out/${TAG}_$n.json | cut -c1-200)"
 }
 [ "${BENCH:-1}" = 1 ] && {
@@ -29,5 +29,5 @@ run c5_bf16_batch16_groups4 --mode long_video --bn batch --bn-groups 4
 run c5_fp32_batch16_stride4 --mode long_video --bn batch --precision fp32 --stride 4
 }
 [ "${SWEEP:-0}" = 1 ] || exit 0
-timeout -k 10 1100 python -u tools/cpu_sweep.py ${SWEEP_WHAT:-all} ${SWEEP_ARGS:-} --out gpurun_out/${TAG}_cpu_sweep.jsonl 2>&1 | tee gpurun_out/${TAG}_cpu_sweep.log || { echo "sweep failed"; tail -5 gpurun_out/${TAG}_cpu_sweep.log; exit 4; }
+timeout -k 10 1100 python -u tools/cpu_sweep.py ${SWEEP_WHAT:-all} ${SWEEP_ARGS:-} --out gpurun_out/${TAG}_cpu_sweep.jsonl 2>&1 | tee gpurun_out/${TAG}_cpu_sweep.log || { echo "sweep failed"; tail -5 gpurun_out/${TAG}_cpu_sweep.log; exit 6; }
 cat gpurun_out/${TAG}_cpu_sweep.jsonl | cut -c1-220

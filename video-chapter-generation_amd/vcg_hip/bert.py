@@ -111,30 +111,44 @@ class Packing:
 
 
 class PackingRequest:
-    """The packing of a device attention mask without stalling the GPU: the mask's device-to-host copy is issued on
-    the caller's stream now (behind whatever produced the mask), the host waits for it only in get() -- TwoStream
-    enqueues the trunk forward in between. The result is cached per mask tensor object and version, so a batch fed
-    again (bench.py's synthetic step) costs no copy."""
-    _last = None  # (weakref to the mask, its _version, Packing)
+    """The packing of a device attention mask: the host needs the mask, so a device-to-host copy is issued on the
+    caller's stream (behind whatever produced the mask) and waited for in get(). The host copy is kept per base tensor
+    (a mask that is a view -- long_video.score_windows' batches are slices of one mask of the whole video -- is read
+    from its base's copy: one copy for all batches, no wait after the first), so a batch fed again, or the next slice
+    of the same base, costs no device round trip while the base's version is unchanged."""
+    _mirror = None  # (weakref to the base tensor, its _version, pinned host copy of the base)
+    _last = None    # (weakref to the mask, its _version, its Packing)
 
     def __init__(self, mask):
+        base = mask._base if mask._base is not None else mask
+        self.mask, self.base, self.pk, self.ev = mask, base, None, None
         last = PackingRequest._last
         if last is not None and last[0]() is mask and last[1] == mask._version:
-            self.pk, self.ev = last[2], None
+            self.pk = last[2]
             return
-        self.mask = mask
-        self.host = torch.empty(mask.shape, dtype=mask.dtype, pin_memory=True)
-        self.host.copy_(mask, non_blocking=True)
+        mir = PackingRequest._mirror
+        if mir is not None and mir[0]() is base and mir[1] == base._version:
+            self.host = mir[2]
+            return
+        self.host = torch.empty(base.shape, dtype=base.dtype, pin_memory=True)
+        self.host.copy_(base, non_blocking=True)
         self.ev = torch.cuda.Event()
         self.ev.record()
-        self.pk = None
 
     def get(self):
         if self.pk is None:
-            self.ev.synchronize()
-            self.pk = Packing(self.host.numpy(), self.mask.device)
-            PackingRequest._last = (weakref.ref(self.mask), self.mask._version, self.pk)
-            self.mask = self.host = None
+            if self.ev is not None:
+                self.ev.synchronize()
+                PackingRequest._mirror = (weakref.ref(self.base), self.base._version, self.host)
+                self.ev = None
+            m, b = self.mask, self.base
+            flat = self.host.reshape(-1).numpy()
+            it = flat.itemsize
+            view = np.lib.stride_tricks.as_strided(flat[m.storage_offset() - b.storage_offset():], shape=tuple(m.shape),
+                                                   strides=tuple(st * it for st in m.stride()), writeable=False)
+            self.pk = Packing(np.ascontiguousarray(view), m.device)
+            PackingRequest._last = (weakref.ref(m), m._version, self.pk)
+            self.mask = self.base = self.host = None
         return self.pk
 
 
