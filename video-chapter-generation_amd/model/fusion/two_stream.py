@@ -120,8 +120,6 @@ class TwoStream(NativeRoot, nn.Module):
 
     # BERT on a side HIP stream beside the trunk (bench.py --one-stream and the instrumented step set it False)
     overlap_streams = True
-    # that stream's priority (torch.cuda.Stream: lower = higher priority; 0 = the default)
-    side_priority = 0
     # batch-statistics scoring of several batches in ONE forward (long_video.score_windows(groups=K), bench.py
     # --bn-groups K): with bn_group = G windows, a no-grad forward whose trunk BatchNorms use batch statistics runs the
     # trunk once per consecutive group of G windows (each group its own statistics: the reference harness's batches,
@@ -140,8 +138,8 @@ class TwoStream(NativeRoot, nn.Module):
         if not self.overlap_streams or dev.type != "cuda":
             return None
         s = getattr(self, "_vcg_side", None)
-        if s is None or s.device != dev or s.priority != self.side_priority:
-            s = torch.cuda.Stream(device=dev, priority=self.side_priority)
+        if s is None or s.device != dev:
+            s = torch.cuda.Stream(device=dev)
             object.__setattr__(self, "_vcg_side", s)
         return s
 

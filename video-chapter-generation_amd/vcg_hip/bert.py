@@ -158,6 +158,9 @@ class BertEncoderEngine:
     # unpadded sequences (Packing) where the caller reads only the pooler output and the fused attention applies;
     # False: every padded row is computed (tests compare both)
     unpad = True
+    # bf16 backward: the Linear weight / bias gradients (split-K GEMMs + column sums) on a side stream, concurrently
+    # with the input-gradient chain they branch off; False: one stream
+    wgrad_stream = True
 
     def __init__(self, model, flat, dtype):
         self.m = model
@@ -297,6 +300,8 @@ class BertEncoderEngine:
             raise RuntimeError("BertEncoderEngine: the unpadded forward has no last hidden state to differentiate")
         p_h, p_a, scale, seed = sv["p_h"], sv["p_a"], sv["scale"], sv["seed"]
         dev = sv["ids"].device
+        side = _WSide(dev) if (BertEncoderEngine.wgrad_stream and dt == torch.bfloat16 and dev.type == "cuda") else None
+        wg = side.run if side is not None else (lambda fn, *t: fn())
         # the residual-gradient stream (the gradient w.r.t. each LayerNorm output, summed over the skip and the next
         # layer's input gradient) stays fp32 between the LayerNorm backwards, as torch autocast keeps it (its
         # LayerNorm outputs are fp32): bf16 roundings of it compounded over 24 LayerNorms
@@ -331,18 +336,22 @@ class BertEncoderEngine:
             ln2 = layer.output.LayerNorm
             dfo, dh1_res = ops.ln_bwd(dh_, s["fo"], s["h1"], ln2.weight, s["m2"], s["r2"], ln2.weight.grad,
                                       ln2.bias.grad, rows, H, p_h, s["s2"], bias_grad=out.bias.grad)
-            ops.gemm_splitk(dfo, s["ff"], out.weight.grad, H, I, rows, H, I, transA=True, transB=True)
+            wg(lambda: ops.gemm_splitk(dfo, s["ff"], out.weight.grad, H, I, rows, H, I, transA=True, transB=True),
+               dfo, s["ff"])
             dpre = self._gemm_dx(dfo, self._w(out.weight), rows, I, H, act=ops.ACT_GELU_BWD, residual=s["pre"], ldr=I)
             del dfo
-            ops.gemm_splitk(dpre, s["h1"], inter.weight.grad, I, H, rows, I, H, transA=True, transB=True)
-            ops.colsum(dpre, I, rows, I, inter.bias.grad)
+            def ffn1_w(dpre=dpre, h1=s["h1"]):
+                ops.gemm_splitk(dpre, h1, inter.weight.grad, I, H, rows, I, H, transA=True, transB=True)
+                ops.colsum(dpre, I, rows, I, inter.bias.grad)
+            wg(ffn1_w, dpre, s["h1"])
             dh1 = self._gemm_dx(dpre, self._w(inter.weight), rows, H, I, f32_out=g32, residual=dh1_res, ldr=H)
             del dpre, dh1_res
             ln1 = at.output.LayerNorm
             od = at.output.dense
             dao, dh_res = ops.ln_bwd(dh1, s["ao"], s["h"], ln1.weight, s["m1"], s["r1"], ln1.weight.grad,
                                      ln1.bias.grad, rows, H, p_h, s["s1"], bias_grad=od.bias.grad)
-            ops.gemm_splitk(dao, s["ctx"], od.weight.grad, H, H, rows, H, H, transA=True, transB=True)
+            wg(lambda: ops.gemm_splitk(dao, s["ctx"], od.weight.grad, H, H, rows, H, H, transA=True, transB=True),
+               dao, s["ctx"])
             dctx = self._gemm_dx(dao, self._w(od.weight), rows, H, H)
             del dao
             # ---- attention backward
@@ -354,13 +363,18 @@ class BertEncoderEngine:
             if sq.weight.requires_grad:
                 gW = flat.contiguous_view([sq.weight, sk.weight, svv.weight], (3 * H, H), "grad")
                 gb = flat.contiguous_view([sq.bias, sk.bias, svv.bias], (3 * H,), "grad")
-                ops.gemm_splitk(dqkv, s["h"], gW, 3 * H, H, rows, 3 * H, H, transA=True, transB=True)
-                ops.colsum(dqkv, 3 * H, rows, 3 * H, gb)
+                def qkv_w(dqkv=dqkv, h=s["h"], gW=gW, gb=gb):
+                    ops.gemm_splitk(dqkv, h, gW, 3 * H, H, rows, 3 * H, H, transA=True, transB=True)
+                    ops.colsum(dqkv, 3 * H, rows, 3 * H, gb)
+                wg(qkv_w, dqkv, s["h"])
             Wqkv = flat.compute_contiguous([sq.weight, sk.weight, svv.weight], (3 * H, H), dt)
             dh_ = self._gemm_dx(dqkv, Wqkv, rows, H, 3 * H, f32_out=g32, residual=dh_res, ldr=H)
             del dqkv, dh_res, s
-            if hooks is not None:
-                hooks(list(layer.parameters()))
+            if hooks is not None:  # (after the layer's weight gradients: on their stream)
+                if side is not None:
+                    side.run(lambda: hooks(list(layer.parameters())))
+                else:
+                    hooks(list(layer.parameters()))
         emb = m.embeddings
         if packing is not None:  # back to the padded rows (zero gradient at the dropped ones)
             dpad = torch.zeros((B * L, H), dtype=dh_.dtype, device=dev)
@@ -373,6 +387,38 @@ class BertEncoderEngine:
                          pad_idx=-1 if emb.word_embeddings.padding_idx is None else emb.word_embeddings.padding_idx)
         if hooks is not None:
             hooks(list(emb.parameters()))
+        if side is not None:  # every weight gradient is complete on the caller's stream
+            side.join()
+
+
+class _WSide:
+    """BERT's weight-gradient side stream (one per device): run(fn, *tensors) issues fn there after everything issued so
+    far on the caller's stream and keeps `tensors` referenced until an event after fn has completed (as the trunk's
+    ResNetTrunk._hold; record_stream's deferred frees grow the pool when the side stream trails); join() makes the
+    caller's stream wait for it."""
+    _streams = {}
+
+    def __init__(self, dev):
+        key = dev.index if dev.index is not None else torch.cuda.current_device()
+        st = _WSide._streams.get(key)
+        if st is None:
+            st = _WSide._streams[key] = torch.cuda.Stream(device=dev)
+        self.s, self.pending = st, []
+
+    def run(self, fn, *tensors):
+        self.s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.s):
+            out = fn()
+        ev = torch.cuda.Event()
+        ev.record(self.s)
+        self.pending.append((ev, tensors))
+        while self.pending and self.pending[0][0].query():
+            self.pending.pop(0)
+        return out
+
+    def join(self):
+        torch.cuda.current_stream().wait_stream(self.s)
+        self.pending.clear()
 
 
 def attention_fwd(qkv_buf, mask, B, nh, L, Lp, dh, scale, p_a, seed, fused, seq=None, rows=None):
