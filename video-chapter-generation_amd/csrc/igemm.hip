@@ -560,7 +560,10 @@ static void splitk_reduce(hipStream_t stream, const float* ws, int splits, long 
 
 // Split-K target: tiles x splits ~ this many workgroups (2 rounds of 2 workgroups per CU; 512 and 2048 measured
 // -2.4 % / -1.3 % per step, profiles/r05_splitk_target_ab.txt). Fewer splits write and re-read fewer fp32 slabs.
-static int splitk_target() { return 1024; }
+#ifndef VCG_SPLITK_TARGET
+#define VCG_SPLITK_TARGET 1024
+#endif
+static int splitk_target() { return VCG_SPLITK_TARGET; }
 
 static int choose_splits(int M, int N, int K, int BK) {
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
