@@ -564,10 +564,13 @@ static void splitk_reduce(hipStream_t stream, const float* ws, int splits, long 
 #define VCG_SPLITK_TARGET 1024
 #endif
 static int splitk_target() { return VCG_SPLITK_TARGET; }
+#ifndef VCG_SPLITK_TARGET_DENSE
+#define VCG_SPLITK_TARGET_DENSE VCG_SPLITK_TARGET
+#endif
 
-static int choose_splits(int M, int N, int K, int BK) {
+static int choose_splits(int M, int N, int K, int BK, int target = splitk_target()) {
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  int splits = (splitk_target() + tiles - 1) / tiles;
+  int splits = (target + tiles - 1) / tiles;
   const int max_splits = (K + 16 * BK - 1) / (16 * BK);  // at least 16 k-tiles per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -1524,7 +1527,7 @@ VCG_API int vcg_gemm(int dtype, int transA, int transB, int M, int N, int K, con
 }
 
 VCG_API long long vcg_gemm_splitk_ws_bytes(int dtype, int M, int N, int K) {
-  const int splits = choose_splits(M, N, K, dtype == VCG_BF16 ? 32 : 16);
+  const int splits = choose_splits(M, N, K, dtype == VCG_BF16 ? 32 : 16, VCG_SPLITK_TARGET_DENSE);
   return (long long)splits * M * N * 4;
 }
 
@@ -1534,7 +1537,7 @@ VCG_API int vcg_gemm_splitk(int dtype, int transA, int transB, int M, int N, int
                             hipStream_t stream) {
   const int BK = dtype == VCG_BF16 ? 32 : 16;
   // (the Linear weight gradients with a 256-workgroup target: -2.1 % per step, profiles/r06_vs_r05_same_box.txt)
-  int splits = choose_splits(M, N, K, BK);
+  int splits = choose_splits(M, N, K, BK, VCG_SPLITK_TARGET_DENSE);
   VCG_REQUIRE(ws_bytes >= (long long)splits * M * N * 4, "workspace too small");
   int kps = (K + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
