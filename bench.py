@@ -206,6 +206,8 @@ def long_video_bench(args):
     idx, ids, mask = (torch.from_numpy(a).to(dev) for a in (idx, ids, mask))
     K = args.scoring_streams
     G = args.bn_groups
+    if args.bn_group_streams > 0:
+        model.bn_group_streams = args.bn_group_streams
     # re-bias the random-init 2-way head (untimed, as tests/test_gpu_long_video.py does) so its decisions split
     # about evenly: otherwise every window sits on one side of 0.5, no cut point is predicted and F is 0 / undefined
     samp = torch.from_numpy(np.linspace(0, len(win) - 1, 256).astype(np.int64)).to(dev)

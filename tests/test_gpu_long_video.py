@@ -275,7 +275,7 @@ def test_c5_stride4_f1_vs_oracle_golden():
             assert m32[k] == float(g["metric_" + k]), k
 
 
-@pytest.mark.parametrize("precision,streams", [("bf16", 2), ("bf16", 1), ("fp32", 2)])
+@pytest.mark.parametrize("precision,streams", [("bf16", 3), ("bf16", 1), ("fp32", 3)])
 def test_score_windows_groups_identical(precision, streams):
     """Batch-statistics scoring with 4 batches of 16 windows per forward (TwoStream.bn_group: the trunk per batch with
     its own BatchNorm statistics -- the groups' trunks on `streams` HIP streams --, BERT and the head once over all 64

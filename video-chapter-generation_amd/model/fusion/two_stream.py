@@ -127,11 +127,11 @@ class TwoStream(NativeRoot, nn.Module):
     # of the batch -- once over all windows at full chip fill. Bit-identical to forwarding the groups one by one.
     # None: the statistics span the whole batch (the reference forward).
     bn_group = None
-    # ... the groups' trunks round-robin on this many HIP streams (1: one after another on the caller's stream); a
-    # concurrent group's downsample branches run inline (the trunk's shared side stream would couple the groups).
-    # 4 x 16 windows (profiles/r06_scoring_groups.txt): 1 stream 2154, 2 streams 2553, 4 streams 2555 windows/s;
-    # one batch of 64 (the bound) 2617; one forward per batch of 16: 2090
-    bn_group_streams = 2
+    # ... the groups' trunks round-robin on this many HIP streams, the caller's included (1: one after another on the
+    # caller's stream); a concurrent group's downsample branches run inline (the trunk's shared side stream would
+    # couple the groups). 4 x 16 windows (profiles/r06_scoring_groups.txt): 3 streams 2550 (C2) / 2443 (C5) windows/s,
+    # 2: 2379 / 2446, 4: 2371 / 2452, 5: 2345 / 2452; one forward per batch of 16: 2090 / 2175
+    bn_group_streams = 3
 
     def _side_stream(self, dev):
         """The BERT side stream (None: one stream), created once per device."""
@@ -144,9 +144,9 @@ class TwoStream(NativeRoot, nn.Module):
         return s
 
     def _group_streams(self, dev):
-        """The streams of concurrent per-group trunks ([]: the caller's stream only)."""
-        n = self.bn_group_streams
-        if n <= 1 or dev.type != "cuda":
+        """The extra streams of concurrent per-group trunks, besides the caller's ([]: the caller's stream only)."""
+        n = self.bn_group_streams - 1
+        if n <= 0 or dev.type != "cuda":
             return []
         pool = getattr(self, "_vcg_group_streams", None)
         if pool is None or len(pool) != n or pool[0].device != dev:
@@ -216,20 +216,21 @@ class TwoStream(NativeRoot, nn.Module):
         if G is not None and not need_grad and 0 < G < batch_size and self._trunk_batch_stats():
             T = img.shape[0] // batch_size
             main = torch.cuda.current_stream(dev)
-            pool = self._group_streams(dev)
+            pool = [main] + self._group_streams(dev)  # (the caller's stream takes every n-th group itself)
             embs = []
             for k, g0 in enumerate(range(0, batch_size, G)):
                 trunk = ResNetTrunk(self.vision_model, dt)
                 trunk.staged = staged
-                st = pool[k % len(pool)] if pool else main
-                if st is not main:
+                st = pool[k % len(pool)]
+                if len(pool) > 1:
                     trunk.ds_stream = False
+                if st is not main:
                     st.wait_stream(main)
                 with torch.cuda.stream(st):
                     embs.append(TrunkFn.apply(img[g0 * T:min(batch_size, g0 + G) * T], anchor, trunk, False, hooks))
                 if st is not main:
                     embs[-1].record_stream(main)  # (allocated on st, read and freed on main)
-            for st in pool:
+            for st in pool[1:]:
                 main.wait_stream(st)
             vision_emb = torch.cat(embs)
         else:
