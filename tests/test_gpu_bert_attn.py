@@ -171,7 +171,8 @@ def test_varlen_attention_matches_padded(p):
             assert torch.equal(ctx_k[a], ctx_p[c]) and torch.equal(dqkv_k[a], dqkv_p[c]), b
 
 
-def test_unpadded_bert_in_two_stream_step(monkeypatch):
+@pytest.mark.parametrize("case", ["prefix", "holes"])
+def test_unpadded_bert_in_two_stream_step(monkeypatch, case):
     """A whole bf16 TwoStream train step (dropout 0) with BERT's padded rows dropped (BertEncoderEngine.unpad) vs
     every row computed: logits bit-identical (prefix masks: the kept rows see the padded computation exactly), every
     parameter gradient within fp32 summation-order rounding (the weight-gradient and bias sums run over fewer rows)."""
@@ -183,6 +184,10 @@ def test_unpadded_bert_in_two_stream_step(monkeypatch):
     T, HW, L = 2, 64, 128
     frames, ids, mask, labels = synth.clip_batch(6, T, HW, HW, L, seed=21, device=DEV)
     assert (mask == 0).any()
+    if case == "holes":  # masked positions inside the text, a masked CLS, a window without any key
+        mask[0, 10:20] = 0
+        mask[1, 0] = 0
+        mask[2] = 0
     res = {}
     for unpad in (True, False):
         monkeypatch.setattr(BertEncoderEngine, "unpad", unpad)
@@ -194,8 +199,11 @@ def test_unpadded_bert_in_two_stream_step(monkeypatch):
         res[unpad] = (logits.detach().float().cpu(),
                       {n: p.grad.detach().double().cpu().clone() for n, p in m.named_parameters() if p.grad is not None})
     (l1, g1), (l0, g0) = res[True], res[False]
-    assert torch.equal(l1, l0)
+    if case == "prefix":
+        assert torch.equal(l1, l0)
+    else:  # (shifted key positions: the same sums in another order)
+        assert (l1 - l0).abs().max().item() < 2e-3
     assert g1.keys() == g0.keys()
     errs = sorted((rel(g1[n], g0[n]), n) for n in g1 if g0[n].norm() > 1e-3 * max(v.norm() for v in g0.values()))
-    print("unpadded vs padded grad rel errors: median %.3e, worst %s" % (errs[len(errs) // 2][0], errs[-3:]))
-    assert errs[-1][0] < 2e-3, errs[-3:]
+    print(f"{case}: unpadded vs padded grad rel errors: median %.3e, worst %s" % (errs[len(errs) // 2][0], errs[-3:]))
+    assert errs[-1][0] < (2e-3 if case == "prefix" else 5e-2), errs[-3:]
