@@ -173,8 +173,8 @@ def test_varlen_attention_matches_padded(p):
 
 @pytest.mark.parametrize("case", ["prefix", "holes"])
 def test_unpadded_bert_in_two_stream_step(monkeypatch, case):
-    """A whole bf16 TwoStream train step (dropout 0) with BERT's padded rows dropped (BertEncoderEngine.unpad) vs
-    every row computed: logits bit-identical (prefix masks: the kept rows see the padded computation exactly), every
+    """A whole bf16 TwoStream train step (dropout 0) with BERT's padded rows dropped (BertEncoderEngine.unpad) and its
+    last layer past the attention on the position-0 rows only (cls_last) vs every row computed: logits bit-identical (prefix masks: the kept rows see the padded computation exactly), every
     parameter gradient within fp32 summation-order rounding (the weight-gradient and bias sums run over fewer rows)."""
     from vcg_hip import _lib, synth
     from vcg_hip.bert import BertEncoderEngine, PackingRequest
@@ -189,8 +189,9 @@ def test_unpadded_bert_in_two_stream_step(monkeypatch, case):
         mask[1, 0] = 0
         mask[2] = 0
     res = {}
-    for unpad in (True, False):
+    for unpad in (True, False):  # (the reference arm also runs the last layer on every row: cls_last off)
         monkeypatch.setattr(BertEncoderEngine, "unpad", unpad)
+        monkeypatch.setattr(BertEncoderEngine, "cls_last", unpad)
         PackingRequest._last = PackingRequest._mirror = None
         m = build_two_stream(clip_frame_num=T, seed=5, device=DEV, precision="bf16", dropout=0.0).train()
         logits, _ = m(frames, ids, mask)

@@ -161,6 +161,9 @@ class BertEncoderEngine:
     # bf16 backward: the Linear weight / bias gradients (split-K GEMMs + column sums) on a side stream, concurrently
     # with the input-gradient chain they branch off; False: one stream
     wgrad_stream = True
+    # where only the pooler output is read: the last layer after its attention (output projection, LayerNorms, FFN)
+    # runs on the B position-0 rows only -- the pooler reads nothing else (its K / V still cover every row)
+    cls_last = True
 
     def __init__(self, model, flat, dtype):
         self.m = model
@@ -249,6 +252,11 @@ class BertEncoderEngine:
         if packing is not None:
             h = h.index_select(0, packing.rows)
         att_mask, seq = (mask, None) if packing is None else (packing.keys, packing.seq)
+        co = (BertEncoderEngine.cls_last and self.pooled_only and m.pooler is not None and self._fused_attn(L, dh))
+        cls_idx = None
+        if co:
+            cls_idx = packing.cls if packing is not None else torch.arange(0, B * L, L, dtype=torch.int64, device=dev)
+        nl = len(m.encoder.layer)
         saved_layers = []
         for i, layer in enumerate(m.encoder.layer):
             at = layer.attention
@@ -261,43 +269,50 @@ class BertEncoderEngine:
             sa = _seed(seed, i + 1, 1)
             ctx, att = attention_fwd(qkv_buf, att_mask, B, nh, L, Lp, dh, scale, p_a, sa, self._fused_attn(L, dh),
                                      seq=seq, rows=rows)
-            ao = ops.gemm(ctx, self._w(at.output.dense.weight), rows, H, H, H, H, bias=at.output.dense.bias, act=lib)
+            lco = co and i == nl - 1  # (the last layer past its attention: the CLS rows only)
+            hs, ctxs, lr = (h.index_select(0, cls_idx), ctx.index_select(0, cls_idx), B) if lco else (h, ctx, rows)
+            ao = ops.gemm(ctxs, self._w(at.output.dense.weight), lr, H, H, H, H, bias=at.output.dense.bias, act=lib)
             s1 = _seed(seed, i + 1, 2)
-            h1, m1, r1 = ops.ln_fwd(ao, h, at.output.LayerNorm.weight, at.output.LayerNorm.bias, rows, H, eps, p_h, s1)
+            h1, m1, r1 = ops.ln_fwd(ao, hs, at.output.LayerNorm.weight, at.output.LayerNorm.bias, lr, H, eps, p_h, s1)
             inter, out = layer.intermediate.dense, layer.output.dense
             I = inter.out_features
-            pre = torch.empty((rows, I), dtype=dt, device=dev) if need_grad else None
-            ff = ops.gemm(h1, self._w(inter.weight), rows, I, H, H, H, bias=inter.bias, act=ops.ACT_GELU | lib, aux=pre)
-            fo = ops.gemm(ff, self._w(out.weight), rows, H, I, I, I, bias=out.bias, act=lib)
+            pre = torch.empty((lr, I), dtype=dt, device=dev) if need_grad else None
+            ff = ops.gemm(h1, self._w(inter.weight), lr, I, H, H, H, bias=inter.bias, act=ops.ACT_GELU | lib, aux=pre)
+            fo = ops.gemm(ff, self._w(out.weight), lr, H, I, I, I, bias=out.bias, act=lib)
             s2 = _seed(seed, i + 1, 3)
-            h2, m2, r2 = ops.ln_fwd(fo, h1, layer.output.LayerNorm.weight, layer.output.LayerNorm.bias, rows, H, eps,
+            h2, m2, r2 = ops.ln_fwd(fo, h1, layer.output.LayerNorm.weight, layer.output.LayerNorm.bias, lr, H, eps,
                                     p_h, s2)
             if need_grad:
-                saved_layers.append(dict(h=h, qkv_buf=qkv_buf, att=att, ctx=ctx, ao=ao, h1=h1, pre=pre, ff=ff,
-                                         fo=fo, m1=m1, r1=r1, m2=m2, r2=r2, sa=sa, s1=s1, s2=s2))
+                saved_layers.append(dict(h=h, hs=hs, qkv_buf=qkv_buf, att=att, ctxs=ctxs, ao=ao, h1=h1, pre=pre,
+                                         ff=ff, fo=fo, m1=m1, r1=r1, m2=m2, r2=r2, sa=sa, s1=s1, s2=s2, lr=lr,
+                                         lco=lco))
             h = h2
         pooled = None
-        cls = h if packing is None else h.index_select(0, packing.cls)  # (packed: the B position-0 rows)
-        lda = L * H if packing is None else H
+        if co:  # (h is already the B position-0 rows)
+            cls, lda = h, H
+        else:
+            cls = h if packing is None else h.index_select(0, packing.cls)  # (packed: the B position-0 rows)
+            lda = L * H if packing is None else H
         if m.pooler is not None:
             pd = m.pooler.dense
             pooled = ops.gemm(cls, self._w(pd.weight), B, H, H, lda, H, bias=pd.bias, act=ops.ACT_TANH)
         saved = None
         if need_grad:
-            saved = dict(ids=ids, mask=att_mask, seq=seq, packing=packing, layers=saved_layers, e_mean=e_mean,
+            saved = dict(ids=ids, mask=att_mask, seq=seq, packing=packing, co=co, cls_idx=cls_idx, layers=saved_layers,
+                         e_mean=e_mean,
                          e_rstd=e_rstd, h_last=cls, lda=lda, pooled=pooled, B=B, L=L, Lp=Lp, H=H, nh=nh, dh=dh,
                          p_h=p_h, p_a=p_a, scale=scale, seed=seed)
-        if packing is not None:
-            h = h.new_empty((0, H))  # (the padded rows' hidden states were not computed)
+        if packing is not None or co:
+            h = h.new_empty((0, H))  # (the padded rows' / the last layer's hidden states were not all computed)
         return pooled, h, saved
 
     def backward(self, d_pooled, d_last, sv, hooks=None):
         m, dt, flat = self.m, self.dtype, self.flat
         B, L, Lp, H, nh, dh = sv["B"], sv["L"], sv["Lp"], sv["H"], sv["nh"], sv["dh"]
-        packing = sv["packing"]
+        packing, co, cls_idx = sv["packing"], sv["co"], sv["cls_idx"]
         rows = B * L if packing is None else packing.R
-        if packing is not None and d_last is not None and d_last.numel():
-            raise RuntimeError("BertEncoderEngine: the unpadded forward has no last hidden state to differentiate")
+        if (packing is not None or co) and d_last is not None and d_last.numel():
+            raise RuntimeError("BertEncoderEngine: the pooled-only forward has no last hidden state to differentiate")
         p_h, p_a, scale, seed = sv["p_h"], sv["p_a"], sv["scale"], sv["seed"]
         dev = sv["ids"].device
         side = _WSide(dev) if (BertEncoderEngine.wgrad_stream and dt == torch.bfloat16 and dev.type == "cuda") else None
@@ -309,8 +324,8 @@ class BertEncoderEngine:
         gd = torch.float32 if g32 else dt
         if d_last is not None and d_last.numel():
             dh_ = d_last.to(gd).contiguous().clone()
-        else:
-            dh_ = torch.zeros((rows, H), dtype=gd, device=dev)
+        else:  # (co: the last layer's output is the B position-0 rows)
+            dh_ = torch.zeros((B if co else rows, H), dtype=gd, device=dev)
         if d_pooled is not None and m.pooler is not None:
             pd = m.pooler.dense
             dpp = ops.tanh_bwd(d_pooled.to(dt).contiguous(), sv["pooled"])
@@ -320,7 +335,9 @@ class BertEncoderEngine:
                 ops.colsum(dpp, H, B, H, pd.bias.grad)
             # dh[b*L] += dpp @ Wp (B rows: an fp32 GEMM on the fp32 stream)
             dpw = (dpp.float(), pd.weight.data) if g32 else (dpp, self._w(pd.weight))
-            if packing is None:
+            if co:
+                ops.gemm(dpw[0], dpw[1], B, H, H, H, H, transB=True, out=dh_, ldc=H, residual=dh_, ldr=H)
+            elif packing is None:
                 ops.gemm(dpw[0], dpw[1], B, H, H, H, H, transB=True, out=dh_, ldc=L * H, residual=dh_, ldr=L * H)
             else:  # (dh_ is zero: the CLS rows receive the product)
                 dh_.index_copy_(0, packing.cls, ops.gemm(dpw[0], dpw[1], B, H, H, H, H, transB=True,
@@ -329,34 +346,38 @@ class BertEncoderEngine:
                 hooks(list(m.pooler.parameters()))
         for i in reversed(range(len(sv["layers"]))):
             s = sv["layers"].pop()
+            lr = s["lr"]  # (rows past the attention: B for the CLS-only last layer)
             layer = m.encoder.layer[i]
             at = layer.attention
             inter, out = layer.intermediate.dense, layer.output.dense
             I = inter.out_features
             ln2 = layer.output.LayerNorm
             dfo, dh1_res = ops.ln_bwd(dh_, s["fo"], s["h1"], ln2.weight, s["m2"], s["r2"], ln2.weight.grad,
-                                      ln2.bias.grad, rows, H, p_h, s["s2"], bias_grad=out.bias.grad)
-            wg(lambda: ops.gemm_splitk(dfo, s["ff"], out.weight.grad, H, I, rows, H, I, transA=True, transB=True),
+                                      ln2.bias.grad, lr, H, p_h, s["s2"], bias_grad=out.bias.grad)
+            wg(lambda: ops.gemm_splitk(dfo, s["ff"], out.weight.grad, H, I, lr, H, I, transA=True, transB=True),
                dfo, s["ff"])
-            dpre = self._gemm_dx(dfo, self._w(out.weight), rows, I, H, act=ops.ACT_GELU_BWD, residual=s["pre"], ldr=I)
+            dpre = self._gemm_dx(dfo, self._w(out.weight), lr, I, H, act=ops.ACT_GELU_BWD, residual=s["pre"], ldr=I)
             del dfo
             def ffn1_w(dpre=dpre, h1=s["h1"]):
-                ops.gemm_splitk(dpre, h1, inter.weight.grad, I, H, rows, I, H, transA=True, transB=True)
-                ops.colsum(dpre, I, rows, I, inter.bias.grad)
+                ops.gemm_splitk(dpre, h1, inter.weight.grad, I, H, lr, I, H, transA=True, transB=True)
+                ops.colsum(dpre, I, lr, I, inter.bias.grad)
             wg(ffn1_w, dpre, s["h1"])
-            dh1 = self._gemm_dx(dpre, self._w(inter.weight), rows, H, I, f32_out=g32, residual=dh1_res, ldr=H)
+            dh1 = self._gemm_dx(dpre, self._w(inter.weight), lr, H, I, f32_out=g32, residual=dh1_res, ldr=H)
             del dpre, dh1_res
             ln1 = at.output.LayerNorm
             od = at.output.dense
-            dao, dh_res = ops.ln_bwd(dh1, s["ao"], s["h"], ln1.weight, s["m1"], s["r1"], ln1.weight.grad,
-                                     ln1.bias.grad, rows, H, p_h, s["s1"], bias_grad=od.bias.grad)
-            wg(lambda: ops.gemm_splitk(dao, s["ctx"], od.weight.grad, H, H, rows, H, H, transA=True, transB=True),
-               dao, s["ctx"])
-            dctx = self._gemm_dx(dao, self._w(od.weight), rows, H, H)
+            dao, dh_res = ops.ln_bwd(dh1, s["ao"], s["hs"], ln1.weight, s["m1"], s["r1"], ln1.weight.grad,
+                                     ln1.bias.grad, lr, H, p_h, s["s1"], bias_grad=od.bias.grad)
+            wg(lambda: ops.gemm_splitk(dao, s["ctxs"], od.weight.grad, H, H, lr, H, H, transA=True, transB=True),
+               dao, s["ctxs"])
+            dctx = self._gemm_dx(dao, self._w(od.weight), lr, H, H)
             del dao
+            if s["lco"]:  # back to every row: the attention's other rows (and the residual) receive zero
+                dctx = torch.zeros((rows, H), dtype=dctx.dtype, device=dev).index_copy_(0, cls_idx, dctx)
+                dh_res = torch.zeros((rows, H), dtype=dh_res.dtype, device=dev).index_copy_(0, cls_idx, dh_res)
             # ---- attention backward
             qkv_buf = s["qkv_buf"]
-            dqkv = attention_bwd(qkv_buf, dctx, s["ctx"], sv["mask"], s["att"], B, nh, L, Lp, dh, scale, p_a,
+            dqkv = attention_bwd(qkv_buf, dctx, None, sv["mask"], s["att"], B, nh, L, Lp, dh, scale, p_a,
                                  s["sa"], seq=sv["seq"], rows=rows)
             del dctx
             sq, sk, svv = at.self.query, at.self.key, at.self.value
